@@ -1,0 +1,103 @@
+"""Loader for libgmz.so (the HIP kernels + C ABI of include/gmz.h).
+
+The product path has NO fallback: if the shared library is missing or was built for another
+ABI, importing this module raises.  ``torch`` is imported first so that libgmz.so binds to the
+same HIP runtime (soname libamdhip64.so.7) that torch's allocator and streams use.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the CDLL load: shared HIP runtime)
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libgmz.so")
+ABI_VERSION = 1
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+U64 = ctypes.c_uint64
+
+
+class EngineCfg(ctypes.Structure):
+    _fields_ = [("num_games", ctypes.c_int32), ("board_size", ctypes.c_int32), ("n_in_row", ctypes.c_int32),
+                ("num_simulations", ctypes.c_int32), ("num_top_actions", ctypes.c_int32), ("mode", ctypes.c_int32),
+                ("c_visit", ctypes.c_int32), ("reserved", ctypes.c_int32), ("c_scale", ctypes.c_double),
+                ("minmax_delta", ctypes.c_double), ("discount", ctypes.c_double)]
+
+
+_SIGS = {
+    "gmz_last_error": ([], ctypes.c_char_p),
+    "gmz_abi_version": ([], I),
+    "gmz_device_synchronize": ([], I),
+    "gmz_game_check_win": ([P, I, I, I, P, P, P], I),
+    "gmz_game_board_state": ([P, I, I, P, P, P, P], I),
+    "gmz_game_play": ([P, I, I, I, P, P, P, P, P, P], I),
+    "gmz_engine_create": ([ctypes.POINTER(EngineCfg), ctypes.POINTER(P)], I),
+    "gmz_engine_destroy": ([P], I),
+    "gmz_engine_game_state": ([P, ctypes.POINTER(P), ctypes.POINTER(P), ctypes.POINTER(P), ctypes.POINTER(P)], I),
+    "gmz_engine_copy_state": ([P, I, P, P, P, P, P], I),
+    "gmz_engine_reset_games": ([P, P, P], I),
+    "gmz_engine_begin_move": ([P, P, U64, P, P], I),
+    "gmz_engine_set_root": ([P, P, P, P], I),
+    "gmz_engine_select": ([P, P, P, P, P, P], I),
+    "gmz_engine_expand_backup": ([P, P, P, P, P], I),
+    "gmz_engine_pending_waves": ([P, P], I),
+    "gmz_engine_waves_for_legal": ([ctypes.POINTER(EngineCfg), P, I, P], I),
+    "gmz_engine_finish_move": ([P, P, P, P, P], I),
+    "gmz_engine_play": ([P, P, P, I, P], I),
+    "gmz_engine_root_stats": ([P, P, P, P, P, P, P], I),
+    "gmz_hashnet_initial": ([P, I, I, P, P, P, P, P], I),
+    "gmz_hashnet_recurrent": ([P, P, P, P, I, I, P, P, P, P], I),
+}
+
+# symbols added by the network kernels (declared in include/gmz.h too)
+_NET_SIGS = {}
+
+_lib = None
+
+
+class GmzError(RuntimeError):
+    pass
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise GmzError("libgmz.so not built (%s); run __graft_entry__.build() or make -C csrc" % LIB_PATH)
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (args, res) in list(_SIGS.items()) + list(_NET_SIGS.items()):
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    if lib.gmz_abi_version() != ABI_VERSION:
+        raise GmzError("libgmz.so ABI %d != %d" % (lib.gmz_abi_version(), ABI_VERSION))
+    _lib = lib
+    return lib
+
+
+def register(sigs):
+    """Extend the signature table (used by modules that add exported symbols)."""
+    _NET_SIGS.update(sigs)
+    if _lib is not None:
+        for name, (args, res) in sigs.items():
+            fn = getattr(_lib, name)
+            fn.argtypes = args
+            fn.restype = res
+
+
+def check(rc):
+    if rc != 0:
+        raise GmzError(load().gmz_last_error().decode(errors="replace"))
+    return rc
+
+
+def ptr(t):
+    """Device/host pointer of a torch tensor (or None → NULL)."""
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream_ptr(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)

@@ -1,0 +1,910 @@
+// gmz_tree.hip — batched Gumbel MuZero / AlphaZero tree search for gfx950 (the ★ hot path).
+//
+// One wavefront (64 lanes) owns one game's tree; a 256-thread workgroup searches 4 games.
+// Every step of /root/reference/mcts.py is restated for G games at once:
+//   begin_move      mcts.py:288-306  tree reset, root legal set, root observation, Gumbel noise
+//   set_root        mcts.py:308-317  root.expand, _backpropagate([root]), Gumbel top-k
+//   select          mcts.py:88-117   descend: root = least-visited selected action,
+//                                    non-root = argmax(improved policy - N/(1+sum N))
+//                   mcts.py:236-251  (AlphaZero) replay the path on the root board -> observation
+//   expand_backup   mcts.py:339-350  expand + k-fold duplicate-leaf backup (mcts.py:119-138),
+//                   mcts.py:158-185  sequential-halving schedule
+//   finish_move     mcts.py:353-362  improved policy, root value, argmax visits (set-order ties)
+//
+// HBM layout (SoA per game):
+//   Edge edges[G][S][A]   {child, N, W, R} 16 B per (node, action): one dwordx4 per lane per
+//                         action, coalesced across the wave when a node's children are scanned
+//   float logits[G][S][A] node policy logits (network output)
+//   int path_u/path_a[G][S], node_parent/node_action[G][S], per-game scalars GameState[G]
+// S = num_simulations + 2 node slots per game (root + <= 1 new node per wave + 1 scratch slot).
+//
+// Numerics: float32 statistics with -ffp-contract=off and IEEE division reproduce the reference's
+// numpy-float32 arithmetic bit-for-bit; the completed-Q/softmax path is float64 exactly where the
+// reference's arrays are float64 (see oracle/gmz_oracle.c header for the promotion rules).
+#include "gmz_common.h"
+#include "gmz_device.h"
+#include "../../include/gmz.h"
+
+#include <math.h>
+#include <string.h>
+#include <vector>
+
+namespace gmz {
+
+struct Edge {
+  int32_t child;
+  int32_t n;
+  float w;
+  float r;
+};
+
+struct GameState {
+  int32_t n_nodes, sim, phase, m_cur;
+  int32_t next_phase, root_n, n_sel, active;
+  int32_t depth, k, leaf, n_legal;
+  float root_w, mm_max, mm_min, pad0;
+  double used;
+  int32_t pad1[2];
+};
+
+struct Dev {
+  Edge *edges;
+  float *logits;
+  int32_t *node_parent, *node_action, *path_u, *path_a, *sel;
+  GameState *gs;
+  uint64_t *legal;  // [G][NJ]
+  int16_t *set_rank;
+  double *gumbel;
+  int8_t *boards, *players;
+  int32_t *last_moves, *move_counts;
+  int G, A, S, size, n_sims, m_top, c_visit, mode;
+  double c_scale;
+  float disc_f, delta_f;
+};
+
+__device__ __forceinline__ float clip1(float v) { return v < -1.f ? -1.f : (v > 1.f ? 1.f : v); }
+
+__device__ __forceinline__ const Edge *edge_row(const Dev &D, int g, int u) {
+  return D.edges + ((size_t)g * D.S + u) * D.A;
+}
+__device__ __forceinline__ Edge *edge_row_w(const Dev &D, int g, int u) {
+  return D.edges + ((size_t)g * D.S + u) * D.A;
+}
+
+// get_qsa (mcts.py:35-38) for the lane's actions a = lane + 64 j.
+__device__ __forceinline__ void row_load(const Dev &D, const Edge *row, int lane, int (&n)[NJ], float (&q)[NJ]) {
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int a = lane + WAVE * j;
+    n[j] = 0;
+    q[j] = 0.f;
+    if (a < D.A) {
+      const Edge e = row[a];
+      n[j] = e.n;
+      if (e.n > 0) {
+        const float v = e.w / (float)e.n;
+        const float dv = D.disc_f * v;
+        q[j] = e.r + dv;
+      }
+    }
+  }
+}
+
+// _get_transformed_completed_Qs (mcts.py:141-149) with MinMaxStats.normalize (utils.py:19-25).
+// Returns 1 when the reference array is float32 (t32 valid), else 0 (t64 valid).
+__device__ int transformed_q(const Dev &D, int lane, const int (&n)[NJ], const float (&q)[NJ], float mm_max,
+                             float mm_min, double (&t64)[NJ], float (&t32)[NJ], int &max_n_out) {
+  int mx = 0, allv = 1;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int a = lane + WAVE * j;
+    if (a < D.A) {
+      mx = max(mx, n[j]);
+      allv &= (n[j] > 0);
+    }
+  }
+  mx = wave_max_i(mx);
+  allv = wave_and(allv);
+  max_n_out = mx;
+  const double scale = (double)(D.c_visit + mx) * D.c_scale;
+  const bool have_range = mm_max > mm_min;
+  const float den_f = (mm_max - mm_min) + D.delta_f;
+  if (!allv) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      double nq = 0.0;
+      if (have_range) {
+        double x = ((double)q[j] - (double)mm_min) / (double)den_f;
+        x = (x < 1.0) ? x : 1.0;
+        nq = (x > 0.0) ? x : 0.0;
+      }
+      t64[j] = scale * nq;
+    }
+    return 0;
+  }
+  // every child visited: float32 array unless a clamp/no-range returned a python float
+  float nf[NJ];
+  int promote = have_range ? 0 : 1;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    float x = 0.f;
+    if (have_range && lane + WAVE * j < D.A) {
+      x = (q[j] - mm_min) / den_f;
+      if (!(x < 1.0f)) { x = 1.0f; promote = 1; }
+      if (!(x > 0.0f)) { x = 0.0f; promote = 1; }
+    }
+    nf[j] = x;
+  }
+  promote = wave_or(promote);
+  if (promote) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) t64[j] = scale * (double)nf[j];
+    return 0;
+  }
+  const float sf = (float)scale;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) t32[j] = sf * nf[j];
+  return 1;
+}
+
+// _get_improved_policy (mcts.py:151-156): softmax over the root legal set of logits + transformed Q.
+__device__ void improved_policy(const Dev &D, int g, int lane, const float *logit_row, const int (&n)[NJ],
+                                const float (&q)[NJ], float mm_max, float mm_min, double (&p)[NJ], int &max_n) {
+  double t64[NJ];
+  float t32[NJ];
+  const int is32 = transformed_q(D, lane, n, q, mm_max, mm_min, t64, t32, max_n);
+  const uint64_t *lg = D.legal + (size_t)g * NJ;
+  if (!is32) {
+    double x[NJ], m = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int a = lane + WAVE * j;
+      const bool ok = a < D.A && ((lg[j] >> lane) & 1ull);
+      x[j] = ok ? (double)logit_row[a] + t64[j] : -INFINITY;
+      m = fmax(m, x[j]);
+    }
+    m = wave_max_d(m);
+    double s = 0.0;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      x[j] = (x[j] == -INFINITY) ? 0.0 : exp(x[j] - m);
+      s += x[j];
+    }
+    s = wave_sum_d(s);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) p[j] = x[j] / s;
+  } else {
+    float x[NJ], m = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int a = lane + WAVE * j;
+      const bool ok = a < D.A && ((lg[j] >> lane) & 1ull);
+      x[j] = ok ? logit_row[a] + t32[j] : -INFINITY;
+      m = fmaxf(m, x[j]);
+    }
+    m = wave_max_f(m);
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      x[j] = (x[j] == -INFINITY) ? 0.f : expf(x[j] - m);
+      s += x[j];
+    }
+    s = wave_sum_f(s);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) p[j] = (double)(x[j] / s);
+  }
+}
+
+// _select_action at a non-root node (mcts.py:106-117).
+__device__ int select_nonroot(const Dev &D, int g, int u, int lane, float mm_max, float mm_min) {
+  int n[NJ];
+  float q[NJ];
+  double p[NJ];
+  row_load(D, edge_row(D, g, u), lane, n, q);
+  int max_n;
+  improved_policy(D, g, lane, D.logits + ((size_t)g * D.S + u) * D.A, n, q, mm_max, mm_min, p, max_n);
+  int tot = 0;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) tot += n[j];
+  tot = wave_sum_i(tot);
+  const uint64_t *lg = D.legal + (size_t)g * NJ;
+  double best = -INFINITY;
+  int besta = 1 << 30;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int a = lane + WAVE * j;
+    if (a < D.A && ((lg[j] >> lane) & 1ull)) {
+      const double s = p[j] - (double)n[j] / (double)(1 + tot);
+      if (s > best) { best = s; besta = a; }
+    }
+  }
+  wave_argmax_first(best, besta);
+  return besta == (1 << 30) ? 0 : besta;
+}
+
+// _select_action at the root (mcts.py:96-104): first least-visited entry of the selected list.
+__device__ int select_root(const Dev &D, int g, int lane, int n_sel) {
+  int v = 0x7fffffff, i = 64 + lane, a = -1;
+  if (lane < n_sel) {
+    a = D.sel[g * MAX_TOP + lane];
+    v = edge_row(D, g, 0)[a].n;
+    i = lane;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    int ov = __shfl_xor(v, o, 64), oi = __shfl_xor(i, o, 64), oa = __shfl_xor(a, o, 64);
+    if (ov < v || (ov == v && oi < i)) { v = ov; i = oi; a = oa; }
+  }
+  return a;
+}
+
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_begin_move(Dev D, const double *__restrict__ gumbel_in, uint64_t seed,
+                                                    uint32_t counter, float *__restrict__ obs) {
+  __shared__ int16_t table[4][2048];
+  __shared__ int16_t oldk[4][512];
+  const int w = threadIdx.x / WAVE, lane = threadIdx.x & (WAVE - 1);
+  const int g = blockIdx.x * 4 + w;
+  if (g >= D.G) return;
+  const int A = D.A;
+  const int8_t *b = D.boards + (size_t)g * A;
+  const int8_t pl = D.players[g];
+  const int lm = D.last_moves[g];
+  int nl = 0;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int a = lane + WAVE * j;
+    const bool ok = a < A && b[a] == 0;
+    const uint64_t bal = __ballot(ok);
+    if (lane == 0) D.legal[(size_t)g * NJ + j] = bal;
+    nl += __popcll(bal);
+  }
+  // observation planes (game.py:12-17)
+  float *o = obs + (size_t)g * 3 * A;
+  for (int a = lane; a < A; a += WAVE) {
+    const int8_t v = b[a];
+    o[a] = v == pl ? 1.f : 0.f;
+    o[A + a] = v == -pl ? 1.f : 0.f;
+    o[2 * A + a] = a == lm ? 1.f : 0.f;
+  }
+  // tree reset: root = node 0 with an empty edge row
+  Edge *root = edge_row_w(D, g, 0);
+  for (int a = lane; a < A; a += WAVE) root[a] = Edge{-1, 0, 0.f, 0.f};
+  // Gumbel noise for this move (mcts.py:312)
+  double *gm = D.gumbel + (size_t)g * A;
+  for (int a = lane; a < A; a += WAVE) {
+    double gv;
+    if (gumbel_in) {
+      gv = gumbel_in[(size_t)g * A + a];
+    } else {
+      const uint32_t h1 = mix32((uint32_t)seed ^ mix32(counter * 0x9E3779B1u + (uint32_t)g * 0x85EBCA77u));
+      const uint32_t h2 = mix32(h1 ^ mix32((uint32_t)a + 0x68E31DA4u) ^ (uint32_t)(seed >> 32));
+      const uint32_t h3 = mix32(h2 + 0x1B873593u);
+      const uint64_t bits = ((uint64_t)h2 << 21) ^ (uint64_t)h3;  // 53 random bits
+      double u = (double)(bits & ((1ull << 53) - 1)) * 0x1.0p-53;
+      if (u <= 0.0) u = 0x1.0p-53;
+      gv = -log(-log(1.0 - u));
+    }
+    gm[a] = gv;
+  }
+  // CPython set iteration rank of the legal actions (decides ties in mcts.py:356-357)
+  int16_t *T = table[w];
+  if (lane == 0) {
+    int mask = 7, fill = 0;
+    for (int i = 0; i < 8; ++i) T[i] = -1;
+    for (int a = 0; a < A; ++a) {
+      if (b[a] != 0) continue;
+      // set_add_entry probing
+      unsigned perturb = (unsigned)a, i = (unsigned)a & mask;
+      for (;;) {
+        if (T[i] < 0) break;
+        bool found = false;
+        if (i + 9 <= (unsigned)mask)
+          for (unsigned jj = 1; jj <= 9; ++jj)
+            if (T[i + jj] < 0) { i += jj; found = true; break; }
+        if (found) break;
+        perturb >>= 5;
+        i = (i * 5 + 1 + perturb) & mask;
+      }
+      T[i] = (int16_t)a;
+      fill++;
+      if (fill * 5 >= mask * 3) {
+        int ns = 8;
+        while (ns <= fill * 4) ns <<= 1;
+        // move old entries (slot order) to the tail region, then reinsert
+        int16_t *old = oldk[w];
+        int no = 0;
+        for (int s = 0; s <= mask; ++s)
+          if (T[s] >= 0) old[no++] = T[s];
+        mask = ns - 1;
+        for (int s = 0; s <= mask; ++s) T[s] = -1;
+        for (int t = 0; t < no; ++t) {
+          unsigned key = (unsigned)old[t], pp = key, ii = key & mask;
+          for (;;) {
+            if (T[ii] < 0) break;
+            bool f2 = false;
+            if (ii + 9 <= (unsigned)mask)
+              for (unsigned jj = 1; jj <= 9; ++jj)
+                if (T[ii + jj] < 0) { ii += jj; f2 = true; break; }
+            if (f2) break;
+            pp >>= 5;
+            ii = (ii * 5 + 1 + pp) & mask;
+          }
+          T[ii] = (int16_t)key;
+        }
+      }
+    }
+    int16_t *rank = D.set_rank + (size_t)g * A;
+    int r = 0;
+    for (int s = 0; s <= mask; ++s)
+      if (T[s] >= 0) rank[T[s]] = (int16_t)(r++);
+    GameState st;
+    st.n_nodes = 1; st.sim = 0; st.phase = 0; st.m_cur = D.m_top;
+    st.next_phase = 0; st.root_n = 0; st.n_sel = 0; st.active = 0;
+    st.depth = 0; st.k = 0; st.leaf = -1; st.n_legal = nl;
+    st.root_w = 0.f; st.mm_max = -INFINITY; st.mm_min = INFINITY; st.pad0 = 0.f;
+    st.used = 0.0; st.pad1[0] = st.pad1[1] = 0;
+    D.gs[g] = st;
+    D.node_parent[(size_t)g * D.S] = -1;
+    D.node_action[(size_t)g * D.S] = -1;
+  }
+}
+
+// schedule (mcts.py:158-164)
+__device__ void schedule_init(const Dev &D, GameState &st) {
+  const int n = D.n_sims, m = D.m_top;
+  st.phase = 0; st.m_cur = m; st.used = 0.0;
+  if (m <= 1 || log2((double)m) <= 0) st.next_phase = n;
+  else {
+    const double x = floor((double)n / (log2((double)m) * m)) * m;
+    st.next_phase = (int)(x < n ? x : n);
+  }
+}
+// mcts.py:166-180
+__device__ int ready_next_phase(const Dev &D, GameState &st) {
+  if (st.sim < st.next_phase) return 0;
+  st.phase += 1;
+  st.m_cur /= 2;
+  if (st.m_cur < 1) return 0;
+  const int n = D.n_sims, m = D.m_top, cm = st.m_cur;
+  double extra;
+  if (cm <= 1 || log2((double)m) <= 0) extra = (double)n - st.used;
+  else extra = floor((double)n / (log2((double)m) * cm)) * cm;
+  st.used += extra;
+  const long long nx = (long long)st.next_phase + (long long)extra;
+  st.next_phase = (int)(nx < n ? nx : n);
+  return 1;
+}
+
+__global__ void __launch_bounds__(256) k_set_root(Dev D, const float *__restrict__ logits_in,
+                                                  const float *__restrict__ value_in) {
+  const int w = threadIdx.x / WAVE, lane = threadIdx.x & (WAVE - 1);
+  const int g = blockIdx.x * 4 + w;
+  if (g >= D.G) return;
+  const int A = D.A;
+  GameState st = D.gs[g];
+  float *rl = D.logits + (size_t)g * D.S * A;
+  for (int a = lane; a < A; a += WAVE) rl[a] = logits_in[(size_t)g * A + a];
+  // _backpropagate([root], [value]) (mcts.py:309): root W = clip(v), N = 1
+  st.root_w = 0.f + clip1(value_in[g]);
+  st.root_n = 1;
+  st.sim = 1;
+  schedule_init(D, st);
+  // Gumbel top-k: sorted(zip(g + logit, action), reverse=True)[:m] (mcts.py:313-317)
+  const uint64_t *lg = D.legal + (size_t)g * NJ;
+  double sc[NJ];
+  unsigned picked = 0;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int a = lane + WAVE * j;
+    sc[j] = (a < A && ((lg[j] >> lane) & 1ull)) ? D.gumbel[(size_t)g * A + a] + (double)logits_in[(size_t)g * A + a]
+                                                : -INFINITY;
+  }
+  const int k = min(st.m_cur, st.n_legal);
+  for (int r = 0; r < k; ++r) {
+    double bv = -INFINITY;
+    int ba = -1;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int a = lane + WAVE * j;
+      if (!((picked >> j) & 1u) && sc[j] != -INFINITY && (sc[j] > bv || (sc[j] == bv && a > ba))) { bv = sc[j]; ba = a; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const double ov = __shfl_xor(bv, o, 64);
+      const int oa = __shfl_xor(ba, o, 64);
+      if (ov > bv || (ov == bv && oa > ba)) { bv = ov; ba = oa; }
+    }
+    if (ba >= 0 && (ba & 63) == lane) picked |= 1u << (ba >> 6);
+    if (lane == 0) D.sel[g * MAX_TOP + r] = ba;
+  }
+  st.n_sel = k;
+  st.active = (st.n_legal > 0 && st.sim < D.n_sims) ? 1 : 0;
+  if (lane == 0) D.gs[g] = st;
+}
+
+// one wave: select the leaf of every active game and emit its network request
+__global__ void __launch_bounds__(256) k_select(Dev D, int32_t *__restrict__ in_slot, int32_t *__restrict__ act_out,
+                                                int32_t *__restrict__ out_slot, float *__restrict__ obs) {
+  const int w = threadIdx.x / WAVE, lane = threadIdx.x & (WAVE - 1);
+  const int g = blockIdx.x * 4 + w;
+  if (g >= D.G) return;
+  const int A = D.A, S = D.S;
+  GameState st = D.gs[g];
+  if (!st.active) {
+    if (lane == 0) {
+      in_slot[g] = -1;
+      out_slot[g] = -1;
+      act_out[g] = 0;
+    }
+    if (D.mode == 0 && obs) {
+      float *o = obs + (size_t)g * 3 * A;
+      for (int a = lane; a < 3 * A; a += WAVE) o[a] = 0.f;
+    }
+    return;
+  }
+  // AlphaZero replay state (mcts.py:236-248): lane-owned cells of the root board
+  int8_t cell[NJ];
+  const int8_t *b = D.boards + (size_t)g * A;
+  int cp = D.players[g];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int a = lane + WAVE * j;
+    cell[j] = a < A ? b[a] : 0;
+  }
+  int u = 0, d = 0, a = 0, last = -1;
+  int32_t *pu = D.path_u + (size_t)g * S, *pa = D.path_a + (size_t)g * S;
+  for (;;) {
+    a = (u == 0) ? select_root(D, g, lane, st.n_sel) : select_nonroot(D, g, u, lane, st.mm_max, st.mm_min);
+    if (lane == 0) {
+      pu[d] = u;
+      pa[d] = a;
+    }
+    d++;
+    // replay do_move(a) on the lane-owned copy (no legality check, as the reference)
+    if ((a & 63) == lane) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        if ((a >> 6) == j) cell[j] = (int8_t)cp;
+    }
+    cp = -cp;
+    last = a;
+    const int c = edge_row(D, g, u)[a].child;
+    if (c < 0) break;
+    u = c;
+    if (d >= S - 1) break;  // cannot happen (tree depth < nodes); keeps the loop bounded
+  }
+  const int leaf = st.n_nodes;
+  if (lane == 0) {
+    st.n_nodes = leaf + 1;
+    st.depth = d;
+    st.leaf = leaf;
+    st.k = (D.mode == 1) ? st.n_sel : 1;
+    D.gs[g] = st;
+    in_slot[g] = g * S + u;
+    act_out[g] = a;
+    out_slot[g] = g * S + leaf;
+  }
+  if (D.mode == 0 && obs) {  // observation of the replayed board (mcts.py:251)
+    float *o = obs + (size_t)g * 3 * A;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int c = lane + WAVE * j;
+      if (c < A) {
+        o[c] = cell[j] == cp ? 1.f : 0.f;
+        o[A + c] = cell[j] == -cp ? 1.f : 0.f;
+        o[2 * A + c] = c == last ? 1.f : 0.f;
+      }
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) k_expand_backup(Dev D, const float *__restrict__ logits_in,
+                                                       const float *__restrict__ value_in,
+                                                       const float *__restrict__ reward_in) {
+  const int w = threadIdx.x / WAVE, lane = threadIdx.x & (WAVE - 1);
+  const int g = blockIdx.x * 4 + w;
+  if (g >= D.G) return;
+  const int A = D.A, S = D.S;
+  GameState st = D.gs[g];
+  if (!st.active) return;
+  const int d = st.depth, leaf = st.leaf, k = st.k;
+  const int32_t *pu = D.path_u + (size_t)g * S, *pa = D.path_a + (size_t)g * S;
+  // Node.expand (mcts.py:24-25): logits, reward; children row starts empty
+  float *nl = D.logits + ((size_t)g * S + leaf) * A;
+  Edge *nrow = edge_row_w(D, g, leaf);
+  for (int a = lane; a < A; a += WAVE) {
+    nl[a] = logits_in[(size_t)g * A + a];
+    nrow[a] = Edge{-1, 0, 0.f, 0.f};
+  }
+  if (lane == 0) {
+    D.node_parent[(size_t)g * S + leaf] = pu[d - 1];
+    D.node_action[(size_t)g * S + leaf] = pa[d - 1];
+  }
+  const float r_leaf = reward_in ? reward_in[g] : 0.f;
+  // _backpropagate (mcts.py:119-138), k duplicate leaves (mcts.py:326-345): the value chain is the
+  // same for every duplicate, so each level applies its k sequential float32 updates locally.
+  float v = clip1(value_in[g]);
+  float mx = -INFINITY, mn = INFINITY;
+  for (int base = 0; base <= d; base += WAVE) {
+    const int j = base + lane;
+    Edge e = Edge{0, 0, 0.f, 0.f};
+    Edge *ep = nullptr;
+    if (j < d) {
+      ep = edge_row_w(D, g, pu[d - 1 - j]) + pa[d - 1 - j];
+      e = *ep;
+      if (j == 0) { e.child = leaf; e.r = r_leaf; }
+    }
+    const float rj = e.r;
+    const int cnt = min(WAVE, d + 1 - base);
+    float myv = 0.f;
+    for (int i = 0; i < cnt; ++i) {
+      const float ri = __shfl(rj, i, 64);
+      if (lane == i) myv = v;
+      if (base + i < d) {
+        const float dv = D.disc_f * v;
+        v = clip1(ri + dv);
+      }
+    }
+    if (j < d) {
+      float W = e.w;
+      int N = e.n;
+      for (int t = 0; t < k; ++t) {
+        W = W + myv;
+        N += 1;
+        const float vq = W / (float)N;
+        const float dq = D.disc_f * vq;
+        const float q = e.r + dq;
+        mx = fmaxf(mx, q);
+        mn = fminf(mn, q);
+      }
+      e.w = W;
+      e.n = N;
+      *ep = e;
+    } else if (j == d) {
+      float W = st.root_w;
+      for (int t = 0; t < k; ++t) W = W + myv;
+      st.root_w = W;
+      st.root_n += k;
+    }
+  }
+  mx = wave_max_f(mx);
+  mn = wave_min_f(mn);
+  // root lane (level d) owns the updated root stats; broadcast them
+  const int root_lane = d & (WAVE - 1);
+  st.root_w = __shfl(st.root_w, root_lane, 64);
+  st.root_n = __shfl(st.root_n, root_lane, 64);
+  if (mx > st.mm_max) st.mm_max = mx;
+  if (mn < st.mm_min) st.mm_min = mn;
+  st.sim += k;
+  if (ready_next_phase(D, st)) {  // _sequential_halving (mcts.py:182-185)
+    int n[NJ];
+    float q[NJ];
+    double t64[NJ];
+    float t32[NJ];
+    int max_n;
+    row_load(D, edge_row(D, g, 0), lane, n, q);
+    const int is32 = transformed_q(D, lane, n, q, st.mm_max, st.mm_min, t64, t32, max_n);
+    const int ks = st.n_sel;
+    const int ai = lane < ks ? D.sel[g * MAX_TOP + lane] : 0;
+    double ti = 0.0;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const double tv = is32 ? (double)t32[j] : t64[j];
+      const double got = __shfl(tv, ai & 63, 64);
+      if ((ai >> 6) == j) ti = got;
+    }
+    const double si = lane < ks ? (D.gumbel[(size_t)g * A + ai] + (double)D.logits[(size_t)g * S * A + ai]) + ti : 0.0;
+    int rank = 0;
+    for (int jj = 0; jj < ks; ++jj) {
+      const double sj = __shfl(si, jj, 64);
+      if (sj > si || (sj == si && jj < lane)) rank++;
+    }
+    const int keep = min(ks, st.m_cur);
+    if (lane < ks && rank < keep) D.sel[g * MAX_TOP + rank] = ai;
+    st.n_sel = keep;
+  }
+  if (st.sim >= D.n_sims) st.active = 0;
+  if (lane == 0) D.gs[g] = st;
+}
+
+__global__ void __launch_bounds__(256) k_finish(Dev D, double *__restrict__ policy, float *__restrict__ value,
+                                                int32_t *__restrict__ action) {
+  const int w = threadIdx.x / WAVE, lane = threadIdx.x & (WAVE - 1);
+  const int g = blockIdx.x * 4 + w;
+  if (g >= D.G) return;
+  const int A = D.A;
+  const GameState st = D.gs[g];
+  double *po = policy + (size_t)g * A;
+  if (st.n_legal == 0) {  // mcts.py:305-306
+    for (int a = lane; a < A; a += WAVE) po[a] = 0.0;
+    if (lane == 0) { value[g] = 0.f; action[g] = -1; }
+    return;
+  }
+  int n[NJ];
+  float q[NJ];
+  double p[NJ];
+  int max_n;
+  row_load(D, edge_row(D, g, 0), lane, n, q);
+  improved_policy(D, g, lane, D.logits + (size_t)g * D.S * A, n, q, st.mm_max, st.mm_min, p, max_n);
+  const uint64_t *lg = D.legal + (size_t)g * NJ;
+  const int16_t *rk = D.set_rank + (size_t)g * A;
+  int bn = -1, br = 1 << 20, ba = -1;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int a = lane + WAVE * j;
+    if (a < A) {
+      const bool ok = (lg[j] >> lane) & 1ull;
+      po[a] = ok ? p[j] : 0.0;
+      if (ok) {
+        const int r = rk[a];
+        if (n[j] > bn || (n[j] == bn && r < br)) { bn = n[j]; br = r; ba = a; }
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const int on = __shfl_xor(bn, o, 64), orr = __shfl_xor(br, o, 64), oa = __shfl_xor(ba, o, 64);
+    if (on > bn || (on == bn && orr < br)) { bn = on; br = orr; ba = oa; }
+  }
+  if (lane == 0) {
+    value[g] = st.root_w / (float)st.root_n;  // Node.get_value (mcts.py:32-33)
+    action[g] = ba;
+  }
+}
+
+__global__ void k_play_engine(Dev D, int n_in_row, const int32_t *__restrict__ actions, int8_t *__restrict__ status,
+                              int reset_finished) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= D.G) return;
+  play_one(D.boards + (size_t)g * D.A, D.size, n_in_row, D.players + g, D.last_moves + g, D.move_counts + g,
+           actions[g], status + g, reset_finished);
+}
+
+__global__ void k_reset_games(Dev D, const uint8_t *__restrict__ mask) {
+  const int g = blockIdx.y;
+  if (g >= D.G || (mask && !mask[g])) return;
+  for (int a = blockIdx.x * blockDim.x + threadIdx.x; a < D.A; a += gridDim.x * blockDim.x)
+    D.boards[(size_t)g * D.A + a] = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    D.players[g] = 1;
+    D.last_moves[g] = -1;
+    D.move_counts[g] = 0;
+  }
+}
+
+__global__ void k_root_stats(Dev D, int32_t *visits, int32_t *root_n, float *root_w, float *mm_max, float *mm_min) {
+  const int g = blockIdx.y;
+  const Edge *row = edge_row(D, g, 0);
+  for (int a = blockIdx.x * blockDim.x + threadIdx.x; a < D.A; a += gridDim.x * blockDim.x)
+    visits[(size_t)g * D.A + a] = row[a].n;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const GameState st = D.gs[g];
+    root_n[g] = st.root_n;
+    root_w[g] = st.root_w;
+    mm_max[g] = st.mm_max;
+    mm_min[g] = st.mm_min;
+  }
+}
+
+}  // namespace gmz
+
+using namespace gmz;
+
+struct gmz_engine {
+  gmz_engine_cfg cfg;
+  Dev D;
+  int n_in_row;
+  uint32_t counter;
+  void *bufs[32];
+  int nbufs;
+};
+
+template <typename T>
+static int dalloc(gmz_engine *e, T **p, size_t count) {
+  void *q = nullptr;
+  GMZ_HIP(hipMalloc(&q, count * sizeof(T) + 16));
+  e->bufs[e->nbufs++] = q;
+  *p = (T *)q;
+  return 0;
+}
+
+GMZ_EXPORT int gmz_engine_create(const gmz_engine_cfg *cfg, gmz_engine **out) {
+  if (!cfg || !out) return fail("gmz_engine_create: null argument");
+  const int A = cfg->board_size * cfg->board_size;
+  if (cfg->num_games <= 0 || A <= 0 || A > MAX_A) return fail("gmz_engine_create: need 0 < board_size^2 <= 512");
+  if (cfg->num_top_actions < 1 || cfg->num_top_actions > MAX_TOP) return fail("gmz_engine_create: num_top_actions must be in [1, 64]");
+  if (cfg->num_simulations < 1) return fail("gmz_engine_create: num_simulations must be >= 1");
+  if (cfg->mode != 0 && cfg->mode != 1) return fail("gmz_engine_create: mode must be 0 (AlphaZero) or 1 (MuZero)");
+  gmz_engine *e = new gmz_engine();
+  memset(e, 0, sizeof(*e));
+  e->cfg = *cfg;
+  e->n_in_row = cfg->n_in_row;
+  Dev &D = e->D;
+  D.G = cfg->num_games;
+  D.A = A;
+  D.size = cfg->board_size;
+  D.S = cfg->num_simulations + 2;
+  D.n_sims = cfg->num_simulations;
+  D.m_top = cfg->num_top_actions;
+  D.c_visit = cfg->c_visit;
+  D.mode = cfg->mode;
+  D.c_scale = cfg->c_scale;
+  D.disc_f = (float)cfg->discount;
+  D.delta_f = (float)cfg->minmax_delta;
+  const size_t G = D.G, S = D.S;
+  int rc = 0;
+  rc |= dalloc(e, &D.edges, G * S * A);
+  rc |= dalloc(e, &D.logits, G * S * A);
+  rc |= dalloc(e, &D.node_parent, G * S);
+  rc |= dalloc(e, &D.node_action, G * S);
+  rc |= dalloc(e, &D.path_u, G * S);
+  rc |= dalloc(e, &D.path_a, G * S);
+  rc |= dalloc(e, &D.sel, G * MAX_TOP);
+  rc |= dalloc(e, &D.gs, G);
+  rc |= dalloc(e, &D.legal, G * NJ);
+  rc |= dalloc(e, &D.set_rank, G * A);
+  rc |= dalloc(e, &D.gumbel, G * A);
+  rc |= dalloc(e, &D.boards, G * A);
+  rc |= dalloc(e, &D.players, G);
+  rc |= dalloc(e, &D.last_moves, G);
+  rc |= dalloc(e, &D.move_counts, G);
+  if (rc) {
+    gmz_engine_destroy(e);
+    return -1;
+  }
+  if (hipMemset(D.gs, 0, G * sizeof(GameState)) != hipSuccess) {
+    gmz_engine_destroy(e);
+    return fail("gmz_engine_create: hipMemset failed");
+  }
+  hipLaunchKernelGGL(k_reset_games, dim3(1, D.G), dim3(256), 0, 0, D, (const uint8_t *)nullptr);
+  if (hipDeviceSynchronize() != hipSuccess) {
+    gmz_engine_destroy(e);
+    return fail("gmz_engine_create: init kernel failed");
+  }
+  *out = e;
+  return 0;
+}
+
+GMZ_EXPORT int gmz_engine_destroy(gmz_engine *e) {
+  if (!e) return 0;
+  for (int i = 0; i < e->nbufs; ++i) (void)hipFree(e->bufs[i]);
+  delete e;
+  return 0;
+}
+
+GMZ_EXPORT int gmz_engine_game_state(gmz_engine *e, int8_t **boards, int8_t **players, int32_t **last_moves,
+                                     int32_t **move_counts) {
+  if (!e) return fail("null engine");
+  if (boards) *boards = e->D.boards;
+  if (players) *players = e->D.players;
+  if (last_moves) *last_moves = e->D.last_moves;
+  if (move_counts) *move_counts = e->D.move_counts;
+  return 0;
+}
+
+GMZ_EXPORT int gmz_engine_copy_state(gmz_engine *e, int direction, int8_t *boards, int8_t *players,
+                                     int32_t *last_moves, int32_t *move_counts, void *stream) {
+  if (!e || !boards || !players || !last_moves || !move_counts) return fail("gmz_engine_copy_state: null argument");
+  const Dev &D = e->D;
+  const size_t G = D.G, A = D.A;
+  hipStream_t s = (hipStream_t)stream;
+  void *eng[4] = {D.boards, D.players, D.last_moves, D.move_counts};
+  void *usr[4] = {boards, players, last_moves, move_counts};
+  const size_t bytes[4] = {G * A, G, G * 4, G * 4};
+  for (int i = 0; i < 4; ++i) {
+    if (direction == 0) GMZ_HIP(hipMemcpyAsync(usr[i], eng[i], bytes[i], hipMemcpyDeviceToDevice, s));
+    else GMZ_HIP(hipMemcpyAsync(eng[i], usr[i], bytes[i], hipMemcpyDeviceToDevice, s));
+  }
+  return 0;
+}
+
+GMZ_EXPORT int gmz_engine_reset_games(gmz_engine *e, const uint8_t *mask, void *stream) {
+  if (!e) return fail("null engine");
+  hipLaunchKernelGGL(k_reset_games, dim3(1, e->D.G), dim3(256), 0, (hipStream_t)stream, e->D, mask);
+  GMZ_LAUNCH_CHECK();
+  return 0;
+}
+
+static inline dim3 wave_grid(const gmz_engine *e) { return dim3((e->D.G + 3) / 4); }
+
+GMZ_EXPORT int gmz_engine_begin_move(gmz_engine *e, const double *gumbel, uint64_t seed, float *obs, void *stream) {
+  if (!e || !obs) return fail("gmz_engine_begin_move: null argument");
+  hipLaunchKernelGGL(k_begin_move, wave_grid(e), dim3(256), 0, (hipStream_t)stream, e->D, gumbel, seed, e->counter++,
+                     obs);
+  GMZ_LAUNCH_CHECK();
+  return 0;
+}
+
+GMZ_EXPORT int gmz_engine_set_root(gmz_engine *e, const float *logits, const float *value, void *stream) {
+  if (!e || !logits || !value) return fail("gmz_engine_set_root: null argument");
+  hipLaunchKernelGGL(k_set_root, wave_grid(e), dim3(256), 0, (hipStream_t)stream, e->D, logits, value);
+  GMZ_LAUNCH_CHECK();
+  return 0;
+}
+
+GMZ_EXPORT int gmz_engine_select(gmz_engine *e, int32_t *in_slot, int32_t *action, int32_t *out_slot, float *obs,
+                                 void *stream) {
+  if (!e || !in_slot || !action || !out_slot) return fail("gmz_engine_select: null argument");
+  if (e->D.mode == 0 && !obs) return fail("gmz_engine_select: AlphaZero mode needs obs");
+  hipLaunchKernelGGL(k_select, wave_grid(e), dim3(256), 0, (hipStream_t)stream, e->D, in_slot, action, out_slot, obs);
+  GMZ_LAUNCH_CHECK();
+  return 0;
+}
+
+GMZ_EXPORT int gmz_engine_expand_backup(gmz_engine *e, const float *logits, const float *value, const float *reward,
+                                        void *stream) {
+  if (!e || !logits || !value) return fail("gmz_engine_expand_backup: null argument");
+  if (e->D.mode == 1 && !reward) return fail("gmz_engine_expand_backup: MuZero mode needs reward");
+  hipLaunchKernelGGL(k_expand_backup, wave_grid(e), dim3(256), 0, (hipStream_t)stream, e->D, logits, value,
+                     e->D.mode == 1 ? reward : nullptr);
+  GMZ_LAUNCH_CHECK();
+  return 0;
+}
+
+GMZ_EXPORT int gmz_engine_pending_waves(gmz_engine *e, int32_t *out) {
+  if (!e || !out) return fail("null argument");
+  std::vector<GameState> st(e->D.G);
+  GMZ_HIP(hipMemcpy(st.data(), e->D.gs, sizeof(GameState) * e->D.G, hipMemcpyDeviceToHost));
+  int any = 0;
+  for (auto &s : st) any += s.active;
+  *out = any;
+  return 0;
+}
+
+GMZ_EXPORT int gmz_engine_waves_for_legal(const gmz_engine_cfg *cfg, const int32_t *n_legal, int G, int32_t *out) {
+  if (!cfg || !n_legal || !out) return fail("null argument");
+  const int n = cfg->num_simulations, m = cfg->num_top_actions;
+  int best = 0;
+  for (int g = 0; g < G; ++g) {
+    const int L = n_legal[g];
+    if (L <= 0) continue;
+    // replay of the per-game schedule: k = len(selected) per wave (mcts.py:326), 1 for AlphaZero
+    int sim = 1, waves = 0, ksel = L < m ? L : m, mcur = m, next;
+    double used = 0.0;
+    if (m <= 1 || log2((double)m) <= 0) next = n;
+    else { double x = floor((double)n / (log2((double)m) * m)) * m; next = (int)(x < n ? x : n); }
+    while (sim < n) {
+      sim += cfg->mode == 1 ? ksel : 1;
+      waves++;
+      if (sim >= next) {
+        mcur /= 2;
+        if (mcur >= 1) {
+          double extra = (mcur <= 1 || log2((double)m) <= 0) ? (double)n - used
+                                                              : floor((double)n / (log2((double)m) * mcur)) * mcur;
+          used += extra;
+          long long nx = (long long)next + (long long)extra;
+          next = (int)(nx < n ? nx : n);
+          ksel = ksel < mcur ? ksel : mcur;
+        }
+      }
+    }
+    if (waves > best) best = waves;
+  }
+  *out = best;
+  return 0;
+}
+
+GMZ_EXPORT int gmz_engine_finish_move(gmz_engine *e, double *policy, float *value, int32_t *action, void *stream) {
+  if (!e || !policy || !value || !action) return fail("gmz_engine_finish_move: null argument");
+  hipLaunchKernelGGL(k_finish, wave_grid(e), dim3(256), 0, (hipStream_t)stream, e->D, policy, value, action);
+  GMZ_LAUNCH_CHECK();
+  return 0;
+}
+
+GMZ_EXPORT int gmz_engine_play(gmz_engine *e, const int32_t *action, int8_t *status, int reset_finished, void *stream) {
+  if (!e || !action || !status) return fail("gmz_engine_play: null argument");
+  hipLaunchKernelGGL(k_play_engine, dim3((e->D.G + 255) / 256), dim3(256), 0, (hipStream_t)stream, e->D, e->n_in_row,
+                     action, status, reset_finished);
+  GMZ_LAUNCH_CHECK();
+  return 0;
+}
+
+GMZ_EXPORT int gmz_engine_root_stats(gmz_engine *e, int32_t *visits, int32_t *root_n, float *root_w, float *mm_max,
+                                     float *mm_min, void *stream) {
+  if (!e) return fail("null engine");
+  hipLaunchKernelGGL(k_root_stats, dim3(1, e->D.G), dim3(256), 0, (hipStream_t)stream, e->D, visits, root_n, root_w,
+                     mm_max, mm_min);
+  GMZ_LAUNCH_CHECK();
+  return 0;
+}

@@ -1,0 +1,203 @@
+"""BatchedSelfPlayEngine — G concurrent games searched and played on one MI355X.
+
+Host orchestration of the HIP kernels in csrc/gmz_tree.hip (C ABI: include/gmz.h).  One call of
+:meth:`search` performs, for every game at once, exactly what one ``MuZeroMCTS.search(game)``
+(/root/reference/mcts.py:288-362) or ``AlphaZeroMCTS.search(game)`` (mcts.py:197-280) does for
+one game; :meth:`play` is ``game.do_move`` + ``get_game_ended`` (workers.py:178-181).
+
+The network is a pluggable *device backend* (``initial`` / ``recurrent`` writing straight into
+the engine's slot-indexed buffers) — the in-process replacement of the reference's
+InferenceServer queue round trip (workers.py:331-369).  Backends: ``HashNetBackend`` (tree
+parity) and ``network.GomokuNetHip`` (GomokuNetEZ on MFMA kernels).
+
+Everything stays resident in HBM; the only host<->device traffic per move is the game status
+(G bytes) used to size the next move's wave loop, plus whatever the caller copies out.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from .config import from_any
+from ._lib import check, ptr
+
+
+class HashNetBackend:
+    """HashNet test network on the device (oracle/hashnet.py definition, csrc/gmz_hashnet.hip)."""
+
+    def __init__(self, num_slots, action_space, device="cuda"):
+        self.A = action_space
+        self.pool = torch.zeros(num_slots, dtype=torch.int32, device=device)  # uint32 ids
+
+    def initial(self, obs, out_slot, logits, value, stream):
+        check(_lib.load().gmz_hashnet_initial(ptr(obs), obs.shape[0], self.A, ptr(out_slot), ptr(self.pool),
+                                              ptr(logits), ptr(value), stream))
+
+    def recurrent(self, in_slot, action, out_slot, logits, value, reward, stream):
+        check(_lib.load().gmz_hashnet_recurrent(ptr(self.pool), ptr(in_slot), ptr(action), ptr(out_slot),
+                                                in_slot.shape[0], self.A, ptr(logits), ptr(value), ptr(reward),
+                                                stream))
+
+
+class BatchedSelfPlayEngine:
+    """G games per GPU.  ``cfg``: any object with the reference config attribute names."""
+
+    def __init__(self, cfg=None, num_games=1, net=None, device="cuda", seed=0, **overrides):
+        self.cfg = from_any(cfg, **overrides)
+        c = self.cfg
+        if c.MCTS_IMPLEMENTATION not in ("AlphaZero", "MuZero"):
+            raise ValueError("Unknown MCTS implementation in config: '%s'" % c.MCTS_IMPLEMENTATION)  # workers.py:140-142
+        self.lib = _lib.load()
+        self.device = torch.device(device)
+        self.G, self.A, self.size = int(num_games), c.ACTION_SPACE_SIZE, c.BOARD_SIZE
+        self.mode = 1 if c.MCTS_IMPLEMENTATION == "MuZero" else 0
+        self.slots_per_game = c.NUM_SIMULATIONS + 2
+        self.ecfg = _lib.EngineCfg(self.G, c.BOARD_SIZE, c.N_IN_ROW, c.NUM_SIMULATIONS, c.NUM_TOP_ACTIONS, self.mode,
+                                   int(c.C_VISIT), 0, float(c.C_SCALE), float(c.VALUE_MINMAX_DELTA), float(c.DISCOUNT))
+        h = ctypes.c_void_p()
+        check(self.lib.gmz_engine_create(ctypes.byref(self.ecfg), ctypes.byref(h)))
+        self.handle = h
+        self.seed = int(seed)
+        G, A, dev = self.G, self.A, self.device
+        self.net = net if net is not None else HashNetBackend(G * self.slots_per_game, A, device)
+        f32, i32 = torch.float32, torch.int32
+        self.obs = torch.zeros(G, 3, c.BOARD_SIZE, c.BOARD_SIZE, dtype=f32, device=dev)
+        self.logits = torch.zeros(G, A, dtype=f32, device=dev)
+        self.value = torch.zeros(G, dtype=f32, device=dev)
+        self.reward = torch.zeros(G, dtype=f32, device=dev)
+        self.in_slot = torch.zeros(G, dtype=i32, device=dev)
+        self.out_slot = torch.zeros(G, dtype=i32, device=dev)
+        self.act_req = torch.zeros(G, dtype=i32, device=dev)
+        self.root_slot = torch.arange(G, dtype=i32, device=dev) * self.slots_per_game
+        self.policy = torch.zeros(G, A, dtype=torch.float64, device=dev)
+        self.root_value = torch.zeros(G, dtype=f32, device=dev)
+        self.action = torch.zeros(G, dtype=i32, device=dev)
+        self.status = torch.zeros(G, dtype=torch.int8, device=dev)
+        self._status_host = torch.zeros(G, dtype=torch.int8).pin_memory()
+        self._status_event = None
+        self._n_legal = np.full(G, A, dtype=np.int32)
+        self._last_reset = True
+        self.waves_last = 0
+
+    # ------------------------------------------------------------------ lifecycle
+    def close(self):
+        if getattr(self, "handle", None):
+            self.lib.gmz_engine_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _stream(self, stream=None):
+        return _lib.stream_ptr(stream)
+
+    # ------------------------------------------------------------------ game state
+    def game_state(self):
+        """Copies of the engine-owned game state: boards int8[G,S,S], players int8[G],
+        last_moves int32[G], move_counts int32[G] (device tensors)."""
+        G, A, dev = self.G, self.A, self.device
+        b = torch.empty(G, A, dtype=torch.int8, device=dev)
+        p = torch.empty(G, dtype=torch.int8, device=dev)
+        lm = torch.empty(G, dtype=torch.int32, device=dev)
+        mc = torch.empty(G, dtype=torch.int32, device=dev)
+        check(self.lib.gmz_engine_copy_state(self.handle, 0, ptr(b), ptr(p), ptr(lm), ptr(mc), self._stream()))
+        return b.view(G, self.size, self.size), p, lm, mc
+
+    def set_positions(self, boards, players, last_moves, move_counts=None):
+        """Load G positions: boards int8[G,S,S], players ±1, last_moves (-1 = none)."""
+        G, A, dev = self.G, self.A, self.device
+        b = torch.as_tensor(np.ascontiguousarray(boards, dtype=np.int8).reshape(G, A))
+        nz = (b != 0).sum(dim=1).to(torch.int32)
+        p = torch.as_tensor(np.ascontiguousarray(players, dtype=np.int8).reshape(G))
+        lm = torch.as_tensor(np.ascontiguousarray(last_moves, dtype=np.int32).reshape(G))
+        mc = nz if move_counts is None else torch.as_tensor(np.asarray(move_counts, dtype=np.int32).reshape(G))
+        b, p, lm, mc = (t.to(dev).contiguous() for t in (b, p, lm, mc))
+        check(self.lib.gmz_engine_copy_state(self.handle, 1, ptr(b), ptr(p), ptr(lm), ptr(mc), self._stream()))
+        torch.cuda.current_stream().synchronize()
+        self._n_legal = (A - nz.numpy()).astype(np.int32)
+        self._status_event = None
+
+    def reset_games(self, mask=None):
+        m = None
+        if mask is not None:
+            m = torch.as_tensor(np.asarray(mask, dtype=np.uint8)).to(self.device)
+            self._n_legal[np.asarray(mask, dtype=bool)] = self.A
+        else:
+            self._n_legal[:] = self.A
+        check(self.lib.gmz_engine_reset_games(self.handle, ptr(m), self._stream()))
+
+    # ------------------------------------------------------------------ search
+    def _sync_status(self):
+        if self._status_event is not None:
+            self._status_event.synchronize()
+            st = self._status_host.numpy()
+            ended = st != 2
+            played = st != 3
+            self._n_legal[played & ~ended] -= 1
+            if self._last_reset:
+                self._n_legal[played & ended] = self.A
+            else:
+                self._n_legal[played & ended] = np.maximum(self._n_legal[played & ended] - 1, 0)
+            self._status_event = None
+
+    def waves_needed(self):
+        out = ctypes.c_int32()
+        nl = np.ascontiguousarray(self._n_legal, dtype=np.int32)
+        check(self.lib.gmz_engine_waves_for_legal(ctypes.byref(self.ecfg), nl.ctypes.data_as(ctypes.c_void_p),
+                                                  self.G, ctypes.byref(out)))
+        return out.value
+
+    def search(self, gumbel=None, stream=None):
+        """One search for every game (mcts.py:288-362 / 197-280).  ``gumbel``: optional f64[G,A]
+        noise (host or device); default = device noise from (seed, move counter).
+        Returns device tensors (policy f64[G,A], value f32[G], action int32[G])."""
+        s = self._stream(stream)
+        L = self.lib
+        g = None
+        if gumbel is not None:
+            g = torch.as_tensor(gumbel, dtype=torch.float64).to(self.device).contiguous()
+        check(L.gmz_engine_begin_move(self.handle, ptr(g), self.seed, ptr(self.obs), s))
+        self.net.initial(self.obs, self.root_slot, self.logits, self.value, s)
+        check(L.gmz_engine_set_root(self.handle, ptr(self.logits), ptr(self.value), s))
+        self._sync_status()  # previous move's status → legal counts (overlaps the root inference)
+        waves = self.waves_needed()
+        self.waves_last = waves
+        for _ in range(waves):
+            check(L.gmz_engine_select(self.handle, ptr(self.in_slot), ptr(self.act_req), ptr(self.out_slot),
+                                      ptr(self.obs), s))
+            if self.mode == 1:
+                self.net.recurrent(self.in_slot, self.act_req, self.out_slot, self.logits, self.value, self.reward, s)
+            else:
+                self.net.initial(self.obs, self.out_slot, self.logits, self.value, s)
+            check(L.gmz_engine_expand_backup(self.handle, ptr(self.logits), ptr(self.value),
+                                             ptr(self.reward) if self.mode == 1 else None, s))
+        check(L.gmz_engine_finish_move(self.handle, ptr(self.policy), ptr(self.root_value), ptr(self.action), s))
+        return self.policy, self.root_value, self.action
+
+    def play(self, action=None, reset_finished=True, stream=None):
+        """do_move + get_game_ended for all games.  Returns the device status tensor
+        (+1/-1 winner, 0 draw, 2 ongoing, 3 untouched)."""
+        s = self._stream(stream)
+        a = self.action if action is None else torch.as_tensor(action, dtype=torch.int32).to(self.device)
+        check(self.lib.gmz_engine_play(self.handle, ptr(a), ptr(self.status), 1 if reset_finished else 0, s))
+        self._status_host.copy_(self.status, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream() if stream is None else stream)
+        self._status_event = ev
+        self._last_reset = bool(reset_finished)
+        return self.status
+
+    def root_stats(self):
+        G, A, dev = self.G, self.A, self.device
+        visits = torch.zeros(G, A, dtype=torch.int32, device=dev)
+        rn = torch.zeros(G, dtype=torch.int32, device=dev)
+        rw = torch.zeros(G, dtype=torch.float32, device=dev)
+        mx = torch.zeros(G, dtype=torch.float32, device=dev)
+        mn = torch.zeros(G, dtype=torch.float32, device=dev)
+        check(self.lib.gmz_engine_root_stats(self.handle, ptr(visits), ptr(rn), ptr(rw), ptr(mx), ptr(mn),
+                                             self._stream()))
+        return visits, rn, rw, mx, mn

@@ -1,0 +1,145 @@
+/*
+ * gmz.h — C ABI of libgmz.so, the MI355X-native (gfx950) batched Gomoku Gumbel-MuZero/AlphaZero
+ * self-play engine.  Drop-in boundary for the reference's self-play hot path.
+ *
+ * Conventions (all entry points):
+ *   - return int: 0 = ok, < 0 = error; gmz_last_error() returns a message for the calling thread;
+ *   - no C++ types, no exceptions, no torch types cross this ABI: plain pointers, sizes, hipStream_t
+ *     passed as void*;
+ *   - pointers named *_dev are device pointers (HBM), caller-owned unless stated; every launch is
+ *     stream-ordered on the given stream (NULL = default stream); nothing here synchronises the
+ *     device except the functions documented as "synchronous";
+ *   - one engine per device, not thread-safe.
+ *
+ * Reference interfaces replaced (file:line under /root/reference):
+ *   game.py:4-63        GomokuGame.do_move / check_win / get_game_ended / get_board_state
+ *                        -> gmz_game_* (batched over G boards)
+ *   mcts.py:50-64       MCTS.search(game) -> (policy, value, action)
+ *   mcts.py:288-362     MuZeroMCTS.search, mcts.py:197-280 AlphaZeroMCTS.search
+ *                        -> gmz_engine_begin_move / set_root / select / expand_backup / finish_move
+ *                           (one call of each step advances ALL G games; the Python adapters in
+ *                           datou-gomoku-muzero_amd/mcts.py restore the per-game search() contract)
+ *   workers.py:339-369  inference_server_worker request/reply batching -> in-process, the network
+ *                        reads/writes the engine's slot arrays directly (gmz_net_*, gmz_hashnet_*)
+ *   network.py:137-152  GomokuNetEZ.initial_inference / recurrent_inference -> gmz_net_*
+ */
+#ifndef GMZ_H
+#define GMZ_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GMZ_ABI_VERSION 1
+
+/* ------------------------------------------------------------------ misc */
+const char *gmz_last_error(void);
+int gmz_abi_version(void);
+/* Synchronous: hipDeviceSynchronize on the current device (test helper). */
+int gmz_device_synchronize(void);
+
+/* ------------------------------------------------------------------ batched game (game.py) */
+/* game.py:25-58 check_win at move (r, c) = moves[g] for each board g (moves[g] < 0 -> 0).
+ * boards_dev int8[G][S*S], moves_dev int32[G], out_dev uint8[G]. */
+int gmz_game_check_win(const int8_t *boards_dev, int G, int size, int n_in_row, const int32_t *moves_dev,
+                       uint8_t *out_dev, void *stream);
+/* game.py:12-17 planes [board==player, board==-player, onehot(last_move)] -> obs_dev f32[G][3][S*S]. */
+int gmz_game_board_state(const int8_t *boards_dev, int G, int size, const int8_t *players_dev,
+                         const int32_t *last_moves_dev, float *obs_dev, void *stream);
+/* game.py:20-23 do_move + game.py:60-63 get_game_ended, in place on G games.
+ * status_dev int8[G]: +1/-1 winner, 0 draw, 2 not ended.  actions[g] < 0 leaves game g untouched
+ * (status 3). */
+int gmz_game_play(int8_t *boards_dev, int G, int size, int n_in_row, int8_t *players_dev,
+                  int32_t *last_moves_dev, int32_t *move_counts_dev, const int32_t *actions_dev,
+                  int8_t *status_dev, void *stream);
+
+/* ------------------------------------------------------------------ search engine */
+typedef struct gmz_engine gmz_engine;
+
+typedef struct gmz_engine_cfg {
+  int32_t num_games;        /* G games searched together on this device */
+  int32_t board_size;       /* config.BOARD_SIZE (A = size*size <= 512) */
+  int32_t n_in_row;         /* config.N_IN_ROW */
+  int32_t num_simulations;  /* config.NUM_SIMULATIONS */
+  int32_t num_top_actions;  /* config.NUM_TOP_ACTIONS (<= 64) */
+  int32_t mode;             /* 0 = AlphaZero (mcts.py:197), 1 = MuZero (mcts.py:288) */
+  int32_t c_visit;          /* config.C_VISIT */
+  int32_t reserved;
+  double c_scale;           /* config.C_SCALE */
+  double minmax_delta;      /* config.VALUE_MINMAX_DELTA */
+  double discount;          /* config.DISCOUNT */
+} gmz_engine_cfg;
+
+/* Synchronous (allocates HBM pools).  Node slots per game = num_simulations + 2 (root, one new node per wave, scratch). */
+int gmz_engine_create(const gmz_engine_cfg *cfg, gmz_engine **out);
+int gmz_engine_destroy(gmz_engine *e);
+/* Device pointers to the engine-owned game state (valid for the engine's lifetime):
+ * boards int8[G][A], players int8[G], last_moves int32[G], move_counts int32[G]. */
+int gmz_engine_game_state(gmz_engine *e, int8_t **boards, int8_t **players, int32_t **last_moves,
+                          int32_t **move_counts);
+/* Copy the game state between the engine and caller device buffers (same layouts as above).
+ * direction 0: engine -> caller, 1: caller -> engine.  Stream-ordered. */
+int gmz_engine_copy_state(gmz_engine *e, int direction, int8_t *boards_dev, int8_t *players_dev,
+                          int32_t *last_moves_dev, int32_t *move_counts_dev, void *stream);
+/* Reset games whose mask_dev[g] != 0 to the empty board (player 1, no last move). NULL = all. */
+int gmz_engine_reset_games(gmz_engine *e, const uint8_t *mask_dev, void *stream);
+
+/* Step 1 (mcts.py:288-306): reset every tree, legal set = empty cells of the current board,
+ * root observation obs_dev f32[G][3][A] (input of initial_inference).
+ * Gumbel noise (mcts.py:312, np.random.gumbel(0,1,A)): gumbel_dev f64[G][A] if not NULL,
+ * else generated on device from (seed, game, move counter) — see DESIGN.md. */
+int gmz_engine_begin_move(gmz_engine *e, const double *gumbel_dev, uint64_t seed, float *obs_dev, void *stream);
+/* Step 2 (mcts.py:308-317): root.expand(logits), backup(root value), Gumbel top-k.
+ * logits_dev f32[G][A], value_dev f32[G] = initial_inference outputs for obs of step 1. */
+int gmz_engine_set_root(gmz_engine *e, const float *logits_dev, const float *value_dev, void *stream);
+/* Step 3 (mcts.py:326-336 / 233-253): one wave.  For each game with an unfinished search:
+ * descend to the leaf, allocate its node, and emit the network request
+ *   MuZero:    in_slot_dev[g] = g*slots + parent node, action_dev[g] = leaf action,
+ *              out_slot_dev[g] = g*slots + new node (slots = num_simulations + 2);
+ *   AlphaZero: obs_dev[g] = observation of the root board replayed along the path,
+ *              out_slot_dev[g] as above.
+ * Games whose search has finished get in_slot = out_slot = -1 (network rows may be skipped). */
+int gmz_engine_select(gmz_engine *e, int32_t *in_slot_dev, int32_t *action_dev, int32_t *out_slot_dev,
+                      float *obs_dev, void *stream);
+/* Step 4 (mcts.py:339-350 / 258-268): expand the wave's leaf with the network outputs
+ * (logits_dev f32[G][A], value_dev f32[G], reward_dev f32[G] or NULL = 0 for AlphaZero),
+ * back it up k = len(selected_children_actions) times (the reference's k duplicate leaves),
+ * advance the sequential-halving schedule. */
+int gmz_engine_expand_backup(gmz_engine *e, const float *logits_dev, const float *value_dev,
+                             const float *reward_dev, void *stream);
+/* Number of waves still needed by the slowest game (<= 0: all searches done).  Synchronous. */
+int gmz_engine_pending_waves(gmz_engine *e, int32_t *out);
+/* Upper bound of waves for this move computed on the host from legal-move counts (no sync):
+ * n_legal_host int32[G] -> *out.  Pure function of (num_simulations, num_top_actions, n_legal). */
+int gmz_engine_waves_for_legal(const gmz_engine_cfg *cfg, const int32_t *n_legal_host, int G, int32_t *out);
+/* Step 5 (mcts.py:353-362): policy_dev f64[G][A] (improved policy over the legal set),
+ * value_dev f32[G] (root.get_value()), action_dev int32[G] (argmax root visits, ties broken in
+ * CPython set-iteration order as the reference's dict/max does; -1 when no legal move). */
+int gmz_engine_finish_move(gmz_engine *e, double *policy_dev, float *value_dev, int32_t *action_dev,
+                           void *stream);
+/* Step 6 (workers.py:178-181): do_move(action) + get_game_ended on the engine's games.
+ * status_dev int8[G] as gmz_game_play.  reset_finished != 0 -> ended games restart empty. */
+int gmz_engine_play(gmz_engine *e, const int32_t *action_dev, int8_t *status_dev, int reset_finished,
+                    void *stream);
+/* Diagnostics (device pointers into engine pools, for tests): root child visit counts
+ * int32[G][A], root (N, W) and MinMaxStats (max, min) per game. */
+int gmz_engine_root_stats(gmz_engine *e, int32_t *visits_dev, int32_t *root_n_dev, float *root_w_dev,
+                          float *mm_max_dev, float *mm_min_dev, void *stream);
+
+/* ------------------------------------------------------------------ HashNet test network */
+/* Deterministic integer-hash network (definition: oracle/hashnet.py) used for tree parity.
+ * Hidden state = uint32 id per slot in hid_pool_dev[G*slots].
+ * initial:   obs_dev f32[rows][3][A] -> logits f32[rows][A], value f32[rows], hid_pool[out_slot[r]]
+ * recurrent: hid_pool[in_slot[r]], action[r] -> logits, value, reward, hid_pool[out_slot[r]]
+ * Rows with out_slot < 0 are skipped. */
+int gmz_hashnet_initial(const float *obs_dev, int rows, int A, const int32_t *out_slot_dev,
+                        uint32_t *hid_pool_dev, float *logits_dev, float *value_dev, void *stream);
+int gmz_hashnet_recurrent(uint32_t *hid_pool_dev, const int32_t *in_slot_dev, const int32_t *action_dev,
+                          const int32_t *out_slot_dev, int rows, int A, float *logits_dev, float *value_dev,
+                          float *reward_dev, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GMZ_H */
