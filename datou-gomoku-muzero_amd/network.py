@@ -1,0 +1,263 @@
+"""GomokuNetEZ inference on MI355X: weight packing + the device backend used by the engine.
+
+``pack_weights`` turns a reference ``state_dict`` (network.py:109-123 key names, e.g. the
+``ModelWeightsUpdate.weights`` the trainer sends, workers.py:332-335) into the kernel layouts of
+csrc/gmz_net.hip:
+  * eval-mode BatchNorm (eps 1e-4, network.py:34,37,53,62,65,82) folded into conv weight/bias;
+  * 3x3 conv weights as bf16 in v_mfma_f32_16x16x32_bf16 A-operand fragment order
+    [tap][k-step][n-tile][lane][8] (rows = output channels), so a 16 KB weight stage is a
+    linear copy and every fragment read is one conflict-free ds_read_b128;
+  * the dynamics action embedding (one-hot plane -> 1x1 conv, network.py:90-92) folded into a
+    [9][C] per-tap additive term of the dynamics conv (exact algebra: the plane has one 1);
+  * reward_fc.0 permuted from NCHW-flatten to the NHWC hidden-state order, bf16 B-fragment order.
+
+``GomokuNetHip`` owns the bf16 hidden-state slot pool (HBM) and launches the kernels through the
+C ABI (include/gmz.h gmz_net_*).  It is the ``net`` backend of engine.BatchedSelfPlayEngine.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import P, I, check, ptr
+from .config import from_any
+
+EPS = 1e-4
+C = 128
+
+
+class NetWeights(ctypes.Structure):
+    _fields_ = [("board_size", ctypes.c_int32), ("channels", ctypes.c_int32), ("blocks", ctypes.c_int32),
+                ("head_hidden", ctypes.c_int32)] + [(n, ctypes.c_void_p) for n in (
+                    "repr_stem_w", "repr_stem_b", "repr_convs", "repr_bias", "dyn_convs", "dyn_bias", "dyn_action",
+                    "head_conv_w", "head_conv_b", "policy_fc_w", "policy_fc_b", "value_fc1_w", "value_fc1_b",
+                    "value_fc2_w", "value_fc2_b", "reward_fc1_w", "reward_fc1_b", "reward_fc2_w", "reward_fc2_b")]
+
+
+_lib.register({
+    "gmz_net_workspace_bytes": ([ctypes.POINTER(NetWeights), I, ctypes.POINTER(ctypes.c_size_t)], I),
+    "gmz_net_initial": ([ctypes.POINTER(NetWeights), P, I, P, P, P, P, P, P], I),
+    "gmz_net_recurrent": ([ctypes.POINTER(NetWeights), P, P, P, P, I, P, P, P, P, P], I),
+    "gmz_net_recurrent_tower": ([ctypes.POINTER(NetWeights), P, P, P, P, I, P, P], I),
+    "gmz_net_recurrent_heads": ([ctypes.POINTER(NetWeights), P, P, I, P, P, P, P, P], I),
+})
+
+
+def _f32(x):
+    return np.asarray(x, dtype=np.float32)
+
+
+def fold_bn(sd, prefix):
+    g, b, m, v = (_f32(sd[prefix + k]) for k in (".weight", ".bias", ".running_mean", ".running_var"))
+    s = g / np.sqrt(v + np.float32(EPS))
+    return s.astype(np.float32), (b - m * s).astype(np.float32)
+
+
+def _bf16_bits(x):
+    t = torch.from_numpy(np.ascontiguousarray(x, dtype=np.float32)).to(torch.bfloat16)
+    return t.view(torch.int16).numpy().view(np.uint16)
+
+
+def pack_conv3x3(wf):
+    """[128(n), 128(c), 3, 3] f32 -> bf16 [9][4][8][64][8]: frag(t, ks, nt, l, j) =
+    W[n = nt*16 + (l&15)][c = ks*32 + 8*(l>>4) + j][t // 3][t % 3]."""
+    Wt = wf.transpose(2, 3, 0, 1).reshape(9, C, C)  # [t][n][c]
+    ks, nt, l, j = np.meshgrid(np.arange(4), np.arange(8), np.arange(64), np.arange(8), indexing="ij")
+    n = nt * 16 + (l & 15)
+    c = ks * 32 + 8 * (l >> 4) + j
+    out = Wt[:, n, c]  # [9][4][8][64][8]
+    return _bf16_bits(out)
+
+
+def pack_stem(wf):
+    """conv 3->128 [128, 3, 3, 3] -> bf16 [8][64][8] with k = tap*3 + c (27, zero-padded to 32)."""
+    Wk = np.zeros((C, 32), np.float32)
+    for dy in range(3):
+        for dx in range(3):
+            for c in range(3):
+                Wk[:, (dy * 3 + dx) * 3 + c] = wf[:, c, dy, dx]
+    nt, l, j = np.meshgrid(np.arange(8), np.arange(64), np.arange(8), indexing="ij")
+    return _bf16_bits(Wk[nt * 16 + (l & 15), 8 * (l >> 4) + j])
+
+
+def pack_reward_fc1(w, A):
+    """reward_fc.0.weight [hd, C*A] (NCHW-flatten input) -> bf16 B fragments [K/32][hd/16][64][8]
+    over the NHWC hidden order k = p*C + c."""
+    hd = w.shape[0]
+    Wn = w.reshape(hd, C, A).transpose(2, 1, 0).reshape(A * C, hd)  # [k = p*C + c][n]
+    kk, nt, l, j = np.meshgrid(np.arange(A * C // 32), np.arange(hd // 16), np.arange(64), np.arange(8), indexing="ij")
+    return _bf16_bits(Wn[kk * 32 + 8 * (l >> 4) + j, nt * 16 + (l & 15)])
+
+
+def pack_weights(sd, cfg):
+    """Reference state_dict (numpy or torch tensors) -> dict of packed numpy arrays."""
+    sd = {k: (v.detach().cpu().numpy() if hasattr(v, "detach") else np.asarray(v)) for k, v in sd.items()}
+    H = cfg.BOARD_SIZE
+    A = H * H
+    nb = cfg.NUM_RES_BLOCKS
+    out = {}
+    s, b = fold_bn(sd, "representation_net.bn")
+    out["repr_stem_w"] = pack_stem(_f32(sd["representation_net.conv.weight"]) * s[:, None, None, None])
+    out["repr_stem_b"] = b
+
+    def tower(prefix):
+        convs, biases = [], []
+        for i in range(nb):
+            for k in (1, 2):
+                p = "%s.resblocks.%d." % (prefix, i)
+                s, b = fold_bn(sd, p + "bn%d" % k)
+                convs.append(pack_conv3x3(_f32(sd[p + "conv%d.weight" % k]) * s[:, None, None, None]))
+                biases.append(b)
+        return convs, biases
+
+    convs, biases = tower("representation_net")
+    out["repr_convs"] = np.stack(convs)
+    out["repr_bias"] = np.stack(biases)
+    s, b = fold_bn(sd, "dynamics_net.bn")
+    wd = _f32(sd["dynamics_net.conv.weight"]) * s[:, None, None, None]  # [C, C+16, 3, 3]
+    emb = _f32(sd["dynamics_net.action_embed_conv.weight"]).reshape(16)
+    act = np.einsum("ncyx,c->yxn", wd[:, C:], emb).reshape(9, C)
+    convs, biases = tower("dynamics_net")
+    out["dyn_convs"] = np.stack([pack_conv3x3(wd[:, :C])] + convs)
+    out["dyn_bias"] = np.stack([b] + biases)
+    out["dyn_action"] = act.astype(np.float32)
+    sp, bp = fold_bn(sd, "prediction_net.policy_bn")
+    sv, bv = fold_bn(sd, "prediction_net.value_bn")
+    hw = np.concatenate([_f32(sd["prediction_net.policy_conv.weight"]).reshape(2, C) * sp[:, None],
+                         _f32(sd["prediction_net.value_conv.weight"]).reshape(1, C) * sv[:, None]])
+    hb = np.concatenate([_f32(sd["prediction_net.policy_conv.bias"]) * sp + bp,
+                         _f32(sd["prediction_net.value_conv.bias"]) * sv + bv])
+    out["head_conv_w"], out["head_conv_b"] = hw.astype(np.float32), hb.astype(np.float32)
+    out["policy_fc_w"] = np.ascontiguousarray(_f32(sd["prediction_net.policy_fc.weight"]).T)
+    out["policy_fc_b"] = _f32(sd["prediction_net.policy_fc.bias"])
+    out["value_fc1_w"] = np.ascontiguousarray(_f32(sd["prediction_net.value_fc1.weight"]).T)
+    out["value_fc1_b"] = _f32(sd["prediction_net.value_fc1.bias"])
+    out["value_fc2_w"] = np.ascontiguousarray(_f32(sd["prediction_net.value_fc2.weight"]).T)
+    out["value_fc2_b"] = _f32(sd["prediction_net.value_fc2.bias"])
+    out["reward_fc1_w"] = pack_reward_fc1(_f32(sd["dynamics_net.reward_fc.0.weight"]), A)
+    out["reward_fc1_b"] = _f32(sd["dynamics_net.reward_fc.0.bias"])
+    out["reward_fc2_w"] = np.ascontiguousarray(_f32(sd["dynamics_net.reward_fc.2.weight"]).T)
+    out["reward_fc2_b"] = _f32(sd["dynamics_net.reward_fc.2.bias"])
+    return out
+
+
+class KernelTimer:
+    """HIP-event pairs recorded on the launch stream around one kernel; read after a sync."""
+
+    def __init__(self, stream=None):
+        self.stream = stream if stream is not None else torch.cuda.current_stream()
+        self.pairs = []
+
+    def start(self):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(self.stream)
+        self.pairs.append([e, None, 0])
+
+    def stop(self, units):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(self.stream)
+        self.pairs[-1][1] = e
+        self.pairs[-1][2] = units
+
+    def reset(self):
+        self.pairs = []
+
+    def summary(self):
+        """(launches, mean ms per launch, mean units per launch)."""
+        if not self.pairs:
+            return 0, 0.0, 0.0
+        ms = [a.elapsed_time(b) for a, b, _ in self.pairs]
+        return len(ms), sum(ms) / len(ms), sum(u for _, _, u in self.pairs) / len(ms)
+
+
+class GomokuNetHip:
+    """GomokuNetEZ initial/recurrent inference on the device (engine ``net`` backend).
+
+    ``num_slots`` hidden-state slots of bf16 [A][128] live in ``self.pool`` (HBM); the engine
+    addresses them as ``game * slots_per_game + node``.
+    """
+
+    def __init__(self, state_dict, cfg=None, num_slots=1, max_rows=1, device="cuda", **overrides):
+        self.cfg = from_any(cfg, **overrides)
+        c = self.cfg
+        if c.NUM_FILTERS != C or c.HEAD_HIDDEN_DIM != 64 or c.BOARD_SIZE not in (6, 9, 15):
+            raise ValueError("GomokuNetHip: kernels support NUM_FILTERS=128, HEAD_HIDDEN_DIM=64, BOARD_SIZE 6/9/15")
+        self.device = torch.device(device)
+        self.A = c.ACTION_SPACE_SIZE
+        self.lib = _lib.load()
+        self.max_rows = int(max_rows)
+        self.pool = torch.empty(int(num_slots) * self.A * C, dtype=torch.int16, device=self.device)
+        self.tower_timer = None  # optional KernelTimer around the dynamics tower launches (bench.py)
+        self.load_state_dict(state_dict)
+
+    def load_state_dict(self, state_dict):
+        """Hot-swap weights (ModelWeightsUpdate, workers.py:332-335)."""
+        packed = pack_weights(state_dict, self.cfg)
+        self._tensors = {k: torch.from_numpy(np.ascontiguousarray(v)).to(self.device) for k, v in packed.items()}
+        c = self.cfg
+        w = NetWeights(c.BOARD_SIZE, C, c.NUM_RES_BLOCKS, c.HEAD_HIDDEN_DIM)
+        for k, t in self._tensors.items():
+            setattr(w, k, t.data_ptr())
+        self.w = w
+        nbytes = ctypes.c_size_t()
+        check(self.lib.gmz_net_workspace_bytes(ctypes.byref(w), self.max_rows, ctypes.byref(nbytes)))
+        self.workspace = torch.empty(nbytes.value, dtype=torch.uint8, device=self.device)
+
+    def _ws(self, rows):
+        if rows > self.max_rows:  # grow the scratch (k_heads / reward split-K partials)
+            self.max_rows = rows
+            nbytes = ctypes.c_size_t()
+            check(self.lib.gmz_net_workspace_bytes(ctypes.byref(self.w), rows, ctypes.byref(nbytes)))
+            self.workspace = torch.empty(nbytes.value, dtype=torch.uint8, device=self.device)
+        return ptr(self.workspace)
+
+    # ---- engine backend interface
+    def initial(self, obs, out_slot, logits, value, stream):
+        rows = obs.shape[0]
+        check(self.lib.gmz_net_initial(ctypes.byref(self.w), ptr(obs), rows, ptr(out_slot), ptr(self.pool),
+                                       ptr(logits), ptr(value), self._ws(rows), stream))
+
+    def recurrent(self, in_slot, action, out_slot, logits, value, reward, stream):
+        rows = in_slot.shape[0]
+        ws = self._ws(rows)
+        t = self.tower_timer
+        if t is not None:
+            t.start()
+        check(self.lib.gmz_net_recurrent_tower(ctypes.byref(self.w), ptr(self.pool), ptr(in_slot), ptr(action),
+                                               ptr(out_slot), rows, ws, stream))
+        if t is not None:
+            t.stop(rows)
+        check(self.lib.gmz_net_recurrent_heads(ctypes.byref(self.w), ptr(self.pool), ptr(out_slot), rows,
+                                               ptr(logits), ptr(value), ptr(reward), ws, stream))
+
+    # ---- convenience (tests / single-game adapters): slots 0..rows-1 are used as scratch
+    def hidden(self, slots):
+        """bf16 hidden states of the given slots as float32 [n, C, H, W] (NCHW, like the reference)."""
+        H = self.cfg.BOARD_SIZE
+        idx = torch.as_tensor(np.asarray(slots, dtype=np.int64), device=self.device)
+        hv = self.pool.view(-1, self.A, C)[idx]  # [n][A][C] bf16 bits
+        f = hv.view(torch.bfloat16).float()
+        return f.permute(0, 2, 1).reshape(len(slots), C, H, H)
+
+    def initial_inference(self, obs, slots=None):
+        obs = torch.as_tensor(obs, dtype=torch.float32).to(self.device).contiguous()
+        n = obs.shape[0]
+        slots = torch.arange(n, dtype=torch.int32, device=self.device) if slots is None else \
+            torch.as_tensor(slots, dtype=torch.int32).to(self.device)
+        lg = torch.empty(n, self.A, dtype=torch.float32, device=self.device)
+        v = torch.empty(n, dtype=torch.float32, device=self.device)
+        self.initial(obs, slots, lg, v, _lib.stream_ptr())
+        return lg, v, slots
+
+    def recurrent_inference(self, in_slots, actions, out_slots):
+        dev = self.device
+        i_s = torch.as_tensor(in_slots, dtype=torch.int32).to(dev)
+        a = torch.as_tensor(actions, dtype=torch.int32).to(dev)
+        o_s = torch.as_tensor(out_slots, dtype=torch.int32).to(dev)
+        n = i_s.shape[0]
+        lg = torch.empty(n, self.A, dtype=torch.float32, device=dev)
+        v = torch.empty(n, dtype=torch.float32, device=dev)
+        r = torch.empty(n, dtype=torch.float32, device=dev)
+        self.recurrent(i_s, a, o_s, lg, v, r, _lib.stream_ptr())
+        return lg, v, r

@@ -25,6 +25,7 @@
  */
 #ifndef GMZ_H
 #define GMZ_H
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -138,6 +139,57 @@ int gmz_hashnet_initial(const float *obs_dev, int rows, int A, const int32_t *ou
 int gmz_hashnet_recurrent(uint32_t *hid_pool_dev, const int32_t *in_slot_dev, const int32_t *action_dev,
                           const int32_t *out_slot_dev, int rows, int A, float *logits_dev, float *value_dev,
                           float *reward_dev, void *stream);
+
+
+/* ------------------------------------------------------------------ GomokuNetEZ (network.py) */
+/* Device pointers to the packed inference weights (datou-gomoku-muzero_amd/network.py:pack_weights
+ * builds them from a reference state_dict: BatchNorm folded, bf16 conv weights in MFMA fragment
+ * order).  Kernels are specialised for channels == 128, head_hidden == 64, 3 support bins,
+ * board_size in {6, 9, 15}. */
+typedef struct gmz_net_weights {
+  int32_t board_size, channels, blocks, head_hidden;
+  const uint16_t *repr_stem_w;  /* bf16 [8][64][8]       conv 3->C, k = tap*3 + c (27 -> 32)      */
+  const float *repr_stem_b;     /* [C]                                                             */
+  const uint16_t *repr_convs;   /* bf16 [2*blocks][9][4][8][64][8] ResBlock convs                 */
+  const float *repr_bias;       /* [2*blocks][C]                                                   */
+  const uint16_t *dyn_convs;    /* bf16 [1+2*blocks][9][4][8][64][8] (layer 0 = dynamics conv,     */
+  const float *dyn_bias;        /*      hidden-state channels only)  [1+2*blocks][C]              */
+  const float *dyn_action;      /* [9][C] action-embedding contribution per tap (BN folded)        */
+  const float *head_conv_w;     /* [3][C] policy (2) + value (1) 1x1 convs, BN folded              */
+  const float *head_conv_b;     /* [3]                                                             */
+  const float *policy_fc_w;     /* [2A][A]  (input-major)                                          */
+  const float *policy_fc_b;     /* [A]                                                             */
+  const float *value_fc1_w;     /* [A][hd]                                                         */
+  const float *value_fc1_b;     /* [hd]                                                            */
+  const float *value_fc2_w;     /* [hd][3]                                                         */
+  const float *value_fc2_b;     /* [3]                                                             */
+  const uint16_t *reward_fc1_w; /* bf16 [A*C/32][hd/16][64][8] fragment order, NHWC input order    */
+  const float *reward_fc1_b;    /* [hd]                                                            */
+  const float *reward_fc2_w;    /* [hd][3]                                                         */
+  const float *reward_fc2_b;    /* [3]                                                             */
+} gmz_net_weights;
+
+/* Scratch needed by gmz_net_initial / gmz_net_recurrent for `rows` rows (caller allocates). */
+int gmz_net_workspace_bytes(const gmz_net_weights *w, int rows, size_t *out);
+/* network.py:137-143 initial_inference: obs_dev f32[rows][3][A] -> logits f32[rows][A],
+ * value f32[rows] (support_to_scalar), hidden state -> hid_pool_dev[out_slot[r]] (bf16 [A][C]).
+ * Rows with out_slot[r] < 0 are skipped. */
+int gmz_net_initial(const gmz_net_weights *w, const float *obs_dev, int rows, const int32_t *out_slot_dev,
+                    uint16_t *hid_pool_dev, float *logits_dev, float *value_dev, void *workspace_dev,
+                    void *stream);
+/* network.py:145-152 recurrent_inference: hid_pool[in_slot[r]], action[r] -> logits, value,
+ * reward f32[rows], next hidden state -> hid_pool[out_slot[r]]. */
+int gmz_net_recurrent(const gmz_net_weights *w, uint16_t *hid_pool_dev, const int32_t *in_slot_dev,
+                      const int32_t *action_dev, const int32_t *out_slot_dev, int rows, float *logits_dev,
+                      float *value_dev, float *reward_dev, void *workspace_dev, void *stream);
+/* gmz_net_recurrent in two stream-ordered halves (lets a caller time the dynamics tower alone):
+ * the tower writes the next hidden state + head features into the workspace; the heads read them. */
+int gmz_net_recurrent_tower(const gmz_net_weights *w, uint16_t *hid_pool_dev, const int32_t *in_slot_dev,
+                            const int32_t *action_dev, const int32_t *out_slot_dev, int rows, void *workspace_dev,
+                            void *stream);
+int gmz_net_recurrent_heads(const gmz_net_weights *w, const uint16_t *hid_pool_dev, const int32_t *out_slot_dev,
+                            int rows, float *logits_dev, float *value_dev, float *reward_dev, void *workspace_dev,
+                            void *stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,176 @@
+"""GPU numerics of the HIP GomokuNetEZ (csrc/gmz_net.hip) against the float32 oracle
+(oracle/netref.py, itself pinned to the reference forward) and the reference fixture net_c15.npz.
+
+The HIP path computes in bf16 (weights and activations) with float32 accumulation and a float32
+residual stream.  Tolerances (stated here):
+  policy logits : |Δ| <= 0.03 * max|logit| + 0.01       (per row)
+  value, reward : |Δ| <= 0.03                          (scalars in [-1, 1])
+  hidden state  : relative L2 error <= 3e-2
+  top-1 policy agreement >= 90 % of rows
+"""
+import numpy as np
+import pytest
+
+import netref
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+LOGIT_REL, LOGIT_ABS, SCALAR_ABS, HID_REL = 0.03, 0.01, 0.03, 3e-2
+
+
+@pytest.fixture(scope="module")
+def mods():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from datou_gomoku_muzero_amd import network as N, weights as W
+    from datou_gomoku_muzero_amd.config import GmzConfig
+    return N, W, GmzConfig
+
+
+def _positions(size, n, rs):
+    A = size * size
+    obs = np.zeros((n, 3, size, size), np.float32)
+    for i in range(n):
+        k = rs.randint(0, min(A - 1, 60))
+        cells = rs.permutation(A)[:k]
+        b = np.zeros(A, np.int8)
+        p = 1
+        for c in cells:
+            b[c] = p
+            p = -p
+        obs[i, 0] = (b == p).reshape(size, size)
+        obs[i, 1] = (b == -p).reshape(size, size)
+        if k:
+            obs[i, 2].reshape(-1)[cells[-1]] = 1
+    return obs
+
+
+def _check(p, v, pr, vr, what):
+    err = np.abs(p - pr).max(axis=1)
+    bound = LOGIT_REL * np.abs(pr).max(axis=1) + LOGIT_ABS
+    top1 = (p.argmax(1) == pr.argmax(1)).mean()
+    print("%s: max|dlogit| %.4g (bound %.4g), max|dv| %.4g, top1 %.3f" % (what, err.max(), bound.min(),
+                                                                          np.abs(v - vr).max(), top1))
+    assert (err <= bound).all()
+    assert np.abs(v - vr).max() <= SCALAR_ABS
+    assert top1 >= 0.9
+
+
+@pytest.mark.parametrize("size,blocks", [(15, 8), (9, 2), (6, 1)])
+def test_hip_net_matches_oracle(mods, size, blocks):
+    N, W, GmzConfig = mods
+    cfg = GmzConfig(BOARD_SIZE=size, NUM_RES_BLOCKS=blocks)
+    sd = W.synthetic_state_dict(cfg, seed=size + blocks, with_projection=False)
+    rs = np.random.RandomState(size)
+    n = 48
+    obs = _positions(size, n, rs)
+    net = N.GomokuNetHip(sd, cfg, num_slots=2 * n, max_rows=n)
+    lg, v, slots = net.initial_inference(obs)
+    torch.cuda.synchronize()
+    pr, vr, hr = netref.initial_inference(sd, obs)
+    _check(lg.cpu().numpy(), v.cpu().numpy(), pr, vr[:, 0], "initial %dx%d" % (size, size))
+    h = net.hidden(np.arange(n)).cpu().numpy()
+    rel = np.linalg.norm((h - hr).reshape(n, -1), axis=1) / np.linalg.norm(hr.reshape(n, -1), axis=1)
+    assert rel.max() <= HID_REL, rel.max()
+    # recurrent from the HIP hidden states; the oracle starts from the same (bf16-rounded) states
+    acts = rs.randint(0, size * size, n)
+    lg2, v2, r2 = net.recurrent_inference(np.arange(n), acts, np.arange(n, 2 * n))
+    torch.cuda.synchronize()
+    p2r, v2r, h2r, r2r = netref.recurrent_inference(sd, h, acts)
+    _check(lg2.cpu().numpy(), v2.cpu().numpy(), p2r, v2r[:, 0], "recurrent %dx%d" % (size, size))
+    assert np.abs(r2.cpu().numpy() - r2r[:, 0]).max() <= SCALAR_ABS
+    h2 = net.hidden(np.arange(n, 2 * n)).cpu().numpy()
+    rel2 = np.linalg.norm((h2 - h2r).reshape(n, -1), axis=1) / np.linalg.norm(h2r.reshape(n, -1), axis=1)
+    assert rel2.max() <= HID_REL, rel2.max()
+
+
+def test_hip_net_matches_reference_fixture(mods, golden):
+    """Reference network.py forward (tests/golden/net_c15.npz) on the same numpy-seeded weights."""
+    N, W, GmzConfig = mods
+    d = golden("net_c15.npz")
+    cfg = GmzConfig(BOARD_SIZE=15, NUM_RES_BLOCKS=8)
+    sd = W.synthetic_state_dict(cfg, seed=int(d["seed"]))
+    net = N.GomokuNetHip(sd, cfg, num_slots=8, max_rows=4)
+    lg, v, _ = net.initial_inference(d["obs"])
+    lg2, v2, r2 = net.recurrent_inference([0, 1], d["actions"], [2, 3])
+    torch.cuda.synchronize()
+    _check(lg.cpu().numpy(), v.cpu().numpy(), d["p"], d["v"][:, 0], "fixture initial")
+    _check(lg2.cpu().numpy(), v2.cpu().numpy(), d["p2"], d["v2"][:, 0], "fixture recurrent")
+    assert np.abs(r2.cpu().numpy() - d["r2"][:, 0]).max() <= SCALAR_ABS
+    h2 = net.hidden([2, 3]).cpu().numpy().astype(np.float64)
+    assert np.allclose(h2.sum(axis=(1, 2, 3)), d["h2_sum"], rtol=HID_REL)
+
+
+def test_skipped_rows_untouched(mods):
+    N, W, GmzConfig = mods
+    cfg = GmzConfig(BOARD_SIZE=9, NUM_RES_BLOCKS=1)
+    sd = W.synthetic_state_dict(cfg, seed=1, with_projection=False)
+    net = N.GomokuNetHip(sd, cfg, num_slots=4, max_rows=4)
+    obs = _positions(9, 2, np.random.RandomState(0))
+    lg, v, _ = net.initial_inference(obs, slots=[0, -1])
+    torch.cuda.synchronize()
+    assert torch.isfinite(lg[0]).all()
+
+
+@pytest.mark.parametrize("size,sims,mode,blocks,G", [(15, 400, "MuZero", 2, 6), (9, 50, "AlphaZero", 1, 6)])
+def test_engine_with_hip_net_matches_oracle_driving_same_net(mods, size, sims, mode, blocks, G):
+    """Engine + GomokuNetHip (batched, slot-indexed) vs the C oracle's search driving the SAME HIP
+    network row-by-row through callbacks.  Every network row is computed by its own workgroup with a
+    fixed instruction order, so outputs are batch-invariant and the two searches must agree exactly."""
+    import oracle
+    import datou_gomoku_muzero_amd.engine as E
+    N, W, GmzConfig = mods
+    cfg = GmzConfig(BOARD_SIZE=size, NUM_SIMULATIONS=sims, MCTS_IMPLEMENTATION=mode, NUM_RES_BLOCKS=blocks)
+    sd = W.synthetic_state_dict(cfg, seed=3, with_projection=False)
+    A = size * size
+    net = N.GomokuNetHip(sd, cfg, num_slots=G * (sims + 2), max_rows=G)
+    eng = E.BatchedSelfPlayEngine(cfg, num_games=G, net=net)
+    rs = np.random.RandomState(11)
+    boards = np.zeros((G, A), np.int8)
+    players = np.ones(G, np.int8)
+    lastm = np.full(G, -1, np.int32)
+    for g in range(G):
+        cells = rs.permutation(A)[: rs.randint(0, 30)]
+        p = 1
+        for c in cells:
+            boards[g, c] = p
+            p = -p
+        players[g], lastm[g] = p, (cells[-1] if len(cells) else -1)
+    gumbel = rs.gumbel(0, 1, (G, A))
+    eng.set_positions(boards, players, lastm)
+    pol, val, act = eng.search(gumbel=gumbel)
+    visits = eng.root_stats()[0]
+    torch.cuda.synchronize()
+    pol, val, act, visits = pol.cpu().numpy(), val.cpu().numpy(), act.cpu().numpy(), visits.cpu().numpy()
+
+    onet = N.GomokuNetHip(sd, cfg, num_slots=4096, max_rows=16)
+    nxt = [0]
+
+    def alloc(n):
+        s = list(range(nxt[0], nxt[0] + n))
+        nxt[0] += n
+        assert nxt[0] <= 4096
+        return s
+
+    def init(obs):
+        slots = alloc(obs.shape[0])
+        lg, v, _ = onet.initial_inference(obs, slots=slots)
+        torch.cuda.synchronize()
+        return lg.cpu().numpy(), v.cpu().numpy(), slots
+
+    def rec(hs, acts):
+        out = alloc(len(hs))
+        lg, v, r = onet.recurrent_inference(hs, acts, out)
+        torch.cuda.synchronize()
+        return lg.cpu().numpy(), v.cpu().numpy(), r.cpu().numpy(), out
+
+    cb = oracle.CallbackNet(A, size, init, rec)
+    ocfg = oracle.make_cfg(size, sims, mode, hashnet=False)
+    for g in range(G):
+        nxt[0] = 0
+        cb.reset()
+        opol, oval, oact, orv, _ = oracle.search(ocfg, boards[g], players[g], None if lastm[g] < 0 else lastm[g],
+                                                 int(np.count_nonzero(boards[g])), gumbel[g], net=cb)
+        assert act[g] == oact and val[g] == oval and (visits[g] == orv).all(), g
+        assert np.abs(pol[g] - opol).max() <= 1e-12
