@@ -24,8 +24,6 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
 
 constexpr int C = 128;            // NUM_FILTERS (kernel specialised)
-constexpr int STAGE_ELEMS = 8192; // bf16 per weight stage = 2 k-steps x 8 n-tiles x 64 lanes x 8
-constexpr int STAGES_PER_CONV = 18;
 
 template <int H>
 struct Geo {
@@ -33,7 +31,7 @@ struct Geo {
 };
 
 struct TowerArgs {
-  const uint16_t *convs;   // [layers][18 stages][8192] bf16 fragment order
+  const uint16_t *convs;   // [layers][9 taps][4 k-steps][8 n-tiles][64 lanes][8] bf16 fragments
   const float *bias;       // [layers][128]
   int n_layers;
   const uint16_t *stem_w;  // REPR: [8][64][8] bf16 (k = tap*3 + c, 27 -> 32)
@@ -53,57 +51,100 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
 }
 __device__ __forceinline__ float bf2f(uint16_t u) { return __uint_as_float(((uint32_t)u) << 16); }
 
-template <int H, bool DYN>
+// LDS image of the padded board: position q = (y+1)*HP + (x+1) owns 256 B = 16 chunks of 8 channels.
+// Chunk c of position q lives in 16-B slot (c + key(q)) & 15 with key(q) = (y*H + x) & 15 computed
+// from the *virtual* index y*H + x (also for border cells, y or x = -1 or H).  For every tap the
+// neighbours of 16 consecutive output positions then have 16 consecutive keys, even across a board
+// row wrap.  Together with the k-chunk pairing {2s, 2s+8, 2s+1, 2s+9} of lane groups 0..3 and the
+// column permutation sigma(j) = j < 8 ? j ^ 4 : j, every ds_read_b128 lane group (4 x 16 lanes)
+// touches 16 distinct slots: conflict-free B-operand reads.
+__device__ __forceinline__ int sigma16(int j) { return j < 8 ? (j ^ 4) : j; }
+
+constexpr int TAP_BYTES = 32768;  // one tap of one conv: 4 k-steps x 8 n-tiles x 64 lanes x 16 B
+
+// ABL (ablation bits, 0 in the product; tools/tower_ablate.hip times variants): 1 = no weight
+// stream (LDS-DMA + vmcnt wait), 2 = no per-tap barrier, 4 = no MFMA, 8 = no B-fragment LDS reads,
+// 16 = no per-layer epilogue (bias/residual/ReLU/LDS store), 32 = no per-board I/O (input staging,
+// hidden-state store, head 1x1 convs)
+template <int H, bool DYN, int ABL = 0>
 __global__ void __launch_bounds__(512) k_tower(TowerArgs t) {
   using G = Geo<H>;
   constexpr int A = G::A, HP = G::HP, AP = G::AP, NPT = G::NPT, PTW = G::PTW;
-  __shared__ __attribute__((aligned(16))) uint16_t act[AP * C];
-  __shared__ __attribute__((aligned(16))) uint16_t wst[2][STAGE_ELEMS];
-  uint4 *act4 = (uint4 *)act;
+  constexpr int ACT_BYTES = AP * C * 2;
+  constexpr int MAX_LAYERS = 17;
+  constexpr int BIAS_BYTES = (MAX_LAYERS + 9) * C * 4;  // per-layer bias + DYN action term, LDS-resident
+  // ONE shared arena (a second __shared__ object next to LDS-DMA targets can make hipcc drain vmcnt)
+  __shared__ __attribute__((aligned(16))) uint8_t smem[ACT_BYTES + 2 * TAP_BYTES + BIAS_BYTES];
+  uint8_t *act = smem;
+  uint8_t *wst = smem + ACT_BYTES;
+  float *sbias = (float *)(smem + ACT_BYTES + 2 * TAP_BYTES);
+  float *saction = sbias + MAX_LAYERS * C;
 
   const int r = blockIdx.x;
   const int os = t.out_slot[r];
   if (os < 0) return;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int nh = w >> 2, pg = w & 3;
+  const int g4 = lane >> 4;
+  const int cg = (g4 & 1) * 8 + (g4 >> 1);  // {0, 8, 1, 9}
+
+  auto chunk_addr = [&](int q, int key, int c) -> int { return q * 256 + (((c + key) & 15) << 4); };
+  auto key_of_q = [&](int q) -> int { return ((q / HP - 1) * H + (q % HP - 1)) & 15; };
 
   // ---- border of the padded board = zero padding of every conv
   for (int i = tid; i < (4 * HP - 4) * 16; i += 512) {
     const int b = i >> 4, ch = i & 15;
     int q;
-    if (b < HP) q = b;                                  // top row
-    else if (b < 2 * HP) q = (HP - 1) * HP + (b - HP);  // bottom row
+    if (b < HP) q = b;
+    else if (b < 2 * HP) q = (HP - 1) * HP + (b - HP);
     else {
-      const int k = b - 2 * HP;                         // left/right columns (rows 1..HP-2)
+      const int k = b - 2 * HP;
       q = (1 + (k >> 1)) * HP + ((k & 1) ? HP - 1 : 0);
     }
-    act4[q * 16 + ch] = make_uint4(0, 0, 0, 0);
+    *(uint4 *)(act + q * 256 + ch * 16) = make_uint4(0, 0, 0, 0);
   }
+  // ---- LDS-DMA weight stream: tap-stage s -> wst[s & 1]; wave w moves KB chunks w, w+8, w+16, w+24
+  const uint8_t *wsrc = (const uint8_t *)t.convs;
+  const int total_stages = t.n_layers * 9;
+  auto issue_stage = [&](int st) {
+    const uint8_t *src = wsrc + (size_t)st * TAP_BYTES + lane * 16;
+    uint8_t *dst = wst + (st & 1) * TAP_BYTES;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int kb = w + 8 * i;
+      __builtin_amdgcn_global_load_lds((const void *)(src + kb * 1024),
+                                       (__attribute__((address_space(3))) void *)(dst + kb * 1024), 16, 0, 0);
+    }
+  };
+  if (!(ABL & 1)) issue_stage(0);
+  for (int i = tid; i < t.n_layers * C; i += 512) sbias[i] = t.bias[i];
+  if (DYN)
+    for (int i = tid; i < 9 * C; i += 512) saction[i] = t.action_term[i];
   // ---- DYN input: parent hidden state (network.py:89-93 input `state`)
-  if constexpr (DYN) {
+  if constexpr (DYN && !(ABL & 32)) {
     const uint4 *src = (const uint4 *)(t.pool + (size_t)t.in_slot[r] * A * C);
     for (int i = tid; i < A * 16; i += 512) {
       const int p = i >> 4, ch = i & 15;
       const int q = (p / H + 1) * HP + (p % H + 1);
-      act4[q * 16 + (ch ^ (q & 15))] = src[i];
+      *(uint4 *)(act + chunk_addr(q, p & 15, ch)) = src[i];
     }
   }
-  // ---- per-wave position tiles
+  // ---- per-wave position tiles (column j of tile i = position pt*16 + sigma(j))
   int qc[PTW];
 #pragma unroll
   for (int i = 0; i < PTW; ++i) {
     const int pt = pg + 4 * i;
-    const int p = pt * 16 + (lane & 15);
+    const int p = pt * 16 + sigma16(lane & 15);
     qc[i] = (pt < NPT && p < A) ? (p / H + 1) * HP + (p % H + 1) : -1;
   }
   f32x4 acc[4][PTW], xres[4][PTW];
 
-  // ---- weight stream prologue
-  const uint4 *wsrc = (const uint4 *)t.convs;
-  const int total_stages = t.n_layers * STAGES_PER_CONV;
-  uint4 pf0 = wsrc[tid], pf1 = wsrc[512 + tid];
-  ((uint4 *)wst[0])[tid] = pf0;
-  ((uint4 *)wst[0])[512 + tid] = pf1;
+  auto epilogue_store = [&](int nt, int i, const u16x4 &o) {
+    const int q = qc[i];
+    const int p = (pg + 4 * i) * 16 + sigma16(lane & 15);
+    const int n0 = (nh * 4 + nt) * 16 + g4 * 4;
+    *(u16x4 *)(act + chunk_addr(q, p & 15, n0 >> 3) + (n0 & 4) * 2) = o;
+  };
 
   // ---- REPR stem: conv3x3(3 -> 128) as one MFMA k-step on an im2col operand (k = tap*3 + c)
   if constexpr (!DYN) {
@@ -116,12 +157,12 @@ __global__ void __launch_bounds__(512) k_tower(TowerArgs t) {
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) acc[nt][i] = f32x4{0.f, 0.f, 0.f, 0.f};
       if (pg + 4 * i >= NPT) continue;
-      const int p = (pg + 4 * i) * 16 + (lane & 15);
+      const int p = (pg + 4 * i) * 16 + sigma16(lane & 15);
       const int y = p / H, x = p % H;
       bf16x8_t b;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int k = 8 * (lane >> 4) + j;
+        const int k = 8 * g4 + j;
         float v = 0.f;
         if (k < 27 && p < A) {
           const int tap = k / 3, c = k % 3;
@@ -135,7 +176,7 @@ __global__ void __launch_bounds__(512) k_tower(TowerArgs t) {
     }
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
-      const int n0 = (nh * 4 + nt) * 16 + (lane >> 4) * 4;
+      const int n0 = (nh * 4 + nt) * 16 + g4 * 4;
 #pragma unroll
       for (int i = 0; i < PTW; ++i) {
         if (qc[i] < 0) continue;
@@ -146,94 +187,127 @@ __global__ void __launch_bounds__(512) k_tower(TowerArgs t) {
           xres[nt][i][e] = v;
           o[e] = f2bf(v);
         }
-        const int q = qc[i];
-        *(u16x4 *)(act + q * C + (((n0 >> 3) ^ (q & 15)) << 3) + (n0 & 4)) = o;
+        epilogue_store(nt, i, o);
       }
     }
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  // ---- the conv stream
+  // ---- the conv stream: one tap (4 k-steps of 32 channels) per stage, one barrier per stage
   int s = 0;
   for (int L = 0; L < t.n_layers; ++L) {
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
       for (int i = 0; i < PTW; ++i) acc[nt][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int sl = 0; sl < STAGES_PER_CONV; ++sl, ++s) {
-      const bool more = s + 1 < total_stages;
-      if (more) {
-        pf0 = wsrc[(size_t)(s + 1) * 1024 + tid];
-        pf1 = wsrc[(size_t)(s + 1) * 1024 + 512 + tid];
+    for (int tap = 0; tap < 9; ++tap, ++s) {
+      if (!(ABL & 1) && s + 1 < total_stages) issue_stage(s + 1);
+      const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+      const int offq = dy * HP + dx, offv = dy * H + dx;
+      int base[PTW], rot[PTW];
+#pragma unroll
+      for (int i = 0; i < PTW; ++i) {
+        const bool ok = qc[i] >= 0;
+        const int p = (pg + 4 * i) * 16 + sigma16(lane & 15);
+        base[i] = ok ? (qc[i] + offq) * 256 : 0;
+        rot[i] = ok ? (p + offv + cg) : 0;
       }
-      const uint16_t *wb = wst[s & 1];
-      const int tap = sl >> 1;
-      const int off = (tap / 3 - 1) * HP + (tap % 3 - 1);
+      const uint8_t *wb = wst + (s & 1) * TAP_BYTES + (nh * 4 * 64 + lane) * 16;
+      // every wave computes PTW tiles unconditionally (tiles past the board read the zero row and
+      // are never stored): branch-free code lets hipcc count lgkmcnt waits per k-step
+      bf16x8_t a[2][4], b[2][PTW];
+      auto load = [&](int buf, int ks) {
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        bf16x8_t a[4];
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) a[nt] = *(const bf16x8_t *)(wb + ((kk * 8 + nh * 4 + nt) * 64 + lane) * 8);
-        const int chunk = ((sl & 1) * 2 + kk) * 4 + (lane >> 4);
+        for (int nt = 0; nt < 4; ++nt) a[buf][nt] = *(const bf16x8_t *)(wb + (ks * 8 + nt) * 1024);
 #pragma unroll
         for (int i = 0; i < PTW; ++i) {
-          if (pg + 4 * i >= NPT) continue;
-          const int q = qc[i] >= 0 ? qc[i] + off : 0;
-          const bf16x8_t b = *(const bf16x8_t *)(act + q * C + ((chunk ^ (q & 15)) << 3));
-#pragma unroll
-          for (int nt = 0; nt < 4; ++nt) acc[nt][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[nt], b, acc[nt][i], 0, 0, 0);
+          if (ABL & 8) b[buf][i] = a[buf][i & 3];
+          else b[buf][i] = *(const bf16x8_t *)(act + base[i] + (((rot[i] + 2 * ks) & 15) << 4));
         }
+      };
+      load(0, 0);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        // pin the schedule: next k-step's 8 fragment reads are issued before this k-step's 16 MFMAs
+        // (hipcc otherwise recycles one fragment register and waits lgkmcnt(0) every 4 MFMAs)
+        if (ks < 3) load((ks + 1) & 1, ks + 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < PTW; ++i)
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt) {
+            if (ABL & 4) {
+              asm volatile("" ::"v"(a[ks & 1][nt]), "v"(b[ks & 1][i]));
+            } else {
+              acc[nt][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks & 1][nt], b[ks & 1][i], acc[nt][i], 0, 0, 0);
+            }
+          }
+        __builtin_amdgcn_sched_barrier(0);
       }
-      if (more) {
-        ((uint4 *)wst[(s + 1) & 1])[tid] = pf0;
-        ((uint4 *)wst[(s + 1) & 1])[512 + tid] = pf1;
+      if (tap < 8) {
+        if (!(ABL & 1)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (!(ABL & 2)) __syncthreads();
       }
-      __syncthreads();
     }
-    // epilogue: layer kind
+    if (ABL & 16) {  // keep the accumulators live (guide rule 17) so the MFMAs are not DCE'd
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int i = 0; i < PTW; ++i) asm volatile("" ::"v"(acc[nt][i]));
+      if (!(ABL & 1)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (!(ABL & 2)) __syncthreads();
+      continue;
+    }
+    // epilogue, part 1 (before the barrier, overlapping the partner wave's MFMA tail):
+    // bias (+ action term) (+ residual) + ReLU in registers, packed to bf16
     const int kind = DYN ? (L == 0 ? 0 : ((L - 1) & 1) + 1) : ((L & 1) + 1);  // 0 stem, 1 conv1, 2 conv2
-    const float *bias = t.bias + L * C;
+    const float *bias = sbias + L * C;
     int ay = 0, ax = 0;
     if (DYN && kind == 0) {
       const int av = t.action[r];
       ay = av / H;
       ax = av % H;
     }
+    u16x4 outv[4][PTW];
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
-      const int n0 = (nh * 4 + nt) * 16 + (lane >> 4) * 4;
+      const int n0 = (nh * 4 + nt) * 16 + g4 * 4;
+      const f32x4 bv = *(const f32x4 *)(bias + n0);
 #pragma unroll
       for (int i = 0; i < PTW; ++i) {
-        if (qc[i] < 0) continue;
-        const int p = (pg + 4 * i) * 16 + (lane & 15);
-        int tapi = -1;
+        const int p = (pg + 4 * i) * 16 + sigma16(lane & 15);
+        f32x4 v = acc[nt][i] + bv;
         if (DYN && kind == 0) {
-          const int dy = ay - p / H + 1, dx = ax - p % H + 1;
-          if (dy >= 0 && dy <= 2 && dx >= 0 && dx <= 2) tapi = dy * 3 + dx;
+          const int ddy = ay - p / H + 1, ddx = ax - p % H + 1;
+          if (ddy >= 0 && ddy <= 2 && ddx >= 0 && ddx <= 2) v += *(const f32x4 *)(saction + (ddy * 3 + ddx) * C + n0);
         }
-        u16x4 o;
+        if (kind == 2) v += xres[nt][i];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float v = acc[nt][i][e] + bias[n0 + e];
-          if (tapi >= 0) v += t.action_term[tapi * C + n0 + e];
-          if (kind == 2) v += xres[nt][i][e];
-          v = fmaxf(v, 0.f);
-          if (kind != 1) xres[nt][i][e] = v;
-          o[e] = f2bf(v);
-        }
-        const int q = qc[i];
-        *(u16x4 *)(act + q * C + (((n0 >> 3) ^ (q & 15)) << 3) + (n0 & 4)) = o;
+        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+        if (kind != 1) xres[nt][i] = v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) outv[nt][i][e] = f2bf(v[e]);
       }
     }
+    if (!(ABL & 1)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // every wave is done reading this layer's input
+    // epilogue, part 2: store the layer output into the LDS image
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int i = 0; i < PTW; ++i)
+        if (qc[i] >= 0) epilogue_store(nt, i, outv[nt][i]);
     __syncthreads();
   }
 
-  // ---- hidden state -> slot pool (un-swizzled NHWC bf16)
+  if (ABL & 32) return;
+  // ---- hidden state -> slot pool (NHWC bf16)
   uint4 *dst = (uint4 *)(t.pool + (size_t)os * A * C);
   for (int i = tid; i < A * 16; i += 512) {
     const int p = i >> 4, ch = i & 15;
     const int q = (p / H + 1) * HP + (p % H + 1);
-    dst[i] = act4[q * 16 + (ch ^ (q & 15))];
+    dst[i] = *(const uint4 *)(act + chunk_addr(q, p & 15, ch));
   }
   // ---- prediction-head 1x1 convs + BN + ReLU (network.py:69,71), flattened NCHW
   for (int i = tid; i < 3 * A; i += 512) {
@@ -243,7 +317,7 @@ __global__ void __launch_bounds__(512) k_tower(TowerArgs t) {
     float sum = t.head_b[o];
 #pragma unroll 4
     for (int ch = 0; ch < 16; ++ch) {
-      const uint4 v = act4[q * 16 + (ch ^ (q & 15))];
+      const uint4 v = *(const uint4 *)(act + chunk_addr(q, p & 15, ch));
       const uint32_t wds[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -253,6 +327,7 @@ __global__ void __launch_bounds__(512) k_tower(TowerArgs t) {
     }
     t.pv_feat[(size_t)r * 3 * A + i] = fmaxf(sum, 0.f);
   }
+  (void)key_of_q;
 }
 
 // reward_fc.0 : [rows, A*128] (NHWC hidden, gathered by slot) x [A*128, 64], split-K partials

@@ -59,13 +59,21 @@ def _bf16_bits(x):
     return t.view(torch.int16).numpy().view(np.uint16)
 
 
+CHUNK_OF_GROUP = np.array([0, 8, 1, 9])  # lane group g of k-step s reads channel chunk 2s + CHUNK_OF_GROUP[g]
+
+
+def conv_input_channel(ks, l, j):
+    """Input channel fed to MFMA k-slot 8*(l>>4)+j of k-step ks (see the LDS layout note in gmz_net.hip)."""
+    return (2 * ks + CHUNK_OF_GROUP[l >> 4]) * 8 + j
+
+
 def pack_conv3x3(wf):
     """[128(n), 128(c), 3, 3] f32 -> bf16 [9][4][8][64][8]: frag(t, ks, nt, l, j) =
-    W[n = nt*16 + (l&15)][c = ks*32 + 8*(l>>4) + j][t // 3][t % 3]."""
+    W[n = nt*16 + (l&15)][c = conv_input_channel(ks, l, j)][t // 3][t % 3]."""
     Wt = wf.transpose(2, 3, 0, 1).reshape(9, C, C)  # [t][n][c]
     ks, nt, l, j = np.meshgrid(np.arange(4), np.arange(8), np.arange(64), np.arange(8), indexing="ij")
     n = nt * 16 + (l & 15)
-    c = ks * 32 + 8 * (l >> 4) + j
+    c = conv_input_channel(ks, l, j)
     out = Wt[:, n, c]  # [9][4][8][64][8]
     return _bf16_bits(out)
 

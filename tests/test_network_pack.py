@@ -17,7 +17,7 @@ def bf(u16):
 def unpack_conv(pk):  # [9][4][8][64][8] -> [9][n][c]
     out = np.zeros((9, 128, 128), np.float32)
     ks, nt, l, j = np.meshgrid(np.arange(4), np.arange(8), np.arange(64), np.arange(8), indexing="ij")
-    out[:, nt * 16 + (l & 15), ks * 32 + 8 * (l >> 4) + j] = bf(pk)
+    out[:, nt * 16 + (l & 15), N.conv_input_channel(ks, l, j)] = bf(pk)
     return out
 
 
