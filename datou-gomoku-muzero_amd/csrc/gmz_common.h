@@ -82,6 +82,50 @@ __device__ __forceinline__ void wave_argmax_first(double &v, int &i) {
   }
 }
 
+// ------------------------------------------------------------ DPP wave reductions (wave64)
+// quad xor-1, quad xor-2, row_half_mirror, row_mirror make every 16-lane row uniform; the four row
+// values are then combined through v_readlane (scalar).  ~4 DPP ops + 4 readlanes instead of six
+// ds_bpermute LDS round trips.  Every lane must be active.  Result is wave-uniform.
+constexpr int DPP_QXOR1 = 0xB1, DPP_QXOR2 = 0x4E, DPP_HALF_MIRROR = 0x141, DPP_MIRROR = 0x140;
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) { return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false); }
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) { return __int_as_float(dpp_i<CTRL>(__float_as_int(v))); }
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  return __hiloint2double(dpp_i<CTRL>(__double2hiint(v)), dpp_i<CTRL>(__double2loint(v)));
+}
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l), __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+__device__ __forceinline__ float readlane_f(float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); }
+
+#define GMZ_DPP_REDUCE(T, v, OP, DPP, RL)                                            \
+  do {                                                                                \
+    v = OP(v, DPP<DPP_QXOR1>(v));                                                     \
+    v = OP(v, DPP<DPP_QXOR2>(v));                                                     \
+    v = OP(v, DPP<DPP_HALF_MIRROR>(v));                                               \
+    v = OP(v, DPP<DPP_MIRROR>(v));                                                    \
+    const T r0 = RL(v, 0), r1 = RL(v, 16), r2 = RL(v, 32), r3 = RL(v, 48);            \
+    v = OP(OP(r0, r1), OP(r2, r3));                                                   \
+  } while (0)
+
+__device__ __forceinline__ int op_max_i(int a, int b) { return a > b ? a : b; }
+__device__ __forceinline__ int op_sum_i(int a, int b) { return a + b; }
+__device__ __forceinline__ double op_max_d(double a, double b) { return fmax(a, b); }
+__device__ __forceinline__ double op_sum_d(double a, double b) { return a + b; }
+__device__ __forceinline__ float op_max_f(float a, float b) { return fmaxf(a, b); }
+__device__ __forceinline__ float op_min_f(float a, float b) { return fminf(a, b); }
+__device__ __forceinline__ float op_sum_f(float a, float b) { return a + b; }
+
+__device__ __forceinline__ int dred_max_i(int v) { GMZ_DPP_REDUCE(int, v, op_max_i, dpp_i, __builtin_amdgcn_readlane); return v; }
+__device__ __forceinline__ int dred_sum_i(int v) { GMZ_DPP_REDUCE(int, v, op_sum_i, dpp_i, __builtin_amdgcn_readlane); return v; }
+__device__ __forceinline__ double dred_max_d(double v) { GMZ_DPP_REDUCE(double, v, op_max_d, dpp_d, readlane_d); return v; }
+__device__ __forceinline__ double dred_sum_d(double v) { GMZ_DPP_REDUCE(double, v, op_sum_d, dpp_d, readlane_d); return v; }
+__device__ __forceinline__ float dred_max_f(float v) { GMZ_DPP_REDUCE(float, v, op_max_f, dpp_f, readlane_f); return v; }
+__device__ __forceinline__ float dred_min_f(float v) { GMZ_DPP_REDUCE(float, v, op_min_f, dpp_f, readlane_f); return v; }
+__device__ __forceinline__ float dred_sum_f(float v) { GMZ_DPP_REDUCE(float, v, op_sum_f, dpp_f, readlane_f); return v; }
+
 __host__ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
   x ^= x >> 16; x *= 0x7FEB352Du; x ^= x >> 15; x *= 0x846CA68Bu; x ^= x >> 16;
   return x;

@@ -330,33 +330,45 @@ __global__ void __launch_bounds__(512) k_tower(TowerArgs t) {
   (void)key_of_q;
 }
 
-// reward_fc.0 : [rows, A*128] (NHWC hidden, gathered by slot) x [A*128, 64], split-K partials
-__global__ void __launch_bounds__(64) k_reward_fc1(const uint16_t *__restrict__ pool, const int32_t *__restrict__ out_slot,
-                                                   int rows, int K, const uint16_t *__restrict__ wpk, int nks, int ksplit,
-                                                   float *__restrict__ part) {
-  const int lane = threadIdx.x;
-  const int rt = blockIdx.x, ks = blockIdx.y;
-  const int m = rt * 16 + (lane & 15);
+// reward_fc.0 : [rows, A*128] (NHWC hidden, gathered by slot) x [A*128, 64], split-K partials.
+// 256-thread block = 4 waves x 16 rows; the 4 waves read the same B fragments (L1-shared), each
+// wave keeps 4 k-steps of loads in flight.
+constexpr int RFC_UNROLL = 4;
+__global__ void __launch_bounds__(256) k_reward_fc1(const uint16_t *__restrict__ pool, const int32_t *__restrict__ out_slot,
+                                                    int rows, int K, const uint16_t *__restrict__ wpk, int nks, int ksplit,
+                                                    float *__restrict__ part) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int rbase = blockIdx.x * 64 + w * 16, ks = blockIdx.y;
+  const int m = rbase + (lane & 15);
   const int slot = m < rows ? out_slot[m] : -1;
-  const uint16_t *hrow = slot >= 0 ? pool + (size_t)slot * K : nullptr;
+  const uint16_t *hrow = pool + (size_t)(slot >= 0 ? slot : 0) * K + 8 * (lane >> 4);
   const int k0 = (int)((long long)nks * ks / ksplit), k1 = (int)((long long)nks * (ks + 1) / ksplit);
   f32x4 acc[4] = {};
-  const bf16x8_t *wv = (const bf16x8_t *)wpk;
-  for (int kk = k0; kk < k1; ++kk) {
-    bf16x8_t a;
-    if (hrow) a = *(const bf16x8_t *)(hrow + kk * 32 + 8 * (lane >> 4));
-    else a = bf16x8_t{};
+  const bf16x8_t *wv = (const bf16x8_t *)wpk + lane;
+  int kk = k0;
+  for (; kk + RFC_UNROLL <= k1; kk += RFC_UNROLL) {
+    bf16x8_t a[RFC_UNROLL], b[RFC_UNROLL][4];
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      const bf16x8_t b = wv[(kk * 4 + nt) * 64 + lane];
-      acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[nt], 0, 0, 0);
+    for (int u = 0; u < RFC_UNROLL; ++u) {
+      a[u] = *(const bf16x8_t *)(hrow + (kk + u) * 32);
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) b[u][nt] = wv[((kk + u) * 4 + nt) * 64];
     }
+#pragma unroll
+    for (int u = 0; u < RFC_UNROLL; ++u)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u], b[u][nt], acc[nt], 0, 0, 0);
+  }
+  for (; kk < k1; ++kk) {
+    const bf16x8_t a = *(const bf16x8_t *)(hrow + kk * 32);
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wv[(kk * 4 + nt) * 64], acc[nt], 0, 0, 0);
   }
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int mm = rt * 16 + (lane >> 4) * 4 + e;
+      const int mm = rbase + (lane >> 4) * 4 + e;
       if (mm < rows) part[((size_t)ks * rows + mm) * 64 + nt * 16 + (lane & 15)] = acc[nt][e];
     }
 }
@@ -379,46 +391,84 @@ __device__ __forceinline__ float support3(float l0, float l1, float l2) {
   return (-1.f * p0 + 0.f * p1) + 1.f * p2;
 }
 
+// Prediction heads (+ reward head): 4 rows per 256-thread block so every weight is read once per
+// block; features are staged k-major ([k][4 rows]) so one ds_read_b128 feeds 4 FMAs.
+constexpr int HEAD_ROWS = 4;
 __global__ void __launch_bounds__(256) k_heads(HeadArgs h) {
   extern __shared__ float sm[];
-  const int r = blockIdx.x, tid = threadIdx.x;
-  if (h.out_slot[r] < 0) return;
+  const int r0 = blockIdx.x * HEAD_ROWS, tid = threadIdx.x;
   const int A = h.A, hd = h.hd;
-  float *feat = sm, *hv = sm + 3 * A, *hr = hv + 64;
-  for (int i = tid; i < 3 * A; i += 256) feat[i] = h.pv_feat[(size_t)r * 3 * A + i];
+  float *feat = sm;                        // [3A][4]
+  float *hv = sm + 3 * A * HEAD_ROWS;      // [4][64]
+  float *hr = hv + HEAD_ROWS * 64;         // [4][64]
+  bool valid[HEAD_ROWS];
+#pragma unroll
+  for (int i = 0; i < HEAD_ROWS; ++i) valid[i] = r0 + i < h.rows && h.out_slot[r0 + i] >= 0;
+  for (int idx = tid; idx < 3 * A * HEAD_ROWS; idx += 256) {
+    const int k = idx >> 2, i = idx & 3;
+    feat[idx] = valid[i] ? h.pv_feat[(size_t)(r0 + i) * 3 * A + k] : 0.f;
+  }
   __syncthreads();
   for (int a = tid; a < A; a += 256) {  // policy_fc (network.py:70)
-    float s = h.pfc_b[a];
-    for (int k = 0; k < 2 * A; ++k) s += feat[k] * h.pfc_w[(size_t)k * A + a];
-    h.logits[(size_t)r * A + a] = s;
+    const float b = h.pfc_b[a];
+    f32x4 acc = {b, b, b, b};
+    const float *wcol = h.pfc_w + a;
+    int k = 0;
+    for (; k + 16 <= 2 * A; k += 16) {  // 16 independent weight loads in flight per thread
+      float wv[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) wv[u] = wcol[(size_t)(k + u) * A];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) acc += *(const f32x4 *)(feat + 4 * (k + u)) * wv[u];
+    }
+    for (; k < 2 * A; ++k) acc += *(const f32x4 *)(feat + 4 * k) * wcol[(size_t)k * A];
+#pragma unroll
+    for (int i = 0; i < HEAD_ROWS; ++i)
+      if (valid[i]) h.logits[(size_t)(r0 + i) * A + a] = acc[i];
   }
   if (tid < hd) {  // value_fc1 + ReLU (network.py:72)
-    float s = h.vfc1_b[tid];
-    for (int p = 0; p < A; ++p) s += feat[2 * A + p] * h.vfc1_w[p * hd + tid];
-    hv[tid] = fmaxf(s, 0.f);
+    const float b = h.vfc1_b[tid];
+    f32x4 acc = {b, b, b, b};
+    const float *wcol = h.vfc1_w + tid;
+    int p = 0;
+    for (; p + 16 <= A; p += 16) {
+      float wv[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) wv[u] = wcol[(p + u) * hd];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) acc += *(const f32x4 *)(feat + 4 * (2 * A + p + u)) * wv[u];
+    }
+    for (; p < A; ++p) acc += *(const f32x4 *)(feat + 4 * (2 * A + p)) * wcol[p * hd];
+#pragma unroll
+    for (int i = 0; i < HEAD_ROWS; ++i) hv[i * 64 + tid] = fmaxf(acc[i], 0.f);
   } else if (h.reward && tid >= 64 && tid < 64 + hd) {  // reward_fc.0 bias + ReLU (network.py:84-86)
     const int j = tid - 64;
-    float s = h.rfc1_b[j];
-    for (int k = 0; k < h.ksplit; ++k) s += h.rpart[((size_t)k * h.rows + r) * 64 + j];
-    hr[j] = fmaxf(s, 0.f);
+#pragma unroll
+    for (int i = 0; i < HEAD_ROWS; ++i) {
+      float s = h.rfc1_b[j];
+      if (valid[i])
+        for (int k = 0; k < h.ksplit; ++k) s += h.rpart[((size_t)k * h.rows + r0 + i) * 64 + j];
+      hr[i * 64 + j] = fmaxf(s, 0.f);
+    }
   }
   __syncthreads();
-  if (tid == 0) {
+  if (tid < HEAD_ROWS && valid[tid]) {
     float l[3];
     for (int k = 0; k < 3; ++k) {
       float s = h.vfc2_b[k];
-      for (int j = 0; j < hd; ++j) s += hv[j] * h.vfc2_w[j * 3 + k];
+      for (int j = 0; j < hd; ++j) s += hv[tid * 64 + j] * h.vfc2_w[j * 3 + k];
       l[k] = s;
     }
-    h.value[r] = support3(l[0], l[1], l[2]);
-  } else if (tid == 64 && h.reward) {
+    h.value[r0 + tid] = support3(l[0], l[1], l[2]);
+  } else if (h.reward && tid >= 64 && tid < 64 + HEAD_ROWS && valid[tid - 64]) {
+    const int i = tid - 64;
     float l[3];
     for (int k = 0; k < 3; ++k) {
       float s = h.rfc2_b[k];
-      for (int j = 0; j < hd; ++j) s += hr[j] * h.rfc2_w[j * 3 + k];
+      for (int j = 0; j < hd; ++j) s += hr[i * 64 + j] * h.rfc2_w[j * 3 + k];
       l[k] = s;
     }
-    h.reward[r] = support3(l[0], l[1], l[2]);
+    h.reward[r0 + i] = support3(l[0], l[1], l[2]);
   }
 }
 
@@ -442,7 +492,7 @@ static int tower(int H, bool dyn, const TowerArgs &a, hipStream_t s) {
   }
 }
 
-static constexpr int KSPLIT = 9;
+static constexpr int KSPLIT = 16;
 
 static size_t ws_bytes(int A, int rows) {
   return (size_t)rows * 3 * A * sizeof(float) + (size_t)KSPLIT * rows * 64 * sizeof(float) + 256;
@@ -468,8 +518,8 @@ static int heads(const gmz_net_weights *w, const float *pv, const int32_t *out_s
   HeadArgs h{pv, out_slot, w->policy_fc_w, w->policy_fc_b, w->value_fc1_w, w->value_fc1_b, w->value_fc2_w,
              w->value_fc2_b, rpart, w->reward_fc1_b, w->reward_fc2_w, w->reward_fc2_b, rows, A, w->head_hidden,
              KSPLIT, logits, value, reward};
-  const size_t smem = (3 * A + 128) * sizeof(float);
-  hipLaunchKernelGGL(k_heads, dim3(rows), dim3(256), smem, s, h);
+  const size_t smem = (3 * A * HEAD_ROWS + 2 * HEAD_ROWS * 64) * sizeof(float);
+  hipLaunchKernelGGL(k_heads, dim3((rows + HEAD_ROWS - 1) / HEAD_ROWS), dim3(256), smem, s, h);
   GMZ_LAUNCH_CHECK();
   return 0;
 }
@@ -508,7 +558,7 @@ GMZ_EXPORT int gmz_net_recurrent_heads(const gmz_net_weights *w, const uint16_t 
   float *pv = (float *)workspace;
   float *rpart = pv + (size_t)rows * 3 * A;
   const int K = A * C, nks = K / 32;
-  hipLaunchKernelGGL(k_reward_fc1, dim3((rows + 15) / 16, KSPLIT), dim3(64), 0, s, pool, out_slot, rows, K,
+  hipLaunchKernelGGL(k_reward_fc1, dim3((rows + 63) / 64, KSPLIT), dim3(256), 0, s, pool, out_slot, rows, K,
                      w->reward_fc1_w, nks, KSPLIT, rpart);
   GMZ_LAUNCH_CHECK();
   return heads(w, pv, out_slot, rows, rpart, logits, value, reward, s);

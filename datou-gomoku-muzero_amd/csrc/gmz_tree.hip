@@ -71,16 +71,23 @@ __device__ __forceinline__ Edge *edge_row_w(const Dev &D, int g, int u) {
   return D.edges + ((size_t)g * D.S + u) * D.A;
 }
 
-// get_qsa (mcts.py:35-38) for the lane's actions a = lane + 64 j.
-__device__ __forceinline__ void row_load(const Dev &D, const Edge *row, int lane, int (&n)[NJ], float (&q)[NJ]) {
+// All per-action device code is templated on NJ = ceil(A / 64) (actions per lane) so that a 15x15
+// board runs 4 slots, not the 8 needed for the largest supported board.
+
+// get_qsa (mcts.py:35-38) for the lane's actions a = lane + 64 j (child ids optionally kept).
+template <int NJ>
+__device__ __forceinline__ void row_load(const Dev &D, const Edge *row, int lane, int (&n)[NJ], float (&q)[NJ],
+                                         int *child = nullptr) {
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int a = lane + WAVE * j;
     n[j] = 0;
     q[j] = 0.f;
+    if (child) child[j] = -1;
     if (a < D.A) {
       const Edge e = row[a];
       n[j] = e.n;
+      if (child) child[j] = e.child;
       if (e.n > 0) {
         const float v = e.w / (float)e.n;
         const float dv = D.disc_f * v;
@@ -92,19 +99,21 @@ __device__ __forceinline__ void row_load(const Dev &D, const Edge *row, int lane
 
 // _get_transformed_completed_Qs (mcts.py:141-149) with MinMaxStats.normalize (utils.py:19-25).
 // Returns 1 when the reference array is float32 (t32 valid), else 0 (t64 valid).
+template <int NJ>
 __device__ int transformed_q(const Dev &D, int lane, const int (&n)[NJ], const float (&q)[NJ], float mm_max,
                              float mm_min, double (&t64)[NJ], float (&t32)[NJ], int &max_n_out) {
-  int mx = 0, allv = 1;
+  int mx = 0;
+  bool unvisited = false;
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int a = lane + WAVE * j;
     if (a < D.A) {
       mx = max(mx, n[j]);
-      allv &= (n[j] > 0);
+      unvisited |= (n[j] == 0);
     }
   }
-  mx = wave_max_i(mx);
-  allv = wave_and(allv);
+  mx = dred_max_i(mx);
+  const int allv = __ballot(unvisited) == 0ull;
   max_n_out = mx;
   const double scale = (double)(D.c_visit + mx) * D.c_scale;
   const bool have_range = mm_max > mm_min;
@@ -135,7 +144,7 @@ __device__ int transformed_q(const Dev &D, int lane, const int (&n)[NJ], const f
     }
     nf[j] = x;
   }
-  promote = wave_or(promote);
+  promote = __ballot(promote != 0) != 0ull;
   if (promote) {
 #pragma unroll
     for (int j = 0; j < NJ; ++j) t64[j] = scale * (double)nf[j];
@@ -148,12 +157,14 @@ __device__ int transformed_q(const Dev &D, int lane, const int (&n)[NJ], const f
 }
 
 // _get_improved_policy (mcts.py:151-156): softmax over the root legal set of logits + transformed Q.
-__device__ void improved_policy(const Dev &D, int g, int lane, const float *logit_row, const int (&n)[NJ],
-                                const float (&q)[NJ], float mm_max, float mm_min, double (&p)[NJ], int &max_n) {
+// lg[j] = legal-move bitmask word j (bit = lane), wave-uniform.
+template <int NJ>
+__device__ void improved_policy(const Dev &D, const uint64_t (&lg)[NJ], int lane, const float *logit_row,
+                                const int (&n)[NJ], const float (&q)[NJ], float mm_max, float mm_min, double (&p)[NJ],
+                                int &max_n) {
   double t64[NJ];
   float t32[NJ];
-  const int is32 = transformed_q(D, lane, n, q, mm_max, mm_min, t64, t32, max_n);
-  const uint64_t *lg = D.legal + (size_t)g * NJ;
+  const int is32 = transformed_q<NJ>(D, lane, n, q, mm_max, mm_min, t64, t32, max_n);
   if (!is32) {
     double x[NJ], m = -INFINITY;
 #pragma unroll
@@ -163,14 +174,14 @@ __device__ void improved_policy(const Dev &D, int g, int lane, const float *logi
       x[j] = ok ? (double)logit_row[a] + t64[j] : -INFINITY;
       m = fmax(m, x[j]);
     }
-    m = wave_max_d(m);
+    m = dred_max_d(m);
     double s = 0.0;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       x[j] = (x[j] == -INFINITY) ? 0.0 : exp(x[j] - m);
       s += x[j];
     }
-    s = wave_sum_d(s);
+    s = dred_sum_d(s);
 #pragma unroll
     for (int j = 0; j < NJ; ++j) p[j] = x[j] / s;
   } else {
@@ -182,63 +193,92 @@ __device__ void improved_policy(const Dev &D, int g, int lane, const float *logi
       x[j] = ok ? logit_row[a] + t32[j] : -INFINITY;
       m = fmaxf(m, x[j]);
     }
-    m = wave_max_f(m);
+    m = dred_max_f(m);
     float s = 0.f;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       x[j] = (x[j] == -INFINITY) ? 0.f : expf(x[j] - m);
       s += x[j];
     }
-    s = wave_sum_f(s);
+    s = dred_sum_f(s);
 #pragma unroll
     for (int j = 0; j < NJ; ++j) p[j] = (double)(x[j] / s);
   }
 }
 
-// _select_action at a non-root node (mcts.py:106-117).
-__device__ int select_nonroot(const Dev &D, int g, int u, int lane, float mm_max, float mm_min) {
-  int n[NJ];
+// value held by lane (a & 63) in register slot (a >> 6) for a wave-uniform a, broadcast (v_readlane)
+template <int NJ>
+__device__ __forceinline__ int bcast_slot(const int (&v)[NJ], int a) {
+  int out = 0;
+  const int src = __builtin_amdgcn_readfirstlane(a & 63), js = __builtin_amdgcn_readfirstlane(a >> 6);
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+    if (js == j) out = __builtin_amdgcn_readlane(v[j], src);
+  return out;
+}
+
+template <int NJ>
+__device__ __forceinline__ void load_legal(const Dev &D, int g, uint64_t (&lg)[NJ]) {
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) lg[j] = D.legal[(size_t)g * gmz::NJ + j];
+}
+
+// _select_action at a non-root node (mcts.py:106-117).  Returns the action; *child = its child id
+// (taken from the already-loaded edge row: no second dependent memory round trip per level).
+template <int NJ>
+__device__ int select_nonroot(const Dev &D, const uint64_t (&lg)[NJ], int g, int u, int lane, float mm_max,
+                              float mm_min, int *child) {
+  int n[NJ], ch[NJ];
   float q[NJ];
   double p[NJ];
-  row_load(D, edge_row(D, g, u), lane, n, q);
+  row_load<NJ>(D, edge_row(D, g, u), lane, n, q, ch);
   int max_n;
-  improved_policy(D, g, lane, D.logits + ((size_t)g * D.S + u) * D.A, n, q, mm_max, mm_min, p, max_n);
+  improved_policy<NJ>(D, lg, lane, D.logits + ((size_t)g * D.S + u) * D.A, n, q, mm_max, mm_min, p, max_n);
   int tot = 0;
 #pragma unroll
   for (int j = 0; j < NJ; ++j) tot += n[j];
-  tot = wave_sum_i(tot);
-  const uint64_t *lg = D.legal + (size_t)g * NJ;
-  double best = -INFINITY;
-  int besta = 1 << 30;
+  tot = dred_sum_i(tot);
+  double sc[NJ], best = -INFINITY;
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int a = lane + WAVE * j;
-    if (a < D.A && ((lg[j] >> lane) & 1ull)) {
-      const double s = p[j] - (double)n[j] / (double)(1 + tot);
-      if (s > best) { best = s; besta = a; }
-    }
+    sc[j] = -INFINITY;
+    if (a < D.A && ((lg[j] >> lane) & 1ull)) sc[j] = p[j] - (double)n[j] / (double)(1 + tot);
+    best = fmax(best, sc[j]);
   }
-  wave_argmax_first(best, besta);
-  return besta == (1 << 30) ? 0 : besta;
+  best = dred_max_d(best);
+  // np.argmax: first (lowest) action whose score equals the maximum
+  int a = 0;
+#pragma unroll
+  for (int j = NJ - 1; j >= 0; --j) {
+    const uint64_t m = __ballot(sc[j] == best && best != -INFINITY);
+    if (m) a = WAVE * j + __builtin_ctzll(m);
+  }
+  *child = bcast_slot<NJ>(ch, a);
+  return a;
 }
 
 // _select_action at the root (mcts.py:96-104): first least-visited entry of the selected list.
-__device__ int select_root(const Dev &D, int g, int lane, int n_sel) {
-  int v = 0x7fffffff, i = 64 + lane, a = -1;
+__device__ int select_root(const Dev &D, int g, int lane, int n_sel, int *child) {
+  int v = 0x7fffffff, i = 64 + lane, a = -1, c = -1;
   if (lane < n_sel) {
     a = D.sel[g * MAX_TOP + lane];
-    v = edge_row(D, g, 0)[a].n;
+    const Edge e = edge_row(D, g, 0)[a];
+    v = e.n;
+    c = e.child;
     i = lane;
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
-    int ov = __shfl_xor(v, o, 64), oi = __shfl_xor(i, o, 64), oa = __shfl_xor(a, o, 64);
-    if (ov < v || (ov == v && oi < i)) { v = ov; i = oi; a = oa; }
+    int ov = __shfl_xor(v, o, 64), oi = __shfl_xor(i, o, 64), oa = __shfl_xor(a, o, 64), oc = __shfl_xor(c, o, 64);
+    if (ov < v || (ov == v && oi < i)) { v = ov; i = oi; a = oa; c = oc; }
   }
+  *child = c;
   return a;
 }
 
 // ------------------------------------------------------------------------------------------
+template <int NJ>
 __global__ void __launch_bounds__(256) k_begin_move(Dev D, const double *__restrict__ gumbel_in, uint64_t seed,
                                                     uint32_t counter, float *__restrict__ obs) {
   __shared__ int16_t table[4][2048];
@@ -256,7 +296,7 @@ __global__ void __launch_bounds__(256) k_begin_move(Dev D, const double *__restr
     const int a = lane + WAVE * j;
     const bool ok = a < A && b[a] == 0;
     const uint64_t bal = __ballot(ok);
-    if (lane == 0) D.legal[(size_t)g * NJ + j] = bal;
+    if (lane == 0) D.legal[(size_t)g * gmz::NJ + j] = bal;
     nl += __popcll(bal);
   }
   // observation planes (game.py:12-17)
@@ -376,6 +416,7 @@ __device__ int ready_next_phase(const Dev &D, GameState &st) {
   return 1;
 }
 
+template <int NJ>
 __global__ void __launch_bounds__(256) k_set_root(Dev D, const float *__restrict__ logits_in,
                                                   const float *__restrict__ value_in) {
   const int w = threadIdx.x / WAVE, lane = threadIdx.x & (WAVE - 1);
@@ -391,7 +432,8 @@ __global__ void __launch_bounds__(256) k_set_root(Dev D, const float *__restrict
   st.sim = 1;
   schedule_init(D, st);
   // Gumbel top-k: sorted(zip(g + logit, action), reverse=True)[:m] (mcts.py:313-317)
-  const uint64_t *lg = D.legal + (size_t)g * NJ;
+  uint64_t lg[NJ];
+  load_legal<NJ>(D, g, lg);
   double sc[NJ];
   unsigned picked = 0;
 #pragma unroll
@@ -424,6 +466,7 @@ __global__ void __launch_bounds__(256) k_set_root(Dev D, const float *__restrict
 }
 
 // one wave: select the leaf of every active game and emit its network request
+template <int NJ>
 __global__ void __launch_bounds__(256) k_select(Dev D, int32_t *__restrict__ in_slot, int32_t *__restrict__ act_out,
                                                 int32_t *__restrict__ out_slot, float *__restrict__ obs) {
   const int w = threadIdx.x / WAVE, lane = threadIdx.x & (WAVE - 1);
@@ -454,8 +497,11 @@ __global__ void __launch_bounds__(256) k_select(Dev D, int32_t *__restrict__ in_
   }
   int u = 0, d = 0, a = 0, last = -1;
   int32_t *pu = D.path_u + (size_t)g * S, *pa = D.path_a + (size_t)g * S;
+  uint64_t lg[NJ];
+  load_legal<NJ>(D, g, lg);
   for (;;) {
-    a = (u == 0) ? select_root(D, g, lane, st.n_sel) : select_nonroot(D, g, u, lane, st.mm_max, st.mm_min);
+    int c;
+    a = (u == 0) ? select_root(D, g, lane, st.n_sel, &c) : select_nonroot<NJ>(D, lg, g, u, lane, st.mm_max, st.mm_min, &c);
     if (lane == 0) {
       pu[d] = u;
       pa[d] = a;
@@ -469,7 +515,6 @@ __global__ void __launch_bounds__(256) k_select(Dev D, int32_t *__restrict__ in_
     }
     cp = -cp;
     last = a;
-    const int c = edge_row(D, g, u)[a].child;
     if (c < 0) break;
     u = c;
     if (d >= S - 1) break;  // cannot happen (tree depth < nodes); keeps the loop bounded
@@ -499,6 +544,7 @@ __global__ void __launch_bounds__(256) k_select(Dev D, int32_t *__restrict__ in_
   }
 }
 
+template <int NJ>
 __global__ void __launch_bounds__(256) k_expand_backup(Dev D, const float *__restrict__ logits_in,
                                                        const float *__restrict__ value_in,
                                                        const float *__restrict__ reward_in) {
@@ -568,8 +614,8 @@ __global__ void __launch_bounds__(256) k_expand_backup(Dev D, const float *__res
       st.root_n += k;
     }
   }
-  mx = wave_max_f(mx);
-  mn = wave_min_f(mn);
+  mx = dred_max_f(mx);
+  mn = dred_min_f(mn);
   // root lane (level d) owns the updated root stats; broadcast them
   const int root_lane = d & (WAVE - 1);
   st.root_w = __shfl(st.root_w, root_lane, 64);
@@ -583,8 +629,8 @@ __global__ void __launch_bounds__(256) k_expand_backup(Dev D, const float *__res
     double t64[NJ];
     float t32[NJ];
     int max_n;
-    row_load(D, edge_row(D, g, 0), lane, n, q);
-    const int is32 = transformed_q(D, lane, n, q, st.mm_max, st.mm_min, t64, t32, max_n);
+    row_load<NJ>(D, edge_row(D, g, 0), lane, n, q);
+    const int is32 = transformed_q<NJ>(D, lane, n, q, st.mm_max, st.mm_min, t64, t32, max_n);
     const int ks = st.n_sel;
     const int ai = lane < ks ? D.sel[g * MAX_TOP + lane] : 0;
     double ti = 0.0;
@@ -608,6 +654,7 @@ __global__ void __launch_bounds__(256) k_expand_backup(Dev D, const float *__res
   if (lane == 0) D.gs[g] = st;
 }
 
+template <int NJ>
 __global__ void __launch_bounds__(256) k_finish(Dev D, double *__restrict__ policy, float *__restrict__ value,
                                                 int32_t *__restrict__ action) {
   const int w = threadIdx.x / WAVE, lane = threadIdx.x & (WAVE - 1);
@@ -625,9 +672,10 @@ __global__ void __launch_bounds__(256) k_finish(Dev D, double *__restrict__ poli
   float q[NJ];
   double p[NJ];
   int max_n;
-  row_load(D, edge_row(D, g, 0), lane, n, q);
-  improved_policy(D, g, lane, D.logits + (size_t)g * D.S * A, n, q, st.mm_max, st.mm_min, p, max_n);
-  const uint64_t *lg = D.legal + (size_t)g * NJ;
+  uint64_t lg[NJ];
+  load_legal<NJ>(D, g, lg);
+  row_load<NJ>(D, edge_row(D, g, 0), lane, n, q);
+  improved_policy<NJ>(D, lg, lane, D.logits + (size_t)g * D.S * A, n, q, st.mm_max, st.mm_min, p, max_n);
   const int16_t *rk = D.set_rank + (size_t)g * A;
   int bn = -1, br = 1 << 20, ba = -1;
 #pragma unroll
@@ -808,18 +856,29 @@ GMZ_EXPORT int gmz_engine_reset_games(gmz_engine *e, const uint8_t *mask, void *
 
 static inline dim3 wave_grid(const gmz_engine *e) { return dim3((e->D.G + 3) / 4); }
 
+// launch KERNEL<NJ> with NJ = ceil(A / 64) in {1, 2, 4, 6, 8}
+#define GMZ_LAUNCH_NJ(KERNEL, e, stream, ...)                                                                      \
+  do {                                                                                                             \
+    const int nj_ = ((e)->D.A + 63) / 64;                                                                          \
+    hipStream_t s_ = (hipStream_t)(stream);                                                                        \
+    if (nj_ <= 1) hipLaunchKernelGGL(KERNEL<1>, wave_grid(e), dim3(256), 0, s_, __VA_ARGS__);                     \
+    else if (nj_ <= 2) hipLaunchKernelGGL(KERNEL<2>, wave_grid(e), dim3(256), 0, s_, __VA_ARGS__);                \
+    else if (nj_ <= 4) hipLaunchKernelGGL(KERNEL<4>, wave_grid(e), dim3(256), 0, s_, __VA_ARGS__);                \
+    else if (nj_ <= 6) hipLaunchKernelGGL(KERNEL<6>, wave_grid(e), dim3(256), 0, s_, __VA_ARGS__);                \
+    else hipLaunchKernelGGL(KERNEL<8>, wave_grid(e), dim3(256), 0, s_, __VA_ARGS__);                              \
+    GMZ_LAUNCH_CHECK();                                                                                            \
+  } while (0)
+
 GMZ_EXPORT int gmz_engine_begin_move(gmz_engine *e, const double *gumbel, uint64_t seed, float *obs, void *stream) {
   if (!e || !obs) return fail("gmz_engine_begin_move: null argument");
-  hipLaunchKernelGGL(k_begin_move, wave_grid(e), dim3(256), 0, (hipStream_t)stream, e->D, gumbel, seed, e->counter++,
-                     obs);
-  GMZ_LAUNCH_CHECK();
+  const uint32_t ctr = e->counter++;
+  GMZ_LAUNCH_NJ(k_begin_move, e, stream, e->D, gumbel, seed, ctr, obs);
   return 0;
 }
 
 GMZ_EXPORT int gmz_engine_set_root(gmz_engine *e, const float *logits, const float *value, void *stream) {
   if (!e || !logits || !value) return fail("gmz_engine_set_root: null argument");
-  hipLaunchKernelGGL(k_set_root, wave_grid(e), dim3(256), 0, (hipStream_t)stream, e->D, logits, value);
-  GMZ_LAUNCH_CHECK();
+  GMZ_LAUNCH_NJ(k_set_root, e, stream, e->D, logits, value);
   return 0;
 }
 
@@ -827,8 +886,7 @@ GMZ_EXPORT int gmz_engine_select(gmz_engine *e, int32_t *in_slot, int32_t *actio
                                  void *stream) {
   if (!e || !in_slot || !action || !out_slot) return fail("gmz_engine_select: null argument");
   if (e->D.mode == 0 && !obs) return fail("gmz_engine_select: AlphaZero mode needs obs");
-  hipLaunchKernelGGL(k_select, wave_grid(e), dim3(256), 0, (hipStream_t)stream, e->D, in_slot, action, out_slot, obs);
-  GMZ_LAUNCH_CHECK();
+  GMZ_LAUNCH_NJ(k_select, e, stream, e->D, in_slot, action, out_slot, obs);
   return 0;
 }
 
@@ -836,9 +894,8 @@ GMZ_EXPORT int gmz_engine_expand_backup(gmz_engine *e, const float *logits, cons
                                         void *stream) {
   if (!e || !logits || !value) return fail("gmz_engine_expand_backup: null argument");
   if (e->D.mode == 1 && !reward) return fail("gmz_engine_expand_backup: MuZero mode needs reward");
-  hipLaunchKernelGGL(k_expand_backup, wave_grid(e), dim3(256), 0, (hipStream_t)stream, e->D, logits, value,
-                     e->D.mode == 1 ? reward : nullptr);
-  GMZ_LAUNCH_CHECK();
+  const float *rw = e->D.mode == 1 ? reward : nullptr;
+  GMZ_LAUNCH_NJ(k_expand_backup, e, stream, e->D, logits, value, rw);
   return 0;
 }
 
@@ -887,8 +944,7 @@ GMZ_EXPORT int gmz_engine_waves_for_legal(const gmz_engine_cfg *cfg, const int32
 
 GMZ_EXPORT int gmz_engine_finish_move(gmz_engine *e, double *policy, float *value, int32_t *action, void *stream) {
   if (!e || !policy || !value || !action) return fail("gmz_engine_finish_move: null argument");
-  hipLaunchKernelGGL(k_finish, wave_grid(e), dim3(256), 0, (hipStream_t)stream, e->D, policy, value, action);
-  GMZ_LAUNCH_CHECK();
+  GMZ_LAUNCH_NJ(k_finish, e, stream, e->D, policy, value, action);
   return 0;
 }
 

@@ -182,6 +182,7 @@ typedef struct gmzo_stats {
   int32_t root_n;
   float root_w, mm_max, mm_min;
   int32_t n_initial, n_recurrent, recurrent_rows, waves, nodes;
+  int32_t max_depth, sum_depth; /* leaf depth over the waves (diagnostic) */
 } gmzo_stats;
 
 typedef struct {
@@ -334,9 +335,11 @@ static int select_action(otree *t, int u) {
   return besta;
 }
 
+static int g_last_depth;
 static int select_leaf(otree *t) { /* mcts.py:88-93 */
-  int u = 0;
-  while (t->nodes[u].expanded) u = get_child(t, u, select_action(t, u));
+  int u = 0, d = 0;
+  while (t->nodes[u].expanded) { u = get_child(t, u, select_action(t, u)); d++; }
+  g_last_depth = d;
   return u;
 }
 
@@ -526,6 +529,8 @@ GMZO_API int gmzo_search(const gmzo_cfg *cfg, const int8_t *board, int current_p
       sim += 1;
     }
     st->waves++;
+    st->sum_depth += g_last_depth;
+    if (g_last_depth > st->max_depth) st->max_depth = g_last_depth;
     if (ready_next_phase(&t, sim)) sequential_halving(&t);
   }
 
