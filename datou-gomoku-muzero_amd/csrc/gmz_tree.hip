@@ -20,7 +20,7 @@
 //
 // Numerics: float32 statistics with -ffp-contract=off and IEEE division reproduce the reference's
 // numpy-float32 arithmetic bit-for-bit; the completed-Q/softmax path is float64 exactly where the
-// reference's arrays are float64 (see oracle/gmz_oracle.c header for the promotion rules).
+// reference's arrays are float64 (promotion rules: DESIGN.md §4).
 #include "gmz_common.h"
 #include "gmz_device.h"
 #include "../../include/gmz.h"
@@ -721,6 +721,13 @@ __global__ void k_reset_games(Dev D, const uint8_t *__restrict__ mask) {
   }
 }
 
+__global__ void k_wave_k(Dev D, int32_t *k) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= D.G) return;
+  const GameState st = D.gs[g];
+  k[g] = st.active ? st.k : 0;
+}
+
 __global__ void k_root_stats(Dev D, int32_t *visits, int32_t *root_n, float *root_w, float *mm_max, float *mm_min) {
   const int g = blockIdx.y;
   const Edge *row = edge_row(D, g, 0);
@@ -952,6 +959,13 @@ GMZ_EXPORT int gmz_engine_play(gmz_engine *e, const int32_t *action, int8_t *sta
   if (!e || !action || !status) return fail("gmz_engine_play: null argument");
   hipLaunchKernelGGL(k_play_engine, dim3((e->D.G + 255) / 256), dim3(256), 0, (hipStream_t)stream, e->D, e->n_in_row,
                      action, status, reset_finished);
+  GMZ_LAUNCH_CHECK();
+  return 0;
+}
+
+GMZ_EXPORT int gmz_engine_wave_k(gmz_engine *e, int32_t *k_dev, void *stream) {
+  if (!e || !k_dev) return fail("gmz_engine_wave_k: null argument");
+  hipLaunchKernelGGL(k_wave_k, dim3((e->D.G + 255) / 256), dim3(256), 0, (hipStream_t)stream, e->D, k_dev);
   GMZ_LAUNCH_CHECK();
   return 0;
 }

@@ -123,6 +123,10 @@ int gmz_engine_finish_move(gmz_engine *e, double *policy_dev, float *value_dev, 
  * status_dev int8[G] as gmz_game_play.  reset_finished != 0 -> ended games restart empty. */
 int gmz_engine_play(gmz_engine *e, const int32_t *action_dev, int8_t *status_dev, int reset_finished,
                     void *stream);
+/* Duplicate count of the wave just selected, per game: k_dev int32[G] = len(selected_children_actions)
+ * for MuZero (mcts.py:326), 1 for AlphaZero, 0 for games whose search is finished.  Used by the
+ * single-game adapters to send the reference's k-row 'recurrent_batch' requests. */
+int gmz_engine_wave_k(gmz_engine *e, int32_t *k_dev, void *stream);
 /* Diagnostics (device pointers into engine pools, for tests): root child visit counts
  * int32[G][A], root (N, W) and MinMaxStats (max, min) per game. */
 int gmz_engine_root_stats(gmz_engine *e, int32_t *visits_dev, int32_t *root_n_dev, float *root_w_dev,

@@ -1,0 +1,116 @@
+"""Drop-in adapters (datou-gomoku-muzero_amd/mcts.py) and the worker (worker.py) on the GPU:
+the reference's own test contracts (tests/test_mcts_logic.py:116-165) and bit-exact parity with
+the reference fixtures through the queue protocol."""
+import glob
+import os
+import queue
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from queue_helpers import Game, MockQueue, ServerQueue
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def M():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from datou_gomoku_muzero_amd import mcts
+    from datou_gomoku_muzero_amd.config import GmzConfig
+    return mcts, GmzConfig
+
+
+def test_request_counts_like_reference(M):
+    """test_mcts_logic.py:116-136: AZ -> NUM_SIMULATIONS 'initial', 0 recurrent; MZ -> 1 initial, >0 recurrent."""
+    mcts, GmzConfig = M
+    cfg = GmzConfig(BOARD_SIZE=6, NUM_SIMULATIONS=15)
+    q = MockQueue(36)
+    az = mcts.HipAlphaZeroMCTS(0, q, q, cfg=cfg)
+    az.search(Game(np.zeros((6, 6)), 1, None))
+    kinds = [r[1] for r in q.put_log]
+    assert kinds.count("initial") == 15 and kinds.count("recurrent_batch") == 0
+    q2 = MockQueue(36)
+    mz = mcts.HipMuZeroMCTS(0, q2, q2, cfg=cfg)
+    mz.search(Game(np.zeros((6, 6)), 1, None))
+    kinds = [r[1] for r in q2.put_log]
+    assert kinds.count("initial") == 1 and kinds.count("recurrent_batch") > 0
+
+
+def test_output_contract_like_reference(M):
+    """test_mcts_logic.py:138-165."""
+    mcts, GmzConfig = M
+    cfg = GmzConfig(BOARD_SIZE=6, NUM_SIMULATIONS=15)
+    rs = np.random.RandomState(3)
+    b = np.zeros(36, np.int8)
+    cells = rs.permutation(36)[:8]
+    p = 1
+    for c in cells:
+        b[c] = p
+        p = -p
+    game = Game(b.reshape(6, 6), p, (cells[-1] // 6, cells[-1] % 6))
+    for cls in (mcts.HipAlphaZeroMCTS, mcts.HipMuZeroMCTS):
+        q = MockQueue(36)
+        policy, value, action = cls(0, q, q, cfg=cfg).search(game)
+        assert isinstance(policy, np.ndarray) and abs(policy.sum() - 1.0) < 1e-5
+        assert isinstance(action, int) and b[action] == 0
+        assert isinstance(value, (float, np.floating)) and -1.0 <= value <= 1.0
+
+
+MCTS_FILES = sorted(os.path.basename(f) for f in glob.glob(os.path.join(GOLDEN, "mcts_*.npz")))
+
+
+@pytest.mark.parametrize("fname", [f for f in MCTS_FILES if "19" not in f])
+def test_adapter_reproduces_reference_fixture(M, golden, fname):
+    """Seeded global RandomState + HashNet server queue -> the reference's exact search results."""
+    mcts, GmzConfig = M
+    d = golden(fname)
+    size, mode, sims = int(d["size"]), str(d["mode"]), int(d["sims"])
+    cfg = GmzConfig(BOARD_SIZE=size, NUM_SIMULATIONS=sims, MCTS_IMPLEMENTATION=mode)
+    q = ServerQueue(size * size)
+    eng = mcts.make_engine(0, q, q, cfg=cfg)
+    np.random.seed(int(d["seed"]))
+    for i in range(len(d["action"])):
+        lm = int(d["lastmove"][i])
+        game = Game(d["board"][i].reshape(size, size), d["player"][i], None if lm < 0 else (lm // size, lm % size))
+        q.log.clear()
+        policy, value, action = eng.search(game)
+        assert action == d["action"][i] and value == d["value"][i]
+        assert np.abs(policy - d["policy"][i]).max() <= (1e-6 if size <= 6 else 1e-12)
+        assert sum(1 for k, _ in q.log if k == "initial") == d["n_initial"][i]
+        assert sum(n for k, n in q.log if k == "recurrent_batch") == d["recurrent_rows"][i]
+
+
+def test_worker_emits_reference_messages(M):
+    """gpu_selfplay_worker: records, slices and status messages for finished games."""
+    from datou_gomoku_muzero_amd.worker import gpu_selfplay_worker
+    mcts, GmzConfig = M
+    cfg = GmzConfig(BOARD_SIZE=6, NUM_SIMULATIONS=16, NUM_RES_BLOCKS=1)
+
+    class Ev:
+        def __init__(self):
+            self.f = False
+
+        def is_set(self):
+            return self.f
+
+    dq, lq, uq, tq = queue.Queue(), queue.Queue(), queue.Queue(), queue.Queue()
+    gpu_selfplay_worker(0, None, dq, lq, uq, Ev(), trainer_event_queue=tq, num_games=8, cfg=cfg, max_moves=40)
+    items = []
+    while not dq.empty():
+        items.append(dq.get())
+    assert items, "no finished game in 40 moves of 6x6"
+    for record, slices, version in items:
+        n = len(record.actions)
+        assert len(slices) == n and len(record.rewards) == n and len(record.values) == n
+        assert record.observations[0].shape == (3, 6, 6) and record.policies[0].shape == (36,)
+        assert slices[0].observation.shape == (6, 3, 6, 6) and slices[0].action_history.dtype == np.int32
+        assert abs(record.rewards[-1]) in (0.0, 1.0)
+    kinds = []
+    while not uq.empty():
+        kinds.append(type(uq.get()).__name__)
+    assert kinds.count("SelfPlayMove") >= 8 * 5 and kinds.count("GameCompletedNotice") == len(items)
+    assert tq.qsize() == len(items) and lq.qsize() == len(items)
