@@ -56,6 +56,34 @@ def parse():
     return ap.parse_args()
 
 
+def collective_max(x, dist, backend="nccl"):
+    """Max of a per-rank float over all ranks (the driver contract's max-over-ranks timing)."""
+    if dist is None:
+        return x
+    dev = "cuda" if backend == "nccl" else "cpu"
+    t = torch.tensor([x], device=dev, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def result_line(args, world, dt, waves, G):
+    """The JSON object rank 0 prints (without roofline / cpu_baseline)."""
+    total_moves = G * args.steps * world
+    return {
+        "metric": "self-play moves/sec (15x15, 400 sims)" if (args.size, args.sims) == (15, 400)
+        else "self-play moves/sec (%dx%d, %d sims)" % (args.size, args.size, args.sims),
+        "value": total_moves / dt, "unit": "moves/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+        "config": {"workload": "%dx%d Gumbel %s, %d sims/move, %d concurrent games per GPU, GomokuNetEZ %d blocks x "
+                               "128 ch (numpy-seeded random init), empty-board starts, device Gumbel RNG"
+                               % (args.size, args.size, args.mode, args.sims, G, args.blocks),
+                   "games_per_gpu": G, "global_games": G * world, "board_size": args.size,
+                   "num_simulations": args.sims, "mcts": args.mode, "waves_per_move": waves / max(1, args.steps),
+                   "parallelism": "dp%d (independent games per GPU, no collective)" % world},
+    }
+
+
 def cpu_baseline(args, sd, cfg):
     """C oracle search + float32 numpy GomokuNetEZ on the host cores (reported baseline)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -158,24 +186,8 @@ def main():
     if dist:
         dist.barrier()
     dt = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([dt], device="cuda", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    total_moves = G * args.steps * world
-    out = {
-        "metric": "self-play moves/sec (15x15, 400 sims)" if (args.size, args.sims) == (15, 400)
-        else "self-play moves/sec (%dx%d, %d sims)" % (args.size, args.size, args.sims),
-        "value": total_moves / dt, "unit": "moves/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
-        "config": {"workload": "%dx%d Gumbel %s, %d sims/move, %d concurrent games per GPU, GomokuNetEZ %d blocks x "
-                               "128 ch (numpy-seeded random init), empty-board starts, device Gumbel RNG"
-                               % (args.size, args.size, args.mode, args.sims, G, args.blocks),
-                   "games_per_gpu": G, "global_games": G * world, "board_size": args.size,
-                   "num_simulations": args.sims, "mcts": args.mode, "waves_per_move": waves / args.steps,
-                   "parallelism": "dp%d (independent games per GPU, no collective)" % world},
-    }
+    dt = collective_max(dt, dist)
+    out = result_line(args, world, dt, waves, G)
     if timer is not None:
         n_launch, ms, rows = timer.summary()
         flop = TOWER_FLOP_PER_ROW.get(args.size, 0) * rows
