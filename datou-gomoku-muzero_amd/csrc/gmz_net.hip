@@ -65,7 +65,7 @@ constexpr int TAP_BYTES = 32768;  // one tap of one conv: 4 k-steps x 8 n-tiles 
 // ABL (ablation bits, 0 in the product; tools/tower_ablate.hip times variants): 1 = no weight
 // stream (LDS-DMA + vmcnt wait), 2 = no per-tap barrier, 4 = no MFMA, 8 = no B-fragment LDS reads,
 // 16 = no per-layer epilogue (bias/residual/ReLU/LDS store), 32 = no per-board I/O (input staging,
-// hidden-state store, head 1x1 convs)
+// hidden-state store, head 1x1 convs), 64 = s_setprio(1) around each MFMA burst (experiment)
 template <int H, bool DYN, int ABL = 0>
 __global__ void __launch_bounds__(512) k_tower(TowerArgs t) {
   using G = Geo<H>;
@@ -137,7 +137,8 @@ __global__ void __launch_bounds__(512) k_tower(TowerArgs t) {
     const int p = pt * 16 + sigma16(lane & 15);
     qc[i] = (pt < NPT && p < A) ? (p / H + 1) * HP + (p % H + 1) : -1;
   }
-  f32x4 acc[4][PTW], xres[4][PTW];
+  f32x4 acc[4][PTW];
+  u16x4 xres[4][PTW];  // residual stream = the bf16 layer output already stored in the LDS image
 
   auto epilogue_store = [&](int nt, int i, const u16x4 &o) {
     const int q = qc[i];
@@ -182,11 +183,8 @@ __global__ void __launch_bounds__(512) k_tower(TowerArgs t) {
         if (qc[i] < 0) continue;
         u16x4 o;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float v = fmaxf(acc[nt][i][e] + t.stem_b[n0 + e], 0.f);
-          xres[nt][i][e] = v;
-          o[e] = f2bf(v);
-        }
+        for (int e = 0; e < 4; ++e) o[e] = f2bf(fmaxf(acc[nt][i][e] + t.stem_b[n0 + e], 0.f));
+        xres[nt][i] = o;
         epilogue_store(nt, i, o);
       }
     }
@@ -201,11 +199,12 @@ __global__ void __launch_bounds__(512) k_tower(TowerArgs t) {
     for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
       for (int i = 0; i < PTW; ++i) acc[nt][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int tap = 0; tap < 9; ++tap, ++s) {
-      if (!(ABL & 1) && s + 1 < total_stages) issue_stage(s + 1);
+    // B fragments of k-step 0 of the current tap; prefetched before the previous tap's barrier
+    // (they only depend on the layer's input image, not on the weights that barrier publishes)
+    bf16x8_t bpre[PTW];
+    auto tap_addr = [&](int tap, int (&base)[PTW], int (&rot)[PTW]) {
       const int dy = tap / 3 - 1, dx = tap % 3 - 1;
       const int offq = dy * HP + dx, offv = dy * H + dx;
-      int base[PTW], rot[PTW];
 #pragma unroll
       for (int i = 0; i < PTW; ++i) {
         const bool ok = qc[i] >= 0;
@@ -213,26 +212,48 @@ __global__ void __launch_bounds__(512) k_tower(TowerArgs t) {
         base[i] = ok ? (qc[i] + offq) * 256 : 0;
         rot[i] = ok ? (p + offv + cg) : 0;
       }
+    };
+    auto readB = [&](bf16x8_t (&dst)[PTW], const int (&base)[PTW], const int (&rot)[PTW], int ks) {
+#pragma unroll
+      for (int i = 0; i < PTW; ++i) {
+        if (ABL & 8) dst[i] = bf16x8_t{};
+        else dst[i] = *(const bf16x8_t *)(act + base[i] + (((rot[i] + 2 * ks) & 15) << 4));
+      }
+    };
+    {
+      int base0[PTW], rot0[PTW];
+      tap_addr(0, base0, rot0);
+      readB(bpre, base0, rot0, 0);
+    }
+    for (int tap = 0; tap < 9; ++tap, ++s) {
+      if (!(ABL & 1) && s + 1 < total_stages) issue_stage(s + 1);
+      int base[PTW], rot[PTW];
+      tap_addr(tap, base, rot);
       const uint8_t *wb = wst + (s & 1) * TAP_BYTES + (nh * 4 * 64 + lane) * 16;
       // every wave computes PTW tiles unconditionally (tiles past the board read the zero row and
       // are never stored): branch-free code lets hipcc count lgkmcnt waits per k-step
       bf16x8_t a[2][4], b[2][PTW];
-      auto load = [&](int buf, int ks) {
+      auto readA = [&](int buf, int ks) {
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) a[buf][nt] = *(const bf16x8_t *)(wb + (ks * 8 + nt) * 1024);
-#pragma unroll
-        for (int i = 0; i < PTW; ++i) {
-          if (ABL & 8) b[buf][i] = a[buf][i & 3];
-          else b[buf][i] = *(const bf16x8_t *)(act + base[i] + (((rot[i] + 2 * ks) & 15) << 4));
-        }
       };
-      load(0, 0);
+      readA(0, 0);
+#pragma unroll
+      for (int i = 0; i < PTW; ++i) b[0][i] = bpre[i];
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
-        // pin the schedule: next k-step's 8 fragment reads are issued before this k-step's 16 MFMAs
+        // pin the schedule: next k-step's fragment reads are issued before this k-step's 16 MFMAs
         // (hipcc otherwise recycles one fragment register and waits lgkmcnt(0) every 4 MFMAs)
-        if (ks < 3) load((ks + 1) & 1, ks + 1);
+        if (ks < 3) {
+          readA((ks + 1) & 1, ks + 1);
+          readB(b[(ks + 1) & 1], base, rot, ks + 1);
+        } else if (tap < 8) {
+          int nbase[PTW], nrot[PTW];
+          tap_addr(tap + 1, nbase, nrot);
+          readB(bpre, nbase, nrot, 0);
+        }
         __builtin_amdgcn_sched_barrier(0);
+        if (ABL & 64) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int i = 0; i < PTW; ++i)
 #pragma unroll
@@ -243,6 +264,7 @@ __global__ void __launch_bounds__(512) k_tower(TowerArgs t) {
               acc[nt][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks & 1][nt], b[ks & 1][i], acc[nt][i], 0, 0, 0);
             }
           }
+        if (ABL & 64) __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_sched_barrier(0);
       }
       if (tap < 8) {
@@ -282,12 +304,13 @@ __global__ void __launch_bounds__(512) k_tower(TowerArgs t) {
           const int ddy = ay - p / H + 1, ddx = ax - p % H + 1;
           if (ddy >= 0 && ddy <= 2 && ddx >= 0 && ddx <= 2) v += *(const f32x4 *)(saction + (ddy * 3 + ddx) * C + n0);
         }
-        if (kind == 2) v += xres[nt][i];
+        if (kind == 2) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
-        if (kind != 1) xres[nt][i] = v;
+          for (int e = 0; e < 4; ++e) v[e] += bf2f(xres[nt][i][e]);
+        }
 #pragma unroll
-        for (int e = 0; e < 4; ++e) outv[nt][i][e] = f2bf(v[e]);
+        for (int e = 0; e < 4; ++e) outv[nt][i][e] = f2bf(fmaxf(v[e], 0.f));
+        if (kind != 1) xres[nt][i] = outv[nt][i];
       }
     }
     if (!(ABL & 1)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -328,6 +351,281 @@ __global__ void __launch_bounds__(512) k_tower(TowerArgs t) {
     t.pv_feat[(size_t)r * 3 * A + i] = fmaxf(sum, 0.f);
   }
   (void)key_of_q;
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_tower2: barrier-light persistent variant (grid = one workgroup per CU, boards strided over it).
+//  * Each wave streams ITS OWN weight fragments global -> VGPR (3-deep register ring; the 4 waves of
+//    a channel half read the same 1 KB lines, served by L1/L2): no LDS weight stage, no per-tap
+//    barrier.  The ring runs modulo the weight set, so the next board's first k-steps are in flight
+//    while the current board finishes.
+//  * The freed LDS double-buffers the activation image: layer L reads img[L&1], its epilogue writes
+//    img[(L+1)&1] -> ONE barrier per layer.
+//  * 17 layers end in img[1] with img[0] free: the NEXT board's input is DMA'd (global_load_lds,
+//    slot swizzle applied on the source side) into img[0] while this board's output stage
+//    (hidden-state store + 1x1 head convs) runs.
+template <int H, bool DYN, int ABL = 0>
+__global__ void __launch_bounds__(512) k_tower2(TowerArgs t) {
+  using G = Geo<H>;
+  constexpr int A = G::A, HP = G::HP, AP = G::AP, NPT = G::NPT, PTW = G::PTW;
+  constexpr int ACT_BYTES = AP * C * 2;
+  constexpr int MAX_LAYERS = 17;
+  constexpr int BIAS_BYTES = (MAX_LAYERS + 9) * C * 4;
+  constexpr int KSTEPS = 36;  // 9 taps x 4 k-steps of 32 input channels
+  constexpr int XW = (H + 3) / 4;  // 4-position DMA groups per board row
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * ACT_BYTES + BIAS_BYTES];
+  float *sbias = (float *)(smem + 2 * ACT_BYTES);
+  float *saction = sbias + MAX_LAYERS * C;
+  uint8_t *img0 = smem;
+
+  auto next_row = [&](int from) {
+    while (from < t.rows && t.out_slot[from] < 0) from += gridDim.x;
+    return from;
+  };
+  int r = next_row(blockIdx.x);
+  if (r >= t.rows) return;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int nh = w >> 2, pg = w & 3;
+  const int g4 = lane >> 4;
+  const int cg = (g4 & 1) * 8 + (g4 >> 1);  // {0, 8, 1, 9}
+  auto chunk_addr = [&](int q, int key, int c) -> int { return q * 256 + (((c + key) & 15) << 4); };
+
+  // ---- DYN input DMA: wave instruction j covers board row j / XW, positions 4*(j % XW) .. +3; lane l
+  //      fills slot l&15 of position +l/16 with chunk (slot - key) & 15 of the parent hidden state
+  auto issue_input = [&](int row) {
+    const uint8_t *src = (const uint8_t *)(t.pool + (size_t)t.in_slot[row] * A * C);
+    for (int j = w; j < H * XW; j += 8) {
+      const int y = j / XW, x0 = 4 * (j % XW);
+      const int x = x0 + (lane >> 4), sl = lane & 15;
+      if (x < H) {
+        const int p = y * H + x;
+        __builtin_amdgcn_global_load_lds((const void *)(src + p * 256 + (((sl - p) & 15) << 4)),
+                                         (__attribute__((address_space(3))) void *)(img0 + ((y + 1) * HP + x0 + 1) * 256),
+                                         16, 0, 0);
+      }
+    }
+  };
+
+  // ---- zero the border of both images, stage biases
+  for (int i = tid; i < 2 * (4 * HP - 4) * 16; i += 512) {
+    const int img = i >= (4 * HP - 4) * 16;
+    const int ii = img ? i - (4 * HP - 4) * 16 : i;
+    const int b = ii >> 4, ch = ii & 15;
+    int q;
+    if (b < HP) q = b;
+    else if (b < 2 * HP) q = (HP - 1) * HP + (b - HP);
+    else {
+      const int k = b - 2 * HP;
+      q = (1 + (k >> 1)) * HP + ((k & 1) ? HP - 1 : 0);
+    }
+    *(uint4 *)(smem + img * ACT_BYTES + q * 256 + ch * 16) = make_uint4(0, 0, 0, 0);
+  }
+  for (int i = tid; i < t.n_layers * C; i += 512) sbias[i] = t.bias[i];
+  if (DYN)
+    for (int i = tid; i < 9 * C; i += 512) saction[i] = t.action_term[i];
+  if constexpr (DYN && !(ABL & (32 | 512))) issue_input(r);
+
+  int qc[PTW];
+#pragma unroll
+  for (int i = 0; i < PTW; ++i) {
+    const int pt = pg + 4 * i;
+    const int p = pt * 16 + sigma16(lane & 15);
+    qc[i] = (pt < NPT && p < A) ? (p / H + 1) * HP + (p % H + 1) : -1;
+  }
+  f32x4 acc[4][PTW];
+  u16x4 xres[4][PTW];
+  auto store_out = [&](uint8_t *img, int nt, int i, const u16x4 &o) {
+    const int q = qc[i];
+    const int p = (pg + 4 * i) * 16 + sigma16(lane & 15);
+    const int n0 = (nh * 4 + nt) * 16 + g4 * 4;
+    *(u16x4 *)(img + chunk_addr(q, p & 15, n0 >> 3) + (n0 & 4) * 2) = o;
+  };
+
+  // ---- weight fragment stream, per wave: k-step gs (modulo the whole set) of n-tile nt at
+  //      convs + gs*8 KB + (nh*4 + nt)*1 KB + lane*16 B   (buffer loads: 32-bit voffset + scalar soffset)
+  const int total_ks = t.n_layers * KSTEPS;
+  const __amdgpu_buffer_rsrc_t wrsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void *)t.convs, (short)0, total_ks * 8192, 0x00020000);
+  const int wvoff = (nh * 4) * 1024 + lane * 16;
+  bf16x8_t ar[3][4];
+  auto loadA = [&](int slot, int gs) {
+    const int soff = (gs < total_ks ? gs : gs - total_ks) * 8192;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(wrsrc, wvoff + nt * 1024, soff, 0);
+      ar[slot][nt] = __builtin_bit_cast(bf16x8_t, v);
+    }
+  };
+  loadA(0, 0);
+  loadA(1, 1);
+
+  while (r < t.rows) {
+    const int os = t.out_slot[r];
+    // ---- REPR stem (one MFMA k-step on an im2col operand) -> img0
+    if constexpr (!DYN) {
+      const float *ob = t.obs + (size_t)r * 3 * A;
+      bf16x8_t a[4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) a[nt] = ((const bf16x8_t *)t.stem_w)[(nh * 4 + nt) * 64 + lane];
+#pragma unroll
+      for (int i = 0; i < PTW; ++i) {
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) acc[nt][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (pg + 4 * i >= NPT) continue;
+        const int p = (pg + 4 * i) * 16 + sigma16(lane & 15);
+        const int y = p / H, x = p % H;
+        bf16x8_t b;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int k = 8 * g4 + j;
+          float v = 0.f;
+          if (k < 27 && p < A) {
+            const int tap = k / 3, c = k % 3;
+            const int yy = y + tap / 3 - 1, xx = x + tap % 3 - 1;
+            if (yy >= 0 && yy < H && xx >= 0 && xx < H) v = ob[c * A + yy * H + xx];
+          }
+          b[j] = (__bf16)v;
+        }
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) acc[nt][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[nt], b, acc[nt][i], 0, 0, 0);
+      }
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int n0 = (nh * 4 + nt) * 16 + g4 * 4;
+#pragma unroll
+        for (int i = 0; i < PTW; ++i) {
+          if (qc[i] < 0) continue;
+          u16x4 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = f2bf(fmaxf(acc[nt][i][e] + t.stem_b[n0 + e], 0.f));
+          xres[nt][i] = o;
+          store_out(img0, nt, i, o);
+        }
+      }
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this board's input DMA has landed
+    }
+    __syncthreads();
+
+    for (int L = 0; L < t.n_layers; ++L) {
+      const uint8_t *img = smem + (L & 1) * ACT_BYTES;
+      uint8_t *nimg = smem + ((L + 1) & 1) * ACT_BYTES;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int i = 0; i < PTW; ++i) acc[nt][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      bf16x8_t b[2][PTW];
+      int base[PTW], rot[PTW];
+      auto tap_addr = [&](int tap) {
+        const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+        const int offq = dy * HP + dx, offv = dy * H + dx;
+#pragma unroll
+        for (int i = 0; i < PTW; ++i) {
+          const bool ok = qc[i] >= 0;
+          const int p = (pg + 4 * i) * 16 + sigma16(lane & 15);
+          base[i] = ok ? (qc[i] + offq) * 256 : 0;
+          rot[i] = ok ? (p + offv + cg) : 0;
+          // opaque per tap: keeps the compiler from hoisting all 144 (tap, k-step, tile) slot
+          // addresses out of the layer loop (they would not fit in VGPRs)
+          asm volatile("" : "+v"(base[i]), "+v"(rot[i]));
+        }
+      };
+      auto readB = [&](int buf, int ks) {
+#pragma unroll
+        for (int i = 0; i < PTW; ++i) b[buf][i] = *(const bf16x8_t *)(img + base[i] + (((rot[i] + 2 * ks) & 15) << 4));
+      };
+      tap_addr(0);
+      readB(0, 0);
+      const int gs0 = L * KSTEPS;
+#pragma unroll
+      for (int st = 0; st < KSTEPS; ++st) {
+        // A for k-step st+2 (3-deep register ring), B for k-step st+1 (double buffer)
+        loadA((st + 2) % 3, gs0 + st + 2);
+        if (st + 1 < KSTEPS) {
+          if (((st + 1) & 3) == 0) tap_addr((st + 1) >> 2);
+          readB((st + 1) & 1, (st + 1) & 3);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < PTW; ++i)
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt)
+            acc[nt][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ar[st % 3][nt], b[st & 1][i], acc[nt][i], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // (36 % 3 == 0: the ring slots of the next layer's k-steps 0, 1 are 0, 1 again)
+      // epilogue: bias (+ action term) (+ residual) + ReLU -> bf16 -> the other image (no barrier
+      // needed before: nobody reads nimg during this layer)
+      const int kind = DYN ? (L == 0 ? 0 : ((L - 1) & 1) + 1) : ((L & 1) + 1);
+      const float *bias = sbias + L * C;
+      int ay = 0, ax = 0;
+      if (DYN && kind == 0) {
+        const int av = t.action[r];
+        ay = av / H;
+        ax = av % H;
+      }
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int n0 = (nh * 4 + nt) * 16 + g4 * 4;
+        const f32x4 bv = *(const f32x4 *)(bias + n0);
+#pragma unroll
+        for (int i = 0; i < PTW; ++i) {
+          const int p = (pg + 4 * i) * 16 + sigma16(lane & 15);
+          f32x4 v = acc[nt][i] + bv;
+          if (DYN && kind == 0) {
+            const int ddy = ay - p / H + 1, ddx = ax - p % H + 1;
+            if (ddy >= 0 && ddy <= 2 && ddx >= 0 && ddx <= 2) v += *(const f32x4 *)(saction + (ddy * 3 + ddx) * C + n0);
+          }
+          if (kind == 2) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += bf2f(xres[nt][i][e]);
+          }
+          u16x4 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = f2bf(fmaxf(v[e], 0.f));
+          if (kind != 1) xres[nt][i] = o;
+          if (qc[i] >= 0) store_out(nimg, nt, i, o);
+        }
+      }
+      __syncthreads();
+    }
+
+    // ---- next board's input -> the free image, overlapped with this board's output stage
+    const int nr = next_row(r + gridDim.x);
+    if constexpr (DYN && !(ABL & (32 | 512))) {
+      if (nr < t.rows) issue_input(nr);  // DYN has 1 + 2*blocks (odd) layers: the result is in img[1]
+    }
+    const uint8_t *fin = smem + (t.n_layers & 1) * ACT_BYTES;
+    if (!(ABL & 32)) {
+      uint4 *dst = (uint4 *)(t.pool + (size_t)os * A * C);
+      if (!(ABL & 256))
+      for (int i = tid; i < A * 16; i += 512) {
+        const int p = i >> 4, ch = i & 15;
+        const int q = (p / H + 1) * HP + (p % H + 1);
+        dst[i] = *(const uint4 *)(fin + chunk_addr(q, p & 15, ch));
+      }
+      if (!(ABL & 128))
+      for (int i = tid; i < 3 * A; i += 512) {
+        const int o = i / A, p = i % A;
+        const int q = (p / H + 1) * HP + (p % H + 1);
+        const float *hw = t.head_w + o * C;
+        float sum = t.head_b[o];
+#pragma unroll 4
+        for (int ch = 0; ch < 16; ++ch) {
+          const uint4 v = *(const uint4 *)(fin + chunk_addr(q, p & 15, ch));
+          const uint32_t wds[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            sum += hw[ch * 8 + 2 * e] * __uint_as_float(wds[e] << 16);
+            sum += hw[ch * 8 + 2 * e + 1] * __uint_as_float(wds[e] & 0xFFFF0000u);
+          }
+        }
+        t.pv_feat[(size_t)r * 3 * A + i] = fmaxf(sum, 0.f);
+      }
+    }
+    __syncthreads();  // the next board's layer 0 overwrites img[1]
+    r = nr;
+  }
 }
 
 // reward_fc.0 : [rows, A*128] (NHWC hidden, gathered by slot) x [A*128, 64], split-K partials.
@@ -476,9 +774,20 @@ __global__ void __launch_bounds__(256) k_heads(HeadArgs h) {
 
 using namespace gmz;
 
+// persistent grid: one 512-thread workgroup per CU (the double-buffered image takes the CU's LDS)
+static int cu_count() {
+  static int n[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!n[dev] && hipDeviceGetAttribute(&n[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) n[dev] = 256;
+  return n[dev];
+}
+
 template <int H, bool DYN>
 static int launch_tower(const TowerArgs &a, hipStream_t s) {
-  hipLaunchKernelGGL((k_tower<H, DYN>), dim3(a.rows), dim3(512), 0, s, a);
+  if (a.rows <= 0) return 0;
+  const int grid = a.rows < cu_count() ? a.rows : cu_count();
+  hipLaunchKernelGGL((k_tower2<H, DYN>), dim3(grid), dim3(512), 0, s, a);
   GMZ_LAUNCH_CHECK();
   return 0;
 }
