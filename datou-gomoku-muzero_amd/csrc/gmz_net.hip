@@ -628,6 +628,267 @@ __global__ void __launch_bounds__(512) k_tower2(TowerArgs t) {
   }
 }
 
+// k_tower3: k_tower2 with a padded, skewed image instead of the rotated one.
+//  Cell (yy, xx) of the (H+2)^2 padded board sits at yy*RS + xx*PS, PS = 272 B (256 B of channels +
+//  16 B pad), RS = HP*PS - 32.  Then (address/16) mod 16 = (yy*H + xx) mod 16 + chunk: the same bank
+//  map as the rotation by virtual key (conflict-free fragment reads), but every tap / k-step of a
+//  B-fragment read is an immediate offset from ONE base register per tile, and stores need no
+//  rotation arithmetic.  Row r's last cell and row r+1's first cell overlap by 32 B: both are
+//  zero borders, never written.  Biases move to a per-layer LDS double buffer filled by LDS-DMA
+//  (the skewed images leave no room for all 17 layers' biases).
+template <int H>
+struct Img3 {
+  static constexpr int HP = H + 2, PS = 272, RS = HP * PS - 32;
+  static constexpr int BYTES = ((HP - 1) * RS + HP * PS + 255) / 256 * 256;
+  static constexpr int RUN = (H - 1) * PS + 256;     // bytes of one board row's interior cells
+  static constexpr int RUN_DMA = (RUN + 1023) / 1024; // 1 KB LDS-DMA pieces per board row
+};
+
+template <int H, bool DYN, int ABL = 0>
+__global__ void __launch_bounds__(512) k_tower3(TowerArgs t) {
+  using G = Geo<H>;
+  using I = Img3<H>;
+  constexpr int A = G::A, NPT = G::NPT, PTW = G::PTW;
+  constexpr int PS = I::PS, RS = I::RS, IMG = I::BYTES;
+  constexpr int KSTEPS = 36;  // 9 taps x 4 k-steps of 32 input channels
+  static_assert(2 * IMG + 2 * C * 4 + 9 * C * 4 <= 163840, "LDS budget");
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * IMG + 2 * C * 4 + 9 * C * 4];
+  float *sbias = (float *)(smem + 2 * IMG);   // [2][128] per-layer double buffer
+  float *saction = sbias + 2 * C;             // DYN: [9][128]
+  uint8_t *img0 = smem;
+
+  auto next_row = [&](int from) {
+    while (from < t.rows && t.out_slot[from] < 0) from += gridDim.x;
+    return from;
+  };
+  int r = next_row(blockIdx.x);
+  if (r >= t.rows) return;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int nh = w >> 2, pg = w & 3;
+  const int g4 = lane >> 4;
+  const int cg = (g4 & 1) * 8 + (g4 >> 1);  // {0, 8, 1, 9}
+  auto cell = [&](int p) { return (p / H + 1) * RS + (p % H + 1) * PS; };
+
+  // ---- DYN input DMA: 1 KB pieces of each board row's interior run; lane l of piece j covers run
+  //      bytes j*1024 + 16*l (chunk (o % PS)/16 of position o / PS); pad chunks and bytes past the
+  //      run are masked off
+  auto issue_input = [&](int row) {
+    const uint8_t *src = (const uint8_t *)(t.pool + (size_t)t.in_slot[row] * A * C);
+    for (int j = w; j < H * I::RUN_DMA; j += 8) {
+      const int y = j / I::RUN_DMA, piece = j % I::RUN_DMA;
+      const int o = piece * 1024 + lane * 16;
+      const int x = o / PS, ch = (o % PS) >> 4;
+      if (o < I::RUN && ch < 16)
+        __builtin_amdgcn_global_load_lds((const void *)(src + (y * H + x) * 256 + ch * 16),
+                                         (__attribute__((address_space(3))) void *)(img0 + (y + 1) * RS + PS + piece * 1024),
+                                         16, 0, 0);
+    }
+  };
+  // ---- bias of layer L -> sbias[slot]: one 512 B LDS-DMA by wave 0 (32 lanes)
+  auto issue_bias = [&](int L, int slot) {
+    if (w == 0 && lane < 32)
+      __builtin_amdgcn_global_load_lds((const void *)(t.bias + L * C + lane * 4),
+                                       (__attribute__((address_space(3))) void *)(sbias + slot * C), 16, 0, 0);
+  };
+
+  // ---- zero both images (borders and pads), biases of layer 0, action term
+  for (int i = tid; i < 2 * IMG / 16; i += 512) *(uint4 *)(smem + i * 16) = make_uint4(0, 0, 0, 0);
+  if (tid < C) sbias[tid] = t.bias[tid];
+  if (DYN)
+    for (int i = tid; i < 9 * C; i += 512) saction[i] = t.action_term[i];
+  __syncthreads();  // zeroing done before the DMA writes the interior
+  if constexpr (DYN && !(ABL & 32)) issue_input(r);
+
+  // per tile: LDS byte offset of the top-left neighbour of this lane's column position (+ its
+  // k-chunk for B reads); -1 marks positions past the board
+  int pos[PTW];
+#pragma unroll
+  for (int i = 0; i < PTW; ++i) {
+    const int pt = pg + 4 * i;
+    const int p = pt * 16 + sigma16(lane & 15);
+    pos[i] = (pt < NPT && p < A) ? (p / H) * RS + (p % H) * PS : -1;
+  }
+  f32x4 acc[4][PTW];
+  u16x4 xres[4][PTW];
+  auto store_out = [&](uint8_t *img, int nt, int i, const u16x4 &o) {
+    const int n0 = (nh * 4 + nt) * 16 + g4 * 4;
+    *(u16x4 *)(img + pos[i] + RS + PS + n0 * 2) = o;
+  };
+
+  // ---- weight fragment stream, per wave: k-step gs (modulo the whole set) of n-tile nt at
+  //      convs + gs*8 KB + (nh*4 + nt)*1 KB + lane*16 B   (buffer loads: 32-bit voffset + scalar soffset)
+  const int total_ks = t.n_layers * KSTEPS;
+  const __amdgpu_buffer_rsrc_t wrsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void *)t.convs, (short)0, total_ks * 8192, 0x00020000);
+  const int wvoff = (nh * 4) * 1024 + lane * 16;
+  bf16x8_t ar[3][4];
+  auto loadA = [&](int slot, int gs) {
+    const int soff = (gs < total_ks ? gs : gs - total_ks) * 8192;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(wrsrc, wvoff + nt * 1024, soff, 0);
+      ar[slot][nt] = __builtin_bit_cast(bf16x8_t, v);
+    }
+  };
+  loadA(0, 0);
+  loadA(1, 1);
+  int gl = 0;  // layers run by this workgroup so far: bias slot = gl & 1
+
+  while (r < t.rows) {
+    const int os = t.out_slot[r];
+    if constexpr (!DYN) {  // ---- REPR stem (one MFMA k-step on an im2col operand) -> img0
+      const float *ob = t.obs + (size_t)r * 3 * A;
+      bf16x8_t a[4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) a[nt] = ((const bf16x8_t *)t.stem_w)[(nh * 4 + nt) * 64 + lane];
+#pragma unroll
+      for (int i = 0; i < PTW; ++i) {
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) acc[nt][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (pg + 4 * i >= NPT) continue;
+        const int p = (pg + 4 * i) * 16 + sigma16(lane & 15);
+        const int y = p / H, x = p % H;
+        bf16x8_t b;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int k = 8 * g4 + j;
+          float v = 0.f;
+          if (k < 27 && p < A) {
+            const int tap = k / 3, c = k % 3;
+            const int yy = y + tap / 3 - 1, xx = x + tap % 3 - 1;
+            if (yy >= 0 && yy < H && xx >= 0 && xx < H) v = ob[c * A + yy * H + xx];
+          }
+          b[j] = (__bf16)v;
+        }
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) acc[nt][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[nt], b, acc[nt][i], 0, 0, 0);
+      }
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int n0 = (nh * 4 + nt) * 16 + g4 * 4;
+#pragma unroll
+        for (int i = 0; i < PTW; ++i) {
+          if (pos[i] < 0) continue;
+          u16x4 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = f2bf(fmaxf(acc[nt][i][e] + t.stem_b[n0 + e], 0.f));
+          xres[nt][i] = o;
+          store_out(img0, nt, i, o);
+        }
+      }
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this board's input DMA has landed
+    }
+    __syncthreads();
+
+    for (int L = 0; L < t.n_layers; ++L, ++gl) {
+      const uint8_t *img = smem + (L & 1) * IMG;
+      uint8_t *nimg = smem + ((L + 1) & 1) * IMG;
+      // the next layer's bias (for the last layer: the next board's layer 0) -> the other slot;
+      // that slot was last read by the previous layer's epilogue, which the barrier has closed
+      issue_bias(L + 1 < t.n_layers ? L + 1 : 0, (gl + 1) & 1);
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int i = 0; i < PTW; ++i) acc[nt][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      int bb[PTW];
+#pragma unroll
+      for (int i = 0; i < PTW; ++i) {
+        bb[i] = (pos[i] < 0 ? 0 : pos[i] + cg * 16) + (int)(size_t)(img - smem);
+        asm volatile("" : "+v"(bb[i]));  // one base VGPR per tile and layer; all else immediates
+      }
+      bf16x8_t b[2][PTW];
+      auto readB = [&](int buf, int st) {
+        const int tap = st >> 2, ks = st & 3;
+        const int off = (tap / 3) * RS + (tap % 3) * PS + ks * 32;
+#pragma unroll
+        for (int i = 0; i < PTW; ++i) b[buf][i] = *(const bf16x8_t *)(smem + bb[i] + off);
+      };
+      readB(0, 0);
+      const int gs0 = L * KSTEPS;
+#pragma unroll
+      for (int st = 0; st < KSTEPS; ++st) {
+        // A for k-step st+2 (3-deep register ring), B for k-step st+1 (double buffer)
+        loadA((st + 2) % 3, gs0 + st + 2);
+        if (st + 1 < KSTEPS) readB((st + 1) & 1, st + 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < PTW; ++i)
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt)
+            acc[nt][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ar[st % 3][nt], b[st & 1][i], acc[nt][i], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // epilogue: bias (+ action term) (+ residual) + ReLU -> bf16 -> the other image
+      const int kind = DYN ? (L == 0 ? 0 : ((L - 1) & 1) + 1) : ((L & 1) + 1);
+      const float *bias = sbias + (gl & 1) * C;
+      int ay = 0, ax = 0;
+      if (DYN && kind == 0) {
+        const int av = t.action[r];
+        ay = av / H;
+        ax = av % H;
+      }
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int n0 = (nh * 4 + nt) * 16 + g4 * 4;
+        const f32x4 bv = *(const f32x4 *)(bias + n0);
+#pragma unroll
+        for (int i = 0; i < PTW; ++i) {
+          f32x4 v = acc[nt][i] + bv;
+          if (DYN && kind == 0) {
+            const int p = (pg + 4 * i) * 16 + sigma16(lane & 15);
+            const int ddy = ay - p / H + 1, ddx = ax - p % H + 1;
+            if (ddy >= 0 && ddy <= 2 && ddx >= 0 && ddx <= 2) v += *(const f32x4 *)(saction + (ddy * 3 + ddx) * C + n0);
+          }
+          if (kind == 2) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += bf2f(xres[nt][i][e]);
+          }
+          u16x4 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = f2bf(fmaxf(v[e], 0.f));
+          if (kind != 1) xres[nt][i] = o;
+          if (pos[i] >= 0) store_out(nimg, nt, i, o);
+        }
+      }
+      // the bias DMA (issued before this layer's 36 k-steps) is older than the 8 ring loads
+      // still in flight: vmcnt(8) retires it before the barrier publishes the slot
+      if (w == 0) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      __syncthreads();
+    }
+
+    // ---- next board's input -> the free image, overlapped with this board's output stage
+    const int nr = next_row(r + gridDim.x);
+    if constexpr (DYN && !(ABL & 32)) {
+      if (nr < t.rows) issue_input(nr);  // DYN has 1 + 2*blocks (odd) layers: the result is in img[1]
+    }
+    const uint8_t *fin = smem + (t.n_layers & 1) * IMG;
+    if (!(ABL & 32)) {
+      uint4 *dst = (uint4 *)(t.pool + (size_t)os * A * C);
+      for (int i = tid; i < A * 16; i += 512) dst[i] = *(const uint4 *)(fin + cell(i >> 4) + (i & 15) * 16);
+      for (int i = tid; i < 3 * A; i += 512) {
+        const int o = i / A, p = i % A;
+        const uint8_t *src = fin + cell(p);
+        const float *hw = t.head_w + o * C;
+        float sum = t.head_b[o];
+#pragma unroll 4
+        for (int ch = 0; ch < 16; ++ch) {
+          const uint4 v = *(const uint4 *)(src + ch * 16);
+          const uint32_t wds[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            sum += hw[ch * 8 + 2 * e] * __uint_as_float(wds[e] << 16);
+            sum += hw[ch * 8 + 2 * e + 1] * __uint_as_float(wds[e] & 0xFFFF0000u);
+          }
+        }
+        t.pv_feat[(size_t)r * 3 * A + i] = fmaxf(sum, 0.f);
+      }
+    }
+    __syncthreads();  // the next board's layer 0 overwrites img[1]
+    r = nr;
+  }
+}
+
 // reward_fc.0 : [rows, A*128] (NHWC hidden, gathered by slot) x [A*128, 64], split-K partials.
 // 256-thread block = 4 waves x 16 rows; the 4 waves read the same B fragments (L1-shared), each
 // wave keeps 4 k-steps of loads in flight.
@@ -787,7 +1048,7 @@ template <int H, bool DYN>
 static int launch_tower(const TowerArgs &a, hipStream_t s) {
   if (a.rows <= 0) return 0;
   const int grid = a.rows < cu_count() ? a.rows : cu_count();
-  hipLaunchKernelGGL((k_tower2<H, DYN>), dim3(grid), dim3(512), 0, s, a);
+  hipLaunchKernelGGL((k_tower3<H, DYN>), dim3(grid), dim3(512), 0, s, a);
   GMZ_LAUNCH_CHECK();
   return 0;
 }

@@ -1,8 +1,8 @@
-"""Summarise rocprofv3 PMC csv dirs for the dynamics tower (k_tower<15, true>)."""
+"""Summarise rocprofv3 PMC csv dirs for the dynamics tower (k_tower3<15, true>)."""
 import collections, csv, glob, json, os, sys
 
 root = sys.argv[1]
-kern = sys.argv[2] if len(sys.argv) > 2 else "k_tower<15, true>"
+kern = sys.argv[2] if len(sys.argv) > 2 else "k_tower3<15, true"
 agg = collections.defaultdict(list)
 dur = []
 for f in glob.glob(os.path.join(root, "*", "pmc_counter_collection.csv")):

@@ -20,7 +20,8 @@ float run(const TowerArgs &a, int reps) {
   (void)hipEventRecord(e0, 0);
   for (int i = 0; i < reps; ++i) {
     if (V == 1) hipLaunchKernelGGL((k_tower<15, true, ABL>), dim3(a.rows), dim3(512), 0, 0, a);
-    else hipLaunchKernelGGL((k_tower2<15, true, ABL>), dim3(V == 2 ? a.rows : 256), dim3(512), 0, 0, a);
+    else if (V <= 3) hipLaunchKernelGGL((k_tower2<15, true, ABL>), dim3(V == 2 ? a.rows : 256), dim3(512), 0, 0, a);
+    else hipLaunchKernelGGL((k_tower3<15, true, ABL>), dim3(256), dim3(512), 0, 0, a);
   }
   (void)hipEventRecord(e1, 0);
   (void)hipEventSynchronize(e1);
@@ -68,16 +69,25 @@ int main(int argc, char **argv) {
     for (size_t i = 0; i < o1.size(); ++i) dh += o1[i] != o2[i];
     for (size_t i = 0; i < p1.size(); ++i) dp += p1[i] != p2[i];
     printf("tower2 vs tower: hidden mismatches %zu / %zu, pv mismatches %zu / %zu\n", dh, o1.size(), dp, p1.size());
+    CK(hipMemset(dpool + (size_t)rows * A * 128, 0, o1.size() * 2));
+    CK(hipMemset(dpv, 0, p1.size() * 4));
+    hipLaunchKernelGGL((k_tower3<15, true, 0>), dim3(256), dim3(512), 0, 0, a);
+    CK(hipMemcpy(o2.data(), dpool + (size_t)rows * A * 128, o2.size() * 2, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(p2.data(), dpv, p2.size() * 4, hipMemcpyDeviceToHost));
+    dh = dp = 0;
+    for (size_t i = 0; i < o1.size(); ++i) dh += o1[i] != o2[i];
+    for (size_t i = 0; i < p1.size(); ++i) dp += p1[i] != p2[i];
+    printf("tower3 vs tower: hidden mismatches %zu / %zu, pv mismatches %zu / %zu\n", dh, o1.size(), dp, p1.size());
   }
   const char *names[] = {"full", "no-wstream(1)", "no-wstream+no-barrier(3)", "no-mfma(4)", "no-Bread(8)",
                          "no-mfma,no-wstream,no-barrier(7)", "only-mfma(1|2|8)", "no-epilogue(16)", "no-io(32)",
-                         "no-epilogue,no-io(48)", "only-mfma,no-epi,no-io(59)", "nothing but loop(63)", "setprio(64)", "TOWER2 full", "TOWER2 no-io(32)", "TOWER2 persistent 256", "T2P no-heads(128)", "T2P no-outstore(256)", "T2P no-input(512)", "T2P no-io(32)"};
-  const int NV = 20;
+                         "no-epilogue,no-io(48)", "only-mfma,no-epi,no-io(59)", "nothing but loop(63)", "setprio(64)", "TOWER2 full", "TOWER2 no-io(32)", "TOWER2 persistent 256", "T2P no-heads(128)", "T2P no-outstore(256)", "T2P no-input(512)", "T2P no-io(32)", "TOWER3", "TOWER3 no-io(32)"};
+  const int NV = 22;
   float best[NV];
   for (int i = 0; i < NV; ++i) best[i] = 1e9f;
   for (int round = 0; round < 5; ++round) {
     float t[NV] = {run<0>(a, 5), run<1>(a, 5), run<3>(a, 5), run<4>(a, 5), run<8>(a, 5), run<7>(a, 5), run<11>(a, 5),
-                   run<16>(a, 5), run<32>(a, 5), run<48>(a, 5), run<59>(a, 5), run<63>(a, 5), run<64>(a, 5), run<0, 2>(a, 5), run<32, 2>(a, 5), run<0, 3>(a, 5), run<128, 3>(a, 5), run<256, 3>(a, 5), run<512, 3>(a, 5), run<32, 3>(a, 5)};
+                   run<16>(a, 5), run<32>(a, 5), run<48>(a, 5), run<59>(a, 5), run<63>(a, 5), run<64>(a, 5), run<0, 2>(a, 5), run<32, 2>(a, 5), run<0, 3>(a, 5), run<128, 3>(a, 5), run<256, 3>(a, 5), run<512, 3>(a, 5), run<32, 3>(a, 5), run<0, 4>(a, 5), run<32, 4>(a, 5)};
     for (int i = 0; i < NV; ++i) best[i] = t[i] < best[i] ? t[i] : best[i];
   }
   for (int i = 0; i < NV; ++i)
