@@ -12,6 +12,7 @@
 //   the prediction head's 1x1 convs (policy 2 + value 1 channels, BN folded) are evaluated.
 // k_reward_fc1: reward_fc.0 (28800 -> 64) as a split-K MFMA GEMM over the hidden slots.
 // k_heads: policy_fc, value MLP, reward fc2, support_to_scalar (network.py:9-13, 58-74, 84-88).
+#include <type_traits>
 #include "gmz_common.h"
 #include "../../include/gmz.h"
 
@@ -354,287 +355,25 @@ __global__ void __launch_bounds__(512) k_tower(TowerArgs t) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_tower2: barrier-light persistent variant (grid = one workgroup per CU, boards strided over it).
-//  * Each wave streams ITS OWN weight fragments global -> VGPR (3-deep register ring; the 4 waves of
-//    a channel half read the same 1 KB lines, served by L1/L2): no LDS weight stage, no per-tap
-//    barrier.  The ring runs modulo the weight set, so the next board's first k-steps are in flight
-//    while the current board finishes.
-//  * The freed LDS double-buffers the activation image: layer L reads img[L&1], its epilogue writes
-//    img[(L+1)&1] -> ONE barrier per layer.
-//  * 17 layers end in img[1] with img[0] free: the NEXT board's input is DMA'd (global_load_lds,
-//    slot swizzle applied on the source side) into img[0] while this board's output stage
+// k_tower3: the tower kernel the library launches.  Persistent (one 512-thread workgroup per CU,
+//  boards strided over the grid) and barrier-light:
+//  * Each wave streams ITS OWN weight fragments global -> VGPR (RD-deep register ring; the 4 waves
+//    of a channel half read the same 1 KB lines, served by L1/L2): no LDS weight stage, no per-tap
+//    barrier.  The ring runs modulo the weight set, so the next board's first k-steps are in
+//    flight while the current board finishes.
+//  * The LDS holds two activation images: layer L reads img[L&1], its epilogue writes
+//    img[(L+1)&1] -> ONE barrier per layer.  17 layers end in img[1] with img[0] free: the NEXT
+//    board's input is DMA'd (global_load_lds) into img[0] while this board's output stage
 //    (hidden-state store + 1x1 head convs) runs.
-template <int H, bool DYN, int ABL = 0>
-__global__ void __launch_bounds__(512) k_tower2(TowerArgs t) {
-  using G = Geo<H>;
-  constexpr int A = G::A, HP = G::HP, AP = G::AP, NPT = G::NPT, PTW = G::PTW;
-  constexpr int ACT_BYTES = AP * C * 2;
-  constexpr int MAX_LAYERS = 17;
-  constexpr int BIAS_BYTES = (MAX_LAYERS + 9) * C * 4;
-  constexpr int KSTEPS = 36;  // 9 taps x 4 k-steps of 32 input channels
-  constexpr int XW = (H + 3) / 4;  // 4-position DMA groups per board row
-  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * ACT_BYTES + BIAS_BYTES];
-  float *sbias = (float *)(smem + 2 * ACT_BYTES);
-  float *saction = sbias + MAX_LAYERS * C;
-  uint8_t *img0 = smem;
-
-  auto next_row = [&](int from) {
-    while (from < t.rows && t.out_slot[from] < 0) from += gridDim.x;
-    return from;
-  };
-  int r = next_row(blockIdx.x);
-  if (r >= t.rows) return;
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  const int nh = w >> 2, pg = w & 3;
-  const int g4 = lane >> 4;
-  const int cg = (g4 & 1) * 8 + (g4 >> 1);  // {0, 8, 1, 9}
-  auto chunk_addr = [&](int q, int key, int c) -> int { return q * 256 + (((c + key) & 15) << 4); };
-
-  // ---- DYN input DMA: wave instruction j covers board row j / XW, positions 4*(j % XW) .. +3; lane l
-  //      fills slot l&15 of position +l/16 with chunk (slot - key) & 15 of the parent hidden state
-  auto issue_input = [&](int row) {
-    const uint8_t *src = (const uint8_t *)(t.pool + (size_t)t.in_slot[row] * A * C);
-    for (int j = w; j < H * XW; j += 8) {
-      const int y = j / XW, x0 = 4 * (j % XW);
-      const int x = x0 + (lane >> 4), sl = lane & 15;
-      if (x < H) {
-        const int p = y * H + x;
-        __builtin_amdgcn_global_load_lds((const void *)(src + p * 256 + (((sl - p) & 15) << 4)),
-                                         (__attribute__((address_space(3))) void *)(img0 + ((y + 1) * HP + x0 + 1) * 256),
-                                         16, 0, 0);
-      }
-    }
-  };
-
-  // ---- zero the border of both images, stage biases
-  for (int i = tid; i < 2 * (4 * HP - 4) * 16; i += 512) {
-    const int img = i >= (4 * HP - 4) * 16;
-    const int ii = img ? i - (4 * HP - 4) * 16 : i;
-    const int b = ii >> 4, ch = ii & 15;
-    int q;
-    if (b < HP) q = b;
-    else if (b < 2 * HP) q = (HP - 1) * HP + (b - HP);
-    else {
-      const int k = b - 2 * HP;
-      q = (1 + (k >> 1)) * HP + ((k & 1) ? HP - 1 : 0);
-    }
-    *(uint4 *)(smem + img * ACT_BYTES + q * 256 + ch * 16) = make_uint4(0, 0, 0, 0);
-  }
-  for (int i = tid; i < t.n_layers * C; i += 512) sbias[i] = t.bias[i];
-  if (DYN)
-    for (int i = tid; i < 9 * C; i += 512) saction[i] = t.action_term[i];
-  if constexpr (DYN && !(ABL & (32 | 512))) issue_input(r);
-
-  int qc[PTW];
-#pragma unroll
-  for (int i = 0; i < PTW; ++i) {
-    const int pt = pg + 4 * i;
-    const int p = pt * 16 + sigma16(lane & 15);
-    qc[i] = (pt < NPT && p < A) ? (p / H + 1) * HP + (p % H + 1) : -1;
-  }
-  f32x4 acc[4][PTW];
-  u16x4 xres[4][PTW];
-  auto store_out = [&](uint8_t *img, int nt, int i, const u16x4 &o) {
-    const int q = qc[i];
-    const int p = (pg + 4 * i) * 16 + sigma16(lane & 15);
-    const int n0 = (nh * 4 + nt) * 16 + g4 * 4;
-    *(u16x4 *)(img + chunk_addr(q, p & 15, n0 >> 3) + (n0 & 4) * 2) = o;
-  };
-
-  // ---- weight fragment stream, per wave: k-step gs (modulo the whole set) of n-tile nt at
-  //      convs + gs*8 KB + (nh*4 + nt)*1 KB + lane*16 B   (buffer loads: 32-bit voffset + scalar soffset)
-  const int total_ks = t.n_layers * KSTEPS;
-  const __amdgpu_buffer_rsrc_t wrsrc =
-      __builtin_amdgcn_make_buffer_rsrc((void *)t.convs, (short)0, total_ks * 8192, 0x00020000);
-  const int wvoff = (nh * 4) * 1024 + lane * 16;
-  bf16x8_t ar[3][4];
-  auto loadA = [&](int slot, int gs) {
-    const int soff = (gs < total_ks ? gs : gs - total_ks) * 8192;
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      const auto v = __builtin_amdgcn_raw_buffer_load_b128(wrsrc, wvoff + nt * 1024, soff, 0);
-      ar[slot][nt] = __builtin_bit_cast(bf16x8_t, v);
-    }
-  };
-  loadA(0, 0);
-  loadA(1, 1);
-
-  while (r < t.rows) {
-    const int os = t.out_slot[r];
-    // ---- REPR stem (one MFMA k-step on an im2col operand) -> img0
-    if constexpr (!DYN) {
-      const float *ob = t.obs + (size_t)r * 3 * A;
-      bf16x8_t a[4];
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) a[nt] = ((const bf16x8_t *)t.stem_w)[(nh * 4 + nt) * 64 + lane];
-#pragma unroll
-      for (int i = 0; i < PTW; ++i) {
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) acc[nt][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (pg + 4 * i >= NPT) continue;
-        const int p = (pg + 4 * i) * 16 + sigma16(lane & 15);
-        const int y = p / H, x = p % H;
-        bf16x8_t b;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int k = 8 * g4 + j;
-          float v = 0.f;
-          if (k < 27 && p < A) {
-            const int tap = k / 3, c = k % 3;
-            const int yy = y + tap / 3 - 1, xx = x + tap % 3 - 1;
-            if (yy >= 0 && yy < H && xx >= 0 && xx < H) v = ob[c * A + yy * H + xx];
-          }
-          b[j] = (__bf16)v;
-        }
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) acc[nt][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[nt], b, acc[nt][i], 0, 0, 0);
-      }
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        const int n0 = (nh * 4 + nt) * 16 + g4 * 4;
-#pragma unroll
-        for (int i = 0; i < PTW; ++i) {
-          if (qc[i] < 0) continue;
-          u16x4 o;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] = f2bf(fmaxf(acc[nt][i][e] + t.stem_b[n0 + e], 0.f));
-          xres[nt][i] = o;
-          store_out(img0, nt, i, o);
-        }
-      }
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this board's input DMA has landed
-    }
-    __syncthreads();
-
-    for (int L = 0; L < t.n_layers; ++L) {
-      const uint8_t *img = smem + (L & 1) * ACT_BYTES;
-      uint8_t *nimg = smem + ((L + 1) & 1) * ACT_BYTES;
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-        for (int i = 0; i < PTW; ++i) acc[nt][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-      bf16x8_t b[2][PTW];
-      int base[PTW], rot[PTW];
-      auto tap_addr = [&](int tap) {
-        const int dy = tap / 3 - 1, dx = tap % 3 - 1;
-        const int offq = dy * HP + dx, offv = dy * H + dx;
-#pragma unroll
-        for (int i = 0; i < PTW; ++i) {
-          const bool ok = qc[i] >= 0;
-          const int p = (pg + 4 * i) * 16 + sigma16(lane & 15);
-          base[i] = ok ? (qc[i] + offq) * 256 : 0;
-          rot[i] = ok ? (p + offv + cg) : 0;
-          // opaque per tap: keeps the compiler from hoisting all 144 (tap, k-step, tile) slot
-          // addresses out of the layer loop (they would not fit in VGPRs)
-          asm volatile("" : "+v"(base[i]), "+v"(rot[i]));
-        }
-      };
-      auto readB = [&](int buf, int ks) {
-#pragma unroll
-        for (int i = 0; i < PTW; ++i) b[buf][i] = *(const bf16x8_t *)(img + base[i] + (((rot[i] + 2 * ks) & 15) << 4));
-      };
-      tap_addr(0);
-      readB(0, 0);
-      const int gs0 = L * KSTEPS;
-#pragma unroll
-      for (int st = 0; st < KSTEPS; ++st) {
-        // A for k-step st+2 (3-deep register ring), B for k-step st+1 (double buffer)
-        loadA((st + 2) % 3, gs0 + st + 2);
-        if (st + 1 < KSTEPS) {
-          if (((st + 1) & 3) == 0) tap_addr((st + 1) >> 2);
-          readB((st + 1) & 1, (st + 1) & 3);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int i = 0; i < PTW; ++i)
-#pragma unroll
-          for (int nt = 0; nt < 4; ++nt)
-            acc[nt][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ar[st % 3][nt], b[st & 1][i], acc[nt][i], 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      // (36 % 3 == 0: the ring slots of the next layer's k-steps 0, 1 are 0, 1 again)
-      // epilogue: bias (+ action term) (+ residual) + ReLU -> bf16 -> the other image (no barrier
-      // needed before: nobody reads nimg during this layer)
-      const int kind = DYN ? (L == 0 ? 0 : ((L - 1) & 1) + 1) : ((L & 1) + 1);
-      const float *bias = sbias + L * C;
-      int ay = 0, ax = 0;
-      if (DYN && kind == 0) {
-        const int av = t.action[r];
-        ay = av / H;
-        ax = av % H;
-      }
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        const int n0 = (nh * 4 + nt) * 16 + g4 * 4;
-        const f32x4 bv = *(const f32x4 *)(bias + n0);
-#pragma unroll
-        for (int i = 0; i < PTW; ++i) {
-          const int p = (pg + 4 * i) * 16 + sigma16(lane & 15);
-          f32x4 v = acc[nt][i] + bv;
-          if (DYN && kind == 0) {
-            const int ddy = ay - p / H + 1, ddx = ax - p % H + 1;
-            if (ddy >= 0 && ddy <= 2 && ddx >= 0 && ddx <= 2) v += *(const f32x4 *)(saction + (ddy * 3 + ddx) * C + n0);
-          }
-          if (kind == 2) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] += bf2f(xres[nt][i][e]);
-          }
-          u16x4 o;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] = f2bf(fmaxf(v[e], 0.f));
-          if (kind != 1) xres[nt][i] = o;
-          if (qc[i] >= 0) store_out(nimg, nt, i, o);
-        }
-      }
-      __syncthreads();
-    }
-
-    // ---- next board's input -> the free image, overlapped with this board's output stage
-    const int nr = next_row(r + gridDim.x);
-    if constexpr (DYN && !(ABL & (32 | 512))) {
-      if (nr < t.rows) issue_input(nr);  // DYN has 1 + 2*blocks (odd) layers: the result is in img[1]
-    }
-    const uint8_t *fin = smem + (t.n_layers & 1) * ACT_BYTES;
-    if (!(ABL & 32)) {
-      uint4 *dst = (uint4 *)(t.pool + (size_t)os * A * C);
-      if (!(ABL & 256))
-      for (int i = tid; i < A * 16; i += 512) {
-        const int p = i >> 4, ch = i & 15;
-        const int q = (p / H + 1) * HP + (p % H + 1);
-        dst[i] = *(const uint4 *)(fin + chunk_addr(q, p & 15, ch));
-      }
-      if (!(ABL & 128))
-      for (int i = tid; i < 3 * A; i += 512) {
-        const int o = i / A, p = i % A;
-        const int q = (p / H + 1) * HP + (p % H + 1);
-        const float *hw = t.head_w + o * C;
-        float sum = t.head_b[o];
-#pragma unroll 4
-        for (int ch = 0; ch < 16; ++ch) {
-          const uint4 v = *(const uint4 *)(fin + chunk_addr(q, p & 15, ch));
-          const uint32_t wds[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            sum += hw[ch * 8 + 2 * e] * __uint_as_float(wds[e] << 16);
-            sum += hw[ch * 8 + 2 * e + 1] * __uint_as_float(wds[e] & 0xFFFF0000u);
-          }
-        }
-        t.pv_feat[(size_t)r * 3 * A + i] = fmaxf(sum, 0.f);
-      }
-    }
-    __syncthreads();  // the next board's layer 0 overwrites img[1]
-    r = nr;
-  }
-}
-
-// k_tower3: k_tower2 with a padded, skewed image instead of the rotated one.
+//  Image layout: padded and skewed instead of rotated (k_tower's LDS image):
 //  Cell (yy, xx) of the (H+2)^2 padded board sits at yy*RS + xx*PS, PS = 272 B (256 B of channels +
 //  16 B pad), RS = HP*PS - 32.  Then (address/16) mod 16 = (yy*H + xx) mod 16 + chunk: the same bank
 //  map as the rotation by virtual key (conflict-free fragment reads), but every tap / k-step of a
 //  B-fragment read is an immediate offset from ONE base register per tile, and stores need no
 //  rotation arithmetic.  Row r's last cell and row r+1's first cell overlap by 32 B: both are
-//  zero borders, never written.  Biases move to a per-layer LDS double buffer filled by LDS-DMA
+//  zero borders, never written.  The residual is read back from the image being overwritten (block
+//  input = layer L-2's output = img[(L+1)&1]) instead of being held in VGPRs, which pays for an
+//  RD-deep weight-fragment ring.  Biases move to a per-layer LDS double buffer filled by LDS-DMA
 //  (the skewed images leave no room for all 17 layers' biases).
 template <int H>
 struct Img3 {
@@ -644,7 +383,7 @@ struct Img3 {
   static constexpr int RUN_DMA = (RUN + 1023) / 1024; // 1 KB LDS-DMA pieces per board row
 };
 
-template <int H, bool DYN, int ABL = 0>
+template <int H, bool DYN, int ABL = 0, int RD = 4>
 __global__ void __launch_bounds__(512) k_tower3(TowerArgs t) {
   using G = Geo<H>;
   using I = Img3<H>;
@@ -709,7 +448,6 @@ __global__ void __launch_bounds__(512) k_tower3(TowerArgs t) {
     pos[i] = (pt < NPT && p < A) ? (p / H) * RS + (p % H) * PS : -1;
   }
   f32x4 acc[4][PTW];
-  u16x4 xres[4][PTW];
   auto store_out = [&](uint8_t *img, int nt, int i, const u16x4 &o) {
     const int n0 = (nh * 4 + nt) * 16 + g4 * 4;
     *(u16x4 *)(img + pos[i] + RS + PS + n0 * 2) = o;
@@ -721,18 +459,22 @@ __global__ void __launch_bounds__(512) k_tower3(TowerArgs t) {
   const __amdgpu_buffer_rsrc_t wrsrc =
       __builtin_amdgcn_make_buffer_rsrc((void *)t.convs, (short)0, total_ks * 8192, 0x00020000);
   const int wvoff = (nh * 4) * 1024 + lane * 16;
-  bf16x8_t ar[3][4];
+  static_assert(KSTEPS % RD == 0, "ring slots must repeat per layer");
+  bf16x8_t ar[RD][4];
   auto loadA = [&](int slot, int gs) {
-    const int soff = (gs < total_ks ? gs : gs - total_ks) * 8192;
+    if constexpr ((ABL & 2) != 0) if (gs >= 2) return;  // ablation: no weight stream in the loop
+    const int soff = (ABL & 1) ? 0 : (gs < total_ks ? gs : gs - total_ks) * 8192;  // ablation: L1-resident
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
       const auto v = __builtin_amdgcn_raw_buffer_load_b128(wrsrc, wvoff + nt * 1024, soff, 0);
       ar[slot][nt] = __builtin_bit_cast(bf16x8_t, v);
     }
   };
-  loadA(0, 0);
-  loadA(1, 1);
+#pragma unroll
+  for (int k = 0; k < RD - 1; ++k) loadA(k, k);
   int gl = 0;  // layers run by this workgroup so far: bias slot = gl & 1
+  uint64_t st_loop = 0, st_epi = 0, st_bar = 0, st_t0 = 0, st_t1 = 0, st_t2 = 0;  // ABL & 128 stamps
+  const uint64_t st_start = (ABL & 128) ? __builtin_amdgcn_s_memtime() : 0;
 
   while (r < t.rows) {
     const int os = t.out_slot[r];
@@ -772,7 +514,6 @@ __global__ void __launch_bounds__(512) k_tower3(TowerArgs t) {
           u16x4 o;
 #pragma unroll
           for (int e = 0; e < 4; ++e) o[e] = f2bf(fmaxf(acc[nt][i][e] + t.stem_b[n0 + e], 0.f));
-          xres[nt][i] = o;
           store_out(img0, nt, i, o);
         }
       }
@@ -805,56 +546,79 @@ __global__ void __launch_bounds__(512) k_tower3(TowerArgs t) {
         for (int i = 0; i < PTW; ++i) b[buf][i] = *(const bf16x8_t *)(smem + bb[i] + off);
       };
       readB(0, 0);
+      if (ABL & 128) st_t0 = __builtin_amdgcn_s_memtime();
       const int gs0 = L * KSTEPS;
 #pragma unroll
       for (int st = 0; st < KSTEPS; ++st) {
-        // A for k-step st+2 (3-deep register ring), B for k-step st+1 (double buffer)
-        loadA((st + 2) % 3, gs0 + st + 2);
+        // A for k-step st+RD-1 (RD-deep register ring), B for k-step st+1 (double buffer)
+        loadA((st + RD - 1) % RD, gs0 + st + RD - 1);
         if (st + 1 < KSTEPS) readB((st + 1) & 1, st + 1);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int i = 0; i < PTW; ++i)
 #pragma unroll
           for (int nt = 0; nt < 4; ++nt)
-            acc[nt][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ar[st % 3][nt], b[st & 1][i], acc[nt][i], 0, 0, 0);
+            acc[nt][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ar[st % RD][nt], b[st & 1][i], acc[nt][i], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
       }
-      // epilogue: bias (+ action term) (+ residual) + ReLU -> bf16 -> the other image
+      if (ABL & 128) { st_t1 = __builtin_amdgcn_s_memtime(); st_loop += st_t1 - st_t0; }
+      // epilogue: bias (+ action term) (+ residual) + ReLU -> bf16 -> the other image.  One
+      // straight-line copy per layer kind; every LDS operand (bias, residual) is read in one batch
+      // before any arithmetic, so the epilogue pays one LDS latency, not one per tile.
       const int kind = DYN ? (L == 0 ? 0 : ((L - 1) & 1) + 1) : ((L & 1) + 1);
       const float *bias = sbias + (gl & 1) * C;
-      int ay = 0, ax = 0;
-      if (DYN && kind == 0) {
-        const int av = t.action[r];
-        ay = av / H;
-        ax = av % H;
-      }
+      auto epilogue = [&](auto kind_c) {
+        constexpr int KIND = decltype(kind_c)::value;
+        f32x4 bv[4];
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        const int n0 = (nh * 4 + nt) * 16 + g4 * 4;
-        const f32x4 bv = *(const f32x4 *)(bias + n0);
+        for (int nt = 0; nt < 4; ++nt) bv[nt] = *(const f32x4 *)(bias + (nh * 4 + nt) * 16 + g4 * 4);
+        u16x4 xr[4][PTW];
+        if constexpr (KIND == 2) {
+          // residual = this block's input, still in the image this epilogue overwrites, at the
+          // very address this lane is about to store (read-then-write by the same lane)
 #pragma unroll
-        for (int i = 0; i < PTW; ++i) {
-          f32x4 v = acc[nt][i] + bv;
-          if (DYN && kind == 0) {
-            const int p = (pg + 4 * i) * 16 + sigma16(lane & 15);
-            const int ddy = ay - p / H + 1, ddx = ax - p % H + 1;
-            if (ddy >= 0 && ddy <= 2 && ddx >= 0 && ddx <= 2) v += *(const f32x4 *)(saction + (ddy * 3 + ddx) * C + n0);
-          }
-          if (kind == 2) {
+          for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] += bf2f(xres[nt][i][e]);
-          }
-          u16x4 o;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] = f2bf(fmaxf(v[e], 0.f));
-          if (kind != 1) xres[nt][i] = o;
-          if (pos[i] >= 0) store_out(nimg, nt, i, o);
+            for (int i = 0; i < PTW; ++i)
+              xr[nt][i] = *(const u16x4 *)(nimg + (pos[i] < 0 ? 0 : pos[i]) + RS + PS + ((nh * 4 + nt) * 16 + g4 * 4) * 2);
         }
-      }
-      // the bias DMA (issued before this layer's 36 k-steps) is older than the 8 ring loads
-      // still in flight: vmcnt(8) retires it before the barrier publishes the slot
-      if (w == 0) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        int ay = 0, ax = 0;
+        if constexpr (DYN && KIND == 0) {
+          const int av = t.action[r];
+          ay = av / H;
+          ax = av % H;
+        }
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+          const int n0 = (nh * 4 + nt) * 16 + g4 * 4;
+#pragma unroll
+          for (int i = 0; i < PTW; ++i) {
+            f32x4 v = acc[nt][i] + bv[nt];
+            if constexpr (DYN && KIND == 0) {
+              const int p = (pg + 4 * i) * 16 + sigma16(lane & 15);
+              const int ddy = ay - p / H + 1, ddx = ax - p % H + 1;
+              if (ddy >= 0 && ddy <= 2 && ddx >= 0 && ddx <= 2) v += *(const f32x4 *)(saction + (ddy * 3 + ddx) * C + n0);
+            }
+            if constexpr (KIND == 2) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] += bf2f(xr[nt][i][e]);
+            }
+            u16x4 o;
+#pragma unroll  // ReLU as med3(v, 0, FLT_MAX): one VALU, no NaN canonicalisation pair
+            for (int e = 0; e < 4; ++e) o[e] = f2bf(__builtin_amdgcn_fmed3f(v[e], 0.f, 3.402823466e38f));
+            if ((3 + 4 * i + 1) * 16 <= A || pos[i] >= 0) store_out(nimg, nt, i, o);
+          }
+        }
+      };
+      if (DYN && kind == 0) epilogue(std::integral_constant<int, 0>{});
+      else if (kind == 1) epilogue(std::integral_constant<int, 1>{});
+      else epilogue(std::integral_constant<int, 2>{});
+      // the bias DMA (issued before this layer's 36 k-steps) is older than the (RD-1)*4 ring loads
+      // still in flight: this count retires it before the barrier publishes the slot
+      if (w == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((RD - 1) * 4) : "memory");
+      if (ABL & 128) { st_t2 = __builtin_amdgcn_s_memtime(); st_epi += st_t2 - st_t1; }
       __syncthreads();
+      if (ABL & 128) st_bar += __builtin_amdgcn_s_memtime() - st_t2;
     }
 
     // ---- next board's input -> the free image, overlapped with this board's output stage
@@ -886,6 +650,11 @@ __global__ void __launch_bounds__(512) k_tower3(TowerArgs t) {
     }
     __syncthreads();  // the next board's layer 0 overwrites img[1]
     r = nr;
+  }
+  if ((ABL & 128) && lane == 0) {  // diagnostic build only: per-wave phase cycles -> pv_feat
+    float *o = t.pv_feat + (blockIdx.x * 8 + w) * 4;
+    o[0] = (float)st_loop; o[1] = (float)st_epi; o[2] = (float)st_bar;
+    o[3] = (float)(__builtin_amdgcn_s_memtime() - st_start);
   }
 }
 

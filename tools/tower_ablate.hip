@@ -5,6 +5,9 @@
 #include <cstdio>
 #include <vector>
 #include <random>
+#include <cstring>
+#include <cmath>
+#include <algorithm>
 
 namespace gmz {
 void set_error(const std::string &) {}
@@ -13,15 +16,14 @@ int fail(const std::string &m) { fprintf(stderr, "%s\n", m.c_str()); return -1; 
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
 
-template <int ABL, int V = 1>
+template <int ABL, int V = 1, int RD = 4>
 float run(const TowerArgs &a, int reps) {
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
   (void)hipEventRecord(e0, 0);
   for (int i = 0; i < reps; ++i) {
     if (V == 1) hipLaunchKernelGGL((k_tower<15, true, ABL>), dim3(a.rows), dim3(512), 0, 0, a);
-    else if (V <= 3) hipLaunchKernelGGL((k_tower2<15, true, ABL>), dim3(V == 2 ? a.rows : 256), dim3(512), 0, 0, a);
-    else hipLaunchKernelGGL((k_tower3<15, true, ABL>), dim3(256), dim3(512), 0, 0, a);
+    else hipLaunchKernelGGL((k_tower3<15, true, ABL, RD>), dim3(256), dim3(512), 0, 0, a);
   }
   (void)hipEventRecord(e1, 0);
   (void)hipEventSynchronize(e1);
@@ -55,43 +57,44 @@ int main(int argc, char **argv) {
   CK(hipMemcpy(dac, action.data(), rows * 4, hipMemcpyHostToDevice));
   TowerArgs a{dw, dbias, L, nullptr, nullptr, dact, nullptr, dpool, din, dac, dout, dhw, dhb, dpv, rows};
   const double flop = 1136505600.0 * rows;
-  {  // k_tower2 must reproduce k_tower bit for bit (same MFMA order, same epilogue)
+  {  // k_tower3 must reproduce k_tower (LDS-staged weights, rotated image) bit for bit
     std::vector<uint16_t> o1((size_t)rows * A * 128), o2(o1.size());
     std::vector<float> p1((size_t)rows * 3 * A), p2(p1.size());
     hipLaunchKernelGGL((k_tower<15, true, 0>), dim3(rows), dim3(512), 0, 0, a);
     CK(hipMemcpy(o1.data(), dpool + (size_t)rows * A * 128, o1.size() * 2, hipMemcpyDeviceToHost));
     CK(hipMemcpy(p1.data(), dpv, p1.size() * 4, hipMemcpyDeviceToHost));
     CK(hipMemset(dpool + (size_t)rows * A * 128, 0, o1.size() * 2));
-    hipLaunchKernelGGL((k_tower2<15, true, 0>), dim3(256), dim3(512), 0, 0, a);
+    CK(hipMemset(dpv, 0, p1.size() * 4));
+    hipLaunchKernelGGL((k_tower3<15, true, 0>), dim3(256), dim3(512), 0, 0, a);
     CK(hipMemcpy(o2.data(), dpool + (size_t)rows * A * 128, o2.size() * 2, hipMemcpyDeviceToHost));
     CK(hipMemcpy(p2.data(), dpv, p2.size() * 4, hipMemcpyDeviceToHost));
     size_t dh = 0, dp = 0;
     for (size_t i = 0; i < o1.size(); ++i) dh += o1[i] != o2[i];
     for (size_t i = 0; i < p1.size(); ++i) dp += p1[i] != p2[i];
-    printf("tower2 vs tower: hidden mismatches %zu / %zu, pv mismatches %zu / %zu\n", dh, o1.size(), dp, p1.size());
-    CK(hipMemset(dpool + (size_t)rows * A * 128, 0, o1.size() * 2));
-    CK(hipMemset(dpv, 0, p1.size() * 4));
-    hipLaunchKernelGGL((k_tower3<15, true, 0>), dim3(256), dim3(512), 0, 0, a);
-    CK(hipMemcpy(o2.data(), dpool + (size_t)rows * A * 128, o2.size() * 2, hipMemcpyDeviceToHost));
-    CK(hipMemcpy(p2.data(), dpv, p2.size() * 4, hipMemcpyDeviceToHost));
-    dh = dp = 0;
-    for (size_t i = 0; i < o1.size(); ++i) dh += o1[i] != o2[i];
-    for (size_t i = 0; i < p1.size(); ++i) dp += p1[i] != p2[i];
     printf("tower3 vs tower: hidden mismatches %zu / %zu, pv mismatches %zu / %zu\n", dh, o1.size(), dp, p1.size());
   }
-  const char *names[] = {"full", "no-wstream(1)", "no-wstream+no-barrier(3)", "no-mfma(4)", "no-Bread(8)",
-                         "no-mfma,no-wstream,no-barrier(7)", "only-mfma(1|2|8)", "no-epilogue(16)", "no-io(32)",
-                         "no-epilogue,no-io(48)", "only-mfma,no-epi,no-io(59)", "nothing but loop(63)", "setprio(64)", "TOWER2 full", "TOWER2 no-io(32)", "TOWER2 persistent 256", "T2P no-heads(128)", "T2P no-outstore(256)", "T2P no-input(512)", "T2P no-io(32)", "TOWER3", "TOWER3 no-io(32)"};
-  const int NV = 22;
+  const char *names[] = {"k_tower (LDS-staged weights)", "k_tower3", "k_tower3 no-io(32)", "k_tower3 A-from-one-kstep(1)",
+                         "k_tower3 no-A-loads(2)", "k_tower3 RD3"};
+  const int NV = 6;
   float best[NV];
   for (int i = 0; i < NV; ++i) best[i] = 1e9f;
   for (int round = 0; round < 5; ++round) {
-    float t[NV] = {run<0>(a, 5), run<1>(a, 5), run<3>(a, 5), run<4>(a, 5), run<8>(a, 5), run<7>(a, 5), run<11>(a, 5),
-                   run<16>(a, 5), run<32>(a, 5), run<48>(a, 5), run<59>(a, 5), run<63>(a, 5), run<64>(a, 5), run<0, 2>(a, 5), run<32, 2>(a, 5), run<0, 3>(a, 5), run<128, 3>(a, 5), run<256, 3>(a, 5), run<512, 3>(a, 5), run<32, 3>(a, 5), run<0, 4>(a, 5), run<32, 4>(a, 5)};
+    float t[NV] = {run<0>(a, 5), run<0, 3>(a, 5), run<32, 3>(a, 5), run<1, 3>(a, 5), run<2, 3>(a, 5), run<0, 3, 3>(a, 5)};
     for (int i = 0; i < NV; ++i) best[i] = t[i] < best[i] ? t[i] : best[i];
   }
   for (int i = 0; i < NV; ++i)
     printf("%-36s %8.3f ms   %7.1f TFLOP/s\n", names[i], best[i], flop / (best[i] * 1e-3) / 1e12);
+  {  // phase stamps of k_tower3 (diagnostic build, ABL 128|32: no IO, stamps into pv_feat)
+    for (int k = 0; k < 3; ++k) run<128 | 32, 3>(a, 5);
+    std::vector<float> st(256 * 8 * 4);
+    CK(hipMemcpy(st.data(), dpv, st.size() * 4, hipMemcpyDeviceToHost));
+    double sum[4] = {0, 0, 0, 0};
+    for (int i = 0; i < 256 * 8; ++i)
+      for (int k = 0; k < 4; ++k) sum[k] += st[i * 4 + k];
+    const double per = 2048.0 * 17 * ((rows + 255) / 256);
+    printf("k_tower3 per layer and wave (s_memtime cycles): k-loop %.0f  epilogue %.0f  barrier %.0f  (whole kernel %.0f)\n",
+           sum[0] / per, sum[1] / per, sum[2] / per, sum[3] / 2048);
+  }
   CK(hipDeviceSynchronize());
   return 0;
 }
