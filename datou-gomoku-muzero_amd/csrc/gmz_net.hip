@@ -719,84 +719,119 @@ __device__ __forceinline__ float support3(float l0, float l1, float l2) {
   return (-1.f * p0 + 0.f * p1) + 1.f * p2;
 }
 
-// Prediction heads (+ reward head): 4 rows per 256-thread block so every weight is read once per
-// block; features are staged k-major ([k][4 rows]) so one ds_read_b128 feeds 4 FMAs.
-constexpr int HEAD_ROWS = 4;
-__global__ void __launch_bounds__(256) k_heads(HeadArgs h) {
+// Prediction heads (+ reward head): 4 rows per 512-thread block so every weight is read once per
+// block; features are staged k-major ([k][4 rows]) so one ds_read_b128 feeds 4 FMAs.  Every phase
+// spreads over the whole block (no serial single-thread tails):
+//   0: stage features, fc2 weights; reduce the reward GEMM's split-K partials (one (row, unit) each)
+//   1: policy_fc in two k-halves (450 threads); 2: combine + bias -> logits, value_fc1 in four
+//   k-quarters (256 threads); 3: value_fc1 bias + ReLU; 4: value / reward fc2 as wave reductions,
+//   support_to_scalar.
+constexpr int HEAD_ROWS = 4, HEAD_THREADS = 512;
+__global__ void __launch_bounds__(HEAD_THREADS) k_heads(HeadArgs h) {
   extern __shared__ float sm[];
   const int r0 = blockIdx.x * HEAD_ROWS, tid = threadIdx.x;
   const int A = h.A, hd = h.hd;
   float *feat = sm;                        // [3A][4]
-  float *hv = sm + 3 * A * HEAD_ROWS;      // [4][64]
+  float *ppart = feat + 3 * A * HEAD_ROWS; // [2][A][4]
+  float *vpart = ppart + 2 * A * HEAD_ROWS;// [4 quarters][4 rows][64]
+  float *hv = vpart + 4 * HEAD_ROWS * 64;  // [4][64]
   float *hr = hv + HEAD_ROWS * 64;         // [4][64]
+  float *w2 = hr + HEAD_ROWS * 64;         // [2][64 * 3]: value_fc2, reward_fc2
   bool valid[HEAD_ROWS];
 #pragma unroll
   for (int i = 0; i < HEAD_ROWS; ++i) valid[i] = r0 + i < h.rows && h.out_slot[r0 + i] >= 0;
-  for (int idx = tid; idx < 3 * A * HEAD_ROWS; idx += 256) {
+  for (int idx = tid; idx < 3 * A * HEAD_ROWS; idx += HEAD_THREADS) {
     const int k = idx >> 2, i = idx & 3;
     feat[idx] = valid[i] ? h.pv_feat[(size_t)(r0 + i) * 3 * A + k] : 0.f;
   }
+  if (tid < hd * 3) {
+    w2[tid] = h.vfc2_w[tid];
+    if (h.reward) w2[192 + tid] = h.rfc2_w[tid];
+  }
+  if (h.reward && tid >= 256 && tid < 256 + HEAD_ROWS * 64) {  // reward_fc.0: bias + partials + ReLU
+    const int i = (tid - 256) >> 6, j = tid & 63;
+    if (j < hd) {
+      float s = h.rfc1_b[j];
+      if (valid[i]) {
+        const float *src = h.rpart + (size_t)(r0 + i) * 64 + j;
+        const size_t stride = (size_t)h.rows * 64;
+        int k = 0;
+        for (; k + 8 <= h.ksplit; k += 8) {
+          float v[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) v[u] = src[(k + u) * stride];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) s += v[u];
+        }
+        for (; k < h.ksplit; ++k) s += src[k * stride];
+      }
+      hr[i * 64 + j] = fmaxf(s, 0.f);
+    }
+  }
   __syncthreads();
-  for (int a = tid; a < A; a += 256) {  // policy_fc (network.py:70)
-    const float b = h.pfc_b[a];
-    f32x4 acc = {b, b, b, b};
+  if (tid < 2 * A) {  // policy_fc (network.py:70), k-half kh of the 2A features
+    const int kh = tid >= A, a = tid - kh * A;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     const float *wcol = h.pfc_w + a;
-    int k = 0;
-    for (; k + 16 <= 2 * A; k += 16) {  // 16 independent weight loads in flight per thread
+    int k = kh * A;
+    const int ke = k + A;
+    for (; k + 16 <= ke; k += 16) {  // 16 independent weight loads in flight per thread
       float wv[16];
 #pragma unroll
       for (int u = 0; u < 16; ++u) wv[u] = wcol[(size_t)(k + u) * A];
 #pragma unroll
       for (int u = 0; u < 16; ++u) acc += *(const f32x4 *)(feat + 4 * (k + u)) * wv[u];
     }
-    for (; k < 2 * A; ++k) acc += *(const f32x4 *)(feat + 4 * k) * wcol[(size_t)k * A];
+    for (; k < ke; ++k) acc += *(const f32x4 *)(feat + 4 * k) * wcol[(size_t)k * A];
+    *(f32x4 *)(ppart + 4 * (kh * A + a)) = acc;
+  }
+  __syncthreads();
+  if (tid < A) {
+    const float b = h.pfc_b[tid];
+    const f32x4 p0 = *(const f32x4 *)(ppart + 4 * tid), p1 = *(const f32x4 *)(ppart + 4 * (A + tid));
 #pragma unroll
     for (int i = 0; i < HEAD_ROWS; ++i)
-      if (valid[i]) h.logits[(size_t)(r0 + i) * A + a] = acc[i];
-  }
-  if (tid < hd) {  // value_fc1 + ReLU (network.py:72)
-    const float b = h.vfc1_b[tid];
-    f32x4 acc = {b, b, b, b};
-    const float *wcol = h.vfc1_w + tid;
-    int p = 0;
-    for (; p + 16 <= A; p += 16) {
-      float wv[16];
+      if (valid[i]) h.logits[(size_t)(r0 + i) * A + tid] = (b + p0[i]) + p1[i];
+  } else if (tid >= 256) {  // value_fc1 (network.py:72), k-quarter q
+    const int q = (tid - 256) >> 6, j = tid & 63;
+    if (j < hd) {
+      const int p0 = q * A / 4, p1 = (q + 1) * A / 4;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      const float *wcol = h.vfc1_w + j;
+      int p = p0;
+      for (; p + 16 <= p1; p += 16) {
+        float wv[16];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) wv[u] = wcol[(p + u) * hd];
+        for (int u = 0; u < 16; ++u) wv[u] = wcol[(p + u) * hd];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) acc += *(const f32x4 *)(feat + 4 * (2 * A + p + u)) * wv[u];
-    }
-    for (; p < A; ++p) acc += *(const f32x4 *)(feat + 4 * (2 * A + p)) * wcol[p * hd];
+        for (int u = 0; u < 16; ++u) acc += *(const f32x4 *)(feat + 4 * (2 * A + p + u)) * wv[u];
+      }
+      for (; p < p1; ++p) acc += *(const f32x4 *)(feat + 4 * (2 * A + p)) * wcol[p * hd];
 #pragma unroll
-    for (int i = 0; i < HEAD_ROWS; ++i) hv[i * 64 + tid] = fmaxf(acc[i], 0.f);
-  } else if (h.reward && tid >= 64 && tid < 64 + hd) {  // reward_fc.0 bias + ReLU (network.py:84-86)
-    const int j = tid - 64;
-#pragma unroll
-    for (int i = 0; i < HEAD_ROWS; ++i) {
-      float s = h.rfc1_b[j];
-      if (valid[i])
-        for (int k = 0; k < h.ksplit; ++k) s += h.rpart[((size_t)k * h.rows + r0 + i) * 64 + j];
-      hr[i * 64 + j] = fmaxf(s, 0.f);
+      for (int i = 0; i < HEAD_ROWS; ++i) vpart[(q * HEAD_ROWS + i) * 64 + j] = acc[i];
     }
   }
   __syncthreads();
-  if (tid < HEAD_ROWS && valid[tid]) {
-    float l[3];
-    for (int k = 0; k < 3; ++k) {
-      float s = h.vfc2_b[k];
-      for (int j = 0; j < hd; ++j) s += hv[tid * 64 + j] * h.vfc2_w[j * 3 + k];
-      l[k] = s;
+  if (tid < HEAD_ROWS * 64) {
+    const int i = tid >> 6, j = tid & 63;
+    if (j < hd)
+      hv[i * 64 + j] = fmaxf(((h.vfc1_b[j] + vpart[(0 * HEAD_ROWS + i) * 64 + j]) + vpart[(1 * HEAD_ROWS + i) * 64 + j]) +
+                                 (vpart[(2 * HEAD_ROWS + i) * 64 + j] + vpart[(3 * HEAD_ROWS + i) * 64 + j]), 0.f);
+  }
+  __syncthreads();
+  const int w = tid >> 6, lane = tid & 63;
+  if (w < 2 && (w == 0 || h.reward)) {  // wave 0: value head, wave 1: reward head (fc2 + support)
+    const float *hx = w == 0 ? hv : hr;
+    const float *wx = w2 + 192 * w;
+    const float *bx = w == 0 ? h.vfc2_b : h.rfc2_b;
+    float *out = w == 0 ? h.value : h.reward;
+#pragma unroll
+    for (int i = 0; i < HEAD_ROWS; ++i) {
+      float l[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) l[k] = dred_sum_f(lane < hd ? hx[i * 64 + lane] * wx[lane * 3 + k] : 0.f) + bx[k];
+      if (lane == 0 && valid[i]) out[r0 + i] = support3(l[0], l[1], l[2]);
     }
-    h.value[r0 + tid] = support3(l[0], l[1], l[2]);
-  } else if (h.reward && tid >= 64 && tid < 64 + HEAD_ROWS && valid[tid - 64]) {
-    const int i = tid - 64;
-    float l[3];
-    for (int k = 0; k < 3; ++k) {
-      float s = h.rfc2_b[k];
-      for (int j = 0; j < hd; ++j) s += hr[i * 64 + j] * h.rfc2_w[j * 3 + k];
-      l[k] = s;
-    }
-    h.reward[r0 + i] = support3(l[0], l[1], l[2]);
   }
 }
 
@@ -831,7 +866,10 @@ static int tower(int H, bool dyn, const TowerArgs &a, hipStream_t s) {
   }
 }
 
-static constexpr int KSPLIT = 16;
+// split-K factor of the reward GEMM: 32 -> (rows/64) x 32 blocks keep ~64 KB of hidden-state reads
+// in flight per CU (16: 31 us, 32: 22 us, 64: 21.5 us at 1024 rows, the partials then cost more in
+// k_heads)
+static constexpr int KSPLIT = 32;
 
 static size_t ws_bytes(int A, int rows) {
   return (size_t)rows * 3 * A * sizeof(float) + (size_t)KSPLIT * rows * 64 * sizeof(float) + 256;
@@ -857,8 +895,8 @@ static int heads(const gmz_net_weights *w, const float *pv, const int32_t *out_s
   HeadArgs h{pv, out_slot, w->policy_fc_w, w->policy_fc_b, w->value_fc1_w, w->value_fc1_b, w->value_fc2_w,
              w->value_fc2_b, rpart, w->reward_fc1_b, w->reward_fc2_w, w->reward_fc2_b, rows, A, w->head_hidden,
              KSPLIT, logits, value, reward};
-  const size_t smem = (3 * A * HEAD_ROWS + 2 * HEAD_ROWS * 64) * sizeof(float);
-  hipLaunchKernelGGL(k_heads, dim3((rows + HEAD_ROWS - 1) / HEAD_ROWS), dim3(256), smem, s, h);
+  const size_t smem = (5 * A * HEAD_ROWS + 6 * HEAD_ROWS * 64 + 2 * 192) * sizeof(float);
+  hipLaunchKernelGGL(k_heads, dim3((rows + HEAD_ROWS - 1) / HEAD_ROWS), dim3(HEAD_THREADS), smem, s, h);
   GMZ_LAUNCH_CHECK();
   return 0;
 }
