@@ -383,11 +383,14 @@ struct Img3 {
   static constexpr int RUN_DMA = (RUN + 1023) / 1024; // 1 KB LDS-DMA pieces per board row
 };
 
-template <int H, bool DYN, int ABL = 0, int RD = 4>
-__global__ void __launch_bounds__(512) k_tower3(TowerArgs t) {
+template <int H, bool DYN, int ABL = 0, int RD = 4, int NQ = 2, int PG = 4>
+__global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
   using G = Geo<H>;
   using I = Img3<H>;
-  constexpr int A = G::A, NPT = G::NPT, PTW = G::PTW;
+  constexpr int A = G::A, NPT = G::NPT;
+  constexpr int NW = NQ * PG, NTHR = 64 * NW;       // waves: NQ channel groups x PG position groups
+  constexpr int NTW = 8 / NQ, PTW = (NPT + PG - 1) / PG;  // n-tiles / position tiles per wave
+  static_assert(8 % NQ == 0, "channel groups");
   constexpr int PS = I::PS, RS = I::RS, IMG = I::BYTES;
   constexpr int KSTEPS = 36;  // 9 taps x 4 k-steps of 32 input channels
   static_assert(2 * IMG + 2 * C * 4 + 9 * C * 4 <= 163840, "LDS budget");
@@ -403,7 +406,7 @@ __global__ void __launch_bounds__(512) k_tower3(TowerArgs t) {
   int r = next_row(blockIdx.x);
   if (r >= t.rows) return;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  const int nh = w >> 2, pg = w & 3;
+  const int nh = w / PG, pg = w % PG;
   const int g4 = lane >> 4;
   const int cg = (g4 & 1) * 8 + (g4 >> 1);  // {0, 8, 1, 9}
   auto cell = [&](int p) { return (p / H + 1) * RS + (p % H + 1) * PS; };
@@ -413,7 +416,7 @@ __global__ void __launch_bounds__(512) k_tower3(TowerArgs t) {
   //      run are masked off
   auto issue_input = [&](int row) {
     const uint8_t *src = (const uint8_t *)(t.pool + (size_t)t.in_slot[row] * A * C);
-    for (int j = w; j < H * I::RUN_DMA; j += 8) {
+    for (int j = w; j < H * I::RUN_DMA; j += NW) {
       const int y = j / I::RUN_DMA, piece = j % I::RUN_DMA;
       const int o = piece * 1024 + lane * 16;
       const int x = o / PS, ch = (o % PS) >> 4;
@@ -431,10 +434,10 @@ __global__ void __launch_bounds__(512) k_tower3(TowerArgs t) {
   };
 
   // ---- zero both images (borders and pads), biases of layer 0, action term
-  for (int i = tid; i < 2 * IMG / 16; i += 512) *(uint4 *)(smem + i * 16) = make_uint4(0, 0, 0, 0);
+  for (int i = tid; i < 2 * IMG / 16; i += NTHR) *(uint4 *)(smem + i * 16) = make_uint4(0, 0, 0, 0);
   if (tid < C) sbias[tid] = t.bias[tid];
   if (DYN)
-    for (int i = tid; i < 9 * C; i += 512) saction[i] = t.action_term[i];
+    for (int i = tid; i < 9 * C; i += NTHR) saction[i] = t.action_term[i];
   __syncthreads();  // zeroing done before the DMA writes the interior
   if constexpr (DYN && !(ABL & 32)) issue_input(r);
 
@@ -443,13 +446,13 @@ __global__ void __launch_bounds__(512) k_tower3(TowerArgs t) {
   int pos[PTW];
 #pragma unroll
   for (int i = 0; i < PTW; ++i) {
-    const int pt = pg + 4 * i;
+    const int pt = pg + PG * i;
     const int p = pt * 16 + sigma16(lane & 15);
     pos[i] = (pt < NPT && p < A) ? (p / H) * RS + (p % H) * PS : -1;
   }
-  f32x4 acc[4][PTW];
+  f32x4 acc[NTW][PTW];
   auto store_out = [&](uint8_t *img, int nt, int i, const u16x4 &o) {
-    const int n0 = (nh * 4 + nt) * 16 + g4 * 4;
+    const int n0 = (nh * NTW + nt) * 16 + g4 * 4;
     *(u16x4 *)(img + pos[i] + RS + PS + n0 * 2) = o;
   };
 
@@ -458,14 +461,14 @@ __global__ void __launch_bounds__(512) k_tower3(TowerArgs t) {
   const int total_ks = t.n_layers * KSTEPS;
   const __amdgpu_buffer_rsrc_t wrsrc =
       __builtin_amdgcn_make_buffer_rsrc((void *)t.convs, (short)0, total_ks * 8192, 0x00020000);
-  const int wvoff = (nh * 4) * 1024 + lane * 16;
+  const int wvoff = (nh * NTW) * 1024 + lane * 16;
   static_assert(KSTEPS % RD == 0, "ring slots must repeat per layer");
-  bf16x8_t ar[RD][4];
+  bf16x8_t ar[RD][NTW];
   auto loadA = [&](int slot, int gs) {
     if constexpr ((ABL & 2) != 0) if (gs >= 2) return;  // ablation: no weight stream in the loop
     const int soff = (ABL & 1) ? 0 : (gs < total_ks ? gs : gs - total_ks) * 8192;  // ablation: L1-resident
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
+    for (int nt = 0; nt < NTW; ++nt) {
       const auto v = __builtin_amdgcn_raw_buffer_load_b128(wrsrc, wvoff + nt * 1024, soff, 0);
       ar[slot][nt] = __builtin_bit_cast(bf16x8_t, v);
     }
@@ -480,15 +483,15 @@ __global__ void __launch_bounds__(512) k_tower3(TowerArgs t) {
     const int os = t.out_slot[r];
     if constexpr (!DYN) {  // ---- REPR stem (one MFMA k-step on an im2col operand) -> img0
       const float *ob = t.obs + (size_t)r * 3 * A;
-      bf16x8_t a[4];
+      bf16x8_t a[NTW];
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) a[nt] = ((const bf16x8_t *)t.stem_w)[(nh * 4 + nt) * 64 + lane];
+      for (int nt = 0; nt < NTW; ++nt) a[nt] = ((const bf16x8_t *)t.stem_w)[(nh * NTW + nt) * 64 + lane];
 #pragma unroll
       for (int i = 0; i < PTW; ++i) {
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) acc[nt][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (pg + 4 * i >= NPT) continue;
-        const int p = (pg + 4 * i) * 16 + sigma16(lane & 15);
+        for (int nt = 0; nt < NTW; ++nt) acc[nt][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (pg + PG * i >= NPT) continue;
+        const int p = (pg + PG * i) * 16 + sigma16(lane & 15);
         const int y = p / H, x = p % H;
         bf16x8_t b;
 #pragma unroll
@@ -503,11 +506,11 @@ __global__ void __launch_bounds__(512) k_tower3(TowerArgs t) {
           b[j] = (__bf16)v;
         }
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) acc[nt][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[nt], b, acc[nt][i], 0, 0, 0);
+        for (int nt = 0; nt < NTW; ++nt) acc[nt][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[nt], b, acc[nt][i], 0, 0, 0);
       }
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        const int n0 = (nh * 4 + nt) * 16 + g4 * 4;
+      for (int nt = 0; nt < NTW; ++nt) {
+        const int n0 = (nh * NTW + nt) * 16 + g4 * 4;
 #pragma unroll
         for (int i = 0; i < PTW; ++i) {
           if (pos[i] < 0) continue;
@@ -529,7 +532,7 @@ __global__ void __launch_bounds__(512) k_tower3(TowerArgs t) {
       // that slot was last read by the previous layer's epilogue, which the barrier has closed
       issue_bias(L + 1 < t.n_layers ? L + 1 : 0, (gl + 1) & 1);
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
+      for (int nt = 0; nt < NTW; ++nt)
 #pragma unroll
         for (int i = 0; i < PTW; ++i) acc[nt][i] = f32x4{0.f, 0.f, 0.f, 0.f};
       int bb[PTW];
@@ -557,7 +560,7 @@ __global__ void __launch_bounds__(512) k_tower3(TowerArgs t) {
 #pragma unroll
         for (int i = 0; i < PTW; ++i)
 #pragma unroll
-          for (int nt = 0; nt < 4; ++nt)
+          for (int nt = 0; nt < NTW; ++nt)
             acc[nt][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ar[st % RD][nt], b[st & 1][i], acc[nt][i], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -569,18 +572,18 @@ __global__ void __launch_bounds__(512) k_tower3(TowerArgs t) {
       const float *bias = sbias + (gl & 1) * C;
       auto epilogue = [&](auto kind_c) {
         constexpr int KIND = decltype(kind_c)::value;
-        f32x4 bv[4];
+        f32x4 bv[NTW];
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) bv[nt] = *(const f32x4 *)(bias + (nh * 4 + nt) * 16 + g4 * 4);
-        u16x4 xr[4][PTW];
+        for (int nt = 0; nt < NTW; ++nt) bv[nt] = *(const f32x4 *)(bias + (nh * NTW + nt) * 16 + g4 * 4);
+        u16x4 xr[NTW][PTW];
         if constexpr (KIND == 2) {
           // residual = this block's input, still in the image this epilogue overwrites, at the
           // very address this lane is about to store (read-then-write by the same lane)
 #pragma unroll
-          for (int nt = 0; nt < 4; ++nt)
+          for (int nt = 0; nt < NTW; ++nt)
 #pragma unroll
             for (int i = 0; i < PTW; ++i)
-              xr[nt][i] = *(const u16x4 *)(nimg + (pos[i] < 0 ? 0 : pos[i]) + RS + PS + ((nh * 4 + nt) * 16 + g4 * 4) * 2);
+              xr[nt][i] = *(const u16x4 *)(nimg + (pos[i] < 0 ? 0 : pos[i]) + RS + PS + ((nh * NTW + nt) * 16 + g4 * 4) * 2);
         }
         int ay = 0, ax = 0;
         if constexpr (DYN && KIND == 0) {
@@ -589,13 +592,13 @@ __global__ void __launch_bounds__(512) k_tower3(TowerArgs t) {
           ax = av % H;
         }
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) {
-          const int n0 = (nh * 4 + nt) * 16 + g4 * 4;
+        for (int nt = 0; nt < NTW; ++nt) {
+          const int n0 = (nh * NTW + nt) * 16 + g4 * 4;
 #pragma unroll
           for (int i = 0; i < PTW; ++i) {
             f32x4 v = acc[nt][i] + bv[nt];
             if constexpr (DYN && KIND == 0) {
-              const int p = (pg + 4 * i) * 16 + sigma16(lane & 15);
+              const int p = (pg + PG * i) * 16 + sigma16(lane & 15);
               const int ddy = ay - p / H + 1, ddx = ax - p % H + 1;
               if (ddy >= 0 && ddy <= 2 && ddx >= 0 && ddx <= 2) v += *(const f32x4 *)(saction + (ddy * 3 + ddx) * C + n0);
             }
@@ -606,16 +609,16 @@ __global__ void __launch_bounds__(512) k_tower3(TowerArgs t) {
             u16x4 o;
 #pragma unroll  // ReLU as med3(v, 0, FLT_MAX): one VALU, no NaN canonicalisation pair
             for (int e = 0; e < 4; ++e) o[e] = f2bf(__builtin_amdgcn_fmed3f(v[e], 0.f, 3.402823466e38f));
-            if ((3 + 4 * i + 1) * 16 <= A || pos[i] >= 0) store_out(nimg, nt, i, o);
+            if ((PG * i + PG) * 16 <= A || pos[i] >= 0) store_out(nimg, nt, i, o);
           }
         }
       };
       if (DYN && kind == 0) epilogue(std::integral_constant<int, 0>{});
       else if (kind == 1) epilogue(std::integral_constant<int, 1>{});
       else epilogue(std::integral_constant<int, 2>{});
-      // the bias DMA (issued before this layer's 36 k-steps) is older than the (RD-1)*4 ring loads
+      // the bias DMA (issued before this layer's 36 k-steps) is older than the (RD-1)*NTW ring loads
       // still in flight: this count retires it before the barrier publishes the slot
-      if (w == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((RD - 1) * 4) : "memory");
+      if (w == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((RD - 1) * NTW) : "memory");
       if (ABL & 128) { st_t2 = __builtin_amdgcn_s_memtime(); st_epi += st_t2 - st_t1; }
       __syncthreads();
       if (ABL & 128) st_bar += __builtin_amdgcn_s_memtime() - st_t2;
@@ -629,8 +632,8 @@ __global__ void __launch_bounds__(512) k_tower3(TowerArgs t) {
     const uint8_t *fin = smem + (t.n_layers & 1) * IMG;
     if (!(ABL & 32)) {
       uint4 *dst = (uint4 *)(t.pool + (size_t)os * A * C);
-      for (int i = tid; i < A * 16; i += 512) dst[i] = *(const uint4 *)(fin + cell(i >> 4) + (i & 15) * 16);
-      for (int i = tid; i < 3 * A; i += 512) {
+      for (int i = tid; i < A * 16; i += NTHR) dst[i] = *(const uint4 *)(fin + cell(i >> 4) + (i & 15) * 16);
+      for (int i = tid; i < 3 * A; i += NTHR) {
         const int o = i / A, p = i % A;
         const uint8_t *src = fin + cell(p);
         const float *hw = t.head_w + o * C;
@@ -652,7 +655,7 @@ __global__ void __launch_bounds__(512) k_tower3(TowerArgs t) {
     r = nr;
   }
   if ((ABL & 128) && lane == 0) {  // diagnostic build only: per-wave phase cycles -> pv_feat
-    float *o = t.pv_feat + (blockIdx.x * 8 + w) * 4;
+    float *o = t.pv_feat + (blockIdx.x * NW + w) * 4;
     o[0] = (float)st_loop; o[1] = (float)st_epi; o[2] = (float)st_bar;
     o[3] = (float)(__builtin_amdgcn_s_memtime() - st_start);
   }
@@ -852,7 +855,9 @@ template <int H, bool DYN>
 static int launch_tower(const TowerArgs &a, hipStream_t s) {
   if (a.rows <= 0) return 0;
   const int grid = a.rows < cu_count() ? a.rows : cu_count();
-  hipLaunchKernelGGL((k_tower3<H, DYN>), dim3(grid), dim3(512), 0, s, a);
+  // 12 waves = 4 channel quarters x 3 position groups (15 tiles of 16 positions at 15x15: no idle
+  // tile, 3 waves per SIMD); RD 3 keeps it within 168 VGPRs
+  hipLaunchKernelGGL((k_tower3<H, DYN, 0, 3, 4, 3>), dim3(grid), dim3(768), 0, s, a);
   GMZ_LAUNCH_CHECK();
   return 0;
 }

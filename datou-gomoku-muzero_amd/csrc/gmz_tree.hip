@@ -119,11 +119,14 @@ __device__ int transformed_q(const Dev &D, int lane, const int (&n)[NJ], const f
   const bool have_range = mm_max > mm_min;
   const float den_f = (mm_max - mm_min) + D.delta_f;
   if (!allv) {
+    // one wave-uniform reciprocal instead of a correctly rounded division per child (<= 1 ulp, the
+    // same order as the reduction-order differences already present; exact ties stay exact)
+    const double inv_den = 1.0 / (double)den_f;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       double nq = 0.0;
       if (have_range) {
-        double x = ((double)q[j] - (double)mm_min) / (double)den_f;
+        double x = ((double)q[j] - (double)mm_min) * inv_den;
         x = (x < 1.0) ? x : 1.0;
         nq = (x > 0.0) ? x : 0.0;
       }
@@ -182,8 +185,9 @@ __device__ void improved_policy(const Dev &D, const uint64_t (&lg)[NJ], int lane
       s += x[j];
     }
     s = dred_sum_d(s);
+    const double inv_s = 1.0 / s;
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) p[j] = x[j] / s;
+    for (int j = 0; j < NJ; ++j) p[j] = x[j] * inv_s;
   } else {
     float x[NJ], m = -INFINITY;
 #pragma unroll
@@ -239,11 +243,12 @@ __device__ int select_nonroot(const Dev &D, const uint64_t (&lg)[NJ], int g, int
   for (int j = 0; j < NJ; ++j) tot += n[j];
   tot = dred_sum_i(tot);
   double sc[NJ], best = -INFINITY;
+  const double inv_tot = 1.0 / (double)(1 + tot);
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int a = lane + WAVE * j;
     sc[j] = -INFINITY;
-    if (a < D.A && ((lg[j] >> lane) & 1ull)) sc[j] = p[j] - (double)n[j] / (double)(1 + tot);
+    if (a < D.A && ((lg[j] >> lane) & 1ull)) sc[j] = p[j] - (double)n[j] * inv_tot;
     best = fmax(best, sc[j]);
   }
   best = dred_max_d(best);

@@ -16,14 +16,14 @@ int fail(const std::string &m) { fprintf(stderr, "%s\n", m.c_str()); return -1; 
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
 
-template <int ABL, int V = 1, int RD = 4>
+template <int ABL, int V = 1, int RD = 4, int NQ = 2, int PG = 4>
 float run(const TowerArgs &a, int reps) {
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
   (void)hipEventRecord(e0, 0);
   for (int i = 0; i < reps; ++i) {
     if (V == 1) hipLaunchKernelGGL((k_tower<15, true, ABL>), dim3(a.rows), dim3(512), 0, 0, a);
-    else hipLaunchKernelGGL((k_tower3<15, true, ABL, RD>), dim3(256), dim3(512), 0, 0, a);
+    else hipLaunchKernelGGL((k_tower3<15, true, ABL, RD, NQ, PG>), dim3(256), dim3(64 * NQ * PG), 0, 0, a);
   }
   (void)hipEventRecord(e1, 0);
   (void)hipEventSynchronize(e1);
@@ -72,14 +72,23 @@ int main(int argc, char **argv) {
     for (size_t i = 0; i < o1.size(); ++i) dh += o1[i] != o2[i];
     for (size_t i = 0; i < p1.size(); ++i) dp += p1[i] != p2[i];
     printf("tower3 vs tower: hidden mismatches %zu / %zu, pv mismatches %zu / %zu\n", dh, o1.size(), dp, p1.size());
+    CK(hipMemset(dpool + (size_t)rows * A * 128, 0, o1.size() * 2));
+    CK(hipMemset(dpv, 0, p1.size() * 4));
+    hipLaunchKernelGGL((k_tower3<15, true, 0, 4, 4, 3>), dim3(256), dim3(768), 0, 0, a);
+    CK(hipMemcpy(o2.data(), dpool + (size_t)rows * A * 128, o2.size() * 2, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(p2.data(), dpv, p2.size() * 4, hipMemcpyDeviceToHost));
+    dh = dp = 0;
+    for (size_t i = 0; i < o1.size(); ++i) dh += o1[i] != o2[i];
+    for (size_t i = 0; i < p1.size(); ++i) dp += p1[i] != p2[i];
+    printf("tower3 12w vs tower: hidden mismatches %zu / %zu, pv mismatches %zu / %zu\n", dh, o1.size(), dp, p1.size());
   }
   const char *names[] = {"k_tower (LDS-staged weights)", "k_tower3", "k_tower3 no-io(32)", "k_tower3 A-from-one-kstep(1)",
-                         "k_tower3 no-A-loads(2)", "k_tower3 RD3"};
-  const int NV = 6;
+                         "k_tower3 no-A-loads(2)", "k_tower3 RD3", "k_tower3 12 waves (4x3)", "k_tower3 12w RD3", "k_tower3 12w no-io", "k_tower3 16w (4x4) RD3", "k_tower3 16w (4x4) RD2", "k_tower3 16w (8x2) RD3"};
+  const int NV = 12;
   float best[NV];
   for (int i = 0; i < NV; ++i) best[i] = 1e9f;
   for (int round = 0; round < 5; ++round) {
-    float t[NV] = {run<0>(a, 5), run<0, 3>(a, 5), run<32, 3>(a, 5), run<1, 3>(a, 5), run<2, 3>(a, 5), run<0, 3, 3>(a, 5)};
+    float t[NV] = {run<0>(a, 5), run<0, 3>(a, 5), run<32, 3>(a, 5), run<1, 3>(a, 5), run<2, 3>(a, 5), run<0, 3, 3>(a, 5), run<0, 3, 4, 4, 3>(a, 5), run<0, 3, 3, 4, 3>(a, 5), run<32, 3, 4, 4, 3>(a, 5), run<0, 3, 3, 4, 4>(a, 5), run<0, 3, 2, 4, 4>(a, 5), run<0, 3, 3, 8, 2>(a, 5)};
     for (int i = 0; i < NV; ++i) best[i] = t[i] < best[i] ? t[i] : best[i];
   }
   for (int i = 0; i < NV; ++i)
