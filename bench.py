@@ -9,7 +9,7 @@ Finished games restart immediately.  Data: synthetic — empty boards, random-in
   python bench.py [--gpus N --steps K --warmup W]              (N > 1: launched by torch.distributed.run)
 
 Prints ONE JSON line on rank 0 (schema: the driver contract) including
-  roofline     : the dominant kernel (dynamics tower k_tower<15,true>) timed with HIP events on its
+  roofline     : the dominant kernel (dynamics tower k_tower3<15,true>) timed with HIP events on its
                  launch stream inside the timed region; achieved = algorithmic FLOP per launch /
                  mean launch duration vs the 2.5 PFLOP/s dense bf16 MFMA peak;
   cpu_baseline : the C oracle's search (oracle/gmz_oracle.c) with the float32 numpy network
@@ -198,7 +198,7 @@ def main():
                 traffic = json.load(open(args.pmc_file)).get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
-        out["roofline"] = {"bound": "mfma", "kernel": "k_tower<15,DYN> (dynamics tower, 17 fused convs)",
+        out["roofline"] = {"bound": "mfma", "kernel": "k_tower3<15,DYN> (dynamics tower, 17 fused convs + head 1x1 convs)",
                            "achieved": achieved, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                            "frac": achieved / PEAK_BF16_TFLOPS, "traffic": traffic,
                            "launches": n_launch, "mean_launch_ms": ms, "rows_per_launch": rows,

@@ -11,7 +11,7 @@ for CTR in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $CTR --kernel-include-regex "k_tower" --output-format csv -d $OUT/pmc_$CTR -o pmc -- \
     python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > $OUT/pmc_$CTR.json 2> $OUT/pmc_$CTR.err || { echo "pmc $CTR failed"; exit 1; }
 done
-python3 tools/pmc_summary.py $OUT "k_tower<15, true" > $OUT/pmc_summary.txt && cat $OUT/pmc_summary.txt
+python3 tools/pmc_summary.py $OUT "k_tower3<15, true" > $OUT/pmc_summary.txt && cat $OUT/pmc_summary.txt
 cp $OUT/pmc_tower.json profiles/pmc_tower_latest.json 2>/dev/null
 timeout -k 10 600 python3 bench.py > $OUT/bench_default.json 2> $OUT/bench_default.err || { echo "bench failed"; tail $OUT/bench_default.err; exit 1; }
 cat $OUT/bench_default.json
