@@ -32,6 +32,7 @@ _SIGS = {
     "gmz_game_check_win": ([P, I, I, I, P, P, P], I),
     "gmz_game_board_state": ([P, I, I, P, P, P, P], I),
     "gmz_game_play": ([P, I, I, I, P, P, P, P, P, P], I),
+    "gmz_game_winning_scan": ([P, P, P, I, I, I, P, P, P, P], I),
     "gmz_engine_create": ([ctypes.POINTER(EngineCfg), ctypes.POINTER(P)], I),
     "gmz_engine_destroy": ([P], I),
     "gmz_engine_game_state": ([P, ctypes.POINTER(P), ctypes.POINTER(P), ctypes.POINTER(P), ctypes.POINTER(P)], I),

@@ -191,6 +191,11 @@ class BatchedSelfPlayEngine:
         self._last_reset = bool(reset_finished)
         return self.status
 
+    def winning_scan(self, boards, players, action=None, counters=None, stream=None):
+        """workers.py:49-123 find_winning_moves_rebuilt on the device for G positions (see
+        ``winning_scan``); ``counters`` = (missed_fives, missed_totals) int32[G] accumulated in place."""
+        return winning_scan(boards, players, action, self.cfg.N_IN_ROW, counters, stream, self.lib)
+
     def root_stats(self):
         G, A, dev = self.G, self.A, self.device
         visits = torch.zeros(G, A, dtype=torch.int32, device=dev)
@@ -201,3 +206,25 @@ class BatchedSelfPlayEngine:
         check(self.lib.gmz_engine_root_stats(self.handle, ptr(visits), ptr(rn), ptr(rw), ptr(mx), ptr(mn),
                                              self._stream()))
         return visits, rn, rw, mx, mn
+
+
+def winning_scan(boards, players, actions=None, n_in_row=5, counters=None, stream=None, lib=None):
+    """Batched workers.py:49-123 ``find_winning_moves_rebuilt`` (``gmz_game_winning_scan``).
+
+    boards int8[G,S,S] and players int8[G] (the player to move) on the device.  Without
+    ``actions``: returns uint8[G,S*S] cell classes (0 none, 1 five, 2 open_four, 3 combo).  With
+    ``actions`` int32[G] and ``counters`` = (missed_fives, missed_totals) int32[G] device tensors:
+    adds the workers.py:191-203 missed-win counts of this position (action < 0: game skipped)."""
+    L = lib if lib is not None else _lib.load()
+    b = torch.as_tensor(boards).contiguous()
+    G, S = b.shape[0], b.shape[-1]
+    p = torch.as_tensor(players, dtype=torch.int8).to(b.device).contiguous()
+    cls, mf, mt, a = None, None, None, None
+    if actions is None:
+        cls = torch.zeros(G, S * S, dtype=torch.uint8, device=b.device)
+    else:
+        a = torch.as_tensor(actions, dtype=torch.int32).to(b.device).contiguous()
+        mf, mt = counters
+    check(L.gmz_game_winning_scan(ptr(b), ptr(p), ptr(a), G, S, int(n_in_row), ptr(cls), ptr(mf), ptr(mt),
+                                  _lib.stream_ptr(stream)))
+    return cls

@@ -87,11 +87,14 @@ def gpu_selfplay_worker(worker_id, worker_mode, data_queue, log_status_queue, ui
     games = [_Game() for _ in range(G)]
     pool = ThreadPoolExecutor(max_workers=4)
     moves_done = 0
+    # missed-win counters of workers.py:191-203, accumulated on the device move by move by the batched
+    # find_winning_moves scan (gmz_game_winning_scan) instead of a Python scan per finished game
+    missed_f = torch.zeros(G, dtype=torch.int32, device=eng.device)
+    missed_t = torch.zeros(G, dtype=torch.int32, device=eng.device)
 
-    def finish_game(g, winner, move_count):
+    def finish_game(g, winner, move_count, mf, mt):
         record, slices = R.build_game_record(g.obs, g.actions, g.policies, g.values, g.boards, winner,
                                              c.DISCOUNT, c.N_STEPS, c.NUM_UNROLL_STEPS)
-        mf, mt = R.missed_wins(g.boards, g.actions, H)
         version = latest_model_step.value if latest_model_step is not None else 0
         if slices:
             data_queue.put((record, slices, version))
@@ -120,10 +123,15 @@ def gpu_selfplay_worker(worker_id, worker_mode, data_queue, log_status_queue, ui
                 pass
         b, p, lm, mc = eng.game_state()
         pol, val, act = eng.search()
+        eng.winning_scan(b, p, act, counters=(missed_f, missed_t))  # position before the move
         status = eng.play(reset_finished=True)
         torch.cuda.synchronize()
+        mf_all, mt_all = missed_f.cpu().numpy(), missed_t.cpu().numpy()
         b, p, lm, mc = b.cpu().numpy(), p.cpu().numpy(), lm.cpu().numpy(), mc.cpu().numpy()
         pol, val, act, status = pol.cpu().numpy(), val.cpu().numpy(), act.cpu().numpy(), status.cpu().numpy()
+        ended = torch.from_numpy((status != 2) & (status != 3)).to(eng.device)
+        missed_f.masked_fill_(ended, 0)
+        missed_t.masked_fill_(ended, 0)
         for i in range(G):
             a = int(act[i])
             if a < 0:  # workers.py:169-170 (no legal move)
@@ -140,7 +148,7 @@ def gpu_selfplay_worker(worker_id, worker_mode, data_queue, log_status_queue, ui
                 ui_queue.put(R.SelfPlayMove())
             st = int(status[i])
             if st != 2:
-                pool.submit(finish_game, gm, st, int(mc[i]) + 1)
+                pool.submit(finish_game, gm, st, int(mc[i]) + 1, int(mf_all[i]), int(mt_all[i]))
                 games[i] = _Game()
         moves_done += 1
         if max_moves is not None and moves_done >= max_moves:

@@ -55,6 +55,17 @@ int gmz_game_play(int8_t *boards_dev, int G, int size, int n_in_row, int8_t *pla
                   int32_t *last_moves_dev, int32_t *move_counts_dev, const int32_t *actions_dev,
                   int8_t *status_dev, void *stream);
 
+/* workers.py:49-123 find_winning_moves_rebuilt for the player to move (players_dev[g]) on every
+ * empty cell of G boards.  cls_dev (nullable) uint8[G][S*S]: 0 none, 1 'five', 2 'open_four',
+ * 3 'combo'.  With actions_dev (nullable) int32[G], the missed-win counters of workers.py:191-203
+ * are accumulated in place (+1 to missed_totals[g] when the winning set is non-empty and
+ * actions[g] is not in it, +1 to missed_fives[g] if additionally a 'five' exists); actions[g] < 0
+ * leaves game g untouched.  Replaces the per-position Python scan the reference runs for every move
+ * of every finished game. */
+int gmz_game_winning_scan(const int8_t *boards_dev, const int8_t *players_dev, const int32_t *actions_dev, int G,
+                          int size, int n_in_row, uint8_t *cls_dev, int32_t *missed_fives_dev,
+                          int32_t *missed_totals_dev, void *stream);
+
 /* ------------------------------------------------------------------ search engine */
 typedef struct gmz_engine gmz_engine;
 

@@ -114,3 +114,9 @@ def test_worker_emits_reference_messages(M):
         kinds.append(type(uq.get()).__name__)
     assert kinds.count("SelfPlayMove") >= 8 * 5 and kinds.count("GameCompletedNotice") == len(items)
     assert tq.qsize() == len(items) and lq.qsize() == len(items)
+    # SelfPlayStatus (move count, missed fives, missed totals) from the device scan == the host
+    # restatement of workers.py:191-203 (pinned to the reference by tests/test_records.py)
+    from datou_gomoku_muzero_amd import records as R
+    got = sorted((s.avg_len, s.miss_five, s.miss_total) for s in (lq.get() for _ in range(lq.qsize())))
+    want = sorted((len(r.actions),) + R.missed_wins(r.board_states, r.actions, 6) for r, _, _ in items)
+    assert got == want
