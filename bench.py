@@ -27,9 +27,14 @@ sys.path.insert(0, REPO)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-# algorithmic FLOP of one dynamics-tower row at 15x15 x 128 ch (network.py:81-83 + 1x1 heads):
-#   conv 144->128: 2*225*128*144*9 ; 16 ResBlock convs: 16*2*225*128*128*9 ; head 1x1 convs: 2*225*128*3
-TOWER_FLOP_PER_ROW = {15: 2 * 225 * 128 * 144 * 9 + 16 * 2 * 225 * 128 * 128 * 9 + 2 * 225 * 128 * 3}
+
+
+def tower_flop_per_row(size, blocks):
+    """Algorithmic FLOP of one dynamics-tower row (network.py:81-83 + the 1x1 head convs):
+    conv 144->128 (2*A*128*144*9) + 2*blocks ResBlock convs (2*A*128*128*9 each) + 2*A*128*3.
+    15x15, 8 blocks: 1,136,505,600."""
+    A = size * size
+    return 2 * A * 128 * 144 * 9 + 2 * blocks * 2 * A * 128 * 128 * 9 + 2 * A * 128 * 3
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, no sparsity)
 PEAK_HBM_GBS = 8000.0
 
@@ -190,19 +195,20 @@ def main():
     out = result_line(args, world, dt, waves, G)
     if timer is not None:
         n_launch, ms, rows = timer.summary()
-        flop = TOWER_FLOP_PER_ROW.get(args.size, 0) * rows
+        flop = tower_flop_per_row(args.size, args.blocks) * rows
         achieved = flop / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
         traffic = None
-        if os.path.exists(args.pmc_file):
+        if os.path.exists(args.pmc_file) and (args.size, args.blocks) == (15, 8):  # the PMC pass's config
             try:
                 traffic = json.load(open(args.pmc_file)).get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
-        out["roofline"] = {"bound": "mfma", "kernel": "k_tower3<15,DYN> (dynamics tower, 17 fused convs + head 1x1 convs)",
+        out["roofline"] = {"bound": "mfma", "kernel": "k_tower3<%d,DYN> (dynamics tower, %d fused convs + head 1x1 "
+                                                     "convs)" % (args.size, 1 + 2 * args.blocks),
                            "achieved": achieved, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                            "frac": achieved / PEAK_BF16_TFLOPS, "traffic": traffic,
                            "launches": n_launch, "mean_launch_ms": ms, "rows_per_launch": rows,
-                           "flop_per_row": TOWER_FLOP_PER_ROW.get(args.size, 0)}
+                           "flop_per_row": tower_flop_per_row(args.size, args.blocks)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.net == "hip":
         log("cpu baseline (bounded sample ~%.0f s)..." % args.cpu_baseline_sec)
         out["cpu_baseline"] = cpu_baseline(args, sd, cfg)

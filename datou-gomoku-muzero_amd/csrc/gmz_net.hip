@@ -44,6 +44,7 @@ struct TowerArgs {
   const float *head_w, *head_b;  // [3][128], [3]
   float *pv_feat;          // [rows][3][A]
   int rows;
+  uint16_t *xres;          // single-image boards (19x19): per-workgroup residual scratch (k_tower3)
 };
 
 __device__ __forceinline__ uint16_t f2bf(float f) {
@@ -393,9 +394,13 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
   static_assert(8 % NQ == 0, "channel groups");
   constexpr int PS = I::PS, RS = I::RS, IMG = I::BYTES;
   constexpr int KSTEPS = 36;  // 9 taps x 4 k-steps of 32 input channels
-  static_assert(2 * IMG + 2 * C * 4 + 9 * C * 4 <= 163840, "LDS budget");
-  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * IMG + 2 * C * 4 + 9 * C * 4];
-  float *sbias = (float *)(smem + 2 * IMG);   // [2][128] per-layer double buffer
+  // two images when they fit (15x15: 2 x 78 KB); otherwise (19x19: 119 KB) ONE image, an extra
+  // barrier per layer before the in-place epilogue, and the residual kept in a global scratch
+  constexpr bool ONE = 2 * IMG + 2 * C * 4 + 9 * C * 4 > 163840;
+  constexpr int NIMG = ONE ? 1 : 2;
+  static_assert(NIMG * IMG + 2 * C * 4 + 9 * C * 4 <= 163840, "LDS budget");
+  __shared__ __attribute__((aligned(16))) uint8_t smem[NIMG * IMG + 2 * C * 4 + 9 * C * 4];
+  float *sbias = (float *)(smem + NIMG * IMG);  // [2][128] per-layer double buffer
   float *saction = sbias + 2 * C;             // DYN: [9][128]
   uint8_t *img0 = smem;
 
@@ -434,7 +439,7 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
   };
 
   // ---- zero both images (borders and pads), biases of layer 0, action term
-  for (int i = tid; i < 2 * IMG / 16; i += NTHR) *(uint4 *)(smem + i * 16) = make_uint4(0, 0, 0, 0);
+  for (int i = tid; i < NIMG * IMG / 16; i += NTHR) *(uint4 *)(smem + i * 16) = make_uint4(0, 0, 0, 0);
   if (tid < C) sbias[tid] = t.bias[tid];
   if (DYN)
     for (int i = tid; i < 9 * C; i += NTHR) saction[i] = t.action_term[i];
@@ -451,6 +456,9 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
     pos[i] = (pt < NPT && p < A) ? (p / H) * RS + (p % H) * PS : -1;
   }
   f32x4 acc[NTW][PTW];
+  // ONE: this lane's residual tile values, [NTW][PTW][64 lanes] x 4 bf16 per wave (same lane writes
+  // and reads back: program order suffices)
+  u16x4 *xs = ONE ? (u16x4 *)t.xres + ((size_t)blockIdx.x * NW + w) * NTW * PTW * 64 + lane : nullptr;
   auto store_out = [&](uint8_t *img, int nt, int i, const u16x4 &o) {
     const int n0 = (nh * NTW + nt) * 16 + g4 * 4;
     *(u16x4 *)(img + pos[i] + RS + PS + n0 * 2) = o;
@@ -507,6 +515,7 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
         }
 #pragma unroll
         for (int nt = 0; nt < NTW; ++nt) acc[nt][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[nt], b, acc[nt][i], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);  // one tile's im2col loads at a time (VGPR budget)
       }
 #pragma unroll
       for (int nt = 0; nt < NTW; ++nt) {
@@ -518,6 +527,7 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) o[e] = f2bf(fmaxf(acc[nt][i][e] + t.stem_b[n0 + e], 0.f));
           store_out(img0, nt, i, o);
+          if constexpr (ONE) xs[(nt * PTW + i) * 64] = o;
         }
       }
     } else {
@@ -526,8 +536,8 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
     __syncthreads();
 
     for (int L = 0; L < t.n_layers; ++L, ++gl) {
-      const uint8_t *img = smem + (L & 1) * IMG;
-      uint8_t *nimg = smem + ((L + 1) & 1) * IMG;
+      const uint8_t *img = smem + (ONE ? 0 : (L & 1) * IMG);
+      uint8_t *nimg = smem + (ONE ? 0 : ((L + 1) & 1) * IMG);
       // the next layer's bias (for the last layer: the next board's layer 0) -> the other slot;
       // that slot was last read by the previous layer's epilogue, which the barrier has closed
       issue_bias(L + 1 < t.n_layers ? L + 1 : 0, (gl + 1) & 1);
@@ -570,13 +580,14 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
       // before any arithmetic, so the epilogue pays one LDS latency, not one per tile.
       const int kind = DYN ? (L == 0 ? 0 : ((L - 1) & 1) + 1) : ((L & 1) + 1);
       const float *bias = sbias + (gl & 1) * C;
+      if constexpr (ONE) __syncthreads();  // every wave is done reading the image it overwrites
       auto epilogue = [&](auto kind_c) {
         constexpr int KIND = decltype(kind_c)::value;
         f32x4 bv[NTW];
 #pragma unroll
         for (int nt = 0; nt < NTW; ++nt) bv[nt] = *(const f32x4 *)(bias + (nh * NTW + nt) * 16 + g4 * 4);
         u16x4 xr[NTW][PTW];
-        if constexpr (KIND == 2) {
+        if constexpr (KIND == 2 && !ONE) {
           // residual = this block's input, still in the image this epilogue overwrites, at the
           // very address this lane is about to store (read-then-write by the same lane)
 #pragma unroll
@@ -594,6 +605,10 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
 #pragma unroll
         for (int nt = 0; nt < NTW; ++nt) {
           const int n0 = (nh * NTW + nt) * 16 + g4 * 4;
+          if constexpr (KIND == 2 && ONE) {  // residual scratch, one n-tile at a time (VGPR budget)
+#pragma unroll
+            for (int i = 0; i < PTW; ++i) xr[nt][i] = xs[(nt * PTW + i) * 64];
+          }
 #pragma unroll
           for (int i = 0; i < PTW; ++i) {
             f32x4 v = acc[nt][i] + bv[nt];
@@ -610,7 +625,9 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
 #pragma unroll  // ReLU as med3(v, 0, FLT_MAX): one VALU, no NaN canonicalisation pair
             for (int e = 0; e < 4; ++e) o[e] = f2bf(__builtin_amdgcn_fmed3f(v[e], 0.f, 3.402823466e38f));
             if ((PG * i + PG) * 16 <= A || pos[i] >= 0) store_out(nimg, nt, i, o);
+            if constexpr (ONE && KIND != 1) xs[(nt * PTW + i) * 64] = o;  // the next block's input
           }
+          if constexpr (ONE) __builtin_amdgcn_sched_barrier(0);
         }
       };
       if (DYN && kind == 0) epilogue(std::integral_constant<int, 0>{});
@@ -626,10 +643,10 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
 
     // ---- next board's input -> the free image, overlapped with this board's output stage
     const int nr = next_row(r + gridDim.x);
-    if constexpr (DYN && !(ABL & 32)) {
+    if constexpr (DYN && !ONE && !(ABL & 32)) {
       if (nr < t.rows) issue_input(nr);  // DYN has 1 + 2*blocks (odd) layers: the result is in img[1]
     }
-    const uint8_t *fin = smem + (t.n_layers & 1) * IMG;
+    const uint8_t *fin = smem + (ONE ? 0 : (t.n_layers & 1) * IMG);
     if (!(ABL & 32)) {
       uint4 *dst = (uint4 *)(t.pool + (size_t)os * A * C);
       for (int i = tid; i < A * 16; i += NTHR) dst[i] = *(const uint4 *)(fin + cell(i >> 4) + (i & 15) * 16);
@@ -652,6 +669,9 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
       }
     }
     __syncthreads();  // the next board's layer 0 overwrites img[1]
+    if constexpr (DYN && ONE && !(ABL & 32)) {
+      if (nr < t.rows) issue_input(nr);  // single image: only now is it free
+    }
     r = nr;
   }
   if ((ABL & 128) && lane == 0) {  // diagnostic build only: per-wave phase cycles -> pv_feat
@@ -772,8 +792,8 @@ __global__ void __launch_bounds__(HEAD_THREADS) k_heads(HeadArgs h) {
     }
   }
   __syncthreads();
-  if (tid < 2 * A) {  // policy_fc (network.py:70), k-half kh of the 2A features
-    const int kh = tid >= A, a = tid - kh * A;
+  for (int ti = tid; ti < 2 * A; ti += HEAD_THREADS) {  // policy_fc (network.py:70), k-half kh of the 2A features
+    const int kh = ti >= A, a = ti - kh * A;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     const float *wcol = h.pfc_w + a;
     int k = kh * A;
@@ -789,13 +809,14 @@ __global__ void __launch_bounds__(HEAD_THREADS) k_heads(HeadArgs h) {
     *(f32x4 *)(ppart + 4 * (kh * A + a)) = acc;
   }
   __syncthreads();
-  if (tid < A) {
-    const float b = h.pfc_b[tid];
-    const f32x4 p0 = *(const f32x4 *)(ppart + 4 * tid), p1 = *(const f32x4 *)(ppart + 4 * (A + tid));
+  for (int a = tid; a < A; a += HEAD_THREADS) {
+    const float b = h.pfc_b[a];
+    const f32x4 p0 = *(const f32x4 *)(ppart + 4 * a), p1 = *(const f32x4 *)(ppart + 4 * (A + a));
 #pragma unroll
     for (int i = 0; i < HEAD_ROWS; ++i)
-      if (valid[i]) h.logits[(size_t)(r0 + i) * A + tid] = (b + p0[i]) + p1[i];
-  } else if (tid >= 256) {  // value_fc1 (network.py:72), k-quarter q
+      if (valid[i]) h.logits[(size_t)(r0 + i) * A + a] = (b + p0[i]) + p1[i];
+  }
+  if (tid >= 256) {  // value_fc1 (network.py:72), k-quarter q
     const int q = (tid - 256) >> 6, j = tid & 63;
     if (j < hd) {
       const int p0 = q * A / 4, p1 = (q + 1) * A / 4;
@@ -851,13 +872,37 @@ static int cu_count() {
   return n[dev];
 }
 
+// wave decomposition per board size.  Default: 12 waves = 4 channel quarters x 3 position groups
+// (15 tiles of 16 positions at 15x15: no idle tile, 3 waves per SIMD; RD 3 keeps it within 168
+// VGPRs).  19x19 (single LDS image, 23 tiles): 8 waves = 2 channel halves x 4 position groups.
+template <int H> struct TowerCfg { static constexpr int NQ = 4, PG = 3, RD = 3; };
+template <> struct TowerCfg<19> { static constexpr int NQ = 2, PG = 4, RD = 2; };
+
+// bytes of k_tower3's per-workgroup residual scratch (single-image boards only)
+template <int H>
+static constexpr size_t tower_xres_bytes() {
+  using T = TowerCfg<H>;
+  constexpr bool one = 2 * Img3<H>::BYTES + 2 * C * 4 + 9 * C * 4 > 163840;
+  constexpr int npt = (H * H + 15) / 16, ptw = (npt + T::PG - 1) / T::PG;
+  return one ? (size_t)T::NQ * T::PG * (8 / T::NQ) * ptw * 64 * 8 : 0;
+}
+static size_t xres_bytes(int H) {
+  switch (H) {
+    case 6: return tower_xres_bytes<6>();
+    case 9: return tower_xres_bytes<9>();
+    case 15: return tower_xres_bytes<15>();
+    case 19: return tower_xres_bytes<19>();
+    default: return 0;
+  }
+}
+
 template <int H, bool DYN>
 static int launch_tower(const TowerArgs &a, hipStream_t s) {
   if (a.rows <= 0) return 0;
+  using T = TowerCfg<H>;
+  if (tower_xres_bytes<H>() && !a.xres) return fail("gmz_net: missing residual scratch");
   const int grid = a.rows < cu_count() ? a.rows : cu_count();
-  // 12 waves = 4 channel quarters x 3 position groups (15 tiles of 16 positions at 15x15: no idle
-  // tile, 3 waves per SIMD); RD 3 keeps it within 168 VGPRs
-  hipLaunchKernelGGL((k_tower3<H, DYN, 0, 3, 4, 3>), dim3(grid), dim3(768), 0, s, a);
+  hipLaunchKernelGGL((k_tower3<H, DYN, 0, T::RD, T::NQ, T::PG>), dim3(grid), dim3(64 * T::NQ * T::PG), 0, s, a);
   GMZ_LAUNCH_CHECK();
   return 0;
 }
@@ -867,7 +912,8 @@ static int tower(int H, bool dyn, const TowerArgs &a, hipStream_t s) {
     case 6: return dyn ? launch_tower<6, true>(a, s) : launch_tower<6, false>(a, s);
     case 9: return dyn ? launch_tower<9, true>(a, s) : launch_tower<9, false>(a, s);
     case 15: return dyn ? launch_tower<15, true>(a, s) : launch_tower<15, false>(a, s);
-    default: return fail("gmz_net: board_size must be one of 6, 9, 15");
+    case 19: return dyn ? launch_tower<19, true>(a, s) : launch_tower<19, false>(a, s);
+    default: return fail("gmz_net: board_size must be one of 6, 9, 15, 19");
   }
 }
 
@@ -876,15 +922,25 @@ static int tower(int H, bool dyn, const TowerArgs &a, hipStream_t s) {
 // k_heads)
 static constexpr int KSPLIT = 32;
 
+// workspace: [pv_feat rows*3*A f32][reward partials KSPLIT*rows*64 f32][residual scratch (19x19)]
+static size_t ws_head_bytes(int A, int rows) {
+  return (size_t)rows * 3 * A * sizeof(float) + (size_t)KSPLIT * rows * 64 * sizeof(float);
+}
 static size_t ws_bytes(int A, int rows) {
-  return (size_t)rows * 3 * A * sizeof(float) + (size_t)KSPLIT * rows * 64 * sizeof(float) + 256;
+  int H = 0;
+  while (H * H < A) ++H;
+  return ws_head_bytes(A, rows) + (size_t)cu_count() * xres_bytes(H) + 256;
+}
+static uint16_t *ws_xres(void *workspace, int A, int rows) {
+  return (uint16_t *)((uint8_t *)workspace + ws_head_bytes(A, rows));
 }
 
 static int check_w(const gmz_net_weights *w) {
   if (!w) return fail("gmz_net: null weights");
   if (w->channels != C) return fail("gmz_net: channels must be 128");
   if (w->head_hidden != 64) return fail("gmz_net: head_hidden must be 64");
-  if (w->board_size != 6 && w->board_size != 9 && w->board_size != 15) return fail("gmz_net: board_size must be 6, 9 or 15");
+  if (w->board_size != 6 && w->board_size != 9 && w->board_size != 15 && w->board_size != 19)
+    return fail("gmz_net: board_size must be 6, 9, 15 or 19");
   return 0;
 }
 
@@ -914,7 +970,7 @@ GMZ_EXPORT int gmz_net_initial(const gmz_net_weights *w, const float *obs, int r
   hipStream_t s = (hipStream_t)stream;
   float *pv = (float *)workspace;
   TowerArgs a{w->repr_convs, w->repr_bias, 2 * w->blocks, w->repr_stem_w, w->repr_stem_b, nullptr, obs, pool,
-              nullptr, nullptr, out_slot, w->head_conv_w, w->head_conv_b, pv, rows};
+              nullptr, nullptr, out_slot, w->head_conv_w, w->head_conv_b, pv, rows, ws_xres(workspace, A, rows)};
   if (tower(H, false, a, s)) return -1;
   (void)A;
   return heads(w, pv, out_slot, rows, nullptr, logits, value, nullptr, s);
@@ -925,8 +981,10 @@ GMZ_EXPORT int gmz_net_recurrent_tower(const gmz_net_weights *w, uint16_t *pool,
                                        void *stream) {
   if (check_w(w)) return -1;
   if (rows <= 0 || !pool || !in_slot || !action || !out_slot || !workspace) return fail("gmz_net_recurrent_tower: bad argument");
+  const int A = w->board_size * w->board_size;
   TowerArgs a{w->dyn_convs, w->dyn_bias, 1 + 2 * w->blocks, nullptr, nullptr, w->dyn_action, nullptr, pool,
-              in_slot, action, out_slot, w->head_conv_w, w->head_conv_b, (float *)workspace, rows};
+              in_slot, action, out_slot, w->head_conv_w, w->head_conv_b, (float *)workspace, rows,
+              ws_xres(workspace, A, rows)};
   return tower(w->board_size, true, a, (hipStream_t)stream);
 }
 

@@ -189,8 +189,8 @@ class GomokuNetHip:
     def __init__(self, state_dict, cfg=None, num_slots=1, max_rows=1, device="cuda", **overrides):
         self.cfg = from_any(cfg, **overrides)
         c = self.cfg
-        if c.NUM_FILTERS != C or c.HEAD_HIDDEN_DIM != 64 or c.BOARD_SIZE not in (6, 9, 15):
-            raise ValueError("GomokuNetHip: kernels support NUM_FILTERS=128, HEAD_HIDDEN_DIM=64, BOARD_SIZE 6/9/15")
+        if c.NUM_FILTERS != C or c.HEAD_HIDDEN_DIM != 64 or c.BOARD_SIZE not in (6, 9, 15, 19):
+            raise ValueError("GomokuNetHip: kernels support NUM_FILTERS=128, HEAD_HIDDEN_DIM=64, BOARD_SIZE 6/9/15/19")
         self.device = torch.device(device)
         self.A = c.ACTION_SPACE_SIZE
         self.lib = _lib.load()

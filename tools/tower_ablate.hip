@@ -74,7 +74,7 @@ int main(int argc, char **argv) {
     printf("tower3 vs tower: hidden mismatches %zu / %zu, pv mismatches %zu / %zu\n", dh, o1.size(), dp, p1.size());
     CK(hipMemset(dpool + (size_t)rows * A * 128, 0, o1.size() * 2));
     CK(hipMemset(dpv, 0, p1.size() * 4));
-    hipLaunchKernelGGL((k_tower3<15, true, 0, 4, 4, 3>), dim3(256), dim3(768), 0, 0, a);
+    hipLaunchKernelGGL((k_tower3<15, true, 0, 3, 4, 3>), dim3(256), dim3(768), 0, 0, a);
     CK(hipMemcpy(o2.data(), dpool + (size_t)rows * A * 128, o2.size() * 2, hipMemcpyDeviceToHost));
     CK(hipMemcpy(p2.data(), dpv, p2.size() * 4, hipMemcpyDeviceToHost));
     dh = dp = 0;
@@ -82,27 +82,29 @@ int main(int argc, char **argv) {
     for (size_t i = 0; i < p1.size(); ++i) dp += p1[i] != p2[i];
     printf("tower3 12w vs tower: hidden mismatches %zu / %zu, pv mismatches %zu / %zu\n", dh, o1.size(), dp, p1.size());
   }
-  const char *names[] = {"k_tower (LDS-staged weights)", "k_tower3", "k_tower3 no-io(32)", "k_tower3 A-from-one-kstep(1)",
-                         "k_tower3 no-A-loads(2)", "k_tower3 RD3", "k_tower3 12 waves (4x3)", "k_tower3 12w RD3", "k_tower3 12w no-io", "k_tower3 16w (4x4) RD3", "k_tower3 16w (4x4) RD2", "k_tower3 16w (8x2) RD3"};
-  const int NV = 12;
+  const char *names[] = {"k_tower (LDS-staged weights)", "k_tower3 8w (2x4) RD4", "k_tower3 12w (4x3) RD3 [product]",
+                         "k_tower3 12w no-io(32)", "k_tower3 12w A-from-one-kstep(1)", "k_tower3 12w no-A-loads(2)"};
+  const int NV = 6;
   float best[NV];
   for (int i = 0; i < NV; ++i) best[i] = 1e9f;
   for (int round = 0; round < 5; ++round) {
-    float t[NV] = {run<0>(a, 5), run<0, 3>(a, 5), run<32, 3>(a, 5), run<1, 3>(a, 5), run<2, 3>(a, 5), run<0, 3, 3>(a, 5), run<0, 3, 4, 4, 3>(a, 5), run<0, 3, 3, 4, 3>(a, 5), run<32, 3, 4, 4, 3>(a, 5), run<0, 3, 3, 4, 4>(a, 5), run<0, 3, 2, 4, 4>(a, 5), run<0, 3, 3, 8, 2>(a, 5)};
+    float t[NV] = {run<0>(a, 5), run<0, 3>(a, 5), run<0, 3, 3, 4, 3>(a, 5), run<32, 3, 3, 4, 3>(a, 5), run<1, 3, 3, 4, 3>(a, 5),
+                   run<2, 3, 3, 4, 3>(a, 5)};
     for (int i = 0; i < NV; ++i) best[i] = t[i] < best[i] ? t[i] : best[i];
   }
   for (int i = 0; i < NV; ++i)
     printf("%-36s %8.3f ms   %7.1f TFLOP/s\n", names[i], best[i], flop / (best[i] * 1e-3) / 1e12);
-  {  // phase stamps of k_tower3 (diagnostic build, ABL 128|32: no IO, stamps into pv_feat)
-    for (int k = 0; k < 3; ++k) run<128 | 32, 3>(a, 5);
-    std::vector<float> st(256 * 8 * 4);
+  {  // phase stamps of the product k_tower3 (12 waves; diagnostic build, ABL 128|32: no IO, stamps into pv_feat)
+    constexpr int NWV = 12;
+    for (int k = 0; k < 3; ++k) run<128 | 32, 3, 3, 4, 3>(a, 5);
+    std::vector<float> st(256 * NWV * 4);
     CK(hipMemcpy(st.data(), dpv, st.size() * 4, hipMemcpyDeviceToHost));
     double sum[4] = {0, 0, 0, 0};
-    for (int i = 0; i < 256 * 8; ++i)
+    for (int i = 0; i < 256 * NWV; ++i)
       for (int k = 0; k < 4; ++k) sum[k] += st[i * 4 + k];
-    const double per = 2048.0 * 17 * ((rows + 255) / 256);
-    printf("k_tower3 per layer and wave (s_memtime cycles): k-loop %.0f  epilogue %.0f  barrier %.0f  (whole kernel %.0f)\n",
-           sum[0] / per, sum[1] / per, sum[2] / per, sum[3] / 2048);
+    const double per = 256.0 * NWV * 17 * ((rows + 255) / 256);
+    printf("k_tower3 (12w) per layer and wave (s_memtime cycles): k-loop %.0f  epilogue %.0f  barrier %.0f  (whole kernel %.0f)\n",
+           sum[0] / per, sum[1] / per, sum[2] / per, sum[3] / (256 * NWV));
   }
   CK(hipDeviceSynchronize());
   return 0;
