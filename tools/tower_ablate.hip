@@ -55,7 +55,9 @@ int main(int argc, char **argv) {
   CK(hipMemcpy(din, in_slot.data(), rows * 4, hipMemcpyHostToDevice));
   CK(hipMemcpy(dout, out_slot.data(), rows * 4, hipMemcpyHostToDevice));
   CK(hipMemcpy(dac, action.data(), rows * 4, hipMemcpyHostToDevice));
-  TowerArgs a{dw, dbias, L, nullptr, nullptr, dact, nullptr, dpool, din, dac, dout, dhw, dhb, dpv, rows};
+  uint16_t *dxres;  // residual scratch of single-image variants: 512 workgroups x up to 128 KB
+  CK(hipMalloc(&dxres, (size_t)512 * 131072));
+  TowerArgs a{dw, dbias, L, nullptr, nullptr, dact, nullptr, dpool, din, dac, dout, dhw, dhb, dpv, rows, dxres};
   const double flop = 1136505600.0 * rows;
   {  // k_tower3 must reproduce k_tower (LDS-staged weights, rotated image) bit for bit
     std::vector<uint16_t> o1((size_t)rows * A * 128), o2(o1.size());
@@ -94,7 +96,23 @@ int main(int argc, char **argv) {
   }
   for (int i = 0; i < NV; ++i)
     printf("%-36s %8.3f ms   %7.1f TFLOP/s\n", names[i], best[i], flop / (best[i] * 1e-3) / 1e12);
-  {  // phase stamps of the product k_tower3 (12 waves; diagnostic build, ABL 128|32: no IO, stamps into pv_feat)
+  auto stamps = [&](const char *what, float ms_per_launch, auto launch) -> int {
+    constexpr int NWV = 12;
+    for (int k = 0; k < 3; ++k) launch();
+    std::vector<float> st(256 * NWV * 4);
+    CK(hipMemcpy(st.data(), dpv, st.size() * 4, hipMemcpyDeviceToHost));
+    double sum[4] = {0, 0, 0, 0};
+    for (int i = 0; i < 256 * NWV; ++i)
+      for (int k = 0; k < 4; ++k) sum[k] += st[i * 4 + k];
+    const double per = 256.0 * NWV * 17 * ((rows + 255) / 256);
+    printf("%s: per layer and wave (cycles) k-loop %.0f  epilogue %.0f  barrier %.0f; kernel %.0f cycles in %.3f ms -> %.2f GHz\n",
+           what, sum[0] / per, sum[1] / per, sum[2] / per, sum[3] / (256 * NWV), ms_per_launch,
+           sum[3] / (256 * NWV) / (ms_per_launch * 1e-3) / 1e9);
+    return 0;
+  };
+  stamps("product (no io)", run<128 | 32, 3, 3, 4, 3>(a, 5), [&] { run<128 | 32, 3, 3, 4, 3>(a, 1); });
+  stamps("no-A-loads (no io)", run<128 | 32 | 2, 3, 3, 4, 3>(a, 5), [&] { run<128 | 32 | 2, 3, 3, 4, 3>(a, 1); });
+  if (0) {
     constexpr int NWV = 12;
     for (int k = 0; k < 3; ++k) run<128 | 32, 3, 3, 4, 3>(a, 5);
     std::vector<float> st(256 * NWV * 4);
