@@ -78,22 +78,35 @@ __device__ __forceinline__ Edge *edge_row_w(const Dev &D, int g, int u) {
 template <int NJ>
 __device__ __forceinline__ void row_load(const Dev &D, const Edge *row, int lane, int (&n)[NJ], float (&q)[NJ],
                                          int *child = nullptr) {
+  // every slot's 16-B edge is loaded unconditionally (index clamped) before any use, so one row
+  // costs ONE memory round trip, not one per slot and field
+  int4 e[NJ];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int a = lane + WAVE * j;
-    n[j] = 0;
+    e[j] = *(const int4 *)(row + (a < D.A ? a : D.A - 1));
+  }
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const bool ok = lane + WAVE * j < D.A;
+    n[j] = ok ? e[j].y : 0;
     q[j] = 0.f;
-    if (child) child[j] = -1;
-    if (a < D.A) {
-      const Edge e = row[a];
-      n[j] = e.n;
-      if (child) child[j] = e.child;
-      if (e.n > 0) {
-        const float v = e.w / (float)e.n;
-        const float dv = D.disc_f * v;
-        q[j] = e.r + dv;
-      }
+    if (child) child[j] = ok ? e[j].x : -1;
+    if (ok && n[j] > 0) {
+      const float v = __int_as_float(e[j].z) / (float)n[j];
+      const float dv = D.disc_f * v;
+      q[j] = __int_as_float(e[j].w) + dv;
     }
+  }
+}
+
+// node logits of the lane's action slots (index clamped, unconditional loads)
+template <int NJ>
+__device__ __forceinline__ void logits_load(const Dev &D, const float *logit_row, int lane, float (&lv)[NJ]) {
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int a = lane + WAVE * j;
+    lv[j] = logit_row[a < D.A ? a : D.A - 1];
   }
 }
 
@@ -162,7 +175,7 @@ __device__ int transformed_q(const Dev &D, int lane, const int (&n)[NJ], const f
 // _get_improved_policy (mcts.py:151-156): softmax over the root legal set of logits + transformed Q.
 // lg[j] = legal-move bitmask word j (bit = lane), wave-uniform.
 template <int NJ>
-__device__ void improved_policy(const Dev &D, const uint64_t (&lg)[NJ], int lane, const float *logit_row,
+__device__ void improved_policy(const Dev &D, const uint64_t (&lg)[NJ], int lane, const float (&lv)[NJ],
                                 const int (&n)[NJ], const float (&q)[NJ], float mm_max, float mm_min, double (&p)[NJ],
                                 int &max_n) {
   double t64[NJ];
@@ -174,7 +187,7 @@ __device__ void improved_policy(const Dev &D, const uint64_t (&lg)[NJ], int lane
     for (int j = 0; j < NJ; ++j) {
       const int a = lane + WAVE * j;
       const bool ok = a < D.A && ((lg[j] >> lane) & 1ull);
-      x[j] = ok ? (double)logit_row[a] + t64[j] : -INFINITY;
+      x[j] = ok ? (double)lv[j] + t64[j] : -INFINITY;
       m = fmax(m, x[j]);
     }
     m = dred_max_d(m);
@@ -194,7 +207,7 @@ __device__ void improved_policy(const Dev &D, const uint64_t (&lg)[NJ], int lane
     for (int j = 0; j < NJ; ++j) {
       const int a = lane + WAVE * j;
       const bool ok = a < D.A && ((lg[j] >> lane) & 1ull);
-      x[j] = ok ? logit_row[a] + t32[j] : -INFINITY;
+      x[j] = ok ? lv[j] + t32[j] : -INFINITY;
       m = fmaxf(m, x[j]);
     }
     m = dred_max_f(m);
@@ -235,9 +248,11 @@ __device__ int select_nonroot(const Dev &D, const uint64_t (&lg)[NJ], int g, int
   int n[NJ], ch[NJ];
   float q[NJ];
   double p[NJ];
+  float lv[NJ];
+  logits_load<NJ>(D, D.logits + ((size_t)g * D.S + u) * D.A, lane, lv);  // in flight with the edge row
   row_load<NJ>(D, edge_row(D, g, u), lane, n, q, ch);
   int max_n;
-  improved_policy<NJ>(D, lg, lane, D.logits + ((size_t)g * D.S + u) * D.A, n, q, mm_max, mm_min, p, max_n);
+  improved_policy<NJ>(D, lg, lane, lv, n, q, mm_max, mm_min, p, max_n);
   int tot = 0;
 #pragma unroll
   for (int j = 0; j < NJ; ++j) tot += n[j];
@@ -679,8 +694,10 @@ __global__ void __launch_bounds__(256) k_finish(Dev D, double *__restrict__ poli
   int max_n;
   uint64_t lg[NJ];
   load_legal<NJ>(D, g, lg);
+  float lv[NJ];
+  logits_load<NJ>(D, D.logits + (size_t)g * D.S * A, lane, lv);
   row_load<NJ>(D, edge_row(D, g, 0), lane, n, q);
-  improved_policy<NJ>(D, lg, lane, D.logits + (size_t)g * D.S * A, n, q, st.mm_max, st.mm_min, p, max_n);
+  improved_policy<NJ>(D, lg, lane, lv, n, q, st.mm_max, st.mm_min, p, max_n);
   const int16_t *rk = D.set_rank + (size_t)g * A;
   int bn = -1, br = 1 << 20, ba = -1;
 #pragma unroll
