@@ -2,6 +2,7 @@
 
     engine = HipMuZeroMCTS(worker_id, request_queue, result_queue)
     policy, value, action = engine.search(game)
+    policies, values, actions = engine.search_batch(games)      # G games in one batched search
 
 The tree search (select / expand / backup / sequential halving / decision) runs in the HIP kernels
 of csrc/gmz_tree.hip on a one-game ``BatchedSelfPlayEngine``; the network is reached through the
@@ -85,7 +86,7 @@ class _HipGumbelMCTS:
         self._engine = None
         self._key = None
 
-    def _get_engine(self):
+    def _get_engine(self, G=1):
         if self._cfg_src is None:
             try:  # the reference's global config singleton, read at call time like mcts.py does
                 from config import config as ref_config  # noqa: WPS433
@@ -95,10 +96,10 @@ class _HipGumbelMCTS:
         else:
             src = self._cfg_src
         cfg = from_any(src, MCTS_IMPLEMENTATION=self.MODE)
-        key = tuple(sorted(cfg.as_dict().items()))
+        key = (G,) + tuple(sorted(cfg.as_dict().items()))
         if self._engine is None or key != self._key:
             net = _QueueNet(self)
-            self._engine = BatchedSelfPlayEngine(cfg, num_games=1, net=net, device=self._device)
+            self._engine = BatchedSelfPlayEngine(cfg, num_games=G, net=net, device=self._device)
             self._net = net
             self._key = key
         return self._engine
@@ -126,6 +127,38 @@ class _HipGumbelMCTS:
         if a < 0:
             return np.zeros(A), 0.0, -1
         return pol[0].cpu().numpy().astype(np.float64), np.float32(val[0].item()), a
+
+
+    def search_batch(self, games):
+        """G games in one batched search -> (policy f64[G,A], value f32[G], action int32[G]).
+
+        Same results as ``[self.search(g) for g in games]`` from the same global RandomState (the
+        Gumbel noise is drawn game after game, mcts.py:312); the network requests still go through
+        the queue protocol, row by row.  An inference timeout returns zeros/0/-1 for every game."""
+        try:
+            while True:
+                self.result_queue.get_nowait()
+        except Empty:
+            pass
+        G = len(games)
+        eng = self._get_engine(G)
+        self._net.hidden.clear()
+        A, S = eng.A, eng.size
+        boards = np.stack([np.asarray(g.board, dtype=np.int8).reshape(-1) for g in games])
+        lms = [-1 if g.last_move is None else int(g.last_move[0]) * S + int(g.last_move[1]) for g in games]
+        mcs = [getattr(g, "move_count", int((b != 0).sum())) for g, b in zip(games, boards)]
+        eng.set_positions(boards, [g.current_player for g in games], lms, mcs)
+        gumbel = np.random.gumbel(0, 1, (G, A))
+        try:
+            pol, val, act = eng.search(gumbel=gumbel)
+        except Empty:
+            self.logger.warning("Worker %s timed out on inference." % self.worker_id)
+            return np.zeros((G, A)), np.zeros(G, np.float32), np.full(G, -1, np.int32)
+        torch.cuda.synchronize()
+        pol, val, act = pol.cpu().numpy().astype(np.float64), val.cpu().numpy().astype(np.float32), act.cpu().numpy()
+        bad = act < 0
+        pol[bad], val[bad] = 0.0, 0.0
+        return pol, val, act.astype(np.int32)
 
 
 class HipMuZeroMCTS(_HipGumbelMCTS):

@@ -120,3 +120,30 @@ def test_worker_emits_reference_messages(M):
     got = sorted((s.avg_len, s.miss_five, s.miss_total) for s in (lq.get() for _ in range(lq.qsize())))
     want = sorted((len(r.actions),) + R.missed_wins(r.board_states, r.actions, 6) for r, _, _ in items)
     assert got == want
+
+
+@pytest.mark.parametrize("fname", ["mcts_mz15_400.npz", "mcts_az9_50.npz", "mcts_mz9_50.npz"])
+def test_search_batch_equals_per_game_search(M, golden, fname):
+    """search_batch(games) == [search(g) for g in games] from the same RandomState."""
+    mcts, GmzConfig = M
+    d = golden(fname)
+    size, mode, sims = int(d["size"]), str(d["mode"]), int(d["sims"])
+    cfg = GmzConfig(BOARD_SIZE=size, NUM_SIMULATIONS=sims, MCTS_IMPLEMENTATION=mode)
+    games = []
+    for i in range(len(d["action"])):
+        lm = int(d["lastmove"][i])
+        games.append(Game(d["board"][i].reshape(size, size), d["player"][i], None if lm < 0 else (lm // size, lm % size)))
+    q1 = ServerQueue(size * size)
+    e1 = mcts.make_engine(0, q1, q1, cfg=cfg)
+    np.random.seed(int(d["seed"]))
+    seq = [e1.search(g) for g in games]
+    q2 = ServerQueue(size * size)
+    e2 = mcts.make_engine(0, q2, q2, cfg=cfg)
+    np.random.seed(int(d["seed"]))
+    pol, val, act = e2.search_batch(games)
+    assert pol.shape == (len(games), size * size) and pol.dtype == np.float64
+    for i, (p, v, a) in enumerate(seq):
+        assert act[i] == a and val[i] == v
+        assert np.abs(pol[i] - p).max() <= 1e-12
+    # and the reference's own outputs
+    assert act.tolist() == d["action"].tolist()
