@@ -48,6 +48,7 @@ _SIGS = {
     "gmz_engine_play": ([P, P, P, I, P], I),
     "gmz_engine_root_stats": ([P, P, P, P, P, P, P], I),
     "gmz_engine_wave_k": ([P, P, P], I),
+    "gmz_engine_wave_depth": ([P, P, P], I),
     "gmz_hashnet_initial": ([P, I, I, P, P, P, P, P], I),
     "gmz_hashnet_recurrent": ([P, P, P, P, I, I, P, P, P, P], I),
 }

@@ -750,6 +750,13 @@ __global__ void k_wave_k(Dev D, int32_t *k) {
   k[g] = st.active ? st.k : 0;
 }
 
+__global__ void k_wave_depth(Dev D, int32_t *depth) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= D.G) return;
+  const GameState st = D.gs[g];
+  depth[g] = st.active ? st.depth : 0;
+}
+
 __global__ void k_root_stats(Dev D, int32_t *visits, int32_t *root_n, float *root_w, float *mm_max, float *mm_min) {
   const int g = blockIdx.y;
   const Edge *row = edge_row(D, g, 0);
@@ -988,6 +995,13 @@ GMZ_EXPORT int gmz_engine_play(gmz_engine *e, const int32_t *action, int8_t *sta
 GMZ_EXPORT int gmz_engine_wave_k(gmz_engine *e, int32_t *k_dev, void *stream) {
   if (!e || !k_dev) return fail("gmz_engine_wave_k: null argument");
   hipLaunchKernelGGL(k_wave_k, dim3((e->D.G + 255) / 256), dim3(256), 0, (hipStream_t)stream, e->D, k_dev);
+  GMZ_LAUNCH_CHECK();
+  return 0;
+}
+
+GMZ_EXPORT int gmz_engine_wave_depth(gmz_engine *e, int32_t *depth_dev, void *stream) {
+  if (!e || !depth_dev) return fail("gmz_engine_wave_depth: null argument");
+  hipLaunchKernelGGL(k_wave_depth, dim3((e->D.G + 255) / 256), dim3(256), 0, (hipStream_t)stream, e->D, depth_dev);
   GMZ_LAUNCH_CHECK();
   return 0;
 }

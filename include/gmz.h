@@ -138,6 +138,10 @@ int gmz_engine_play(gmz_engine *e, const int32_t *action_dev, int8_t *status_dev
  * for MuZero (mcts.py:326), 1 for AlphaZero, 0 for games whose search is finished.  Used by the
  * single-game adapters to send the reference's k-row 'recurrent_batch' requests. */
 int gmz_engine_wave_k(gmz_engine *e, int32_t *k_dev, void *stream);
+/* Tree levels walked by the wave just selected, per game (path length incl. the root level; 0 for
+ * games whose search is finished): the input of the tree kernels' algorithmic-byte count
+ * (tools/tree_microbench.py). */
+int gmz_engine_wave_depth(gmz_engine *e, int32_t *depth_dev, void *stream);
 /* Diagnostics (device pointers into engine pools, for tests): root child visit counts
  * int32[G][A], root (N, W) and MinMaxStats (max, min) per game. */
 int gmz_engine_root_stats(gmz_engine *e, int32_t *visits_dev, int32_t *root_n_dev, float *root_w_dev,
