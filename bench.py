@@ -156,6 +156,9 @@ def main():
                     NUM_RES_BLOCKS=args.blocks)
     G = args.games
     sd = W.synthetic_state_dict(cfg, seed=args.seed, with_projection=False)
+    if dist is not None:  # the self-play tier's one exchange: rank 0's weights -> all ranks (RCCL)
+        from datou_gomoku_muzero_amd.weight_sync import broadcast_state_dict
+        sd = {k: v.cpu().numpy() for k, v in broadcast_state_dict(sd, src=0).items()}
     slots = G * (cfg.NUM_SIMULATIONS + 2)
     if args.net == "hip":
         net = N.GomokuNetHip(sd, cfg, num_slots=slots, max_rows=G)
