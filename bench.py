@@ -144,8 +144,10 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", init_method="env://")
+        # GMZ_DIST_BACKEND=gloo rehearses the N>1 path with several ranks sharing one GPU
+        backend = os.environ.get("GMZ_DIST_BACKEND", "nccl")
+        torch.cuda.set_device(local % torch.cuda.device_count())
+        dist.init_process_group(backend, init_method="env://")
     else:
         torch.cuda.set_device(0)
     import datou_gomoku_muzero_amd.engine as E
@@ -158,7 +160,8 @@ def main():
     sd = W.synthetic_state_dict(cfg, seed=args.seed, with_projection=False)
     if dist is not None:  # the self-play tier's one exchange: rank 0's weights -> all ranks (RCCL)
         from datou_gomoku_muzero_amd.weight_sync import broadcast_state_dict
-        sd = {k: v.cpu().numpy() for k, v in broadcast_state_dict(sd, src=0).items()}
+        dev = "cuda" if os.environ.get("GMZ_DIST_BACKEND", "nccl") == "nccl" else "cpu"
+        sd = {k: v.cpu().numpy() for k, v in broadcast_state_dict(sd, src=0, device=dev).items()}
     slots = G * (cfg.NUM_SIMULATIONS + 2)
     if args.net == "hip":
         net = N.GomokuNetHip(sd, cfg, num_slots=slots, max_rows=G)
@@ -194,7 +197,7 @@ def main():
     if dist:
         dist.barrier()
     dt = time.perf_counter() - t0
-    dt = collective_max(dt, dist)
+    dt = collective_max(dt, dist, os.environ.get("GMZ_DIST_BACKEND", "nccl"))
     out = result_line(args, world, dt, waves, G)
     if timer is not None:
         n_launch, ms, rows = timer.summary()
