@@ -1,0 +1,94 @@
+"""Trainer throughput (B = 360 per GPU, 5 unroll steps, 15x15, 8 blocks):
+training steps/s of datou-gomoku-muzero_amd/trainer.py on synthetic slices resident in a device
+ReplayBuffer (uniform sampling, the reference default; --per for PER).  N>1: launch with
+torch.distributed.run; each rank samples its own batch, gradients are averaged by one RCCL
+all-reduce per step; the line reports steps/s of the job (all ranks step together) and samples/s.
+
+  python tools/bench_trainer.py [--steps 20 --warmup 3 --batch 360 --per]"""
+import argparse
+import json
+import os
+import sys
+import time
+from collections import namedtuple
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--steps", type=int, default=20)
+ap.add_argument("--warmup", type=int, default=3)
+ap.add_argument("--batch", type=int, default=360)
+ap.add_argument("--size", type=int, default=15)
+ap.add_argument("--blocks", type=int, default=8)
+ap.add_argument("--buffer", type=int, default=20000)
+ap.add_argument("--per", action="store_true")
+ap.add_argument("--no-amp", action="store_true")
+ap.add_argument("--bf16", action="store_true", help="autocast to bfloat16 instead of the reference's float16")
+ap.add_argument("--channels-last", action="store_true")
+a = ap.parse_args()
+
+world = int(os.environ.get("WORLD_SIZE", "1"))
+rank = int(os.environ.get("RANK", "0"))
+local = int(os.environ.get("LOCAL_RANK", "0"))
+torch.cuda.set_device(local % torch.cuda.device_count())
+dist = None
+if world > 1:
+    import torch.distributed as dist
+    dist.init_process_group(os.environ.get("GMZ_DIST_BACKEND", "nccl"), init_method="env://")
+from datou_gomoku_muzero_amd import trainer as T  # noqa: E402
+
+cfg = T.TrainConfig(BOARD_SIZE=a.size, NUM_RES_BLOCKS=a.blocks, PHYSICAL_BATCH_SIZE=a.batch,
+                    TRAIN_BUFFER_SIZE=a.buffer, ENABLE_PER=a.per)
+tr = T.Trainer(cfg, device="cuda", amp=not a.no_amp, amp_dtype=torch.bfloat16 if a.bf16 else None,
+               channels_last=a.channels_last)
+rb = T.ReplayBuffer(cfg, device="cuda")
+S = namedtuple("S", "observation action_history reward_history policy_history value_history")
+rs = np.random.RandomState(rank)
+U, A = cfg.NUM_UNROLL_STEPS, a.size * a.size
+chunk = []
+for i in range(a.buffer):
+    ends = rs.randint(1, U + 1)
+    act = rs.randint(0, A, U).astype(np.int32)
+    act[ends:] = -1
+    chunk.append(S((rs.rand(U + 1, 3, a.size, a.size) < 0.2).astype(np.uint8), act,
+                   rs.choice([-1.0, 0.0, 1.0], U).astype(np.float32),
+                   rs.dirichlet(np.ones(A), U + 1).astype(np.float32), rs.uniform(-1, 1, U + 1).astype(np.float32)))
+    if len(chunk) == 2000:
+        rb.add(chunk)
+        chunk = []
+rb.add(chunk)
+
+
+def step():
+    batch, idx, w = rb.sample(a.batch, rs)
+    logs, td = tr.step(batch, w)
+    rb.update_priorities(idx, td)
+    return logs
+
+
+for _ in range(a.warmup):
+    step()
+if dist:
+    dist.barrier()
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+for _ in range(a.steps):
+    logs = step()
+torch.cuda.synchronize()
+if dist:
+    dist.barrier()
+dt = time.perf_counter() - t0
+if dist:
+    t = torch.tensor([dt], device="cuda" if os.environ.get("GMZ_DIST_BACKEND", "nccl") == "nccl" else "cpu",
+                     dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+if rank == 0:
+    print(json.dumps({"metric": "trainer steps/sec (config C4)", "value": a.steps / dt, "unit": "steps/s",
+                      "n_gpus": world, "samples_per_s": a.steps * a.batch * world / dt, "ms_per_step": dt / a.steps * 1e3,
+                      "batch_per_gpu": a.batch, "unroll": U, "board": a.size, "blocks": a.blocks, "amp": ("bf16" if a.bf16 else "fp16") if not a.no_amp else None, "channels_last": a.channels_last,
+                      "per": a.per, "last_loss": logs[0], "data": "synthetic slices in a device ReplayBuffer"}))
+if dist:
+    dist.destroy_process_group()
