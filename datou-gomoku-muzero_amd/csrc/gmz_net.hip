@@ -742,24 +742,26 @@ __device__ __forceinline__ float support3(float l0, float l1, float l2) {
   return (-1.f * p0 + 0.f * p1) + 1.f * p2;
 }
 
-// Prediction heads (+ reward head): 4 rows per 512-thread block so every weight is read once per
-// block; features are staged k-major ([k][4 rows]) so one ds_read_b128 feeds 4 FMAs.  Every phase
-// spreads over the whole block (no serial single-thread tails):
-//   0: stage features, fc2 weights; reduce the reward GEMM's split-K partials (one (row, unit) each)
-//   1: policy_fc in two k-halves (450 threads); 2: combine + bias -> logits, value_fc1 in four
-//   k-quarters (256 threads); 3: value_fc1 bias + ReLU; 4: value / reward fc2 as wave reductions,
-//   support_to_scalar.
-constexpr int HEAD_ROWS = 4, HEAD_THREADS = 512;
+// Prediction heads (+ reward head): 4 rows per 1024-thread block so every weight is read once per
+// block; features are staged k-major ([k][4 rows]) so one ds_read_b128 feeds 4 FMAs.  The block is
+// latency-bound on L2 weight reads, so every reduction is split over enough threads that each keeps
+// at most ~8 batches of 16 loads in flight:
+//   0: stage features and fc2 weights; reward_fc.0 split-K partials reduced in 4 parts per (row, unit)
+//   1: policy_fc in 4 k-parts (4A threads); value_fc1 in 16 k-chunks (1024 threads)
+//   2: combine + bias -> logits; value_fc1 bias + ReLU; reward bias + ReLU
+//   3: value / reward fc2 as wave reductions, support_to_scalar.
+constexpr int HEAD_ROWS = 4, HEAD_THREADS = 1024, HEAD_KP = 4, HEAD_VQ = 16;
 __global__ void __launch_bounds__(HEAD_THREADS) k_heads(HeadArgs h) {
   extern __shared__ float sm[];
   const int r0 = blockIdx.x * HEAD_ROWS, tid = threadIdx.x;
   const int A = h.A, hd = h.hd;
-  float *feat = sm;                        // [3A][4]
-  float *ppart = feat + 3 * A * HEAD_ROWS; // [2][A][4]
-  float *vpart = ppart + 2 * A * HEAD_ROWS;// [4 quarters][4 rows][64]
-  float *hv = vpart + 4 * HEAD_ROWS * 64;  // [4][64]
-  float *hr = hv + HEAD_ROWS * 64;         // [4][64]
-  float *w2 = hr + HEAD_ROWS * 64;         // [2][64 * 3]: value_fc2, reward_fc2
+  float *feat = sm;                               // [3A][4]
+  float *ppart = feat + 3 * A * HEAD_ROWS;        // [KP][A][4]
+  float *vpart = ppart + HEAD_KP * A * HEAD_ROWS; // [VQ][4 rows][64]
+  float *rsum = vpart + HEAD_VQ * HEAD_ROWS * 64; // [4 parts][4 rows][64]
+  float *hv = rsum + 4 * HEAD_ROWS * 64;          // [4][64]
+  float *hr = hv + HEAD_ROWS * 64;                // [4][64]
+  float *w2 = hr + HEAD_ROWS * 64;                // [2][64 * 3]: value_fc2, reward_fc2
   bool valid[HEAD_ROWS];
 #pragma unroll
   for (int i = 0; i < HEAD_ROWS; ++i) valid[i] = r0 + i < h.rows && h.out_slot[r0 + i] >= 0;
@@ -771,33 +773,33 @@ __global__ void __launch_bounds__(HEAD_THREADS) k_heads(HeadArgs h) {
     w2[tid] = h.vfc2_w[tid];
     if (h.reward) w2[192 + tid] = h.rfc2_w[tid];
   }
-  if (h.reward && tid >= 256 && tid < 256 + HEAD_ROWS * 64) {  // reward_fc.0: bias + partials + ReLU
-    const int i = (tid - 256) >> 6, j = tid & 63;
-    if (j < hd) {
-      float s = h.rfc1_b[j];
-      if (valid[i]) {
-        const float *src = h.rpart + (size_t)(r0 + i) * 64 + j;
-        const size_t stride = (size_t)h.rows * 64;
-        int k = 0;
-        for (; k + 8 <= h.ksplit; k += 8) {
-          float v[8];
+  if (h.reward) {  // reward_fc.0 split-K partials: (part, row, unit) per thread
+    const int part = tid >> 8, i = (tid >> 6) & 3, j = tid & 63;
+    float s = 0.f;
+    if (j < hd && valid[i]) {
+      const int k0 = part * h.ksplit / 4, k1 = (part + 1) * h.ksplit / 4;
+      const float *src = h.rpart + (size_t)(r0 + i) * 64 + j;
+      const size_t stride = (size_t)h.rows * 64;
+      int k = k0;
+      for (; k + 8 <= k1; k += 8) {
+        float v[8];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) v[u] = src[(k + u) * stride];
+        for (int u = 0; u < 8; ++u) v[u] = src[(k + u) * stride];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) s += v[u];
-        }
-        for (; k < h.ksplit; ++k) s += src[k * stride];
+        for (int u = 0; u < 8; ++u) s += v[u];
       }
-      hr[i * 64 + j] = fmaxf(s, 0.f);
+      for (; k < k1; ++k) s += src[k * stride];
     }
+    rsum[(part * HEAD_ROWS + i) * 64 + j] = s;
   }
   __syncthreads();
-  for (int ti = tid; ti < 2 * A; ti += HEAD_THREADS) {  // policy_fc (network.py:70), k-half kh of the 2A features
-    const int kh = ti >= A, a = ti - kh * A;
+  const int kchunk = (2 * A + HEAD_KP - 1) / HEAD_KP;
+  for (int ti = tid; ti < HEAD_KP * A; ti += HEAD_THREADS) {  // policy_fc (network.py:70), k-part kp
+    const int kp = ti / A, a = ti - kp * A;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     const float *wcol = h.pfc_w + a;
-    int k = kh * A;
-    const int ke = k + A;
+    int k = kp * kchunk;
+    const int ke = min(k + kchunk, 2 * A);
     for (; k + 16 <= ke; k += 16) {  // 16 independent weight loads in flight per thread
       float wv[16];
 #pragma unroll
@@ -806,41 +808,50 @@ __global__ void __launch_bounds__(HEAD_THREADS) k_heads(HeadArgs h) {
       for (int u = 0; u < 16; ++u) acc += *(const f32x4 *)(feat + 4 * (k + u)) * wv[u];
     }
     for (; k < ke; ++k) acc += *(const f32x4 *)(feat + 4 * k) * wcol[(size_t)k * A];
-    *(f32x4 *)(ppart + 4 * (kh * A + a)) = acc;
+    *(f32x4 *)(ppart + 4 * (kp * A + a)) = acc;
+  }
+  {  // value_fc1 (network.py:72), k-chunk q of the A value features
+    const int q = tid >> 6, j = tid & 63;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    if (j < hd) {
+      const int p0 = q * A / HEAD_VQ, p1 = (q + 1) * A / HEAD_VQ;
+      const float *wcol = h.vfc1_w + j;
+      int p = p0;
+      for (; p + 8 <= p1; p += 8) {
+        float wv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) wv[u] = wcol[(p + u) * hd];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc += *(const f32x4 *)(feat + 4 * (2 * A + p + u)) * wv[u];
+      }
+      for (; p < p1; ++p) acc += *(const f32x4 *)(feat + 4 * (2 * A + p)) * wcol[p * hd];
+    }
+#pragma unroll
+    for (int i = 0; i < HEAD_ROWS; ++i) vpart[(q * HEAD_ROWS + i) * 64 + j] = acc[i];
   }
   __syncthreads();
   for (int a = tid; a < A; a += HEAD_THREADS) {
     const float b = h.pfc_b[a];
-    const f32x4 p0 = *(const f32x4 *)(ppart + 4 * a), p1 = *(const f32x4 *)(ppart + 4 * (A + a));
+    f32x4 sum = *(const f32x4 *)(ppart + 4 * a);
+#pragma unroll
+    for (int kp = 1; kp < HEAD_KP; ++kp) sum += *(const f32x4 *)(ppart + 4 * (kp * A + a));
 #pragma unroll
     for (int i = 0; i < HEAD_ROWS; ++i)
-      if (valid[i]) h.logits[(size_t)(r0 + i) * A + a] = (b + p0[i]) + p1[i];
+      if (valid[i]) h.logits[(size_t)(r0 + i) * A + a] = b + sum[i];
   }
-  if (tid >= 256) {  // value_fc1 (network.py:72), k-quarter q
-    const int q = (tid - 256) >> 6, j = tid & 63;
-    if (j < hd) {
-      const int p0 = q * A / 4, p1 = (q + 1) * A / 4;
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      const float *wcol = h.vfc1_w + j;
-      int p = p0;
-      for (; p + 16 <= p1; p += 16) {
-        float wv[16];
-#pragma unroll
-        for (int u = 0; u < 16; ++u) wv[u] = wcol[(p + u) * hd];
-#pragma unroll
-        for (int u = 0; u < 16; ++u) acc += *(const f32x4 *)(feat + 4 * (2 * A + p + u)) * wv[u];
-      }
-      for (; p < p1; ++p) acc += *(const f32x4 *)(feat + 4 * (2 * A + p)) * wcol[p * hd];
-#pragma unroll
-      for (int i = 0; i < HEAD_ROWS; ++i) vpart[(q * HEAD_ROWS + i) * 64 + j] = acc[i];
-    }
-  }
-  __syncthreads();
-  if (tid < HEAD_ROWS * 64) {
+  if (tid < HEAD_ROWS * 64) {  // value_fc1 bias + ReLU
     const int i = tid >> 6, j = tid & 63;
+    if (j < hd) {
+      float s = 0.f;
+#pragma unroll
+      for (int q = 0; q < HEAD_VQ; ++q) s += vpart[(q * HEAD_ROWS + i) * 64 + j];
+      hv[i * 64 + j] = fmaxf(h.vfc1_b[j] + s, 0.f);
+    }
+  } else if (h.reward && tid < 2 * HEAD_ROWS * 64) {  // reward_fc.0 bias + ReLU (network.py:84-86)
+    const int i = (tid >> 6) & 3, j = tid & 63;
     if (j < hd)
-      hv[i * 64 + j] = fmaxf(((h.vfc1_b[j] + vpart[(0 * HEAD_ROWS + i) * 64 + j]) + vpart[(1 * HEAD_ROWS + i) * 64 + j]) +
-                                 (vpart[(2 * HEAD_ROWS + i) * 64 + j] + vpart[(3 * HEAD_ROWS + i) * 64 + j]), 0.f);
+      hr[i * 64 + j] = fmaxf(h.rfc1_b[j] + ((rsum[(0 * HEAD_ROWS + i) * 64 + j] + rsum[(1 * HEAD_ROWS + i) * 64 + j]) +
+                                            (rsum[(2 * HEAD_ROWS + i) * 64 + j] + rsum[(3 * HEAD_ROWS + i) * 64 + j])), 0.f);
   }
   __syncthreads();
   const int w = tid >> 6, lane = tid & 63;
@@ -956,7 +967,7 @@ static int heads(const gmz_net_weights *w, const float *pv, const int32_t *out_s
   HeadArgs h{pv, out_slot, w->policy_fc_w, w->policy_fc_b, w->value_fc1_w, w->value_fc1_b, w->value_fc2_w,
              w->value_fc2_b, rpart, w->reward_fc1_b, w->reward_fc2_w, w->reward_fc2_b, rows, A, w->head_hidden,
              KSPLIT, logits, value, reward};
-  const size_t smem = (5 * A * HEAD_ROWS + 6 * HEAD_ROWS * 64 + 2 * 192) * sizeof(float);
+  const size_t smem = ((3 + HEAD_KP) * A * HEAD_ROWS + (HEAD_VQ + 4 + 2) * HEAD_ROWS * 64 + 2 * 192) * sizeof(float);
   hipLaunchKernelGGL(k_heads, dim3((rows + HEAD_ROWS - 1) / HEAD_ROWS), dim3(HEAD_THREADS), smem, s, h);
   GMZ_LAUNCH_CHECK();
   return 0;
