@@ -684,7 +684,7 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
 // reward_fc.0 : [rows, A*128] (NHWC hidden, gathered by slot) x [A*128, 64], split-K partials.
 // 256-thread block = 4 waves x 16 rows; the 4 waves read the same B fragments (L1-shared), each
 // wave keeps 4 k-steps of loads in flight.
-constexpr int RFC_UNROLL = 4;
+constexpr int RFC_UNROLL = 8;
 __global__ void __launch_bounds__(256) k_reward_fc1(const uint16_t *__restrict__ pool, const int32_t *__restrict__ out_slot,
                                                     int rows, int K, const uint16_t *__restrict__ wpk, int nks, int ksplit,
                                                     float *__restrict__ part) {
