@@ -115,12 +115,10 @@ def _bn(mod, x, mask=None):
     x = x.float()
     dims = [0] + list(range(2, x.dim()))
     shape = [1, -1] + [1] * (x.dim() - 2)
-    mf = mask.to(torch.float32).reshape([-1] + [1] * (x.dim() - 1))
+    var, mean = torch.var_mean(x[mask], dim=dims, correction=0)  # statistics of the valid rows
     n = mask.sum().to(torch.float32) * (x[0, 0].numel())
-    mean = (x * mf).sum(dims) / n
-    xc = x - mean.reshape(shape)
-    var = (xc * xc * mf).sum(dims) / n
-    y = xc * torch.rsqrt(var + mod.eps).reshape(shape) * mod.weight.reshape(shape) + mod.bias.reshape(shape)
+    scale = torch.rsqrt(var + mod.eps) * mod.weight
+    y = torch.addcmul((mod.bias - mean * scale).reshape(shape), x, scale.reshape(shape))  # one pass
     with torch.no_grad():  # through .data, like the native kernel: no autograd version bump (the
         m = mod.momentum      # unmasked BatchNorm calls of the same module saved these buffers)
         mod.running_mean.data.mul_(1 - m).add_(m * mean.detach())
