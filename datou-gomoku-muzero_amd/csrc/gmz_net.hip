@@ -572,7 +572,9 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
 #pragma unroll
           for (int nt = 0; nt < NTW; ++nt)
             acc[nt][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ar[st % RD][nt], b[st & 1][i], acc[nt][i], 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
+        // the last k-step stays open: the scheduler may start the epilogue of the tiles whose final
+        // MFMA has issued while the remaining ones run (ABL & 256 pins it, for comparison)
+        if ((ABL & 256) || st + 1 < KSTEPS) __builtin_amdgcn_sched_barrier(0);
       }
       if (ABL & 128) { st_t1 = __builtin_amdgcn_s_memtime(); st_loop += st_t1 - st_t0; }
       // epilogue: bias (+ action term) (+ residual) + ReLU -> bf16 -> the other image.  One

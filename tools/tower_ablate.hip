@@ -85,13 +85,13 @@ int main(int argc, char **argv) {
     printf("tower3 12w vs tower: hidden mismatches %zu / %zu, pv mismatches %zu / %zu\n", dh, o1.size(), dp, p1.size());
   }
   const char *names[] = {"k_tower (LDS-staged weights)", "k_tower3 8w (2x4) RD4", "k_tower3 12w (4x3) RD3 [product]",
-                         "k_tower3 12w no-io(32)", "k_tower3 12w A-from-one-kstep(1)", "k_tower3 12w no-A-loads(2)"};
-  const int NV = 6;
+                         "k_tower3 12w no-io(32)", "k_tower3 12w A-from-one-kstep(1)", "k_tower3 12w no-A-loads(2)", "k_tower3 12w last k-step pinned(256)"};
+  const int NV = 7;
   float best[NV];
   for (int i = 0; i < NV; ++i) best[i] = 1e9f;
   for (int round = 0; round < 5; ++round) {
     float t[NV] = {run<0>(a, 5), run<0, 3>(a, 5), run<0, 3, 3, 4, 3>(a, 5), run<32, 3, 3, 4, 3>(a, 5), run<1, 3, 3, 4, 3>(a, 5),
-                   run<2, 3, 3, 4, 3>(a, 5)};
+                   run<2, 3, 3, 4, 3>(a, 5), run<256, 3, 3, 4, 3>(a, 5)};
     for (int i = 0; i < NV; ++i) best[i] = t[i] < best[i] ? t[i] : best[i];
   }
   for (int i = 0; i < NV; ++i)
