@@ -42,6 +42,7 @@ _SIGS = {
     "gmz_engine_set_root": ([P, P, P, P], I),
     "gmz_engine_select": ([P, P, P, P, P, P], I),
     "gmz_engine_expand_backup": ([P, P, P, P, P], I),
+    "gmz_engine_expand_backup_select": ([P, P, P, P, P, P, P, P, P], I),
     "gmz_engine_pending_waves": ([P, P], I),
     "gmz_engine_waves_for_legal": ([ctypes.POINTER(EngineCfg), P, I, P], I),
     "gmz_engine_finish_move": ([P, P, P, P, P], I),

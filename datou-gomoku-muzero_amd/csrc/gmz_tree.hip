@@ -487,11 +487,9 @@ __global__ void __launch_bounds__(256) k_set_root(Dev D, const float *__restrict
 
 // one wave: select the leaf of every active game and emit its network request
 template <int NJ>
-__global__ void __launch_bounds__(256) k_select(Dev D, int32_t *__restrict__ in_slot, int32_t *__restrict__ act_out,
-                                                int32_t *__restrict__ out_slot, float *__restrict__ obs) {
-  const int w = threadIdx.x / WAVE, lane = threadIdx.x & (WAVE - 1);
-  const int g = blockIdx.x * 4 + w;
-  if (g >= D.G) return;
+__device__ __forceinline__ void select_game(const Dev &D, int g, int lane, int32_t *__restrict__ in_slot,
+                                            int32_t *__restrict__ act_out, int32_t *__restrict__ out_slot,
+                                            float *__restrict__ obs) {
   const int A = D.A, S = D.S;
   GameState st = D.gs[g];
   if (!st.active) {
@@ -565,12 +563,9 @@ __global__ void __launch_bounds__(256) k_select(Dev D, int32_t *__restrict__ in_
 }
 
 template <int NJ>
-__global__ void __launch_bounds__(256) k_expand_backup(Dev D, const float *__restrict__ logits_in,
-                                                       const float *__restrict__ value_in,
-                                                       const float *__restrict__ reward_in) {
-  const int w = threadIdx.x / WAVE, lane = threadIdx.x & (WAVE - 1);
-  const int g = blockIdx.x * 4 + w;
-  if (g >= D.G) return;
+__device__ __forceinline__ void expand_backup_game(const Dev &D, int g, int lane, const float *__restrict__ logits_in,
+                                                   const float *__restrict__ value_in,
+                                                   const float *__restrict__ reward_in) {
   const int A = D.A, S = D.S;
   GameState st = D.gs[g];
   if (!st.active) return;
@@ -672,6 +667,38 @@ __global__ void __launch_bounds__(256) k_expand_backup(Dev D, const float *__res
   }
   if (st.sim >= D.n_sims) st.active = 0;
   if (lane == 0) D.gs[g] = st;
+}
+
+template <int NJ>
+__global__ void __launch_bounds__(256) k_select(Dev D, int32_t *__restrict__ in_slot, int32_t *__restrict__ act_out,
+                                                int32_t *__restrict__ out_slot, float *__restrict__ obs) {
+  const int g = blockIdx.x * 4 + threadIdx.x / WAVE;
+  if (g < D.G) select_game<NJ>(D, g, threadIdx.x & (WAVE - 1), in_slot, act_out, out_slot, obs);
+}
+
+template <int NJ>
+__global__ void __launch_bounds__(256) k_expand_backup(Dev D, const float *__restrict__ logits_in,
+                                                       const float *__restrict__ value_in,
+                                                       const float *__restrict__ reward_in) {
+  const int g = blockIdx.x * 4 + threadIdx.x / WAVE;
+  if (g < D.G) expand_backup_game<NJ>(D, g, threadIdx.x & (WAVE - 1), logits_in, value_in, reward_in);
+}
+
+// expand + backup of wave i, then select of wave i+1, in one launch: every game's tree is owned by
+// one wave, so the only dependency between the two phases is that wave's own stores (one kernel
+// boundary per simulation wave fewer)
+template <int NJ>
+__global__ void __launch_bounds__(256) k_expand_select(Dev D, const float *__restrict__ logits_in,
+                                                       const float *__restrict__ value_in,
+                                                       const float *__restrict__ reward_in,
+                                                       int32_t *__restrict__ in_slot, int32_t *__restrict__ act_out,
+                                                       int32_t *__restrict__ out_slot, float *__restrict__ obs) {
+  const int g = blockIdx.x * 4 + threadIdx.x / WAVE, lane = threadIdx.x & (WAVE - 1);
+  if (g >= D.G) return;
+  expand_backup_game<NJ>(D, g, lane, logits_in, value_in, reward_in);
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_s_waitcnt(0);
+  select_game<NJ>(D, g, lane, in_slot, act_out, out_slot, obs);
 }
 
 template <int NJ>
@@ -932,6 +959,18 @@ GMZ_EXPORT int gmz_engine_expand_backup(gmz_engine *e, const float *logits, cons
   if (e->D.mode == 1 && !reward) return fail("gmz_engine_expand_backup: MuZero mode needs reward");
   const float *rw = e->D.mode == 1 ? reward : nullptr;
   GMZ_LAUNCH_NJ(k_expand_backup, e, stream, e->D, logits, value, rw);
+  return 0;
+}
+
+GMZ_EXPORT int gmz_engine_expand_backup_select(gmz_engine *e, const float *logits, const float *value,
+                                               const float *reward, int32_t *in_slot, int32_t *action,
+                                               int32_t *out_slot, float *obs, void *stream) {
+  if (!e || !logits || !value || !in_slot || !action || !out_slot)
+    return fail("gmz_engine_expand_backup_select: null argument");
+  if (e->D.mode == 1 && !reward) return fail("gmz_engine_expand_backup_select: MuZero mode needs reward");
+  if (e->D.mode == 0 && !obs) return fail("gmz_engine_expand_backup_select: AlphaZero mode needs obs");
+  const float *rw = e->D.mode == 1 ? reward : nullptr;
+  GMZ_LAUNCH_NJ(k_expand_select, e, stream, e->D, logits, value, rw, in_slot, action, out_slot, obs);
   return 0;
 }
 

@@ -59,6 +59,7 @@ class BatchedSelfPlayEngine:
         check(self.lib.gmz_engine_create(ctypes.byref(self.ecfg), ctypes.byref(h)))
         self.handle = h
         self.seed = int(seed)
+        self.fuse_waves = True  # expand/backup + next select in one launch (False: the two entry points)
         G, A, dev = self.G, self.A, self.device
         self.net = net if net is not None else HashNetBackend(G * self.slots_per_game, A, device)
         f32, i32 = torch.float32, torch.int32
@@ -166,15 +167,24 @@ class BatchedSelfPlayEngine:
         self._sync_status()  # previous move's status → legal counts (overlaps the root inference)
         waves = self.waves_needed()
         self.waves_last = waves
-        for _ in range(waves):
+        rw = ptr(self.reward) if self.mode == 1 else None
+        if waves > 0:
             check(L.gmz_engine_select(self.handle, ptr(self.in_slot), ptr(self.act_req), ptr(self.out_slot),
                                       ptr(self.obs), s))
+        for w in range(waves):
             if self.mode == 1:
                 self.net.recurrent(self.in_slot, self.act_req, self.out_slot, self.logits, self.value, self.reward, s)
             else:
                 self.net.initial(self.obs, self.out_slot, self.logits, self.value, s)
-            check(L.gmz_engine_expand_backup(self.handle, ptr(self.logits), ptr(self.value),
-                                             ptr(self.reward) if self.mode == 1 else None, s))
+            if w + 1 < waves and self.fuse_waves:  # backup of this wave + selection of the next in one launch
+                check(L.gmz_engine_expand_backup_select(self.handle, ptr(self.logits), ptr(self.value), rw,
+                                                        ptr(self.in_slot), ptr(self.act_req), ptr(self.out_slot),
+                                                        ptr(self.obs), s))
+            else:
+                check(L.gmz_engine_expand_backup(self.handle, ptr(self.logits), ptr(self.value), rw, s))
+                if w + 1 < waves:
+                    check(L.gmz_engine_select(self.handle, ptr(self.in_slot), ptr(self.act_req), ptr(self.out_slot),
+                                              ptr(self.obs), s))
         check(L.gmz_engine_finish_move(self.handle, ptr(self.policy), ptr(self.root_value), ptr(self.action), s))
         return self.policy, self.root_value, self.action
 

@@ -120,6 +120,12 @@ int gmz_engine_select(gmz_engine *e, int32_t *in_slot_dev, int32_t *action_dev, 
  * advance the sequential-halving schedule. */
 int gmz_engine_expand_backup(gmz_engine *e, const float *logits_dev, const float *value_dev,
                              const float *reward_dev, void *stream);
+/* gmz_engine_expand_backup of this wave followed by gmz_engine_select of the next one, in a single
+ * launch (same arguments and results as the two calls in sequence; every game's tree is owned by one
+ * wave, so nothing crosses games between the two steps). */
+int gmz_engine_expand_backup_select(gmz_engine *e, const float *logits_dev, const float *value_dev,
+                                    const float *reward_dev, int32_t *in_slot_dev, int32_t *action_dev,
+                                    int32_t *out_slot_dev, float *obs_dev, void *stream);
 /* Number of waves still needed by the slowest game (<= 0: all searches done).  Synchronous. */
 int gmz_engine_pending_waves(gmz_engine *e, int32_t *out);
 /* Upper bound of waves for this move computed on the host from legal-move counts (no sync):
