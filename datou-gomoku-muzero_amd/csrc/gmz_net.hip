@@ -411,7 +411,9 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
   int r = next_row(blockIdx.x);
   if (r >= t.rows) return;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  const int nh = w / PG, pg = w % PG;
+  // wave w -> (channel group nh, position group pg) = (w % NQ, w / NQ): the waves sharing a SIMD
+  // (w, w+4, ...) get different position groups, so a short last group does not load one SIMD less
+  const int nh = w % NQ, pg = w / NQ;
   const int g4 = lane >> 4;
   const int cg = (g4 & 1) * 8 + (g4 >> 1);  // {0, 8, 1, 9}
   auto cell = [&](int p) { return (p / H + 1) * RS + (p % H + 1) * PS; };
@@ -491,6 +493,10 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
     const int os = t.out_slot[r];
     if constexpr (!DYN) {  // ---- REPR stem (one MFMA k-step on an im2col operand) -> img0
       const float *ob = t.obs + (size_t)r * 3 * A;
+      // opaque per-board copy of the lane id: keeps the compiler from hoisting the PTW x 8 im2col
+      // offsets and masks out of the board loop (they would live across the whole tower and spill)
+      int ln = lane;
+      asm volatile("" : "+v"(ln));
       bf16x8_t a[NTW];
 #pragma unroll
       for (int nt = 0; nt < NTW; ++nt) a[nt] = ((const bf16x8_t *)t.stem_w)[(nh * NTW + nt) * 64 + lane];
@@ -499,12 +505,12 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
 #pragma unroll
         for (int nt = 0; nt < NTW; ++nt) acc[nt][i] = f32x4{0.f, 0.f, 0.f, 0.f};
         if (pg + PG * i >= NPT) continue;
-        const int p = (pg + PG * i) * 16 + sigma16(lane & 15);
+        const int p = (pg + PG * i) * 16 + sigma16(ln & 15);
         const int y = p / H, x = p % H;
         bf16x8_t b;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const int k = 8 * g4 + j;
+          const int k = 8 * (ln >> 4) + j;
           float v = 0.f;
           if (k < 27 && p < A) {
             const int tap = k / 3, c = k % 3;
@@ -551,31 +557,39 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
         bb[i] = (pos[i] < 0 ? 0 : pos[i] + cg * 16) + (int)(size_t)(img - smem);
         asm volatile("" : "+v"(bb[i]));  // one base VGPR per tile and layer; all else immediates
       }
-      bf16x8_t b[2][PTW];
-      auto readB = [&](int buf, int st) {
-        const int tap = st >> 2, ks = st & 3;
-        const int off = (tap / 3) * RS + (tap % 3) * PS + ks * 32;
+      // k-loop over the NTL tiles this wave owns (NTL = PTW, or PTW - 1 for a short last position
+      // group: its empty slot costs neither MFMAs nor LDS reads)
+      auto kloop = [&](auto ntl_c) {
+        constexpr int NTL = decltype(ntl_c)::value;
+        bf16x8_t b[2][NTL];
+        auto readB = [&](int buf, int st) {
+          const int tap = st >> 2, ks = st & 3;
+          const int off = (tap / 3) * RS + (tap % 3) * PS + ks * 32;
 #pragma unroll
-        for (int i = 0; i < PTW; ++i) b[buf][i] = *(const bf16x8_t *)(smem + bb[i] + off);
+          for (int i = 0; i < NTL; ++i) b[buf][i] = *(const bf16x8_t *)(smem + bb[i] + off);
+        };
+        readB(0, 0);
+        if (ABL & 128) st_t0 = __builtin_amdgcn_s_memtime();
+        const int gs0 = L * KSTEPS;
+#pragma unroll
+        for (int st = 0; st < KSTEPS; ++st) {
+          // A for k-step st+RD-1 (RD-deep register ring), B for k-step st+1 (double buffer)
+          loadA((st + RD - 1) % RD, gs0 + st + RD - 1);
+          if (st + 1 < KSTEPS) readB((st + 1) & 1, st + 1);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int i = 0; i < NTL; ++i)
+#pragma unroll
+            for (int nt = 0; nt < NTW; ++nt)
+              acc[nt][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ar[st % RD][nt], b[st & 1][i], acc[nt][i], 0, 0, 0);
+          // the last k-step stays open: the scheduler may start the epilogue of the tiles whose final
+          // MFMA has issued while the remaining ones run (ABL & 256 pins it, for comparison)
+          if ((ABL & 256) || st + 1 < KSTEPS) __builtin_amdgcn_sched_barrier(0);
+        }
       };
-      readB(0, 0);
-      if (ABL & 128) st_t0 = __builtin_amdgcn_s_memtime();
-      const int gs0 = L * KSTEPS;
-#pragma unroll
-      for (int st = 0; st < KSTEPS; ++st) {
-        // A for k-step st+RD-1 (RD-deep register ring), B for k-step st+1 (double buffer)
-        loadA((st + RD - 1) % RD, gs0 + st + RD - 1);
-        if (st + 1 < KSTEPS) readB((st + 1) & 1, st + 1);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int i = 0; i < PTW; ++i)
-#pragma unroll
-          for (int nt = 0; nt < NTW; ++nt)
-            acc[nt][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ar[st % RD][nt], b[st & 1][i], acc[nt][i], 0, 0, 0);
-        // the last k-step stays open: the scheduler may start the epilogue of the tiles whose final
-        // MFMA has issued while the remaining ones run (ABL & 256 pins it, for comparison)
-        if ((ABL & 256) || st + 1 < KSTEPS) __builtin_amdgcn_sched_barrier(0);
-      }
+      if constexpr (PTW * PG == NPT) kloop(std::integral_constant<int, PTW>{});
+      else if (pg + PG * (PTW - 1) < NPT) kloop(std::integral_constant<int, PTW>{});
+      else kloop(std::integral_constant<int, PTW - 1>{});
       if (ABL & 128) { st_t1 = __builtin_amdgcn_s_memtime(); st_loop += st_t1 - st_t0; }
       // epilogue: bias (+ action term) (+ residual) + ReLU -> bf16 -> the other image.  One
       // straight-line copy per layer kind; every LDS operand (bias, residual) is read in one batch
@@ -889,6 +903,7 @@ static int cu_count() {
 // (15 tiles of 16 positions at 15x15: no idle tile, 3 waves per SIMD; RD 3 keeps it within 168
 // VGPRs).  19x19 (single LDS image, 23 tiles): 8 waves = 2 channel halves x 4 position groups.
 template <int H> struct TowerCfg { static constexpr int NQ = 4, PG = 3, RD = 3; };
+template <> struct TowerCfg<15> { static constexpr int NQ = 4, PG = 2, RD = 3; };  // 8 tiles | 7 tiles
 template <> struct TowerCfg<19> { static constexpr int NQ = 2, PG = 4, RD = 2; };
 
 // bytes of k_tower3's per-workgroup residual scratch (single-image boards only)

@@ -83,15 +83,26 @@ int main(int argc, char **argv) {
     for (size_t i = 0; i < o1.size(); ++i) dh += o1[i] != o2[i];
     for (size_t i = 0; i < p1.size(); ++i) dp += p1[i] != p2[i];
     printf("tower3 12w vs tower: hidden mismatches %zu / %zu, pv mismatches %zu / %zu\n", dh, o1.size(), dp, p1.size());
+    CK(hipMemset(dpool + (size_t)rows * A * 128, 0, o1.size() * 2));
+    CK(hipMemset(dpv, 0, p1.size() * 4));
+    hipLaunchKernelGGL((k_tower3<15, true, 0, 3, 4, 2>), dim3(256), dim3(512), 0, 0, a);
+    CK(hipMemcpy(o2.data(), dpool + (size_t)rows * A * 128, o2.size() * 2, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(p2.data(), dpv, p2.size() * 4, hipMemcpyDeviceToHost));
+    dh = dp = 0;
+    for (size_t i = 0; i < o1.size(); ++i) dh += o1[i] != o2[i];
+    for (size_t i = 0; i < p1.size(); ++i) dp += p1[i] != p2[i];
+    printf("tower3 8w (4x2) vs tower: hidden mismatches %zu / %zu, pv mismatches %zu / %zu\n", dh, o1.size(), dp, p1.size());
   }
   const char *names[] = {"k_tower (LDS-staged weights)", "k_tower3 8w (2x4) RD4", "k_tower3 12w (4x3) RD3 [product]",
-                         "k_tower3 12w no-io(32)", "k_tower3 12w A-from-one-kstep(1)", "k_tower3 12w no-A-loads(2)", "k_tower3 12w last k-step pinned(256)"};
-  const int NV = 7;
+                         "k_tower3 12w no-io(32)", "k_tower3 12w no-A-loads(2)", "k_tower3 8w (4x2) RD3",
+                         "k_tower3 8w (4x2) RD4", "k_tower3 8w (4x2) RD2", "k_tower3 4w (2x2) RD3"};
+  const int NV = 9;
   float best[NV];
   for (int i = 0; i < NV; ++i) best[i] = 1e9f;
   for (int round = 0; round < 5; ++round) {
-    float t[NV] = {run<0>(a, 5), run<0, 3>(a, 5), run<0, 3, 3, 4, 3>(a, 5), run<32, 3, 3, 4, 3>(a, 5), run<1, 3, 3, 4, 3>(a, 5),
-                   run<2, 3, 3, 4, 3>(a, 5), run<256, 3, 3, 4, 3>(a, 5)};
+    float t[NV] = {run<0>(a, 5), run<0, 3>(a, 5), run<0, 3, 3, 4, 3>(a, 5), run<32, 3, 3, 4, 3>(a, 5),
+                   run<2, 3, 3, 4, 3>(a, 5), run<0, 3, 3, 4, 2>(a, 5), run<0, 3, 4, 4, 2>(a, 5),
+                   run<0, 3, 2, 4, 2>(a, 5), run<0, 3, 3, 2, 2>(a, 5)};
     for (int i = 0; i < NV; ++i) best[i] = t[i] < best[i] ? t[i] : best[i];
   }
   for (int i = 0; i < NV; ++i)
