@@ -11,7 +11,7 @@ import torch  # noqa: F401  (must precede the CDLL load: shared HIP runtime)
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "libgmz.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 P = ctypes.c_void_p
 I = ctypes.c_int

@@ -4,6 +4,8 @@
 #include <stdint.h>
 #include <string>
 
+#include "gmz.h"  // the C ABI: every exported definition is checked against its declaration
+
 #define GMZ_EXPORT extern "C" __attribute__((visibility("default")))
 
 namespace gmz {

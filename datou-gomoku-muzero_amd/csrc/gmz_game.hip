@@ -55,7 +55,7 @@ __global__ void k_play(int8_t *__restrict__ boards, int G, int size, int n_in_ro
 using namespace gmz;
 
 GMZ_EXPORT const char *gmz_last_error(void) { return g_err.c_str(); }
-GMZ_EXPORT int gmz_abi_version(void) { return 1; }
+GMZ_EXPORT int gmz_abi_version(void) { return GMZ_ABI_VERSION; }
 GMZ_EXPORT int gmz_device_synchronize(void) {
   GMZ_HIP(hipDeviceSynchronize());
   return 0;

@@ -31,6 +31,21 @@ struct Geo {
   static constexpr int A = H * H, HP = H + 2, AP = HP * HP, NPT = (A + 15) / 16, PTW = (NPT + 3) / 4;
 };
 
+// head-feature rows (tower output -> head GEMMs): the two policy planes (k = o*A + p, o < 2) padded
+// with zeros to a multiple of 16, then the value plane padded the same way, so every GEMM k-chunk of
+// 16 floats is a 64-byte aligned, in-bounds read and the zero pads meet zero weight pads
+__host__ __device__ constexpr int r16(int x) { return (x + 15) & ~15; }
+__host__ __device__ constexpr int pv_kpol(int A) { return r16(2 * A); }
+__host__ __device__ constexpr int pv_kval(int A) { return r16(A); }
+__host__ __device__ constexpr int pv_stride(int A) { return pv_kpol(A) + pv_kval(A); }
+// element i of a pv row -> (plane o, position p), o = 3 for a pad
+__device__ __forceinline__ void pv_split(int i, int A, int &o, int &p) {
+  const int kp = pv_kpol(A);
+  if (i < 2 * A) { o = i >= A; p = i - o * A; }
+  else if (i >= kp && i < kp + A) { o = 2; p = i - kp; }
+  else { o = 3; p = 0; }
+}
+
 struct TowerArgs {
   const uint16_t *convs;   // [layers][9 taps][4 k-steps][8 n-tiles][64 lanes][8] bf16 fragments
   const float *bias;       // [layers][128]
@@ -42,7 +57,7 @@ struct TowerArgs {
   uint16_t *pool;          // hidden slots [slot][A][128] bf16
   const int32_t *in_slot, *action, *out_slot;
   const float *head_w, *head_b;  // [3][128], [3]
-  float *pv_feat;          // [rows][3][A]
+  float *pv_feat;          // [rows][pv_stride(A)]: policy planes at [0, 2A), value plane at pv_kpol(A) + p
   int rows;
   uint16_t *xres;          // single-image boards (19x19): per-workgroup residual scratch (k_tower3)
 };
@@ -334,9 +349,11 @@ __global__ void __launch_bounds__(512) k_tower(TowerArgs t) {
     const int q = (p / H + 1) * HP + (p % H + 1);
     dst[i] = *(const uint4 *)(act + chunk_addr(q, p & 15, ch));
   }
-  // ---- prediction-head 1x1 convs + BN + ReLU (network.py:69,71), flattened NCHW
-  for (int i = tid; i < 3 * A; i += 512) {
-    const int o = i / A, p = i % A;
+  // ---- prediction-head 1x1 convs + BN + ReLU (network.py:69,71), flattened NCHW (pv row layout)
+  for (int i = tid; i < pv_stride(A); i += 512) {
+    int o, p;
+    pv_split(i, A, o, p);
+    if (o == 3) { t.pv_feat[(size_t)r * pv_stride(A) + i] = 0.f; continue; }
     const int q = (p / H + 1) * HP + (p % H + 1);
     const float *hw = t.head_w + o * C;
     float sum = t.head_b[o];
@@ -350,7 +367,7 @@ __global__ void __launch_bounds__(512) k_tower(TowerArgs t) {
         sum += hw[ch * 8 + 2 * e + 1] * __uint_as_float(wds[e] & 0xFFFF0000u);
       }
     }
-    t.pv_feat[(size_t)r * 3 * A + i] = fmaxf(sum, 0.f);
+    t.pv_feat[(size_t)r * pv_stride(A) + i] = fmaxf(sum, 0.f);
   }
   (void)key_of_q;
 }
@@ -384,6 +401,10 @@ struct Img3 {
   static constexpr int RUN_DMA = (RUN + 1023) / 1024; // 1 KB LDS-DMA pieces per board row
 };
 
+// k_tower3 ablation bits (0 in the product; timing-only variants in tools/tower_ablate.hip):
+// 1 = A fragments from one k-step (L1-resident), 2 = no weight loads, 32 = no per-board I/O,
+// 128 = s_memtime phase stamps -> pv_feat, 256 = pin the last k-step, 512 = no epilogue,
+// 1024 = no per-layer barrier
 template <int H, bool DYN, int ABL = 0, int RD = 4, int NQ = 2, int PG = 4>
 __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
   using G = Geo<H>;
@@ -646,14 +667,19 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
           if constexpr (ONE) __builtin_amdgcn_sched_barrier(0);
         }
       };
-      if (DYN && kind == 0) epilogue(std::integral_constant<int, 0>{});
+      if constexpr ((ABL & 512) != 0) {  // ablation: no epilogue (timing only; acc kept live)
+#pragma unroll
+        for (int nt = 0; nt < NTW; ++nt)
+#pragma unroll
+          for (int i = 0; i < PTW; ++i) asm volatile("" ::"v"(acc[nt][i]));
+      } else if (DYN && kind == 0) epilogue(std::integral_constant<int, 0>{});
       else if (kind == 1) epilogue(std::integral_constant<int, 1>{});
       else epilogue(std::integral_constant<int, 2>{});
       // the bias DMA (issued before this layer's 36 k-steps) is older than the (RD-1)*NTW ring loads
       // still in flight: this count retires it before the barrier publishes the slot
       if (w == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((RD - 1) * NTW) : "memory");
       if (ABL & 128) { st_t2 = __builtin_amdgcn_s_memtime(); st_epi += st_t2 - st_t1; }
-      __syncthreads();
+      if constexpr (!(ABL & 1024)) __syncthreads();  // ablation 1024: no per-layer barrier (timing only)
       if (ABL & 128) st_bar += __builtin_amdgcn_s_memtime() - st_t2;
     }
 
@@ -666,8 +692,10 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
     if (!(ABL & 32)) {
       uint4 *dst = (uint4 *)(t.pool + (size_t)os * A * C);
       for (int i = tid; i < A * 16; i += NTHR) dst[i] = *(const uint4 *)(fin + cell(i >> 4) + (i & 15) * 16);
-      for (int i = tid; i < 3 * A; i += NTHR) {
-        const int o = i / A, p = i % A;
+      for (int i = tid; i < pv_stride(A); i += NTHR) {  // head 1x1 convs -> pv row (zero pads)
+        int o, p;
+        pv_split(i, A, o, p);
+        if (o == 3) { t.pv_feat[(size_t)r * pv_stride(A) + i] = 0.f; continue; }
         const uint8_t *src = fin + cell(p);
         const float *hw = t.head_w + o * C;
         float sum = t.head_b[o];
@@ -681,7 +709,7 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
             sum += hw[ch * 8 + 2 * e + 1] * __uint_as_float(wds[e] & 0xFFFF0000u);
           }
         }
-        t.pv_feat[(size_t)r * 3 * A + i] = fmaxf(sum, 0.f);
+        t.pv_feat[(size_t)r * pv_stride(A) + i] = fmaxf(sum, 0.f);
       }
     }
     __syncthreads();  // the next board's layer 0 overwrites img[1]
@@ -697,21 +725,42 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
   }
 }
 
-// reward_fc.0 : [rows, A*128] (NHWC hidden, gathered by slot) x [A*128, 64], split-K partials.
-// 256-thread block = 4 waves x 16 rows; the 4 waves read the same B fragments (L1-shared), each
-// wave keeps 4 k-steps of loads in flight.
+// ---- prediction / reward heads (network.py:66-88): two launches per batch
+// k_head_gemm: three GEMM kinds in one grid of 256-thread blocks, no inter-block dependency
+//   [0, nR)          reward_fc.0 [rows, A*128] (NHWC hidden, gathered by slot) x [A*128, 64], bf16
+//                    MFMA, split-K partials; 4 waves x 16 rows, the waves share B fragments in L1
+//   [nR, nR+nP)      policy_fc  [rows, 2A] x [2A, A] + bias -> logits, f32 MFMA (16x16x4), one
+//                    16-row x 16-column tile per wave, 4 column tiles per block (A rows shared in L1)
+//   [nR+nP, ...)     value_fc1  [rows, A] x [A, 64] pre-activation, f32 MFMA, 4 column tiles per block
+// k_head_finish: one wave per row: value_fc1 bias + ReLU, value_fc2, support_to_scalar; reward
+//   partial sums + bias + ReLU, reward_fc2, support_to_scalar.
+// f32 MFMA operands: a k-chunk of 16 is read as one float4 per lane (lane group g = lane/16 holds
+// k = 16c + 4g + j for MFMA j), the same permutation for A and B, so one 16-byte load feeds 4 MFMAs.
 constexpr int RFC_UNROLL = 8;
-__global__ void __launch_bounds__(256) k_reward_fc1(const uint16_t *__restrict__ pool, const int32_t *__restrict__ out_slot,
-                                                    int rows, int K, const uint16_t *__restrict__ wpk, int nks, int ksplit,
-                                                    float *__restrict__ part) {
+struct HeadGemmArgs {
+  const uint16_t *pool;      // reward: hidden slots
+  const int32_t *out_slot;
+  int rows, K, nks, ksplit;  // reward GEMM: K = A*128, nks = K/32 k-steps, split-K factor
+  const uint16_t *rw;        // reward_fc1 fragments
+  float *rpart;              // [ksplit][rows][64]
+  const float *pv;           // [rows][pv_stride(A)]
+  int A, nrt, ncg;           // 16-row tiles, policy column groups (4 tiles each)
+  const float *pw, *pb;      // policy_fc [r16(A)][pv_kpol(A)] output-major, zero padded; bias [A]
+  float *logits;             // [rows][A]
+  const float *vw;           // value_fc1 [64][pv_kval(A)] output-major, zero padded
+  float *vpre;               // [rows][64]
+  int nR, nP;
+};
+
+__device__ __forceinline__ void reward_fc1_block(const HeadGemmArgs &h, int bx, int ks) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int rbase = blockIdx.x * 64 + w * 16, ks = blockIdx.y;
+  const int rbase = bx * 64 + w * 16;
   const int m = rbase + (lane & 15);
-  const int slot = m < rows ? out_slot[m] : -1;
-  const uint16_t *hrow = pool + (size_t)(slot >= 0 ? slot : 0) * K + 8 * (lane >> 4);
-  const int k0 = (int)((long long)nks * ks / ksplit), k1 = (int)((long long)nks * (ks + 1) / ksplit);
+  const int slot = m < h.rows ? h.out_slot[m] : -1;
+  const uint16_t *hrow = h.pool + (size_t)(slot >= 0 ? slot : 0) * h.K + 8 * (lane >> 4);
+  const int k0 = (int)((long long)h.nks * ks / h.ksplit), k1 = (int)((long long)h.nks * (ks + 1) / h.ksplit);
   f32x4 acc[4] = {};
-  const bf16x8_t *wv = (const bf16x8_t *)wpk + lane;
+  const bf16x8_t *wv = (const bf16x8_t *)h.rw + lane;
   int kk = k0;
   for (; kk + RFC_UNROLL <= k1; kk += RFC_UNROLL) {
     bf16x8_t a[RFC_UNROLL], b[RFC_UNROLL][4];
@@ -736,18 +785,73 @@ __global__ void __launch_bounds__(256) k_reward_fc1(const uint16_t *__restrict__
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int mm = rbase + (lane >> 4) * 4 + e;
-      if (mm < rows) part[((size_t)ks * rows + mm) * 64 + nt * 16 + (lane & 15)] = acc[nt][e];
+      if (mm < h.rows) h.rpart[((size_t)ks * h.rows + mm) * 64 + nt * 16 + (lane & 15)] = acc[nt][e];
     }
 }
 
-struct HeadArgs {
-  const float *pv_feat;
-  const int32_t *out_slot;
-  const float *pfc_w, *pfc_b, *vfc1_w, *vfc1_b, *vfc2_w, *vfc2_b;
-  const float *rpart, *rfc1_b, *rfc2_w, *rfc2_b;
-  int rows, A, hd, ksplit;
-  float *logits, *value, *reward;
-};
+// one wave: D[16 rows][16 cols] = pv[rows, koff : koff+K] x W[col][0:K]^T (f32 MFMA), K % 16 == 0
+template <int UNR>
+__device__ __forceinline__ f32x4 f32_tile(const float *__restrict__ pv, int pvs, int row, int koff,
+                                          const float *__restrict__ wrow, int K) {
+  const int g = threadIdx.x & 63;
+  const float *ap = pv + (size_t)row * pvs + koff + 4 * (g >> 4);
+  const float *bp = wrow + 4 * (g >> 4);
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  int c = 0;
+  for (; c + 16 * UNR <= K; c += 16 * UNR) {
+    f32x4 a[UNR], b[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      a[u] = *(const f32x4 *)(ap + c + 16 * u);
+      b[u] = *(const f32x4 *)(bp + c + 16 * u);
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][0], b[u][0], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][1], b[u][1], acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][2], b[u][2], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][3], b[u][3], acc1, 0, 0, 0);
+    }
+  }
+  for (; c < K; c += 16) {
+    const f32x4 a = *(const f32x4 *)(ap + c), b = *(const f32x4 *)(bp + c);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b[0], acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], b[1], acc1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], b[2], acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], b[3], acc1, 0, 0, 0);
+  }
+  return acc0 + acc1;
+}
+
+__global__ void __launch_bounds__(256) k_head_gemm(HeadGemmArgs h) {
+  int b = blockIdx.x;
+  if (b < h.nR) {
+    const int nbx = (h.rows + 63) / 64;
+    reward_fc1_block(h, b % nbx, b / nbx);
+    return;
+  }
+  b -= h.nR;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, A = h.A, pvs = pv_stride(A);
+  const bool pol = b < h.nP;
+  if (!pol) b -= h.nP;
+  const int rt = b % h.nrt, nt = (pol ? (b / h.nrt) * 4 : 0) + w;
+  if (pol && nt * 16 >= A) return;  // the last column group's empty tiles
+  const int ra = min(rt * 16 + (lane & 15), h.rows - 1);  // A-operand row (clamped; rows independent)
+  const int col = nt * 16 + (lane & 15);
+  f32x4 d;
+  if (pol) d = f32_tile<4>(h.pv, pvs, ra, 0, h.pw + (size_t)col * pv_kpol(A), pv_kpol(A));
+  else d = f32_tile<4>(h.pv, pvs, ra, pv_kpol(A), h.vw + (size_t)col * pv_kval(A), pv_kval(A));
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int row = rt * 16 + (lane >> 4) * 4 + e;
+    if (row >= h.rows) continue;
+    if (pol) {
+      if (col < A && h.out_slot[row] >= 0) h.logits[(size_t)row * A + col] = d[e] + h.pb[col];
+    } else {
+      h.vpre[(size_t)row * 64 + col] = d[e];
+    }
+  }
+}
 
 __device__ __forceinline__ float support3(float l0, float l1, float l2) {
   // support_to_scalar with support linspace(-1, 1, 3) (network.py:9-13)
@@ -758,131 +862,45 @@ __device__ __forceinline__ float support3(float l0, float l1, float l2) {
   return (-1.f * p0 + 0.f * p1) + 1.f * p2;
 }
 
-// Prediction heads (+ reward head): 4 rows per 1024-thread block so every weight is read once per
-// block; features are staged k-major ([k][4 rows]) so one ds_read_b128 feeds 4 FMAs.  The block is
-// latency-bound on L2 weight reads, so every reduction is split over enough threads that each keeps
-// at most ~8 batches of 16 loads in flight:
-//   0: stage features and fc2 weights; reward_fc.0 split-K partials reduced in 4 parts per (row, unit)
-//   1: policy_fc in 4 k-parts (4A threads); value_fc1 in 16 k-chunks (1024 threads)
-//   2: combine + bias -> logits; value_fc1 bias + ReLU; reward bias + ReLU
-//   3: value / reward fc2 as wave reductions, support_to_scalar.
-constexpr int HEAD_ROWS = 4, HEAD_THREADS = 1024, HEAD_KP = 4, HEAD_VQ = 16;
-__global__ void __launch_bounds__(HEAD_THREADS) k_heads(HeadArgs h) {
-  extern __shared__ float sm[];
-  const int r0 = blockIdx.x * HEAD_ROWS, tid = threadIdx.x;
-  const int A = h.A, hd = h.hd;
-  float *feat = sm;                               // [3A][4]
-  float *ppart = feat + 3 * A * HEAD_ROWS;        // [KP][A][4]
-  float *vpart = ppart + HEAD_KP * A * HEAD_ROWS; // [VQ][4 rows][64]
-  float *rsum = vpart + HEAD_VQ * HEAD_ROWS * 64; // [4 parts][4 rows][64]
-  float *hv = rsum + 4 * HEAD_ROWS * 64;          // [4][64]
-  float *hr = hv + HEAD_ROWS * 64;                // [4][64]
-  float *w2 = hr + HEAD_ROWS * 64;                // [2][64 * 3]: value_fc2, reward_fc2
-  bool valid[HEAD_ROWS];
+struct HeadFinishArgs {
+  const int32_t *out_slot;
+  int rows, hd, ksplit;
+  const float *vpre, *vb1, *vw2, *vb2;              // value head
+  const float *rpart, *rb1, *rw2, *rb2;             // reward head (rpart == nullptr: none)
+  float *value, *reward;
+};
+
+__global__ void __launch_bounds__(256) k_head_finish(HeadFinishArgs h) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), j = threadIdx.x & 63;
+  if (r >= h.rows || h.out_slot[r] < 0) return;
+  const bool on = j < h.hd;
+  {  // value_fc1 bias + ReLU, value_fc2, support_to_scalar (network.py:72-76)
+    const float v = on ? fmaxf(h.vpre[(size_t)r * 64 + j] + h.vb1[j], 0.f) : 0.f;
+    float l[3];
 #pragma unroll
-  for (int i = 0; i < HEAD_ROWS; ++i) valid[i] = r0 + i < h.rows && h.out_slot[r0 + i] >= 0;
-  for (int idx = tid; idx < 3 * A * HEAD_ROWS; idx += HEAD_THREADS) {
-    const int k = idx >> 2, i = idx & 3;
-    feat[idx] = valid[i] ? h.pv_feat[(size_t)(r0 + i) * 3 * A + k] : 0.f;
+    for (int k = 0; k < 3; ++k) l[k] = dred_sum_f(on ? v * h.vw2[j * 3 + k] : 0.f) + h.vb2[k];
+    if (j == 0) h.value[r] = support3(l[0], l[1], l[2]);
   }
-  if (tid < hd * 3) {
-    w2[tid] = h.vfc2_w[tid];
-    if (h.reward) w2[192 + tid] = h.rfc2_w[tid];
-  }
-  if (h.reward) {  // reward_fc.0 split-K partials: (part, row, unit) per thread
-    const int part = tid >> 8, i = (tid >> 6) & 3, j = tid & 63;
+  if (h.rpart) {  // reward_fc.0 partials + bias + ReLU, reward_fc.2, support_to_scalar (network.py:84-88)
     float s = 0.f;
-    if (j < hd && valid[i]) {
-      const int k0 = part * h.ksplit / 4, k1 = (part + 1) * h.ksplit / 4;
-      const float *src = h.rpart + (size_t)(r0 + i) * 64 + j;
+    if (on) {
+      const float *src = h.rpart + (size_t)r * 64 + j;
       const size_t stride = (size_t)h.rows * 64;
-      int k = k0;
-      for (; k + 8 <= k1; k += 8) {
+      int k = 0;
+      for (; k + 8 <= h.ksplit; k += 8) {
         float v[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) v[u] = src[(k + u) * stride];
 #pragma unroll
         for (int u = 0; u < 8; ++u) s += v[u];
       }
-      for (; k < k1; ++k) s += src[k * stride];
+      for (; k < h.ksplit; ++k) s += src[k * stride];
+      s = fmaxf(h.rb1[j] + s, 0.f);
     }
-    rsum[(part * HEAD_ROWS + i) * 64 + j] = s;
-  }
-  __syncthreads();
-  const int kchunk = (2 * A + HEAD_KP - 1) / HEAD_KP;
-  for (int ti = tid; ti < HEAD_KP * A; ti += HEAD_THREADS) {  // policy_fc (network.py:70), k-part kp
-    const int kp = ti / A, a = ti - kp * A;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    const float *wcol = h.pfc_w + a;
-    int k = kp * kchunk;
-    const int ke = min(k + kchunk, 2 * A);
-    for (; k + 16 <= ke; k += 16) {  // 16 independent weight loads in flight per thread
-      float wv[16];
+    float l[3];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) wv[u] = wcol[(size_t)(k + u) * A];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) acc += *(const f32x4 *)(feat + 4 * (k + u)) * wv[u];
-    }
-    for (; k < ke; ++k) acc += *(const f32x4 *)(feat + 4 * k) * wcol[(size_t)k * A];
-    *(f32x4 *)(ppart + 4 * (kp * A + a)) = acc;
-  }
-  {  // value_fc1 (network.py:72), k-chunk q of the A value features
-    const int q = tid >> 6, j = tid & 63;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    if (j < hd) {
-      const int p0 = q * A / HEAD_VQ, p1 = (q + 1) * A / HEAD_VQ;
-      const float *wcol = h.vfc1_w + j;
-      int p = p0;
-      for (; p + 8 <= p1; p += 8) {
-        float wv[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) wv[u] = wcol[(p + u) * hd];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) acc += *(const f32x4 *)(feat + 4 * (2 * A + p + u)) * wv[u];
-      }
-      for (; p < p1; ++p) acc += *(const f32x4 *)(feat + 4 * (2 * A + p)) * wcol[p * hd];
-    }
-#pragma unroll
-    for (int i = 0; i < HEAD_ROWS; ++i) vpart[(q * HEAD_ROWS + i) * 64 + j] = acc[i];
-  }
-  __syncthreads();
-  for (int a = tid; a < A; a += HEAD_THREADS) {
-    const float b = h.pfc_b[a];
-    f32x4 sum = *(const f32x4 *)(ppart + 4 * a);
-#pragma unroll
-    for (int kp = 1; kp < HEAD_KP; ++kp) sum += *(const f32x4 *)(ppart + 4 * (kp * A + a));
-#pragma unroll
-    for (int i = 0; i < HEAD_ROWS; ++i)
-      if (valid[i]) h.logits[(size_t)(r0 + i) * A + a] = b + sum[i];
-  }
-  if (tid < HEAD_ROWS * 64) {  // value_fc1 bias + ReLU
-    const int i = tid >> 6, j = tid & 63;
-    if (j < hd) {
-      float s = 0.f;
-#pragma unroll
-      for (int q = 0; q < HEAD_VQ; ++q) s += vpart[(q * HEAD_ROWS + i) * 64 + j];
-      hv[i * 64 + j] = fmaxf(h.vfc1_b[j] + s, 0.f);
-    }
-  } else if (h.reward && tid < 2 * HEAD_ROWS * 64) {  // reward_fc.0 bias + ReLU (network.py:84-86)
-    const int i = (tid >> 6) & 3, j = tid & 63;
-    if (j < hd)
-      hr[i * 64 + j] = fmaxf(h.rfc1_b[j] + ((rsum[(0 * HEAD_ROWS + i) * 64 + j] + rsum[(1 * HEAD_ROWS + i) * 64 + j]) +
-                                            (rsum[(2 * HEAD_ROWS + i) * 64 + j] + rsum[(3 * HEAD_ROWS + i) * 64 + j])), 0.f);
-  }
-  __syncthreads();
-  const int w = tid >> 6, lane = tid & 63;
-  if (w < 2 && (w == 0 || h.reward)) {  // wave 0: value head, wave 1: reward head (fc2 + support)
-    const float *hx = w == 0 ? hv : hr;
-    const float *wx = w2 + 192 * w;
-    const float *bx = w == 0 ? h.vfc2_b : h.rfc2_b;
-    float *out = w == 0 ? h.value : h.reward;
-#pragma unroll
-    for (int i = 0; i < HEAD_ROWS; ++i) {
-      float l[3];
-#pragma unroll
-      for (int k = 0; k < 3; ++k) l[k] = dred_sum_f(lane < hd ? hx[i * 64 + lane] * wx[lane * 3 + k] : 0.f) + bx[k];
-      if (lane == 0 && valid[i]) out[r0 + i] = support3(l[0], l[1], l[2]);
-    }
+    for (int k = 0; k < 3; ++k) l[k] = dred_sum_f(on ? s * h.rw2[j * 3 + k] : 0.f) + h.rb2[k];
+    if (j == 0) h.reward[r] = support3(l[0], l[1], l[2]);
   }
 }
 
@@ -947,12 +965,13 @@ static int tower(int H, bool dyn, const TowerArgs &a, hipStream_t s) {
 
 // split-K factor of the reward GEMM: 32 -> (rows/64) x 32 blocks keep ~64 KB of hidden-state reads
 // in flight per CU (16: 31 us, 32: 22 us, 64: 21.5 us at 1024 rows, the partials then cost more in
-// k_heads)
+// k_head_finish)
 static constexpr int KSPLIT = 32;
 
-// workspace: [pv_feat rows*3*A f32][reward partials KSPLIT*rows*64 f32][residual scratch (19x19)]
+// workspace: [pv rows*pv_stride(A) f32][reward partials KSPLIT*rows*64 f32][value_fc1 rows*64 f32]
+//            [residual scratch (19x19)]
 static size_t ws_head_bytes(int A, int rows) {
-  return (size_t)rows * 3 * A * sizeof(float) + (size_t)KSPLIT * rows * 64 * sizeof(float);
+  return ((size_t)rows * pv_stride(A) + (size_t)KSPLIT * rows * 64 + (size_t)rows * 64) * sizeof(float);
 }
 static size_t ws_bytes(int A, int rows) {
   int H = 0;
@@ -978,14 +997,23 @@ GMZ_EXPORT int gmz_net_workspace_bytes(const gmz_net_weights *w, int rows, size_
   return 0;
 }
 
-static int heads(const gmz_net_weights *w, const float *pv, const int32_t *out_slot, int rows, const float *rpart,
+// the heads of `rows` rows whose tower output (pv rows, hidden slots) is in place; reward != nullptr
+// adds the reward head (recurrent rows)
+static int heads(const gmz_net_weights *w, const uint16_t *pool, const int32_t *out_slot, int rows, void *workspace,
                  float *logits, float *value, float *reward, hipStream_t s) {
-  const int A = w->board_size * w->board_size;
-  HeadArgs h{pv, out_slot, w->policy_fc_w, w->policy_fc_b, w->value_fc1_w, w->value_fc1_b, w->value_fc2_w,
-             w->value_fc2_b, rpart, w->reward_fc1_b, w->reward_fc2_w, w->reward_fc2_b, rows, A, w->head_hidden,
-             KSPLIT, logits, value, reward};
-  const size_t smem = ((3 + HEAD_KP) * A * HEAD_ROWS + (HEAD_VQ + 4 + 2) * HEAD_ROWS * 64 + 2 * 192) * sizeof(float);
-  hipLaunchKernelGGL(k_heads, dim3((rows + HEAD_ROWS - 1) / HEAD_ROWS), dim3(HEAD_THREADS), smem, s, h);
+  const int A = w->board_size * w->board_size, K = A * C;
+  float *pv = (float *)workspace;
+  float *rpart = pv + (size_t)rows * pv_stride(A);
+  float *vpre = rpart + (size_t)KSPLIT * rows * 64;
+  const int nrt = (rows + 15) / 16, ncg = ((A + 15) / 16 + 3) / 4;
+  const int nR = reward ? ((rows + 63) / 64) * KSPLIT : 0, nP = nrt * ncg, nV = nrt;
+  HeadGemmArgs g{pool, out_slot, rows, K, K / 32, KSPLIT, w->reward_fc1_w, rpart, pv, A, nrt, ncg,
+                 w->policy_fc_w, w->policy_fc_b, logits, w->value_fc1_w, vpre, nR, nP};
+  hipLaunchKernelGGL(k_head_gemm, dim3(nR + nP + nV), dim3(256), 0, s, g);
+  GMZ_LAUNCH_CHECK();
+  HeadFinishArgs f{out_slot, rows, w->head_hidden, KSPLIT, vpre, w->value_fc1_b, w->value_fc2_w, w->value_fc2_b,
+                   reward ? rpart : nullptr, w->reward_fc1_b, w->reward_fc2_w, w->reward_fc2_b, value, reward};
+  hipLaunchKernelGGL(k_head_finish, dim3((rows + 3) / 4), dim3(256), 0, s, f);
   GMZ_LAUNCH_CHECK();
   return 0;
 }
@@ -1000,8 +1028,7 @@ GMZ_EXPORT int gmz_net_initial(const gmz_net_weights *w, const float *obs, int r
   TowerArgs a{w->repr_convs, w->repr_bias, 2 * w->blocks, w->repr_stem_w, w->repr_stem_b, nullptr, obs, pool,
               nullptr, nullptr, out_slot, w->head_conv_w, w->head_conv_b, pv, rows, ws_xres(workspace, A, rows)};
   if (tower(H, false, a, s)) return -1;
-  (void)A;
-  return heads(w, pv, out_slot, rows, nullptr, logits, value, nullptr, s);
+  return heads(w, pool, out_slot, rows, workspace, logits, value, nullptr, s);
 }
 
 GMZ_EXPORT int gmz_net_recurrent_tower(const gmz_net_weights *w, uint16_t *pool, const int32_t *in_slot,
@@ -1021,15 +1048,7 @@ GMZ_EXPORT int gmz_net_recurrent_heads(const gmz_net_weights *w, const uint16_t 
   if (check_w(w)) return -1;
   if (rows <= 0 || !pool || !out_slot || !logits || !value || !reward || !workspace)
     return fail("gmz_net_recurrent_heads: bad argument");
-  const int A = w->board_size * w->board_size;
-  hipStream_t s = (hipStream_t)stream;
-  float *pv = (float *)workspace;
-  float *rpart = pv + (size_t)rows * 3 * A;
-  const int K = A * C, nks = K / 32;
-  hipLaunchKernelGGL(k_reward_fc1, dim3((rows + 63) / 64, KSPLIT), dim3(256), 0, s, pool, out_slot, rows, K,
-                     w->reward_fc1_w, nks, KSPLIT, rpart);
-  GMZ_LAUNCH_CHECK();
-  return heads(w, pv, out_slot, rows, rpart, logits, value, reward, s);
+  return heads(w, pool, out_slot, rows, workspace, logits, value, reward, (hipStream_t)stream);
 }
 
 GMZ_EXPORT int gmz_net_recurrent(const gmz_net_weights *w, uint16_t *pool, const int32_t *in_slot, const int32_t *action,

@@ -89,6 +89,18 @@ def pack_stem(wf):
     return _bf16_bits(Wk[nt * 16 + (l & 15), 8 * (l >> 4) + j])
 
 
+def r16(x):
+    return (x + 15) // 16 * 16
+
+
+def pad_fc(w, rows, cols):
+    """torch Linear weight [out, in] -> f32 [rows][cols], zero padded (output-major, k contiguous:
+    the f32-MFMA head GEMMs read one 16-float k-chunk per lane group)."""
+    out = np.zeros((rows, cols), np.float32)
+    out[:w.shape[0], :w.shape[1]] = w
+    return out
+
+
 def pack_reward_fc1(w, A):
     """reward_fc.0.weight [hd, C*A] (NCHW-flatten input) -> bf16 B fragments [K/32][hd/16][64][8]
     over the NHWC hidden order k = p*C + c."""
@@ -137,9 +149,9 @@ def pack_weights(sd, cfg):
     hb = np.concatenate([_f32(sd["prediction_net.policy_conv.bias"]) * sp + bp,
                          _f32(sd["prediction_net.value_conv.bias"]) * sv + bv])
     out["head_conv_w"], out["head_conv_b"] = hw.astype(np.float32), hb.astype(np.float32)
-    out["policy_fc_w"] = np.ascontiguousarray(_f32(sd["prediction_net.policy_fc.weight"]).T)
+    out["policy_fc_w"] = pad_fc(_f32(sd["prediction_net.policy_fc.weight"]), r16(A), r16(2 * A))
     out["policy_fc_b"] = _f32(sd["prediction_net.policy_fc.bias"])
-    out["value_fc1_w"] = np.ascontiguousarray(_f32(sd["prediction_net.value_fc1.weight"]).T)
+    out["value_fc1_w"] = pad_fc(_f32(sd["prediction_net.value_fc1.weight"]), 64, r16(A))
     out["value_fc1_b"] = _f32(sd["prediction_net.value_fc1.bias"])
     out["value_fc2_w"] = np.ascontiguousarray(_f32(sd["prediction_net.value_fc2.weight"]).T)
     out["value_fc2_b"] = _f32(sd["prediction_net.value_fc2.bias"])

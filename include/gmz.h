@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define GMZ_ABI_VERSION 1
+#define GMZ_ABI_VERSION 2
 
 /* ------------------------------------------------------------------ misc */
 const char *gmz_last_error(void);
@@ -182,9 +182,9 @@ typedef struct gmz_net_weights {
   const float *dyn_action;      /* [9][C] action-embedding contribution per tap (BN folded)        */
   const float *head_conv_w;     /* [3][C] policy (2) + value (1) 1x1 convs, BN folded              */
   const float *head_conv_b;     /* [3]                                                             */
-  const float *policy_fc_w;     /* [2A][A]  (input-major)                                          */
+  const float *policy_fc_w;     /* [r16(A)][r16(2A)] output-major, zero padded (r16 = round up to 16) */
   const float *policy_fc_b;     /* [A]                                                             */
-  const float *value_fc1_w;     /* [A][hd]                                                         */
+  const float *value_fc1_w;     /* [64][r16(A)] output-major, zero padded                          */
   const float *value_fc1_b;     /* [hd]                                                            */
   const float *value_fc2_w;     /* [hd][3]                                                         */
   const float *value_fc2_b;     /* [3]                                                             */

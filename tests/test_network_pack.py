@@ -81,8 +81,8 @@ def emulate(pk, cfg, obs=None, h=None, action=None):
     B = x.shape[0]
     feat = np.maximum(np.einsum("oc,bchw->bohw", pk["head_conv_w"], x) + pk["head_conv_b"].reshape(1, 3, 1, 1), 0)
     feat = feat.reshape(B, 3 * A)
-    logits = feat[:, :2 * A] @ pk["policy_fc_w"] + pk["policy_fc_b"]
-    hv = np.maximum(feat[:, 2 * A:] @ pk["value_fc1_w"] + pk["value_fc1_b"], 0)
+    logits = feat[:, :2 * A] @ pk["policy_fc_w"][:A, :2 * A].T + pk["policy_fc_b"]
+    hv = np.maximum(feat[:, 2 * A:] @ pk["value_fc1_w"][:, :A].T + pk["value_fc1_b"], 0)
     value = netref.support_to_scalar(hv @ pk["value_fc2_w"] + pk["value_fc2_b"])
     reward = None
     if obs is None:

@@ -44,7 +44,7 @@ int main(int argc, char **argv) {
   uint16_t *dw, *dpool; float *dbias, *dact, *dhw, *dhb, *dpv; int *din, *dout, *dac;
   CK(hipMalloc(&dw, w.size() * 2)); CK(hipMalloc(&dpool, pool.size() * 2));
   CK(hipMalloc(&dbias, bias.size() * 4)); CK(hipMalloc(&dact, act.size() * 4)); CK(hipMalloc(&dhw, hw.size() * 4));
-  CK(hipMalloc(&dhb, 16)); CK(hipMalloc(&dpv, (size_t)rows * 3 * A * 4));
+  CK(hipMalloc(&dhb, 16)); CK(hipMalloc(&dpv, (size_t)rows * pv_stride(A) * 4));
   CK(hipMalloc(&din, rows * 4)); CK(hipMalloc(&dout, rows * 4)); CK(hipMalloc(&dac, rows * 4));
   CK(hipMemcpy(dw, w.data(), w.size() * 2, hipMemcpyHostToDevice));
   CK(hipMemcpy(dpool, pool.data(), pool.size() * 2, hipMemcpyHostToDevice));
@@ -61,7 +61,7 @@ int main(int argc, char **argv) {
   const double flop = 1136505600.0 * rows;
   {  // k_tower3 must reproduce k_tower (LDS-staged weights, rotated image) bit for bit
     std::vector<uint16_t> o1((size_t)rows * A * 128), o2(o1.size());
-    std::vector<float> p1((size_t)rows * 3 * A), p2(p1.size());
+    std::vector<float> p1((size_t)rows * pv_stride(A)), p2(p1.size());
     hipLaunchKernelGGL((k_tower<15, true, 0>), dim3(rows), dim3(512), 0, 0, a);
     CK(hipMemcpy(o1.data(), dpool + (size_t)rows * A * 128, o1.size() * 2, hipMemcpyDeviceToHost));
     CK(hipMemcpy(p1.data(), dpv, p1.size() * 4, hipMemcpyDeviceToHost));
@@ -93,22 +93,21 @@ int main(int argc, char **argv) {
     for (size_t i = 0; i < p1.size(); ++i) dp += p1[i] != p2[i];
     printf("tower3 8w (4x2) vs tower: hidden mismatches %zu / %zu, pv mismatches %zu / %zu\n", dh, o1.size(), dp, p1.size());
   }
-  const char *names[] = {"k_tower (LDS-staged weights)", "k_tower3 8w (2x4) RD4", "k_tower3 12w (4x3) RD3 [product]",
-                         "k_tower3 12w no-io(32)", "k_tower3 12w no-A-loads(2)", "k_tower3 8w (4x2) RD3",
-                         "k_tower3 8w (4x2) RD4", "k_tower3 8w (4x2) RD2", "k_tower3 4w (2x2) RD3"};
+  const char *names[] = {"k_tower (LDS-staged weights)", "k_tower3 12w (4x3) RD3", "k_tower3 8w (4x2) RD3 [product]",
+                         "8w no-io(32)", "8w no-A-loads(2)", "8w no-epilogue(512)", "8w no-barrier(1024)",
+                         "8w no-epilogue no-barrier", "8w A-from-one-kstep(1)"};
   const int NV = 9;
   float best[NV];
   for (int i = 0; i < NV; ++i) best[i] = 1e9f;
   for (int round = 0; round < 5; ++round) {
-    float t[NV] = {run<0>(a, 5), run<0, 3>(a, 5), run<0, 3, 3, 4, 3>(a, 5), run<32, 3, 3, 4, 3>(a, 5),
-                   run<2, 3, 3, 4, 3>(a, 5), run<0, 3, 3, 4, 2>(a, 5), run<0, 3, 4, 4, 2>(a, 5),
-                   run<0, 3, 2, 4, 2>(a, 5), run<0, 3, 3, 2, 2>(a, 5)};
+    float t[NV] = {run<0>(a, 5), run<0, 3, 3, 4, 3>(a, 5), run<0, 3, 3, 4, 2>(a, 5), run<32, 3, 3, 4, 2>(a, 5),
+                   run<2, 3, 3, 4, 2>(a, 5), run<512, 3, 3, 4, 2>(a, 5), run<1024, 3, 3, 4, 2>(a, 5),
+                   run<1536, 3, 3, 4, 2>(a, 5), run<1, 3, 3, 4, 2>(a, 5)};
     for (int i = 0; i < NV; ++i) best[i] = t[i] < best[i] ? t[i] : best[i];
   }
   for (int i = 0; i < NV; ++i)
     printf("%-36s %8.3f ms   %7.1f TFLOP/s\n", names[i], best[i], flop / (best[i] * 1e-3) / 1e12);
-  auto stamps = [&](const char *what, float ms_per_launch, auto launch) -> int {
-    constexpr int NWV = 12;
+  auto stamps = [&](const char *what, int NWV, float ms_per_launch, auto launch) -> int {
     for (int k = 0; k < 3; ++k) launch();
     std::vector<float> st(256 * NWV * 4);
     CK(hipMemcpy(st.data(), dpv, st.size() * 4, hipMemcpyDeviceToHost));
@@ -121,20 +120,9 @@ int main(int argc, char **argv) {
            sum[3] / (256 * NWV) / (ms_per_launch * 1e-3) / 1e9);
     return 0;
   };
-  stamps("product (no io)", run<128 | 32, 3, 3, 4, 3>(a, 5), [&] { run<128 | 32, 3, 3, 4, 3>(a, 1); });
-  stamps("no-A-loads (no io)", run<128 | 32 | 2, 3, 3, 4, 3>(a, 5), [&] { run<128 | 32 | 2, 3, 3, 4, 3>(a, 1); });
-  if (0) {
-    constexpr int NWV = 12;
-    for (int k = 0; k < 3; ++k) run<128 | 32, 3, 3, 4, 3>(a, 5);
-    std::vector<float> st(256 * NWV * 4);
-    CK(hipMemcpy(st.data(), dpv, st.size() * 4, hipMemcpyDeviceToHost));
-    double sum[4] = {0, 0, 0, 0};
-    for (int i = 0; i < 256 * NWV; ++i)
-      for (int k = 0; k < 4; ++k) sum[k] += st[i * 4 + k];
-    const double per = 256.0 * NWV * 17 * ((rows + 255) / 256);
-    printf("k_tower3 (12w) per layer and wave (s_memtime cycles): k-loop %.0f  epilogue %.0f  barrier %.0f  (whole kernel %.0f)\n",
-           sum[0] / per, sum[1] / per, sum[2] / per, sum[3] / (256 * NWV));
-  }
+  stamps("12w (no io)", 12, run<128 | 32, 3, 3, 4, 3>(a, 5), [&] { run<128 | 32, 3, 3, 4, 3>(a, 1); });
+  stamps("8w product (no io)", 8, run<128 | 32, 3, 3, 4, 2>(a, 5), [&] { run<128 | 32, 3, 3, 4, 2>(a, 1); });
+  stamps("8w no-A-loads (no io)", 8, run<128 | 32 | 2, 3, 3, 4, 2>(a, 5), [&] { run<128 | 32 | 2, 3, 3, 4, 2>(a, 1); });
   CK(hipDeviceSynchronize());
   return 0;
 }
