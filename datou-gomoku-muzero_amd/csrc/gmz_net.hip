@@ -67,6 +67,17 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
   return __builtin_bit_cast(uint16_t, b);
 }
 __device__ __forceinline__ float bf2f(uint16_t u) { return __uint_as_float(((uint32_t)u) << 16); }
+// ReLU(bf16(a)), ReLU(bf16(b)) packed: round first, then max(., 0) on the bf16 bit patterns as
+// signed 16-bit integers (negative bf16 <=> sign bit set; -0 -> +0): one v_pk_max_i16 for two
+// values, and round(relu(x)) == relu(round(x)) since rounding keeps the sign
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t relu_bf16x2(float a, float b) {
+  const bf16x2_t h = __builtin_convertvector((f32x2){a, b}, bf16x2_t);  // one v_cvt_pk_bf16_f32
+  const s16x2 v = __builtin_elementwise_max(__builtin_bit_cast(s16x2, h), (s16x2){0, 0});
+  return __builtin_bit_cast(uint32_t, v);
+}
 
 // LDS image of the padded board: position q = (y+1)*HP + (x+1) owns 256 B = 16 chunks of 8 channels.
 // Chunk c of position q lives in 16-B slot (c + key(q)) & 15 with key(q) = (y*H + x) & 15 computed
@@ -568,10 +579,11 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
       // the next layer's bias (for the last layer: the next board's layer 0) -> the other slot;
       // that slot was last read by the previous layer's epilogue, which the barrier has closed
       issue_bias(L + 1 < t.n_layers ? L + 1 : 0, (gl + 1) & 1);
+      // this layer's bias is the C operand of every tile's first MFMA (no bias add in the epilogue)
+      const float *bias = sbias + (gl & 1) * C;
+      f32x4 bv[NTW];
 #pragma unroll
-      for (int nt = 0; nt < NTW; ++nt)
-#pragma unroll
-        for (int i = 0; i < PTW; ++i) acc[nt][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int nt = 0; nt < NTW; ++nt) bv[nt] = *(const f32x4 *)(bias + (nh * NTW + nt) * 16 + g4 * 4);
       int bb[PTW];
 #pragma unroll
       for (int i = 0; i < PTW; ++i) {
@@ -582,6 +594,10 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
       // group: its empty slot costs neither MFMAs nor LDS reads)
       auto kloop = [&](auto ntl_c) {
         constexpr int NTL = decltype(ntl_c)::value;
+#pragma unroll
+        for (int i = NTL; i < PTW; ++i)
+#pragma unroll
+          for (int nt = 0; nt < NTW; ++nt) acc[nt][i] = bv[nt];  // the empty slot (never stored)
         bf16x8_t b[2][NTL];
         auto readB = [&](int buf, int st) {
           const int tap = st >> 2, ks = st & 3;
@@ -602,7 +618,8 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
           for (int i = 0; i < NTL; ++i)
 #pragma unroll
             for (int nt = 0; nt < NTW; ++nt)
-              acc[nt][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ar[st % RD][nt], b[st & 1][i], acc[nt][i], 0, 0, 0);
+              acc[nt][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ar[st % RD][nt], b[st & 1][i],
+                                                                   st == 0 ? bv[nt] : acc[nt][i], 0, 0, 0);
           // the last k-step stays open: the scheduler may start the epilogue of the tiles whose final
           // MFMA has issued while the remaining ones run (ABL & 256 pins it, for comparison)
           if ((ABL & 256) || st + 1 < KSTEPS) __builtin_amdgcn_sched_barrier(0);
@@ -612,17 +629,13 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
       else if (pg + PG * (PTW - 1) < NPT) kloop(std::integral_constant<int, PTW>{});
       else kloop(std::integral_constant<int, PTW - 1>{});
       if (ABL & 128) { st_t1 = __builtin_amdgcn_s_memtime(); st_loop += st_t1 - st_t0; }
-      // epilogue: bias (+ action term) (+ residual) + ReLU -> bf16 -> the other image.  One
-      // straight-line copy per layer kind; every LDS operand (bias, residual) is read in one batch
-      // before any arithmetic, so the epilogue pays one LDS latency, not one per tile.
+      // epilogue: (action term) (+ residual) + ReLU -> bf16 -> the other image.  One straight-line
+      // copy per layer kind; every LDS operand (residual) is read in one batch before any
+      // arithmetic, so the epilogue pays one LDS latency, not one per tile.
       const int kind = DYN ? (L == 0 ? 0 : ((L - 1) & 1) + 1) : ((L & 1) + 1);
-      const float *bias = sbias + (gl & 1) * C;
       if constexpr (ONE) __syncthreads();  // every wave is done reading the image it overwrites
       auto epilogue = [&](auto kind_c) {
         constexpr int KIND = decltype(kind_c)::value;
-        f32x4 bv[NTW];
-#pragma unroll
-        for (int nt = 0; nt < NTW; ++nt) bv[nt] = *(const f32x4 *)(bias + (nh * NTW + nt) * 16 + g4 * 4);
         u16x4 xr[NTW][PTW];
         if constexpr (KIND == 2 && !ONE) {
           // residual = this block's input, still in the image this epilogue overwrites, at the
@@ -648,7 +661,7 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
           }
 #pragma unroll
           for (int i = 0; i < PTW; ++i) {
-            f32x4 v = acc[nt][i] + bv[nt];
+            f32x4 v = acc[nt][i];
             if constexpr (DYN && KIND == 0) {
               const int p = (pg + PG * i) * 16 + sigma16(lane & 15);
               const int ddy = ay - p / H + 1, ddx = ax - p % H + 1;
@@ -658,9 +671,7 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
 #pragma unroll
               for (int e = 0; e < 4; ++e) v[e] += bf2f(xr[nt][i][e]);
             }
-            u16x4 o;
-#pragma unroll  // ReLU as med3(v, 0, FLT_MAX): one VALU, no NaN canonicalisation pair
-            for (int e = 0; e < 4; ++e) o[e] = f2bf(__builtin_amdgcn_fmed3f(v[e], 0.f, 3.402823466e38f));
+            const u16x4 o = __builtin_bit_cast(u16x4, make_uint2(relu_bf16x2(v[0], v[1]), relu_bf16x2(v[2], v[3])));
             if ((PG * i + PG) * 16 <= A || pos[i] >= 0) store_out(nimg, nt, i, o);
             if constexpr (ONE && KIND != 1) xs[(nt * PTW + i) * 64] = o;  // the next block's input
           }

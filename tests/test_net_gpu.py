@@ -54,7 +54,12 @@ def _check(p, v, pr, vr, what):
                                                                           np.abs(v - vr).max(), top1))
     assert (err <= bound).all()
     assert np.abs(v - vr).max() <= SCALAR_ABS
-    assert top1 >= 0.9
+    # top-1 must agree wherever the reference's top-1 margin exceeds twice the logit error seen on
+    # that row: a flip there cannot come from bf16 rounding (near-ties may flip; the rate is printed)
+    srt = np.sort(pr, axis=1)
+    decisive = (srt[:, -1] - srt[:, -2]) > 2 * err
+    assert (p.argmax(1) == pr.argmax(1))[decisive].all()
+    assert decisive.mean() >= 0.5  # the criterion must actually bite
 
 
 @pytest.mark.parametrize("size,blocks", [(15, 8), (9, 2), (6, 1), (19, 16), (19, 2)])
