@@ -1,0 +1,179 @@
+"""On-disk format of the self-play records: the reference's SQLite store.
+
+``RecordStore`` reads and writes the schema of db_manager.py:37-73 — tables ``games`` (pickled
+``GameRecord`` blob, analysis_version, move_count, status, timestamp), ``replay_buffer`` (one pickled
+``TrainingSlice`` blob per move) and ``trainer_state`` — in WAL mode (db_manager.py:19-26), so a
+database written by ``gpu_selfplay_worker``'s records can be resumed by the reference and vice versa.
+
+Blobs are written exactly as the reference writes them (``pickle.dumps(obj, HIGHEST_PROTOCOL)`` of
+``data_structures.GameRecord`` / ``TrainingSlice`` namedtuples holding numpy arrays), and read with a
+RESTRICTED unpickler that resolves only those two classes and numpy's array / dtype / scalar
+constructors: a blob naming anything else is rejected, never executed.  The ``trainer_state`` blob
+(a pickled dict of torch state_dicts and optimiser state, db_manager.py:229-242) is not read: it
+cannot be decoded without executing arbitrary pickled callables, and checkpoints travel as
+state_dicts (weights.py) instead.
+
+Re-analysis (db_manager.py:143-227) belongs to the control plane and is not mirrored.
+"""
+import io
+import os
+import pickle
+import sqlite3
+import sys
+import types
+
+from . import records as R
+
+_SCHEMA = (
+    # db_manager.py:40-48
+    """CREATE TABLE IF NOT EXISTS games (
+                    game_id INTEGER PRIMARY KEY AUTOINCREMENT,
+                    game_record BLOB NOT NULL,
+                    analysis_version INTEGER NOT NULL,
+                    move_count INTEGER NOT NULL,
+                    status TEXT DEFAULT 'PENDING' NOT NULL,
+                    timestamp DATETIME DEFAULT CURRENT_TIMESTAMP
+                )""",
+    "CREATE INDEX IF NOT EXISTS status_version_idx ON games (status, analysis_version);",
+    # db_manager.py:52-60
+    """CREATE TABLE IF NOT EXISTS replay_buffer (
+                    id INTEGER PRIMARY KEY AUTOINCREMENT,
+                    game_id INTEGER NOT NULL,
+                    move_index INTEGER NOT NULL,
+                    slice_data BLOB NOT NULL,
+                    FOREIGN KEY (game_id) REFERENCES games (game_id) ON DELETE CASCADE
+                )""",
+    "CREATE INDEX IF NOT EXISTS game_id_idx ON replay_buffer (game_id);",
+    # db_manager.py:64-69
+    """CREATE TABLE IF NOT EXISTS trainer_state (
+                    key TEXT PRIMARY KEY,
+                    state_blob BLOB
+                )""",
+)
+
+
+def _record_classes():
+    """(GameRecord, TrainingSlice) pickled under the module name ``data_structures``, as the
+    reference's own classes are (data_structures.py:9-26).  Inside the reference project those ARE
+    the classes (records.py imports them); standalone, records.py's field-identical namedtuples are
+    published under that module name so that blobs name the same class path."""
+    G, T = R.GameRecord, R.TrainingSlice
+    if G.__module__ != "data_structures":
+        mod = sys.modules.get("data_structures")
+        if mod is None:
+            mod = types.ModuleType("data_structures")
+            mod.__doc__ = "stand-in published by datou_gomoku_muzero_amd.formats (reference not importable)"
+            sys.modules["data_structures"] = mod
+        if getattr(mod, "GameRecord", None) is None:
+            G.__module__ = T.__module__ = "data_structures"
+            mod.GameRecord, mod.TrainingSlice = G, T
+        G, T = mod.GameRecord, mod.TrainingSlice
+    return G, T
+
+
+_NUMPY_GLOBALS = {
+    # ndarray (protocol 5: _frombuffer; older protocols: _reconstruct + ndarray), dtype, scalars
+    ("numpy._core.numeric", "_frombuffer"), ("numpy.core.numeric", "_frombuffer"),
+    ("numpy._core.multiarray", "_reconstruct"), ("numpy.core.multiarray", "_reconstruct"),
+    ("numpy._core.multiarray", "scalar"), ("numpy.core.multiarray", "scalar"),
+    ("numpy", "ndarray"), ("numpy", "dtype"),
+}
+
+
+class UnsafeBlobError(pickle.UnpicklingError):
+    pass
+
+
+class _RecordUnpickler(pickle.Unpickler):
+    def find_class(self, module, name):
+        if module == "data_structures" and name in ("GameRecord", "TrainingSlice"):
+            G, T = _record_classes()
+            return G if name == "GameRecord" else T
+        if (module, name) in _NUMPY_GLOBALS:
+            return super().find_class(module, name)
+        raise UnsafeBlobError("blob references %s.%s: only GameRecord / TrainingSlice and numpy arrays are "
+                              "decoded" % (module, name))
+
+
+def loads(blob):
+    """Decode a games / replay_buffer blob (restricted: nothing outside the record classes and
+    numpy's array constructors is resolved)."""
+    obj = _RecordUnpickler(io.BytesIO(bytes(blob))).load()
+    if not isinstance(obj, _record_classes()):
+        raise UnsafeBlobError("blob holds a %s, not a GameRecord / TrainingSlice" % type(obj).__name__)
+    return obj
+
+
+def dumps(obj):
+    """Encode a GameRecord / TrainingSlice exactly as db_manager.py:82,90 does."""
+    G, T = _record_classes()
+    if type(obj).__name__ == "GameRecord" and not isinstance(obj, G):
+        obj = G(*obj)
+    elif type(obj).__name__ == "TrainingSlice" and not isinstance(obj, T):
+        obj = T(*obj)
+    return pickle.dumps(obj, protocol=pickle.HIGHEST_PROTOCOL)
+
+
+class RecordStore:
+    """db_manager.DatabaseManager's persistence API for game records and training slices."""
+
+    def __init__(self, db_path="outputs/training_state.db"):
+        self.db_path = db_path
+        d = os.path.dirname(db_path)
+        if d:
+            os.makedirs(d, exist_ok=True)
+        self.conn = sqlite3.connect(db_path, check_same_thread=False, timeout=10)
+        self.conn.execute("PRAGMA journal_mode=WAL;")
+        self.conn.execute("PRAGMA synchronous=NORMAL;")
+        with self.conn:
+            for stmt in _SCHEMA:
+                self.conn.execute(stmt)
+
+    def close(self, checkpoint=True):
+        if checkpoint:  # fold the WAL into the main file (a single self-contained .db)
+            self.conn.execute("PRAGMA wal_checkpoint(TRUNCATE);")
+        self.conn.close()
+
+    def add_game_and_slices(self, game_record, prepared_slices, model_version):
+        """db_manager.py:75-104: one transaction; returns the new game_id (None on failure)."""
+        try:
+            with self.conn:
+                cur = self.conn.cursor()
+                cur.execute("INSERT INTO games (game_record, analysis_version, move_count) VALUES (?, ?, ?)",
+                            (dumps(game_record), model_version, len(game_record.actions)))
+                gid = cur.lastrowid
+                cur.executemany("INSERT INTO replay_buffer (game_id, move_index, slice_data) VALUES (?, ?, ?)",
+                                [(gid, i, dumps(s)) for i, s in enumerate(prepared_slices)])
+            return gid
+        except sqlite3.Error:
+            return None
+
+    def get_game_record_by_id(self, game_id):
+        """db_manager.py:106-112."""
+        row = self.conn.execute("SELECT game_record FROM games WHERE game_id = ?", (game_id,)).fetchone()
+        return loads(row[0]) if row else None
+
+    def load_latest_samples(self, num_samples):
+        """db_manager.py:114-127: the newest slices, returned oldest first (replay warm-up)."""
+        rows = self.conn.execute("SELECT slice_data FROM replay_buffer ORDER BY id DESC LIMIT ?",
+                                 (num_samples,)).fetchall()
+        return [loads(r[0]) for r in reversed(rows)]
+
+    def get_buffer_size(self):
+        """db_manager.py:129-132."""
+        return self.conn.execute("SELECT COUNT(*) FROM replay_buffer").fetchone()[0]
+
+    def trim_buffer(self, capacity):
+        """db_manager.py:134-147: past `capacity` slices, delete (up to) the 100 oldest games.  As in
+        the reference the slices stay (no PRAGMA foreign_keys, so ON DELETE CASCADE is inert)."""
+        if self.get_buffer_size() > capacity:
+            ids = self.conn.execute("SELECT game_id FROM games ORDER BY timestamp ASC LIMIT ?", (100,)).fetchall()
+            if ids:
+                with self.conn:
+                    self.conn.execute("DELETE FROM games WHERE game_id IN (%s)" % ",".join("?" * len(ids)),
+                                      [g[0] for g in ids])
+
+    def games(self):
+        """(game_id, analysis_version, move_count, status) of every stored game, oldest first."""
+        return self.conn.execute("SELECT game_id, analysis_version, move_count, status FROM games "
+                                 "ORDER BY game_id").fetchall()

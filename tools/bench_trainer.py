@@ -27,7 +27,9 @@ ap.add_argument("--per", action="store_true")
 ap.add_argument("--no-amp", action="store_true")
 ap.add_argument("--bf16", action="store_true", help="autocast to bfloat16 instead of the reference's float16")
 ap.add_argument("--channels-last", action="store_true")
+ap.add_argument("--benchmark", action="store_true", help="torch.backends.cudnn.benchmark (MIOpen Find per shape)")
 a = ap.parse_args()
+torch.backends.cudnn.benchmark = a.benchmark
 
 world = int(os.environ.get("WORLD_SIZE", "1"))
 rank = int(os.environ.get("RANK", "0"))
@@ -88,7 +90,7 @@ if dist:
 if rank == 0:
     print(json.dumps({"metric": "trainer steps/sec (config C4)", "value": a.steps / dt, "unit": "steps/s",
                       "n_gpus": world, "samples_per_s": a.steps * a.batch * world / dt, "ms_per_step": dt / a.steps * 1e3,
-                      "batch_per_gpu": a.batch, "unroll": U, "board": a.size, "blocks": a.blocks, "amp": ("bf16" if a.bf16 else "fp16") if not a.no_amp else None, "channels_last": a.channels_last,
+                      "batch_per_gpu": a.batch, "unroll": U, "board": a.size, "blocks": a.blocks, "amp": ("bf16" if a.bf16 else "fp16") if not a.no_amp else None, "channels_last": a.channels_last, "benchmark": a.benchmark,
                       "per": a.per, "last_loss": logs[0], "data": "synthetic slices in a device ReplayBuffer"}))
 if dist:
     dist.destroy_process_group()
