@@ -29,6 +29,13 @@ import torch  # noqa: E402
 
 
 
+def repr_flop_per_row(size, blocks):
+    """Algorithmic FLOP of one representation-tower row (network.py:30-56 + the 1x1 head convs):
+    stem conv 3->128 (2*A*128*3*9) + 2*blocks ResBlock convs + 2*A*128*3."""
+    A = size * size
+    return 2 * A * 128 * 3 * 9 + 2 * blocks * 2 * A * 128 * 128 * 9 + 2 * A * 128 * 3
+
+
 def tower_flop_per_row(size, blocks):
     """Algorithmic FLOP of one dynamics-tower row (network.py:81-83 + the 1x1 head convs):
     conv 144->128 (2*A*128*144*9) + 2*blocks ResBlock convs (2*A*128*128*9 each) + 2*A*128*3.
@@ -180,9 +187,13 @@ def main():
         torch.cuda.synchronize()
         log("warmup %d/%d done" % (i + 1, args.warmup))
     timer = None
+    az = args.mode == "AlphaZero"  # AlphaZero searches run the representation tower per wave
     if args.net == "hip":
         timer = N.KernelTimer()
-        net.tower_timer = timer
+        if az:
+            net.repr_timer = timer
+        else:
+            net.tower_timer = timer
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -201,20 +212,22 @@ def main():
     out = result_line(args, world, dt, waves, G)
     if timer is not None:
         n_launch, ms, rows = timer.summary()
-        flop = tower_flop_per_row(args.size, args.blocks) * rows
+        fpr = (repr_flop_per_row if az else tower_flop_per_row)(args.size, args.blocks)
+        flop = fpr * rows
         achieved = flop / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
         traffic = None
-        if os.path.exists(args.pmc_file) and (args.size, args.blocks) == (15, 8):  # the PMC pass's config
+        if os.path.exists(args.pmc_file) and (args.size, args.blocks) == (15, 8) and not az:  # the PMC pass's config
             try:
                 traffic = json.load(open(args.pmc_file)).get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
-        out["roofline"] = {"bound": "mfma", "kernel": "k_tower3<%d,DYN> (dynamics tower, %d fused convs + head 1x1 "
-                                                     "convs)" % (args.size, 1 + 2 * args.blocks),
+        kname = ("k_tower3<%d,REPR> (representation tower, stem + %d fused convs + head 1x1 convs)" % (args.size, 2 * args.blocks)
+                 if az else "k_tower3<%d,DYN> (dynamics tower, %d fused convs + head 1x1 convs)" % (args.size, 1 + 2 * args.blocks))
+        out["roofline"] = {"bound": "mfma", "kernel": kname,
                            "achieved": achieved, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                            "frac": achieved / PEAK_BF16_TFLOPS, "traffic": traffic,
                            "launches": n_launch, "mean_launch_ms": ms, "rows_per_launch": rows,
-                           "flop_per_row": tower_flop_per_row(args.size, args.blocks)}
+                           "flop_per_row": fpr}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.net == "hip":
         log("cpu baseline (bounded sample ~%.0f s)..." % args.cpu_baseline_sec)
         out["cpu_baseline"] = cpu_baseline(args, sd, cfg)

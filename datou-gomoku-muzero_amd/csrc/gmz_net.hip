@@ -1029,17 +1029,28 @@ static int heads(const gmz_net_weights *w, const uint16_t *pool, const int32_t *
   return 0;
 }
 
+GMZ_EXPORT int gmz_net_initial_tower(const gmz_net_weights *w, const float *obs, int rows, const int32_t *out_slot,
+                                     uint16_t *pool, void *workspace, void *stream) {
+  if (check_w(w)) return -1;
+  if (rows <= 0 || !obs || !out_slot || !pool || !workspace) return fail("gmz_net_initial_tower: bad argument");
+  const int H = w->board_size, A = H * H;
+  TowerArgs a{w->repr_convs, w->repr_bias, 2 * w->blocks, w->repr_stem_w, w->repr_stem_b, nullptr, obs, pool,
+              nullptr, nullptr, out_slot, w->head_conv_w, w->head_conv_b, (float *)workspace, rows,
+              ws_xres(workspace, A, rows)};
+  return tower(H, false, a, (hipStream_t)stream);
+}
+
+GMZ_EXPORT int gmz_net_initial_heads(const gmz_net_weights *w, const uint16_t *pool, const int32_t *out_slot, int rows,
+                                     float *logits, float *value, void *workspace, void *stream) {
+  if (check_w(w)) return -1;
+  if (rows <= 0 || !pool || !out_slot || !logits || !value || !workspace) return fail("gmz_net_initial_heads: bad argument");
+  return heads(w, pool, out_slot, rows, workspace, logits, value, nullptr, (hipStream_t)stream);
+}
+
 GMZ_EXPORT int gmz_net_initial(const gmz_net_weights *w, const float *obs, int rows, const int32_t *out_slot,
                                uint16_t *pool, float *logits, float *value, void *workspace, void *stream) {
-  if (check_w(w)) return -1;
-  if (rows <= 0 || !obs || !out_slot || !pool || !logits || !value || !workspace) return fail("gmz_net_initial: bad argument");
-  const int H = w->board_size, A = H * H;
-  hipStream_t s = (hipStream_t)stream;
-  float *pv = (float *)workspace;
-  TowerArgs a{w->repr_convs, w->repr_bias, 2 * w->blocks, w->repr_stem_w, w->repr_stem_b, nullptr, obs, pool,
-              nullptr, nullptr, out_slot, w->head_conv_w, w->head_conv_b, pv, rows, ws_xres(workspace, A, rows)};
-  if (tower(H, false, a, s)) return -1;
-  return heads(w, pool, out_slot, rows, workspace, logits, value, nullptr, s);
+  if (gmz_net_initial_tower(w, obs, rows, out_slot, pool, workspace, stream)) return -1;
+  return gmz_net_initial_heads(w, pool, out_slot, rows, logits, value, workspace, stream);
 }
 
 GMZ_EXPORT int gmz_net_recurrent_tower(const gmz_net_weights *w, uint16_t *pool, const int32_t *in_slot,

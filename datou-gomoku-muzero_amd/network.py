@@ -38,6 +38,8 @@ class NetWeights(ctypes.Structure):
 _lib.register({
     "gmz_net_workspace_bytes": ([ctypes.POINTER(NetWeights), I, ctypes.POINTER(ctypes.c_size_t)], I),
     "gmz_net_initial": ([ctypes.POINTER(NetWeights), P, I, P, P, P, P, P, P], I),
+    "gmz_net_initial_tower": ([ctypes.POINTER(NetWeights), P, I, P, P, P, P], I),
+    "gmz_net_initial_heads": ([ctypes.POINTER(NetWeights), P, P, I, P, P, P, P], I),
     "gmz_net_recurrent": ([ctypes.POINTER(NetWeights), P, P, P, P, I, P, P, P, P, P], I),
     "gmz_net_recurrent_tower": ([ctypes.POINTER(NetWeights), P, P, P, P, I, P, P], I),
     "gmz_net_recurrent_heads": ([ctypes.POINTER(NetWeights), P, P, I, P, P, P, P, P], I),
@@ -209,6 +211,7 @@ class GomokuNetHip:
         self.max_rows = int(max_rows)
         self.pool = torch.empty(int(num_slots) * self.A * C, dtype=torch.int16, device=self.device)
         self.tower_timer = None  # optional KernelTimer around the dynamics tower launches (bench.py)
+        self.repr_timer = None   # optional KernelTimer around the representation tower launches
         self.load_state_dict(state_dict)
 
     def load_state_dict(self, state_dict):
@@ -235,8 +238,16 @@ class GomokuNetHip:
     # ---- engine backend interface
     def initial(self, obs, out_slot, logits, value, stream):
         rows = obs.shape[0]
-        check(self.lib.gmz_net_initial(ctypes.byref(self.w), ptr(obs), rows, ptr(out_slot), ptr(self.pool),
-                                       ptr(logits), ptr(value), self._ws(rows), stream))
+        ws = self._ws(rows)
+        t = self.repr_timer
+        if t is not None:
+            t.start()
+        check(self.lib.gmz_net_initial_tower(ctypes.byref(self.w), ptr(obs), rows, ptr(out_slot), ptr(self.pool), ws,
+                                             stream))
+        if t is not None:
+            t.stop(rows)
+        check(self.lib.gmz_net_initial_heads(ctypes.byref(self.w), ptr(self.pool), ptr(out_slot), rows, ptr(logits),
+                                             ptr(value), ws, stream))
 
     def recurrent(self, in_slot, action, out_slot, logits, value, reward, stream):
         rows = in_slot.shape[0]

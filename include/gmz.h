@@ -202,6 +202,12 @@ int gmz_net_workspace_bytes(const gmz_net_weights *w, int rows, size_t *out);
 int gmz_net_initial(const gmz_net_weights *w, const float *obs_dev, int rows, const int32_t *out_slot_dev,
                     uint16_t *hid_pool_dev, float *logits_dev, float *value_dev, void *workspace_dev,
                     void *stream);
+/* gmz_net_initial in two stream-ordered halves (representation tower, then the heads), like the
+ * recurrent pair below. */
+int gmz_net_initial_tower(const gmz_net_weights *w, const float *obs_dev, int rows, const int32_t *out_slot_dev,
+                          uint16_t *hid_pool_dev, void *workspace_dev, void *stream);
+int gmz_net_initial_heads(const gmz_net_weights *w, const uint16_t *hid_pool_dev, const int32_t *out_slot_dev, int rows,
+                          float *logits_dev, float *value_dev, void *workspace_dev, void *stream);
 /* network.py:145-152 recurrent_inference: hid_pool[in_slot[r]], action[r] -> logits, value,
  * reward f32[rows], next hidden state -> hid_pool[out_slot[r]]. */
 int gmz_net_recurrent(const gmz_net_weights *w, uint16_t *hid_pool_dev, const int32_t *in_slot_dev,
