@@ -30,6 +30,7 @@ class GmzConfig:
     NUM_UNROLL_STEPS: int = 5            # config.py:71 (TrainingSlice shape)
     N_STEPS: int = 10                    # config.py:100 (n-step value targets)
     NUM_WORKERS: int = 15                # config.py:13
+    REANALYSIS_AGE_THRESHOLD: int = 900  # config.py:89 (re-analysis eligibility, trainer steps)
     ACTION_SPACE_SIZE: int = field(default=None)
 
     def __post_init__(self):

@@ -13,14 +13,19 @@ constructors: a blob naming anything else is rejected, never executed.  The ``tr
 cannot be decoded without executing arbitrary pickled callables, and checkpoints travel as
 state_dicts (weights.py) instead.
 
-Re-analysis (db_manager.py:143-227) belongs to the control plane and is not mirrored.
+Re-analysis bookkeeping (db_manager.py:151-227): eligible-game count, lock of the oldest eligible
+game(s), the sliding-window rewrite of a re-analysed game's slices (same blobs as the reference's
+``finish_reanalysis_for_game``), unlock on error.  The search itself is ``reanalysis.py``.
 """
 import io
 import os
+from collections import deque
 import pickle
 import sqlite3
 import sys
 import types
+
+import numpy as np
 
 from . import records as R
 
@@ -177,3 +182,68 @@ class RecordStore:
         """(game_id, analysis_version, move_count, status) of every stored game, oldest first."""
         return self.conn.execute("SELECT game_id, analysis_version, move_count, status FROM games "
                                  "ORDER BY game_id").fetchall()
+
+    # ---------------------------------------------------------------- re-analysis (db_manager.py:151-227)
+    def get_reanalysis_queue_size(self, current_trainer_step, age_threshold=900):
+        """db_manager.py:151-161: PENDING games whose analysis is more than ``age_threshold``
+        trainer steps old (config.py:89 REANALYSIS_AGE_THRESHOLD)."""
+        return self.conn.execute("SELECT COUNT(*) FROM games WHERE status = 'PENDING' AND ? - analysis_version > ?",
+                                 (current_trainer_step, age_threshold)).fetchone()[0]
+
+    def sample_and_lock_games_for_reanalysis(self, current_trainer_step, age_threshold=900, limit=1):
+        """db_manager.py:163-181 for up to ``limit`` games in one transaction: the oldest-analysed
+        eligible games, marked RUNNING -> [(game_id, GameRecord)].  Same games, in the same order,
+        as ``limit`` successive single-game calls."""
+        with self.conn:
+            rows = self.conn.execute(
+                "SELECT game_id, game_record FROM games WHERE status = 'PENDING' AND ? - analysis_version > ? "
+                "ORDER BY analysis_version ASC LIMIT ?", (current_trainer_step, age_threshold, int(limit))).fetchall()
+            self.conn.executemany("UPDATE games SET status = 'RUNNING' WHERE game_id = ?", [(r[0],) for r in rows])
+        return [(gid, loads(blob)) for gid, blob in rows]
+
+    def sample_and_lock_game_for_reanalysis(self, current_trainer_step, age_threshold=900):
+        """db_manager.py:163-181 -> (game_id, GameRecord) or (None, None)."""
+        got = self.sample_and_lock_games_for_reanalysis(current_trainer_step, age_threshold, 1)
+        return got[0] if got else (None, None)
+
+    def finish_reanalysis_for_game(self, game_id, new_policies, new_value_targets, new_analysis_version,
+                                   unroll_steps=5):
+        """db_manager.py:183-221: windows of ``unroll_steps + 1`` new policies / value targets
+        (zero-padded past the end) replace each stored slice's policy_history / value_history; the
+        game becomes DONE at ``new_analysis_version``.  On failure the game goes back to PENDING
+        and False is returned."""
+        k = unroll_steps + 1
+        num_moves = len(new_policies)
+        pol_q, val_q = deque(maxlen=k), deque(maxlen=k)
+        pi_hists, val_hists = [], []
+        for i in range(num_moves + k - 1):
+            if i < num_moves:
+                pol_q.append(new_policies[i])
+                val_q.append(new_value_targets[i])
+            else:
+                pol_q.append(np.zeros_like(new_policies[0]))
+                val_q.append(0.0)
+            if i >= k - 1:
+                pi_hists.append(np.array(pol_q))
+                val_hists.append(np.array(val_q, dtype=np.float32))
+        try:
+            with self.conn:
+                rows = self.conn.execute("SELECT id, move_index, slice_data FROM replay_buffer WHERE game_id = ? "
+                                         "ORDER BY move_index ASC", (game_id,)).fetchall()
+                upd = [(dumps(loads(blob)._replace(policy_history=pi_hists[mi], value_history=val_hists[mi])), sid)
+                       for sid, mi, blob in rows]
+                self.conn.executemany("UPDATE replay_buffer SET slice_data = ? WHERE id = ?", upd)
+                self.conn.execute("UPDATE games SET analysis_version = ?, status = 'DONE' WHERE game_id = ?",
+                                  (new_analysis_version, game_id))
+            return True
+        except Exception:
+            with self.conn:
+                self.conn.execute("UPDATE games SET status = 'PENDING' WHERE game_id = ?", (game_id,))
+            return False
+
+    def unlock_game_on_error(self, game_id):
+        """db_manager.py:223-227."""
+        if game_id is None:
+            return
+        with self.conn:
+            self.conn.execute("UPDATE games SET status = 'PENDING' WHERE game_id = ?", (game_id,))

@@ -10,7 +10,12 @@ the same messages on the same queues:
 Weights: the inference server's handshake (``InitialModelRequest`` -> ``ModelWeightsUpdate``,
 workers.py:319-322) when ``initial_model_requests_queue``/``model_update_queue`` are given, and
 hot-swap between moves (workers.py:332-335); otherwise ``state_dict`` (or seeded synthetic weights).
-``worker_mode`` 1 (re-analysis, off by default in config.py:85) is out of scope: the worker idles.
+``worker_mode`` 1 (re-analysis, workers.py:243-305; off by default, config.py:85): the worker locks up to
+``reanalysis_games`` stored games of the reference's SQLite database at a time (``db_path``), searches all
+their positions in batches of ``num_games`` on a second engine that shares the network, rewrites their
+slices and posts ``ReAnalysisStatus`` (reanalysis.py).  The current trainer step is
+``latest_model_step.value`` (the reference reads it from the pickled trainer_state blob, which is not
+decoded here; formats.py).  Self-play games in progress are kept and resume in mode 0.
 
 Launch from main.py's ``process_definitions`` in place of the workers + server, e.g.
     mp.Process(target=gpu_selfplay_worker, args=(0, worker_mode, data_queue, log_status_queue,
@@ -52,7 +57,8 @@ def gpu_selfplay_worker(worker_id, worker_mode, data_queue, log_status_queue, ui
                         request_queue=None, result_queue=None, replay_data_queue=None, trainer_event_queue=None,
                         latest_model_step=None, log_queue=None, pause_event=None, *, device=0, num_games=1024,
                         model_update_queue=None, initial_model_requests_queue=None, state_dict=None, cfg=None,
-                        seed=0, max_moves=None, emit_move_notices=True):
+                        seed=0, max_moves=None, emit_move_notices=True, db_path="outputs/training_state.db",
+                        reanalysis_games=64):
     logger = logging.getLogger("GpuSelfPlay-%s" % worker_id)
     if log_queue is not None:
         try:
@@ -107,20 +113,39 @@ def gpu_selfplay_worker(worker_id, worker_mode, data_queue, log_status_queue, ui
         if trainer_event_queue is not None:
             trainer_event_queue.put(R.GameCompletedNotice())
 
+    reanalyser, store = None, None
+
     logger.info("GPU self-play worker %s: %d games on cuda:%d" % (worker_id, G, device))
     while not shutdown_event.is_set():
-        if worker_mode is not None and getattr(worker_mode, "value", 0) != 0:
+        mode = getattr(worker_mode, "value", 0) if worker_mode is not None else 0
+        if mode == 0 and pause_event is not None and pause_event.is_set():  # workers.py:158-160
             time.sleep(5)
             continue
-        if pause_event is not None and pause_event.is_set():
-            time.sleep(5)
-            continue
-        if model_update_queue is not None:
+        if model_update_queue is not None:  # the inference server's hot swap (workers.py:332-335)
             try:
                 net.load_state_dict(model_update_queue.get_nowait().weights)
                 logger.info("Inference model updated.")
             except Empty:
                 pass
+        if mode == 1:  # re-analysis (workers.py:243-305)
+            from . import formats as F, reanalysis as RA
+            if reanalyser is None:
+                reanalyser = RA.Reanalyser(E.BatchedSelfPlayEngine(c, num_games=G, net=net,
+                                                                   seed=seed + 104729 * (int(worker_id) + 1)))
+                store = F.RecordStore(db_path)
+            step = latest_model_step.value if latest_model_step is not None else 0
+            try:
+                n = RA.reanalysis_step(reanalyser, store, step, c, reanalysis_games, ui_queue)
+            except Exception as e:  # workers.py:297-299
+                logger.error("Error in re-analysis for worker %s: %s" % (worker_id, e))
+                n = 0
+            if n == 0:
+                time.sleep(5)
+            continue
+        if mode != 0:  # workers.py:301-303
+            logger.warning("Worker %s: Unknown worker mode '%s'. Sleeping." % (worker_id, mode))
+            time.sleep(10)
+            continue
         b, p, lm, mc = eng.game_state()
         pol, val, act = eng.search()
         eng.winning_scan(b, p, act, counters=(missed_f, missed_t))  # position before the move
@@ -155,3 +180,6 @@ def gpu_selfplay_worker(worker_id, worker_mode, data_queue, log_status_queue, ui
             break
     pool.shutdown(wait=True)
     eng.close()
+    if reanalyser is not None:
+        reanalyser.eng.close()
+        store.close(checkpoint=False)
