@@ -108,33 +108,145 @@ def _bn(mod, x, mask=None):
     """BatchNorm whose training-mode statistics (and running-stat update) cover only the rows
     where ``mask`` is set.  The reference runs the unrolled steps on the sub-batch of games still
     in progress (loss.py:89-93); running every step on the FULL batch with row-masked statistics
-    gives the same values and gradients with fixed shapes, so MIOpen compiles each convolution
-    once instead of once per sub-batch size.  Computed in float32 (as autocast runs BatchNorm)."""
+    gives the same values and gradients with fixed shapes (MIOpen compiles each convolution once
+    instead of once per sub-batch size) and without a host synchronisation (no boolean gather),
+    so a whole training step can be captured in one HIP graph.  ``mask``: bool [B].  Computed in
+    float32 (as autocast runs BatchNorm).  A mask with no row set leaves the running statistics
+    untouched (the reference skips such a step)."""
     if mask is None or not mod.training:
         return mod(x)
     x = x.float()
     dims = [0] + list(range(2, x.dim()))
     shape = [1, -1] + [1] * (x.dim() - 2)
-    var, mean = torch.var_mean(x[mask], dim=dims, correction=0)  # statistics of the valid rows
-    n = mask.sum().to(torch.float32) * (x[0, 0].numel())
+    w = mask.to(torch.float32).reshape([-1] + [1] * (x.dim() - 1))
+    nv = mask.sum()
+    n = nv.to(torch.float32) * (x[0, 0].numel())
+    ns = n.clamp(min=1.0)
+    mean = (x * w).sum(dim=dims) / ns                  # statistics of the valid rows only
+    xc = x - mean.reshape(shape)
+    var = (xc * xc * w).sum(dim=dims) / ns
     scale = torch.rsqrt(var + mod.eps) * mod.weight
-    y = torch.addcmul((mod.bias - mean * scale).reshape(shape), x, scale.reshape(shape))  # one pass
+    y = torch.addcmul(mod.bias.reshape(shape), xc, scale.reshape(shape))
     with torch.no_grad():  # through .data, like the native kernel: no autograd version bump (the
         m = mod.momentum      # unmasked BatchNorm calls of the same module saved these buffers)
-        mod.running_mean.data.mul_(1 - m).add_(m * mean.detach())
-        mod.running_var.data.mul_(1 - m).add_(m * var.detach() * n / (n - 1))
-        mod.num_batches_tracked.data += 1
+        ok = nv > 0
+        rm, rv = mod.running_mean.data, mod.running_var.data
+        rm.copy_(torch.where(ok, rm * (1 - m) + m * mean.detach(), rm))
+        rv.copy_(torch.where(ok, rv * (1 - m) + m * var.detach() * n / (n - 1).clamp(min=1.0), rv))
+        mod.num_batches_tracked.data += ok.to(mod.num_batches_tracked.dtype)
     return y
+
+
+_BN_DTYPES = {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2}
+FUSED_BN = True  # device BatchNorm layers of a training-mode model run the HIP kernels (gmz_train.hip)
+
+
+def _bn_layout(x):
+    """0: NCHW-contiguous, 1: channels-last (NHWC) with an even channel count, None: neither."""
+    if x.is_contiguous():
+        return 0
+    if x.dim() == 4 and x.shape[1] % 2 == 0 and x.shape[1] <= 512 and x.is_contiguous(memory_format=torch.channels_last):
+        return 1
+    return None
+
+
+def _like(t, layout):
+    return t.contiguous(memory_format=torch.channels_last) if layout == 1 else t.contiguous()
+
+
+class _FusedMaskedBN(torch.autograd.Function):
+    """Row-masked training-mode BatchNorm + residual + ReLU as three HIP kernels forward and three
+    backward (``gmz_bn_forward`` / ``gmz_bn_backward``, csrc/gmz_train.hip), on NCHW or channels-last
+    activations.  Same statistics, running-stat update and gradients as ``_bn`` followed by
+    ``+ res`` and ``relu``; the output keeps the activation dtype and memory format (float16 under
+    the reference's autocast)."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, res, mask, running_mean, running_var, num_batches, eps, momentum, relu):
+        from . import _lib
+        L = _lib.load()
+        layout = _bn_layout(x)
+        if layout is None:
+            x, layout = x.contiguous(), 0
+        if res is not None:
+            res = _like(res, layout)
+        B, C = x.shape[0], x.shape[1]
+        S = x[0, 0].numel()
+        y = torch.empty_like(x)
+        save = torch.empty(2, C, dtype=torch.float32, device=x.device)
+        ws = _bn_workspace(layout, B, C, S, x.device)
+        _lib.check(L.gmz_bn_forward(_BN_DTYPES[x.dtype], layout, _lib.ptr(x), _lib.ptr(res), _lib.ptr(mask), B, C,
+                                    S, _lib.ptr(gamma), _lib.ptr(beta), float(eps), float(momentum),
+                                    _lib.ptr(running_mean), _lib.ptr(running_var), _lib.ptr(num_batches),
+                                    int(relu), _lib.ptr(y), _lib.ptr(save), _lib.ptr(ws), _lib.stream_ptr()))
+        ctx.save_for_backward(x, y, mask, gamma, save)
+        ctx.relu, ctx.has_res, ctx.layout = relu, res is not None, layout
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from . import _lib
+        L = _lib.load()
+        x, y, mask, gamma, save = ctx.saved_tensors
+        layout = ctx.layout
+        dy = _like(dy, layout)
+        B, C = x.shape[0], x.shape[1]
+        S = x[0, 0].numel()
+        dx = torch.empty_like(x)
+        dres = torch.empty_like(x) if ctx.has_res else None
+        dgamma = torch.empty(C, dtype=torch.float32, device=x.device)
+        dbeta = torch.empty(C, dtype=torch.float32, device=x.device)
+        ws = _bn_workspace(layout, B, C, S, x.device)
+        _lib.check(L.gmz_bn_backward(_BN_DTYPES[x.dtype], layout, _lib.ptr(x), _lib.ptr(y), _lib.ptr(dy),
+                                     _lib.ptr(mask), B, C, S, _lib.ptr(gamma), _lib.ptr(save), int(ctx.relu),
+                                     _lib.ptr(dx), _lib.ptr(dres), _lib.ptr(dgamma), _lib.ptr(dbeta), _lib.ptr(ws),
+                                     _lib.stream_ptr()))
+        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None
+
+
+_WS_BYTES = {}
+
+
+def _bn_workspace(layout, B, C, S, device):
+    import ctypes
+    from . import _lib
+    key = (layout, B, C, S)
+    if key not in _WS_BYTES:
+        n = ctypes.c_size_t()
+        _lib.check(_lib.load().gmz_bn_workspace_bytes(layout, B, C, S, ctypes.byref(n)))
+        _WS_BYTES[key] = n.value
+    return torch.empty((_WS_BYTES[key] + 7) // 8, dtype=torch.float64, device=device)
+
+
+def _bn_act(mod, x, mask=None, res=None, relu=True):
+    """relu?(BatchNorm(x) (+ res)) with row-masked training statistics (see ``_bn``).  Training-mode
+    BatchNorm on the GPU runs the fused HIP kernels; eval mode and the CPU use PyTorch ops."""
+    if FUSED_BN and mod.training and x.is_cuda and x.dtype in _BN_DTYPES:
+        if res is not None:
+            res = res.to(x.dtype)
+        m = None if mask is None else mask.contiguous().view(torch.uint8)
+        return _FusedMaskedBN.apply(x, mod.weight, mod.bias, res, m, mod.running_mean, mod.running_var,
+                                    mod.num_batches_tracked, mod.eps, mod.momentum, relu)
+    y = _bn(mod, x, mask)
+    if res is not None:
+        y = y + res
+    return F.relu(y) if relu else y
 
 
 def _conv1x1(conv, x):
     """1x1 convolution as a batched GEMM over positions (same parameters as ``conv``).  MIOpen
     has no tuned kernels for the 1- and 2-channel head convolutions and the 1->16 action embedding
     and falls back to naive direct convolutions (tens of ms per weight gradient); as a GEMM they
-    take microseconds."""
+    take microseconds.  A channels-last input stays channels-last (GEMM over the [n, h*w, c] view)."""
     n, c, h, w = x.shape
     wt = conv.weight.reshape(conv.weight.shape[0], c)
-    y = torch.matmul(wt.to(x.dtype) if not torch.is_autocast_enabled() else wt, x.reshape(n, c, h * w))
+    wt = wt.to(x.dtype) if not torch.is_autocast_enabled() else wt
+    if c > 1 and x.is_contiguous(memory_format=torch.channels_last) and not x.is_contiguous():
+        y = torch.matmul(x.permute(0, 2, 3, 1), wt.t())          # [n, h, w, o]
+        if conv.bias is not None:
+            y = y + conv.bias.to(y.dtype)
+        return y.permute(0, 3, 1, 2)                              # channels-last [n, o, h, w]
+    y = torch.matmul(wt, x.reshape(n, c, h * w))
     if conv.bias is not None:
         y = y + conv.bias.reshape(1, -1, 1).to(y.dtype)
     return y.reshape(n, -1, h, w)
@@ -149,8 +261,8 @@ class _Block(nn.Module):
         self.conv2, self.bn2 = _conv3(c, c), nn.BatchNorm2d(c, eps=1e-4)
 
     def forward(self, x, mask=None):
-        y = F.relu(_bn(self.bn1, self.conv1(x), mask))
-        return F.relu(_bn(self.bn2, self.conv2(y), mask) + x)
+        y = _bn_act(self.bn1, self.conv1(x), mask)
+        return _bn_act(self.bn2, self.conv2(y), mask, res=x)
 
 
 class _Trunk(nn.Module):
@@ -162,7 +274,7 @@ class _Trunk(nn.Module):
         self.resblocks = nn.Sequential(*[_Block(c) for _ in range(blocks)])
 
     def forward(self, x, mask=None):
-        h = F.relu(_bn(self.bn, self.conv(x), mask))
+        h = _bn_act(self.bn, self.conv(x), mask)
         for blk in self.resblocks:
             h = blk(h, mask)
         return h
@@ -179,8 +291,8 @@ class _Prediction(nn.Module):
 
     def forward(self, h, mask=None):
         n = h.shape[0]
-        pol = self.policy_fc(F.relu(_bn(self.policy_bn, _conv1x1(self.policy_conv, h), mask)).reshape(n, -1))
-        v = F.relu(self.value_fc1(F.relu(_bn(self.value_bn, _conv1x1(self.value_conv, h), mask)).reshape(n, -1)))
+        pol = self.policy_fc(_bn_act(self.policy_bn, _conv1x1(self.policy_conv, h), mask).reshape(n, -1))
+        v = F.relu(self.value_fc1(_bn_act(self.value_bn, _conv1x1(self.value_conv, h), mask).reshape(n, -1)))
         return pol, self.value_fc2(v)
 
 
@@ -195,7 +307,10 @@ class _Dynamics(_Trunk):
     def forward(self, h, a, mask=None):
         n, _, H, W = h.shape
         plane = F.one_hot(a, H * W).to(h.dtype).reshape(n, 1, H, W)
-        nxt = super().forward(torch.cat((h, _conv1x1(self.action_embed_conv, plane).to(h.dtype)), dim=1), mask)
+        emb = _conv1x1(self.action_embed_conv, plane).to(h.dtype)
+        if h.is_contiguous(memory_format=torch.channels_last) and not h.is_contiguous():
+            emb = emb.contiguous(memory_format=torch.channels_last)   # cat keeps channels-last
+        nxt = super().forward(torch.cat((h, emb), dim=1), mask)
         return nxt, self.reward_fc(nxt.reshape(n, -1))
 
 
@@ -205,7 +320,7 @@ class _Projection(nn.Module):
         self.fc1, self.bn1, self.fc2 = nn.Linear(din, hidden), nn.BatchNorm1d(hidden, eps=1e-4), nn.Linear(hidden, out)
 
     def forward(self, h, mask=None):
-        return self.fc2(F.relu(_bn(self.bn1, self.fc1(h.reshape(h.shape[0], -1)), mask)))
+        return self.fc2(_bn_act(self.bn1, self.fc1(h.reshape(h.shape[0], -1)), mask))
 
 
 class TrainNet(nn.Module):
@@ -225,7 +340,11 @@ class TrainNet(nn.Module):
                 if isinstance(m, _Block):
                     nn.init.zeros_(m.bn2.weight)
 
+    channels_last = False  # set by Trainer(channels_last=True): activations in NHWC memory format
+
     def representation(self, obs, mask=None):
+        if self.channels_last:
+            obs = obs.contiguous(memory_format=torch.channels_last)
         return self.representation_net(obs, mask)
 
     def prediction(self, h, mask=None):
@@ -250,16 +369,20 @@ class TrainNet(nn.Module):
 
 
 # ------------------------------------------------------------------------------ loss
-def barlow_loss(z1, z2, lam):
+def barlow_loss(z1, z2, lam, mask=None):
     """loss.py:10-27: Barlow-twins cross-correlation loss of batch-standardised projections
-    (BatchNorm1d without affine/running stats, eps 1e-5, written out so any row count runs the
-    same elementwise kernels)."""
+    (BatchNorm1d without affine/running stats, eps 1e-5), over the rows where ``mask`` (bool [B])
+    is set — the reference's sub-batch — without gathering them."""
     z1, z2 = z1.float(), z2.float()
-    n = z1.shape[0]
+    if mask is None:
+        w = torch.ones(z1.shape[0], 1, device=z1.device)
+    else:
+        w = mask.to(torch.float32)[:, None]
+    n = w.sum().clamp(min=1.0)
 
     def std(z):
-        zc = z - z.mean(0, keepdim=True)
-        return zc * torch.rsqrt((zc * zc).mean(0, keepdim=True) + 1e-5)
+        zc = z - (z * w).sum(0, keepdim=True) / n
+        return zc * torch.rsqrt((zc * zc * w).sum(0, keepdim=True) / n + 1e-5) * w
 
     c = (std(z1).t() @ std(z2)) / n
     diag = torch.diagonal(c)
@@ -303,20 +426,43 @@ def value_targets(rew, mcts_val, last_value, cfg):
     return out
 
 
-def muzero_loss(model, target_model, batch, is_weights, cfg, k=None, flip=None, amp=False, amp_dtype=None):
+class _HalveGrad(torch.autograd.Function):
+    """Identity forward, gradient x 0.5 (loss.py:107 ``h.register_hook(lambda g: g * 0.5)``)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g * 0.5
+
+
+def muzero_loss(model, target_model, batch, is_weights, cfg, k=None, flip=None, amp=False, amp_dtype=None,
+                sync_logs=True, augmented=False):
     """loss.py:30-158.  ``batch`` = (obs [B,U+1,3,H,W], actions [B,U], rewards [B,U],
     policies [B,U+1,A], search values [B,U+1]).  ``k``/``flip``: the augmentation (default: drawn
-    from numpy's global RandomState in the reference's order).  Returns (weighted loss tensor,
-    (total, policy, value, reward, consistency) floats, |value error| at step 0 as a tensor)."""
-    if k is None:
-        k = np.random.randint(4)
-    if flip is None:
-        flip = bool(np.random.choice([True, False]))
+    from numpy's global RandomState in the reference's order); ``augmented``: the batch is already
+    augmented (k/flip ignored) and carries the augmented actions as a 6th member.  Returns (weighted loss tensor, (total, policy, value, reward,
+    consistency) — floats, or one device tensor [5] with ``sync_logs=False`` — , |value error| at
+    step 0 as a tensor).
+
+    Fixed shapes and no host synchronisation: every unroll step runs on the full batch with the
+    rows of ended games masked out of the BatchNorm statistics, the losses and the consistency
+    loss, and a step with no valid row contributes nothing (the reference skips it), so the same
+    kernels run every call and the step can be captured in a HIP graph."""
+    obs, act, rew, pi, mval = batch[:5]
+    act, rew, mval = act.long(), rew.float(), mval.float()
+    if augmented:
+        act_aug = batch[5]
+    else:
+        if k is None:
+            k = np.random.randint(4)
+        if flip is None:
+            flip = bool(np.random.choice([True, False]))
+        obs, pi, act_aug = augment(obs, pi, act, k, flip)
     model.train()
     target_model.eval()
-    obs, act, rew, pi, mval = batch
-    act, rew, mval = act.long(), rew.float(), mval.float()
-    obs, pi, act_aug = augment(obs, pi, act, k, flip)
     c, W = cfg, cfg.LOSS_WEIGHTS
     vsup = (c.VALUE_SUPPORT_MIN, c.VALUE_SUPPORT_MAX, c.VALUE_SUPPORT_BINS)
     rsup = (c.REWARD_SUPPORT_MIN, c.REWARD_SUPPORT_MAX, c.REWARD_SUPPORT_BINS)
@@ -324,7 +470,9 @@ def muzero_loss(model, target_model, batch, is_weights, cfg, k=None, flip=None, 
         last_v = target_model.initial_value(obs[:, -1])[:, 0]
         z = value_targets(rew, mval, last_v, c)
     dev_type = obs.device.type
-    with torch.autocast(dev_type, enabled=amp and dev_type == "cuda", dtype=amp_dtype or torch.float16):
+    zero = torch.zeros((), device=obs.device)
+    with torch.autocast(dev_type, enabled=amp and dev_type == "cuda", dtype=amp_dtype or torch.float16,
+                        cache_enabled=False):
         h = model.representation(obs[:, 0])
         pl, vl = model.prediction(h)
         lp = F.cross_entropy(pl.float(), pi[:, 0], reduction="none")
@@ -334,36 +482,35 @@ def muzero_loss(model, target_model, batch, is_weights, cfg, k=None, flip=None, 
         v0 = support_to_scalar(F.softmax(vl.float(), dim=1), *vsup)
         td = (v0.detach()[:, 0] - z[:, 0]).abs()
         lr_ = torch.zeros(obs.shape[0], device=obs.device)
-        proj_pairs = []
-        steps = 0
+        steps = zero
+        cons = zero
         for s in range(c.NUM_UNROLL_STEPS):
             m = act[:, s] != -1
-            if not bool(m.any()):
-                continue
-            steps += 1
-            mf = m.to(torch.float32)
+            live = m.any().to(torch.float32)   # 0: the reference's `continue` (loss.py:90-91)
+            steps = steps + live
             # full-batch step, row-masked BatchNorm statistics and losses (== the reference's
             # sub-batch h[m] computation, loss.py:89-107, with fixed shapes)
             hk, rl = model.dynamics(h, torch.where(m, act_aug[:, s], torch.zeros_like(act_aug[:, s])), mask=m)
             plk, vlk = model.prediction(hk, mask=m)
-            lp = lp + mf * F.cross_entropy(plk.float(), pi[:, s + 1], reduction="none")
-            lv = lv + mf * F.cross_entropy(vlk.float(), scalar_to_support(z[:, s + 1], *vsup), reduction="none")
-            lr_ = lr_ + mf * F.cross_entropy(rl.float(), scalar_to_support(rew[:, s], *rsup), reduction="none")
+            lp = lp + torch.where(m, F.cross_entropy(plk.float(), pi[:, s + 1], reduction="none"), zero)
+            lv = lv + torch.where(m, F.cross_entropy(vlk.float(), scalar_to_support(z[:, s + 1], *vsup),
+                                                     reduction="none"), zero)
+            lr_ = lr_ + torch.where(m, F.cross_entropy(rl.float(), scalar_to_support(rew[:, s], *rsup),
+                                                       reduction="none"), zero)
             dyn = model.project(hk, with_grad=True, mask=m)
             with torch.no_grad():
                 tru = model.project(model.representation(obs[:, s + 1], mask=m), with_grad=False, mask=m)
-            proj_pairs.append((dyn[m], tru[m]))
-            nh = torch.where(m[:, None, None, None], hk, h)
-            nh.register_hook(lambda g: g * 0.5)
-            h = nh
+            cons = cons + live * barlow_loss(dyn, tru, c.BARLOW_LAMBDA, m)
+            h = _HalveGrad.apply(torch.where(m[:, None, None, None], hk, h))
     lp = lp / (steps + 1)
     lv = lv / (steps + 1)
-    lr_ = lr_ / steps if steps else torch.zeros_like(lr_)
-    cons = (sum(barlow_loss(a, b, c.BARLOW_LAMBDA) for a, b in proj_pairs) / steps if steps
-            else torch.zeros((), device=obs.device))
+    lr_ = lr_ / steps.clamp(min=1.0)
+    cons = cons / steps.clamp(min=1.0)
     fp, fv, fr = (lp * is_weights).mean(), (lv * is_weights).mean(), (lr_ * is_weights).mean()
     total = W["policy"] * fp + W["value"] * fv + W["reward"] * fr + W["consistency"] * cons
-    logs = tuple(float(x.detach()) for x in (total, fp, fv, fr, cons))
+    logs = torch.stack([x.detach().float() for x in (total, fp, fv, fr, cons)])
+    if sync_logs:
+        logs = tuple(float(x) for x in logs.tolist())
     return total, logs, td
 
 
@@ -442,9 +589,19 @@ class Trainer:
     decay, LinearLR warm-up (1000 updates) then cosine annealing to 1e-7 over 200k updates, AMP
     grad scaler, gradient clipping, soft target update after every optimiser step.  Under an
     initialised torch.distributed every rank trains on its own batch and the gradients are averaged
-    with one all-reduce of a flat bucket (RCCL) before the update."""
+    with one all-reduce of a flat bucket (RCCL) before the update.
 
-    def __init__(self, cfg=None, device="cuda", state_dict=None, amp=None, amp_dtype=None, channels_last=False):
+    MI355X execution: every parameter's gradient is a view of ONE flat buffer (the all-reduce
+    bucket, no gather/scatter copies); on the GPU the optimiser is the fused multi-tensor Adam with
+    the learning rate as a device tensor and the AMP inf-check handed to it on the device; with
+    ``graph=True`` (default on cuda, GRADIENT_ACCUMULATION_STEPS == 1) the whole step — target-net
+    bootstrap, loss, backward, unscale, clip, Adam, scale update, soft target update — is captured
+    once into a HIP graph and replayed (two graphs around the eager RCCL all-reduce when
+    distributed).  The batch is augmented eagerly into static input buffers before each replay.
+    The first ``graph_warmup`` steps run eagerly (they are real steps)."""
+
+    def __init__(self, cfg=None, device="cuda", state_dict=None, amp=None, amp_dtype=None, channels_last=False,
+                 graph=None, graph_warmup=3):
         c = cfg if isinstance(cfg, TrainConfig) else TrainConfig.from_any(cfg)
         self.cfg, self.device = c, torch.device(device)
         self.model = TrainNet(c).to(self.device)
@@ -455,16 +612,27 @@ class Trainer:
         self.amp = (self.device.type == "cuda") if amp is None else amp
         self.amp_dtype = amp_dtype  # None: float16 as the reference's torch.amp.autocast('cuda')
         self.channels_last = channels_last
-        if channels_last:
+        if channels_last:  # NHWC activations: MIOpen's NHWC convolutions without layout transposes
             self.model = self.model.to(memory_format=torch.channels_last)
             self.target = self.target.to(memory_format=torch.channels_last)
+            self.model.channels_last = self.target.channels_last = True
         import torch.distributed as dist
         self.dist = dist if (dist.is_available() and dist.is_initialized()) else None
         if self.dist is not None:  # every rank starts from rank 0's weights
             for t in list(self.model.parameters()) + list(self.model.buffers()):
                 self.dist.broadcast(t.data, 0)
             self.target.load_state_dict(self.model.state_dict())
-        self.opt = torch.optim.Adam(self.model.parameters(), lr=c.LEARNING_RATE, weight_decay=c.WEIGHT_DECAY)
+        # gradients as views of one flat bucket (the all-reduce operand)
+        self.params = [p for p in self.model.parameters() if p.requires_grad]
+        self.flat_grad = torch.zeros(sum(p.numel() for p in self.params), dtype=torch.float32, device=self.device)
+        off = 0
+        for p in self.params:
+            p.grad = self.flat_grad[off:off + p.numel()].view_as(p)
+            off += p.numel()
+        cuda = self.device.type == "cuda"
+        lr = torch.tensor(c.LEARNING_RATE, device=self.device) if cuda else c.LEARNING_RATE
+        self.opt = torch.optim.Adam(self.params, lr=lr, weight_decay=c.WEIGHT_DECAY,
+                                    **(dict(fused=True, capturable=True) if cuda else {}))
         acc = max(1, c.GRADIENT_ACCUMULATION_STEPS)
         warm, total = 1000 // acc, 200000 // acc
         self.sched = torch.optim.lr_scheduler.SequentialLR(self.opt, [
@@ -472,37 +640,88 @@ class Trainer:
             torch.optim.lr_scheduler.CosineAnnealingLR(self.opt, T_max=total - warm, eta_min=1e-7)], milestones=[warm])
         self.scaler = torch.amp.GradScaler(self.device.type, enabled=self.amp and amp_dtype in (None, torch.float16))
         self.step_count = 0
+        self.graph = (cuda and acc == 1) if graph is None else (bool(graph) and cuda and acc == 1)
+        self.graph_warmup = max(1, int(graph_warmup))  # eager steps first: lazy AMP/optimiser state
+        self._graphs = None
+        self._static = None
+
+    # ------------------------------------------------------------------ step pieces
+    def _forward_backward(self, batch, is_weights, acc=1, k=None, flip=None, augmented=False):
+        loss, logs, td = muzero_loss(self.model, self.target, batch, is_weights, self.cfg, k=k, flip=flip,
+                                     amp=self.amp, amp_dtype=self.amp_dtype, sync_logs=False, augmented=augmented)
+        self.scaler.scale(loss / acc).backward()
+        return logs, td
+
+    def _allreduce(self):
+        if self.dist is not None:  # data parallel: ONE all-reduce of the flat gradient bucket (RCCL)
+            self.dist.all_reduce(self.flat_grad)
+            self.flat_grad.div_(self.dist.get_world_size())
+
+    def _update(self):
+        c = self.cfg
+        self.scaler.unscale_(self.opt)
+        torch.nn.utils.clip_grad_norm_(self.params, c.GRAD_CLIP_NORM, foreach=self.device.type == "cuda")
+        self.scaler.step(self.opt)
+        self.scaler.update()
+        self.flat_grad.zero_()
+        with torch.no_grad():  # utils.py:28-31 soft update (parameters only): tau * s + (1 - tau) * t
+            tp, sp = list(self.target.parameters()), list(self.model.parameters())
+            torch._foreach_mul_(tp, 1.0 - c.TARGET_MODEL_TAU)
+            torch._foreach_add_(tp, sp, alpha=c.TARGET_MODEL_TAU)
+
+    def _augment_into_static(self, batch, is_weights, k, flip):
+        obs, act, rew, pi, mval = batch
+        if k is None:
+            k = np.random.randint(4)
+        if flip is None:
+            flip = bool(np.random.choice([True, False]))
+        o, p, a = augment(obs, pi, act.long(), k, flip)
+        src = (o, act.long(), rew.float(), p, mval.float(), a, is_weights.float())
+        if self._static is None:
+            self._static = tuple(torch.empty_like(t).contiguous() for t in src)
+        for dst, t in zip(self._static, src):
+            dst.copy_(t)
+
+    def _capture(self):
+        st = self._static
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g1, stream=s):
+                self._out = self._forward_backward(st[:6], st[6], augmented=True)
+                if self.dist is None:
+                    self._update()
+            if self.dist is not None:
+                with torch.cuda.graph(g2, stream=s, pool=g1.pool()):
+                    self._update()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        self._graphs = (g1, g2 if self.dist is not None else None)
 
     def step(self, batch, is_weights, k=None, flip=None):
+        """One training step -> ((total, policy, value, reward, consistency) floats, td errors [B])."""
         c = self.cfg
         acc = max(1, c.GRADIENT_ACCUMULATION_STEPS)
-        if self.channels_last:
-            batch = (batch[0].contiguous(memory_format=torch.channels_last) if batch[0].dim() == 4 else batch[0],) + tuple(batch[1:])
-        loss, logs, td = muzero_loss(self.model, self.target, batch, is_weights, c, k=k, flip=flip, amp=self.amp,
-                                     amp_dtype=self.amp_dtype)
-        self.scaler.scale(loss / acc).backward()
-        if self.dist is not None:  # data parallel: ONE all-reduce of a flat gradient bucket (RCCL)
-            ps = [p for p in self.model.parameters() if p.grad is not None]
-            flat = torch.cat([p.grad.reshape(-1) for p in ps])
-            self.dist.all_reduce(flat)
-            flat.div_(self.dist.get_world_size())
-            off = 0
-            for p in ps:
-                n = p.grad.numel()
-                p.grad.copy_(flat[off:off + n].view_as(p.grad))
-                off += n
-        if (self.step_count + 1) % acc == 0:
-            self.scaler.unscale_(self.opt)
-            torch.nn.utils.clip_grad_norm_(self.model.parameters(), c.GRAD_CLIP_NORM)
-            self.scaler.step(self.opt)
-            self.scaler.update()
+        if self.graph and self.step_count >= self.graph_warmup:
+            self._augment_into_static(batch, is_weights, k, flip)
+            if self._graphs is None:
+                self._capture()
+            g1, g2 = self._graphs
+            g1.replay()
+            if g2 is not None:
+                self._allreduce()
+                g2.replay()
+            logs, td = self._out
+            td = td.clone()
             self.sched.step()
-            self.opt.zero_grad(set_to_none=True)
-            with torch.no_grad():  # utils.py:28-31 soft update (parameters only)
-                for t, s in zip(self.target.parameters(), self.model.parameters()):
-                    t.copy_(c.TARGET_MODEL_TAU * s + (1.0 - c.TARGET_MODEL_TAU) * t)
+        else:
+            logs, td = self._forward_backward(batch, is_weights, acc, k=k, flip=flip)
+            if (self.step_count + 1) % acc == 0:
+                self._allreduce()
+                self._update()
+                self.sched.step()
         self.step_count += 1
-        return logs, td
+        return tuple(float(x) for x in logs.tolist()), td
 
     def state_dict_cpu(self):
         """ModelWeightsUpdate payload (workers.py:587-593) for the self-play engines."""

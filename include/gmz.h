@@ -222,6 +222,29 @@ int gmz_net_recurrent_heads(const gmz_net_weights *w, const uint16_t *hid_pool_d
                             int rows, float *logits_dev, float *value_dev, float *reward_dev, void *workspace_dev,
                             void *stream);
 
+/* ------------------------------------------------------------------ trainer kernels (trainer.py) */
+/* Row-masked BatchNorm with the residual add and ReLU fused (training mode), replacing the
+ * reference's BatchNorm over the sub-batch of games still in progress (loss.py:89-107, network.py
+ * BatchNorm2d/1d layers): activations of B rows, C channels, S = H*W positions (1 for BatchNorm1d),
+ * layout 0 = NCHW x[B][C][S], 1 = channels-last NHWC x[B][S][C] (C even, <= 512); dtype 0 = f32,
+ * 1 = f16, 2 = bf16 for x / res / y / dy / dx / dres; gamma, beta, statistics f32.
+ * mask_dev: uint8[B], nonzero = the row is in the statistics (NULL = every row).  All rows are
+ * normalised with the statistics of the masked rows.
+ * forward: y = relu?(gamma*(x-mean)*invstd + beta (+ res)); save_dev f32[2][C] = (mean, invstd);
+ *          running_mean/var (momentum, unbiased variance) and num_batches (int64, +1) are updated
+ *          when at least one row is valid (pass NULLs to skip).
+ * backward: dx (rows outside the mask get gamma*invstd*dz), dres = dz (the residual's gradient, may
+ *          be NULL), dgamma/dbeta f32[C] over the masked rows; dz = dy * [y > 0] when relu.
+ * workspace_dev: gmz_bn_workspace_bytes(layout, B, C, S) bytes (8-byte aligned), stream-ordered reuse. */
+int gmz_bn_workspace_bytes(int layout, int B, int C, int S, size_t *out);
+int gmz_bn_forward(int dtype, int layout, const void *x_dev, const void *res_dev, const uint8_t *mask_dev, int B, int C, int S,
+                   const float *gamma_dev, const float *beta_dev, float eps, float momentum, float *running_mean_dev,
+                   float *running_var_dev, int64_t *num_batches_dev, int relu, void *y_dev, float *save_dev,
+                   void *workspace_dev, void *stream);
+int gmz_bn_backward(int dtype, int layout, const void *x_dev, const void *y_dev, const void *dy_dev, const uint8_t *mask_dev, int B,
+                    int C, int S, const float *gamma_dev, const float *save_dev, int relu, void *dx_dev, void *dres_dev,
+                    float *dgamma_dev, float *dbeta_dev, void *workspace_dev, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

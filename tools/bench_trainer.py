@@ -18,7 +18,7 @@ import torch  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--steps", type=int, default=20)
-ap.add_argument("--warmup", type=int, default=3)
+ap.add_argument("--warmup", type=int, default=5)
 ap.add_argument("--batch", type=int, default=360)
 ap.add_argument("--size", type=int, default=15)
 ap.add_argument("--blocks", type=int, default=8)
@@ -27,6 +27,7 @@ ap.add_argument("--per", action="store_true")
 ap.add_argument("--no-amp", action="store_true")
 ap.add_argument("--bf16", action="store_true", help="autocast to bfloat16 instead of the reference's float16")
 ap.add_argument("--channels-last", action="store_true")
+ap.add_argument("--eager", action="store_true", help="no HIP-graph capture of the step")
 ap.add_argument("--benchmark", action="store_true", help="torch.backends.cudnn.benchmark (MIOpen Find per shape)")
 a = ap.parse_args()
 torch.backends.cudnn.benchmark = a.benchmark
@@ -44,7 +45,7 @@ from datou_gomoku_muzero_amd import trainer as T  # noqa: E402
 cfg = T.TrainConfig(BOARD_SIZE=a.size, NUM_RES_BLOCKS=a.blocks, PHYSICAL_BATCH_SIZE=a.batch,
                     TRAIN_BUFFER_SIZE=a.buffer, ENABLE_PER=a.per)
 tr = T.Trainer(cfg, device="cuda", amp=not a.no_amp, amp_dtype=torch.bfloat16 if a.bf16 else None,
-               channels_last=a.channels_last)
+               channels_last=a.channels_last, graph=not a.eager)
 rb = T.ReplayBuffer(cfg, device="cuda")
 S = namedtuple("S", "observation action_history reward_history policy_history value_history")
 rs = np.random.RandomState(rank)
@@ -90,7 +91,7 @@ if dist:
 if rank == 0:
     print(json.dumps({"metric": "trainer steps/sec (config C4)", "value": a.steps / dt, "unit": "steps/s",
                       "n_gpus": world, "samples_per_s": a.steps * a.batch * world / dt, "ms_per_step": dt / a.steps * 1e3,
-                      "batch_per_gpu": a.batch, "unroll": U, "board": a.size, "blocks": a.blocks, "amp": ("bf16" if a.bf16 else "fp16") if not a.no_amp else None, "channels_last": a.channels_last, "benchmark": a.benchmark,
+                      "batch_per_gpu": a.batch, "unroll": U, "board": a.size, "blocks": a.blocks, "amp": ("bf16" if a.bf16 else "fp16") if not a.no_amp else None, "channels_last": a.channels_last, "benchmark": a.benchmark, "graph": tr.graph,
                       "per": a.per, "last_loss": logs[0], "data": "synthetic slices in a device ReplayBuffer"}))
 if dist:
     dist.destroy_process_group()
