@@ -246,10 +246,33 @@ def _conv1x1(conv, x):
         if conv.bias is not None:
             y = y + conv.bias.to(y.dtype)
         return y.permute(0, 3, 1, 2)                              # channels-last [n, o, h, w]
-    y = torch.matmul(wt, x.reshape(n, c, h * w))
+    y = _Conv1x1NCHW.apply(x.reshape(n, c, h * w), wt)
     if conv.bias is not None:
         y = y + conv.bias.reshape(1, -1, 1).to(y.dtype)
     return y.reshape(n, -1, h, w)
+
+
+class _Conv1x1NCHW(torch.autograd.Function):
+    """y[n] = W @ x[n] for x [n, c, s], W [o, c].  Autograd of the broadcast matmul folds the
+    weight gradient into ONE GEMM with K = n*s = 81,000 and an o x c = 2 x 128 (policy), 1 x 128
+    (value) or 16 x 1 (action embedding) output: hipBLASLt runs that on 1-8 workgroups, 0.55-0.63 ms
+    each (7 % of a training step).  Here it is a batched GEMM over n (K = s) reduced over n in float32."""
+
+    @staticmethod
+    def forward(ctx, x, wt):
+        if torch.is_autocast_enabled(x.device.type):
+            dt = torch.get_autocast_dtype(x.device.type)
+            x, wt = x.to(dt), wt.to(dt)
+        ctx.save_for_backward(x, wt)
+        return torch.matmul(wt, x)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, wt = ctx.saved_tensors
+        gy = gy.to(x.dtype)
+        gx = torch.matmul(wt.t(), gy) if ctx.needs_input_grad[0] else None
+        gw = torch.bmm(gy, x.transpose(1, 2)).sum(0, dtype=torch.float32) if ctx.needs_input_grad[1] else None
+        return gx, gw
 
 
 class _Block(nn.Module):
@@ -627,7 +650,7 @@ class Trainer:
         self.flat_grad = torch.zeros(sum(p.numel() for p in self.params), dtype=torch.float32, device=self.device)
         off = 0
         for p in self.params:
-            p.grad = self.flat_grad[off:off + p.numel()].view_as(p)
+            p.grad = self.flat_grad[off:off + p.numel()].as_strided(p.shape, p.stride())  # same layout as p
             off += p.numel()
         cuda = self.device.type == "cuda"
         lr = torch.tensor(c.LEARNING_RATE, device=self.device) if cuda else c.LEARNING_RATE
