@@ -22,6 +22,8 @@
 #include <hip/hip_bf16.h>
 #include <hip/hip_fp16.h>
 
+#include <initializer_list>
+
 namespace gmz {
 namespace {
 
@@ -80,29 +82,33 @@ __global__ void __launch_bounds__(BN_THREADS) k_bn_stats(const T *__restrict__ x
   if (threadIdx.x == 0) {
     int rows = 0;
     for (int b = b0; b < b1; ++b) rows += (!mask || mask[b]) ? 1 : 0;
-    double *o = ws + ((size_t)c * ns + t) * 3;
+    double *o = ws + ((size_t)c * ns + t) * 3;  // (.., .., valid pixels)
     o[0] = s1;
     o[1] = s2;
-    o[2] = rows;
+    o[2] = (double)rows * S;
   }
 }
 
-// per-channel finalisation of the split partials: ws[(c * cs + t * ts) * 3 + k], t < ns
+// per-channel finalisation of the split partials ws[(c * cs + t * ts) * 3 + k], t < ns: one wave per
+// channel, lanes stride the splits (f64), then a wave sum.
 //  forward : save = (mean, invstd), running-stat update (nn.BatchNorm training: unbiased variance)
 //  backward: dgamma = sum dz*xhat, dbeta = sum dz, coef = (mean dz, mean dz*xhat) over the masked rows
-__global__ void k_bn_finalize(const double *__restrict__ ws, int C, int ns, int cs, int ts, int S, int backward,
-                              float eps, float momentum, float *save, float *running_mean, float *running_var,
-                              int64_t *num_batches, float *dgamma, float *dbeta, float *coef) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double a = 0.0, b = 0.0, rows = 0.0;
-  for (int t = 0; t < ns; ++t) {
+__global__ void __launch_bounds__(WAVE) k_bn_finalize(const double *__restrict__ ws, int C, int ns, int cs, int ts,
+                                                      int backward, float eps, float momentum, float *save,
+                                                      float *running_mean, float *running_var, int64_t *num_batches,
+                                                      float *dgamma, float *dbeta, float *coef) {
+  const int c = blockIdx.x;
+  double a = 0.0, b = 0.0, n = 0.0;
+  for (int t = threadIdx.x; t < ns; t += WAVE) {
     const double *p = ws + ((size_t)c * cs + (size_t)t * ts) * 3;
     a += p[0];
     b += p[1];
-    rows += p[2];
+    n += p[2];
   }
-  const double n = rows * S;
+  a = wave_sum_d(a);
+  b = wave_sum_d(b);
+  n = wave_sum_d(n);
+  if (threadIdx.x != 0) return;
   if (!backward) {
     const double nn = n > 0.0 ? n : 1.0;
     const double m = a / nn;
@@ -169,10 +175,10 @@ __global__ void __launch_bounds__(BN_THREADS) k_bn_bwd_red(const T *__restrict__
   if (threadIdx.x == 0) {
     int rows = 0;
     for (int b = b0; b < b1; ++b) rows += (!mask || mask[b]) ? 1 : 0;
-    double *o = ws + ((size_t)c * ns + t) * 3;
+    double *o = ws + ((size_t)c * ns + t) * 3;  // (.., .., valid pixels)
     o[0] = sg;
     o[1] = sgx;
-    o[2] = rows;
+    o[2] = (double)rows * S;
   }
 }
 
@@ -203,206 +209,264 @@ __global__ void __launch_bounds__(BN_THREADS) k_bn_bwd_apply(const T *__restrict
 }
 
 // ---------------------------------------------------------------- channels-last (NHWC) variants
-// x[b][s][c] with C even (<= 2 * BN_THREADS): a thread owns a channel pair, C/2 threads cover one
-// position, BN_THREADS / (C/2) positions per block step; partials ws[t][C][3].
-template <typename T>
-__device__ __forceinline__ void ld2(const T *p, size_t k, float &a, float &b) {
-  a = ld(p, k);
-  b = ld(p, k + 1);
+// x[b][s][c], C even: a thread owns V consecutive channels of one position (V = 8: one 16-B access
+// for f16/bf16; V = 2 when C % 8 != 0 or an operand is not 16-B aligned), C/V threads cover one
+// position, BN_THREADS / (C/V) positions per block step.  The reductions give each of ns workgroups a
+// contiguous pixel range (pixel = b*S + s, ranges cross rows), accumulate per thread in f32 over the
+// ~10 pixels it sees and combine the position groups in f64; partials ws[t][C][3] (sum, sum of
+// squares | sum dz, sum dz*xhat, valid pixels).
+template <typename T, int V>
+struct alignas(sizeof(T) * V) VecT {
+  T v[V];
+};
+template <typename T, int V>
+__device__ __forceinline__ void ldv(const T *p, size_t k, float *o) {
+  const VecT<T, V> r = *reinterpret_cast<const VecT<T, V> *>(p + k);
+#pragma unroll
+  for (int j = 0; j < V; ++j) o[j] = ld(r.v, j);
 }
-__device__ __forceinline__ void ld2(const __half *p, size_t k, float &a, float &b) {
-  const __half2 v = *reinterpret_cast<const __half2 *>(p + k);
-  a = __low2float(v);
-  b = __high2float(v);
-}
-__device__ __forceinline__ void ld2(const float *p, size_t k, float &a, float &b) {
-  const float2 v = *reinterpret_cast<const float2 *>(p + k);
-  a = v.x;
-  b = v.y;
-}
-template <typename T>
-__device__ __forceinline__ void st2(T *p, size_t k, float a, float b) {
-  st(p, k, a);
-  st(p, k + 1, b);
-}
-__device__ __forceinline__ void st2(__half *p, size_t k, float a, float b) {
-  *reinterpret_cast<__half2 *>(p + k) = __floats2half2_rn(a, b);
-}
-__device__ __forceinline__ void st2(float *p, size_t k, float a, float b) {
-  *reinterpret_cast<float2 *>(p + k) = make_float2(a, b);
+template <typename T, int V>
+__device__ __forceinline__ void stv(T *p, size_t k, const float *a) {
+  VecT<T, V> r;
+#pragma unroll
+  for (int j = 0; j < V; ++j) st(r.v, j, a[j]);
+  *reinterpret_cast<VecT<T, V> *>(p + k) = r;
 }
 
-// stats (backward = 0) or dz sums (backward = 1) of the masked rows of block t's row range
-template <typename T, int BWD>
+constexpr int BNL_MAX_SPLITS = 512;
+
+// stats (BWD = 0) or dz sums (BWD = 1) of the masked pixels of workgroup t's pixel range
+template <typename T, int BWD, int V>
 __global__ void __launch_bounds__(BN_THREADS) k_bnl_red(const T *__restrict__ x, const T *__restrict__ y,
                                                         const T *__restrict__ dy, const uint8_t *__restrict__ mask,
                                                         int B, int C, int S, const float *__restrict__ save, int relu,
                                                         double *__restrict__ ws) {
-  __shared__ double red[BN_THREADS][4];
+  __shared__ float red[BN_THREADS * V * 2];  // [group][2][C]
   const int t = blockIdx.x, ns = gridDim.x;
-  const int tpp = C / 2, pl = BN_THREADS / tpp;
+  const int tpp = C / V, pl = BN_THREADS / tpp;
   const int cp = threadIdx.x % tpp, grp = threadIdx.x / tpp;
-  const int c = 2 * cp;
-  int b0, b1;
-  split_rows(B, ns, t, b0, b1);
-  const int npix = (b1 - b0) * S;
-  double a0 = 0.0, a1 = 0.0, q0 = 0.0, q1 = 0.0;
-  float m0 = 0.f, m1 = 0.f, i0 = 0.f, i1 = 0.f;
+  const int c = V * cp;
+  const long P = (long)B * S;
+  const long p0 = P * t / ns, p1 = P * (t + 1) / ns;
+  float a[V], q[V], m[V], is[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    a[j] = q[j] = 0.f;
+    m[j] = is[j] = 0.f;
+  }
   if (BWD) {
-    m0 = save[c];
-    m1 = save[c + 1];
-    i0 = save[C + c];
-    i1 = save[C + c + 1];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      m[j] = save[c + j];
+      is[j] = save[C + c + j];
+    }
   }
   if (grp < pl) {
-    for (int p = grp; p < npix; p += pl) {
-      const int b = b0 + p / S;
-      if (mask && !mask[b]) continue;
-      const size_t k = ((size_t)b0 * S + p) * C + c;
-      float v0, v1;
+    for (long p = p0 + grp; p < p1; p += pl) {
+      if (mask && !mask[p / S]) continue;
+      const size_t k = (size_t)p * C + c;
+      float v[V];
       if (!BWD) {
-        ld2(x, k, v0, v1);
-        a0 += v0;
-        a1 += v1;
-        q0 += (double)v0 * v0;
-        q1 += (double)v1 * v1;
-      } else {
-        float g0, g1, x0, x1;
-        ld2(dy, k, g0, g1);
-        if (relu) {
-          ld2(y, k, v0, v1);
-          if (!(v0 > 0.f)) g0 = 0.f;
-          if (!(v1 > 0.f)) g1 = 0.f;
+        ldv<T, V>(x, k, v);
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          a[j] += v[j];
+          q[j] = fmaf(v[j], v[j], q[j]);
         }
-        ld2(x, k, x0, x1);
-        a0 += g0;
-        a1 += g1;
-        q0 += (double)g0 * (double)((x0 - m0) * i0);
-        q1 += (double)g1 * (double)((x1 - m1) * i1);
+      } else {
+        float g[V], xv[V];
+        ldv<T, V>(dy, k, g);
+        if (relu) {
+          ldv<T, V>(y, k, v);
+#pragma unroll
+          for (int j = 0; j < V; ++j)
+            if (!(v[j] > 0.f)) g[j] = 0.f;
+        }
+        ldv<T, V>(x, k, xv);
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          a[j] += g[j];
+          q[j] = fmaf(g[j], (xv[j] - m[j]) * is[j], q[j]);
+        }
       }
     }
-  }
-  red[threadIdx.x][0] = a0;
-  red[threadIdx.x][1] = a1;
-  red[threadIdx.x][2] = q0;
-  red[threadIdx.x][3] = q1;
-  __syncthreads();
-  if (grp == 0) {
-    for (int g = 1; g < pl; ++g) {
-      const double *r = red[g * tpp + cp];
-      a0 += r[0];
-      a1 += r[1];
-      q0 += r[2];
-      q1 += r[3];
+    float *r = red + (size_t)grp * 2 * C;
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      r[c + j] = a[j];
+      r[C + c + j] = q[j];
     }
-    int rows = 0;
-    for (int b = b0; b < b1; ++b) rows += (!mask || mask[b]) ? 1 : 0;
-    double *o = ws + ((size_t)t * C + c) * 3;
-    o[0] = a0;
-    o[1] = q0;
-    o[2] = rows;
-    o[3] = a1;
-    o[4] = q1;
-    o[5] = rows;
+  }
+  __syncthreads();
+  double cnt = 0.0;
+  if (mask) {
+    for (long b = p0 / S; b * S < p1; ++b) {
+      if (!mask[b]) continue;
+      const long lo = b * S > p0 ? b * S : p0, hi = (b + 1) * S < p1 ? (b + 1) * S : p1;
+      cnt += (double)(hi - lo);
+    }
+  } else {
+    cnt = (double)(p1 - p0);
+  }
+  for (int ch = threadIdx.x; ch < C; ch += BN_THREADS) {
+    double sa = 0.0, sq = 0.0;
+    for (int g = 0; g < pl; ++g) {
+      sa += (double)red[(size_t)g * 2 * C + ch];
+      sq += (double)red[(size_t)g * 2 * C + C + ch];
+    }
+    double *o = ws + ((size_t)t * C + ch) * 3;
+    o[0] = sa;
+    o[1] = sq;
+    o[2] = cnt;
   }
 }
 
-template <typename T>
+// elementwise passes: a thread keeps its V channels' constants in registers and strides over
+// positions (pl positions per block step, grid-stride over the B*S positions)
+template <typename T, int V>
 __global__ void __launch_bounds__(BN_THREADS) k_bnl_apply(const T *__restrict__ x, const T *__restrict__ res,
-                                                          size_t npairs, int C, const float *__restrict__ gamma,
+                                                          long P, int C, const float *__restrict__ gamma,
                                                           const float *__restrict__ beta, int relu,
                                                           T *__restrict__ y, const float *__restrict__ save) {
-  for (size_t i = (size_t)blockIdx.x * BN_THREADS + threadIdx.x; i < npairs; i += (size_t)gridDim.x * BN_THREADS) {
-    const size_t k = 2 * i;
-    const int c = (int)(k % C);
-    float v0, v1;
-    ld2(x, k, v0, v1);
-    v0 = (v0 - save[c]) * (gamma[c] * save[C + c]) + beta[c];
-    v1 = (v1 - save[c + 1]) * (gamma[c + 1] * save[C + c + 1]) + beta[c + 1];
-    if (res) {
-      float r0, r1;
-      ld2(res, k, r0, r1);
-      v0 += r0;
-      v1 += r1;
+  const int tpp = C / V, pl = BN_THREADS / tpp;
+  const int cp = threadIdx.x % tpp, grp = threadIdx.x / tpp;
+  if (grp >= pl) return;
+  const int c = V * cp;
+  float sc[V], sh[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    sc[j] = gamma[c + j] * save[C + c + j];
+    sh[j] = beta[c + j];
+  }
+  float mean[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) mean[j] = save[c + j];
+  for (long p = (long)blockIdx.x * pl + grp; p < P; p += (long)gridDim.x * pl) {
+    const size_t k = (size_t)p * C + c;
+    float v[V], r[V];
+    ldv<T, V>(x, k, v);
+    if (res) ldv<T, V>(res, k, r);
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      v[j] = (v[j] - mean[j]) * sc[j] + sh[j];
+      if (res) v[j] += r[j];
+      if (relu) v[j] = fmaxf(v[j], 0.f);
     }
-    if (relu) {
-      v0 = fmaxf(v0, 0.f);
-      v1 = fmaxf(v1, 0.f);
-    }
-    st2(y, k, v0, v1);
+    stv<T, V>(y, k, v);
   }
 }
 
-template <typename T>
+template <typename T, int V>
 __global__ void __launch_bounds__(BN_THREADS) k_bnl_bwd_apply(const T *__restrict__ x, const T *__restrict__ y,
                                                               const T *__restrict__ dy,
-                                                              const uint8_t *__restrict__ mask, size_t npairs, int C,
+                                                              const uint8_t *__restrict__ mask, long P, int C,
                                                               int S, const float *__restrict__ gamma,
                                                               const float *__restrict__ save, int relu,
                                                               T *__restrict__ dx, T *__restrict__ dres,
                                                               const float *__restrict__ coef) {
-  const size_t rowpairs = (size_t)S * C / 2;
-  for (size_t i = (size_t)blockIdx.x * BN_THREADS + threadIdx.x; i < npairs; i += (size_t)gridDim.x * BN_THREADS) {
-    const size_t k = 2 * i;
-    const int c = (int)(k % C);
-    const bool in = !mask || mask[i / rowpairs];
-    float g0, g1;
-    ld2(dy, k, g0, g1);
+  const int tpp = C / V, pl = BN_THREADS / tpp;
+  const int cp = threadIdx.x % tpp, grp = threadIdx.x / tpp;
+  if (grp >= pl) return;
+  const int c = V * cp;
+  float mean[V], is[V], mg[V], mgx[V], k1[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    mean[j] = save[c + j];
+    is[j] = save[C + c + j];
+    mg[j] = coef[c + j];
+    mgx[j] = coef[C + c + j];
+    k1[j] = gamma[c + j] * is[j];
+  }
+  for (long p = (long)blockIdx.x * pl + grp; p < P; p += (long)gridDim.x * pl) {
+    const size_t k = (size_t)p * C + c;
+    const bool in = !mask || mask[p / S];
+    float g[V], d[V];
+    ldv<T, V>(dy, k, g);
     if (relu) {
-      float y0, y1;
-      ld2(y, k, y0, y1);
-      if (!(y0 > 0.f)) g0 = 0.f;
-      if (!(y1 > 0.f)) g1 = 0.f;
+      float yv[V];
+      ldv<T, V>(y, k, yv);
+#pragma unroll
+      for (int j = 0; j < V; ++j)
+        if (!(yv[j] > 0.f)) g[j] = 0.f;
     }
-    if (dres) st2(dres, k, g0, g1);
-    float d0 = g0, d1 = g1;
+    if (dres) stv<T, V>(dres, k, g);
     if (in) {
-      float x0, x1;
-      ld2(x, k, x0, x1);
-      d0 = g0 - coef[c] - (x0 - save[c]) * save[C + c] * coef[C + c];
-      d1 = g1 - coef[c + 1] - (x1 - save[c + 1]) * save[C + c + 1] * coef[C + c + 1];
+      float xv[V];
+      ldv<T, V>(x, k, xv);
+#pragma unroll
+      for (int j = 0; j < V; ++j) d[j] = g[j] - mg[j] - (xv[j] - mean[j]) * is[j] * mgx[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < V; ++j) d[j] = g[j];
     }
-    st2(dx, k, gamma[c] * save[C + c] * d0, gamma[c + 1] * save[C + c + 1] * d1);
+#pragma unroll
+    for (int j = 0; j < V; ++j) d[j] *= k1[j];
+    stv<T, V>(dx, k, d);
   }
 }
 
-int splits_for(int B, int C, int nhwc) {
-  // NCHW: (C x ns) workgroups, enough to cover the 256 CUs (>= ~2048); NHWC: ns workgroups of all
-  // channels (~1024).  Never more splits than rows.
-  int ns = nhwc ? 1024 : (2048 + C - 1) / C;
-  if (!nhwc && ns > BN_MAX_SPLITS) ns = BN_MAX_SPLITS;
+int splits_for(int B, int C, int S, int nhwc) {
+  // NCHW: (C x ns) workgroups, enough to cover the 256 CUs (>= ~2048), never more splits than rows;
+  // NHWC: ns pixel ranges of all channels, 2 per CU, at least one block step (16 positions at C=128) each.
+  if (nhwc) {
+    const long P = (long)B * S;
+    long ns = P / 16;
+    if (ns > BNL_MAX_SPLITS) ns = BNL_MAX_SPLITS;
+    return ns < 1 ? 1 : (int)ns;
+  }
+  int ns = (2048 + C - 1) / C;
+  if (ns > BN_MAX_SPLITS) ns = BN_MAX_SPLITS;
   if (ns > B) ns = B;
   return ns < 1 ? 1 : ns;
 }
 
-size_t ws_doubles(int B, int C, int nhwc) { return (size_t)C * splits_for(B, C, nhwc) * 3; }
+size_t ws_doubles(int B, int C, int S, int nhwc) { return (size_t)C * splits_for(B, C, S, nhwc) * 3; }
 
-int elementwise_blocks(size_t npairs) {
-  size_t nb = (npairs + BN_THREADS - 1) / BN_THREADS;
+// NHWC elementwise grid: ~4 position steps per thread, at most 4096 workgroups
+int elementwise_blocks(long P, int C, int V) {
+  const long pl = BN_THREADS / (C / V);
+  long nb = (P + 4 * pl - 1) / (4 * pl);
   return (int)(nb < 4096 ? (nb < 1 ? 1 : nb) : 4096);
+}
+
+// channel vector width of the NHWC kernels: 8 when C allows it and every operand is 16-B aligned
+int nhwc_vec(int C, size_t esize, std::initializer_list<const void *> ptrs) {
+  if (C % 8 != 0 || C / 8 > BN_THREADS) return 2;
+  for (const void *p : ptrs)
+    if (p && ((uintptr_t)p % (8 * esize)) != 0) return 2;
+  return 8;
 }
 
 template <typename T>
 int bn_forward(int nhwc, const void *x, const void *res, const uint8_t *mask, int B, int C, int S, const float *gamma,
                const float *beta, float eps, float momentum, float *rm, float *rv, int64_t *nb, int relu, void *y,
                float *save, void *ws, hipStream_t st) {
-  const int ns = splits_for(B, C, nhwc);
+  const int ns = splits_for(B, C, S, nhwc);
+  const int V = nhwc ? nhwc_vec(C, sizeof(T), {x, res, y}) : 0;
   if (nhwc) {
-    hipLaunchKernelGGL((k_bnl_red<T, 0>), dim3(ns), dim3(BN_THREADS), 0, st, (const T *)x, (const T *)nullptr,
-                       (const T *)nullptr, mask, B, C, S, (const float *)nullptr, 0, (double *)ws);
+    if (V == 8)
+      hipLaunchKernelGGL((k_bnl_red<T, 0, 8>), dim3(ns), dim3(BN_THREADS), 0, st, (const T *)x, (const T *)nullptr,
+                         (const T *)nullptr, mask, B, C, S, (const float *)nullptr, 0, (double *)ws);
+    else
+      hipLaunchKernelGGL((k_bnl_red<T, 0, 2>), dim3(ns), dim3(BN_THREADS), 0, st, (const T *)x, (const T *)nullptr,
+                         (const T *)nullptr, mask, B, C, S, (const float *)nullptr, 0, (double *)ws);
   } else {
     hipLaunchKernelGGL(k_bn_stats<T>, dim3(C, ns), dim3(BN_THREADS), 0, st, (const T *)x, mask, B, C, S,
                        (double *)ws);
   }
   GMZ_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_bn_finalize, dim3((C + 255) / 256), dim3(256), 0, st, (const double *)ws, C, ns,
-                     nhwc ? 1 : ns, nhwc ? C : 1, S, 0, eps, momentum, save, rm, rv, nb, (float *)nullptr,
-                     (float *)nullptr, (float *)nullptr);
+  hipLaunchKernelGGL(k_bn_finalize, dim3(C), dim3(WAVE), 0, st, (const double *)ws, C, ns, nhwc ? 1 : ns,
+                     nhwc ? C : 1, 0, eps, momentum, save, rm, rv, nb, (float *)nullptr, (float *)nullptr,
+                     (float *)nullptr);
   GMZ_LAUNCH_CHECK();
   if (nhwc) {
-    const size_t np = (size_t)B * S * C / 2;
-    hipLaunchKernelGGL(k_bnl_apply<T>, dim3(elementwise_blocks(np)), dim3(BN_THREADS), 0, st, (const T *)x,
-                       (const T *)res, np, C, gamma, beta, relu, (T *)y, save);
+    const long P = (long)B * S;
+    if (V == 8)
+      hipLaunchKernelGGL((k_bnl_apply<T, 8>), dim3(elementwise_blocks(P, C, 8)), dim3(BN_THREADS), 0, st,
+                         (const T *)x, (const T *)res, P, C, gamma, beta, relu, (T *)y, save);
+    else
+      hipLaunchKernelGGL((k_bnl_apply<T, 2>), dim3(elementwise_blocks(P, C, 2)), dim3(BN_THREADS), 0, st,
+                         (const T *)x, (const T *)res, P, C, gamma, beta, relu, (T *)y, save);
   } else {
     hipLaunchKernelGGL(k_bn_apply<T>, dim3(C, ns), dim3(BN_THREADS), 0, st, (const T *)x, (const T *)res, B, C, S,
                        gamma, beta, relu, (T *)y, save);
@@ -415,27 +479,70 @@ template <typename T>
 int bn_backward(int nhwc, const void *x, const void *y, const void *dy, const uint8_t *mask, int B, int C, int S,
                 const float *gamma, const float *save, int relu, void *dx, void *dres, float *dgamma, float *dbeta,
                 void *ws, hipStream_t st) {
-  const int ns = splits_for(B, C, nhwc);
-  float *coef = (float *)((double *)ws + ws_doubles(B, C, nhwc));  // f32 [2][C] after the partials
+  const int ns = splits_for(B, C, S, nhwc);
+  const int V = nhwc ? nhwc_vec(C, sizeof(T), {x, y, dy, dx, dres}) : 0;
+  float *coef = (float *)((double *)ws + ws_doubles(B, C, S, nhwc));  // f32 [2][C] after the partials
   if (nhwc) {
-    hipLaunchKernelGGL((k_bnl_red<T, 1>), dim3(ns), dim3(BN_THREADS), 0, st, (const T *)x, (const T *)y,
-                       (const T *)dy, mask, B, C, S, save, relu, (double *)ws);
+    if (V == 8)
+      hipLaunchKernelGGL((k_bnl_red<T, 1, 8>), dim3(ns), dim3(BN_THREADS), 0, st, (const T *)x, (const T *)y,
+                         (const T *)dy, mask, B, C, S, save, relu, (double *)ws);
+    else
+      hipLaunchKernelGGL((k_bnl_red<T, 1, 2>), dim3(ns), dim3(BN_THREADS), 0, st, (const T *)x, (const T *)y,
+                         (const T *)dy, mask, B, C, S, save, relu, (double *)ws);
   } else {
     hipLaunchKernelGGL(k_bn_bwd_red<T>, dim3(C, ns), dim3(BN_THREADS), 0, st, (const T *)x, (const T *)y,
                        (const T *)dy, mask, B, C, S, save, relu, (double *)ws);
   }
   GMZ_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_bn_finalize, dim3((C + 255) / 256), dim3(256), 0, st, (const double *)ws, C, ns,
-                     nhwc ? 1 : ns, nhwc ? C : 1, S, 1, 0.f, 0.f, (float *)nullptr, (float *)nullptr,
-                     (float *)nullptr, (int64_t *)nullptr, dgamma, dbeta, coef);
+  hipLaunchKernelGGL(k_bn_finalize, dim3(C), dim3(WAVE), 0, st, (const double *)ws, C, ns, nhwc ? 1 : ns,
+                     nhwc ? C : 1, 1, 0.f, 0.f, (float *)nullptr, (float *)nullptr, (float *)nullptr,
+                     (int64_t *)nullptr, dgamma, dbeta, coef);
   GMZ_LAUNCH_CHECK();
   if (nhwc) {
-    const size_t np = (size_t)B * S * C / 2;
-    hipLaunchKernelGGL(k_bnl_bwd_apply<T>, dim3(elementwise_blocks(np)), dim3(BN_THREADS), 0, st, (const T *)x,
-                       (const T *)y, (const T *)dy, mask, np, C, S, gamma, save, relu, (T *)dx, (T *)dres, coef);
+    const long P = (long)B * S;
+    if (V == 8)
+      hipLaunchKernelGGL((k_bnl_bwd_apply<T, 8>), dim3(elementwise_blocks(P, C, 8)), dim3(BN_THREADS), 0, st,
+                         (const T *)x, (const T *)y, (const T *)dy, mask, P, C, S, gamma, save, relu, (T *)dx,
+                         (T *)dres, coef);
+    else
+      hipLaunchKernelGGL((k_bnl_bwd_apply<T, 2>), dim3(elementwise_blocks(P, C, 2)), dim3(BN_THREADS), 0, st,
+                         (const T *)x, (const T *)y, (const T *)dy, mask, P, C, S, gamma, save, relu, (T *)dx,
+                         (T *)dres, coef);
   } else {
     hipLaunchKernelGGL(k_bn_bwd_apply<T>, dim3(C, ns), dim3(BN_THREADS), 0, st, (const T *)x, (const T *)y,
                        (const T *)dy, mask, B, C, S, gamma, save, relu, (T *)dx, (T *)dres, coef);
+  }
+  GMZ_LAUNCH_CHECK();
+  return 0;
+}
+
+// eval mode: save = (running_mean, 1/sqrt(running_var + eps))
+__global__ void k_bn_eval_save(const float *__restrict__ rm, const float *__restrict__ rv, int C, float eps,
+                               float *__restrict__ save) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  save[c] = rm[c];
+  save[C + c] = 1.0f / sqrtf(rv[c] + eps);
+}
+
+template <typename T>
+int bn_eval(int nhwc, const void *x, const void *res, int B, int C, int S, const float *gamma, const float *beta,
+            const float *rm, const float *rv, float eps, int relu, void *y, void *ws, hipStream_t st) {
+  float *save = (float *)ws;
+  hipLaunchKernelGGL(k_bn_eval_save, dim3((C + 255) / 256), dim3(256), 0, st, rm, rv, C, eps, save);
+  GMZ_LAUNCH_CHECK();
+  if (nhwc) {
+    const int V = nhwc_vec(C, sizeof(T), {x, res, y});
+    const long P = (long)B * S;
+    if (V == 8)
+      hipLaunchKernelGGL((k_bnl_apply<T, 8>), dim3(elementwise_blocks(P, C, 8)), dim3(BN_THREADS), 0, st,
+                         (const T *)x, (const T *)res, P, C, gamma, beta, relu, (T *)y, (const float *)save);
+    else
+      hipLaunchKernelGGL((k_bnl_apply<T, 2>), dim3(elementwise_blocks(P, C, 2)), dim3(BN_THREADS), 0, st,
+                         (const T *)x, (const T *)res, P, C, gamma, beta, relu, (T *)y, (const float *)save);
+  } else {
+    hipLaunchKernelGGL(k_bn_apply<T>, dim3(C, splits_for(B, C, S, 0)), dim3(BN_THREADS), 0, st, (const T *)x,
+                       (const T *)res, B, C, S, gamma, beta, relu, (T *)y, (const float *)save);
   }
   GMZ_LAUNCH_CHECK();
   return 0;
@@ -455,7 +562,7 @@ static int check_layout(int layout, int C) {
 GMZ_EXPORT int gmz_bn_workspace_bytes(int layout, int B, int C, int S, size_t *out) {
   if (B <= 0 || C <= 0 || S <= 0 || !out) return fail("gmz_bn_workspace_bytes: bad shape");
   if (check_layout(layout, C)) return -1;
-  *out = (ws_doubles(B, C, layout) + (size_t)C) * sizeof(double);  // partials + f32 [2][C] coefficients
+  *out = (ws_doubles(B, C, S, layout) + (size_t)C) * sizeof(double);  // partials + f32 [2][C] coefficients
   return 0;
 }
 
@@ -496,4 +603,21 @@ GMZ_EXPORT int gmz_bn_backward(int dtype, int layout, const void *x, const void 
                                                dbeta, ws, st);
   }
   return fail("gmz_bn_backward: dtype must be 0 (f32), 1 (f16) or 2 (bf16)");
+}
+
+GMZ_EXPORT int gmz_bn_eval(int dtype, int layout, const void *x, const void *res, int B, int C, int S,
+                           const float *gamma, const float *beta, const float *running_mean,
+                           const float *running_var, float eps, int relu, void *y, void *ws, void *stream) {
+  if (B <= 0 || C <= 0 || S <= 0 || (size_t)B * C * S >= (1ull << 31)) return fail("gmz_bn_eval: bad shape");
+  if (check_layout(layout, C)) return -1;
+  if (!x || !y || !gamma || !beta || !running_mean || !running_var || !ws) return fail("gmz_bn_eval: null operand");
+  hipStream_t st = (hipStream_t)stream;
+  switch (dtype) {
+    case 0: return bn_eval<float>(layout, x, res, B, C, S, gamma, beta, running_mean, running_var, eps, relu, y, ws, st);
+    case 1: return bn_eval<__half>(layout, x, res, B, C, S, gamma, beta, running_mean, running_var, eps, relu, y, ws, st);
+    case 2:
+      return bn_eval<__hip_bfloat16>(layout, x, res, B, C, S, gamma, beta, running_mean, running_var, eps, relu, y, ws,
+                                     st);
+  }
+  return fail("gmz_bn_eval: dtype must be 0 (f32), 1 (f16) or 2 (bf16)");
 }

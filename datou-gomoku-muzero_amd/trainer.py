@@ -227,10 +227,31 @@ def _bn_act(mod, x, mask=None, res=None, relu=True):
         m = None if mask is None else mask.contiguous().view(torch.uint8)
         return _FusedMaskedBN.apply(x, mod.weight, mod.bias, res, m, mod.running_mean, mod.running_var,
                                     mod.num_batches_tracked, mod.eps, mod.momentum, relu)
+    if (FUSED_BN and not mod.training and x.is_cuda and x.dtype in _BN_DTYPES and _bn_layout(x) is not None
+            and not (torch.is_grad_enabled() and (x.requires_grad or mod.weight.requires_grad))):
+        return _bn_eval(mod, x, res, relu)
     y = _bn(mod, x, mask)
     if res is not None:
         y = y + res
     return F.relu(y) if relu else y
+
+
+def _bn_eval(mod, x, res, relu):
+    """Eval-mode BatchNorm (running statistics) + residual + ReLU as one HIP pass (``gmz_bn_eval``):
+    the target network's fp32 forward (loss.py:54-55), no autograd."""
+    from . import _lib
+    layout = _bn_layout(x)
+    if res is not None:
+        res = _like(res.to(x.dtype), layout)
+    B, C = x.shape[0], x.shape[1]
+    S = x[0, 0].numel()
+    y = torch.empty_like(x)
+    ws = _bn_workspace(layout, B, C, S, x.device)
+    _lib.check(_lib.load().gmz_bn_eval(_BN_DTYPES[x.dtype], layout, _lib.ptr(x), _lib.ptr(res), B, C, S,
+                                       _lib.ptr(mod.weight), _lib.ptr(mod.bias), _lib.ptr(mod.running_mean),
+                                       _lib.ptr(mod.running_var), float(mod.eps), int(relu), _lib.ptr(y),
+                                       _lib.ptr(ws), _lib.stream_ptr()))
+    return y
 
 
 def _conv1x1(conv, x):
@@ -242,10 +263,10 @@ def _conv1x1(conv, x):
     wt = conv.weight.reshape(conv.weight.shape[0], c)
     wt = wt.to(x.dtype) if not torch.is_autocast_enabled() else wt
     if c > 1 and x.is_contiguous(memory_format=torch.channels_last) and not x.is_contiguous():
-        y = torch.matmul(x.permute(0, 2, 3, 1), wt.t())          # [n, h, w, o]
+        y = _Conv1x1NHWC.apply(x.permute(0, 2, 3, 1).reshape(n, h * w, c), wt)   # [n, s, o]
         if conv.bias is not None:
             y = y + conv.bias.to(y.dtype)
-        return y.permute(0, 3, 1, 2)                              # channels-last [n, o, h, w]
+        return y.reshape(n, h, w, -1).permute(0, 3, 1, 2)        # channels-last [n, o, h, w]
     y = _Conv1x1NCHW.apply(x.reshape(n, c, h * w), wt)
     if conv.bias is not None:
         y = y + conv.bias.reshape(1, -1, 1).to(y.dtype)
@@ -272,6 +293,28 @@ class _Conv1x1NCHW(torch.autograd.Function):
         gy = gy.to(x.dtype)
         gx = torch.matmul(wt.t(), gy) if ctx.needs_input_grad[0] else None
         gw = torch.bmm(gy, x.transpose(1, 2)).sum(0, dtype=torch.float32) if ctx.needs_input_grad[1] else None
+        return gx, gw
+
+
+class _Conv1x1NHWC(torch.autograd.Function):
+    """y[n] = x[n] @ W^T for channels-last x [n, s, c], W [o, c]; the weight gradient as a batched
+    GEMM over n reduced in float32 (see ``_Conv1x1NCHW``: one GEMM with K = n*s ran on 8 workgroups,
+    0.55 ms per call)."""
+
+    @staticmethod
+    def forward(ctx, x, wt):
+        if torch.is_autocast_enabled(x.device.type):
+            dt = torch.get_autocast_dtype(x.device.type)
+            x, wt = x.to(dt), wt.to(dt)
+        ctx.save_for_backward(x, wt)
+        return torch.matmul(x, wt.t())
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, wt = ctx.saved_tensors
+        gy = gy.to(x.dtype)
+        gx = torch.matmul(gy, wt) if ctx.needs_input_grad[0] else None
+        gw = torch.bmm(gy.transpose(1, 2), x).sum(0, dtype=torch.float32) if ctx.needs_input_grad[1] else None
         return gx, gw
 
 
@@ -461,6 +504,9 @@ class _HalveGrad(torch.autograd.Function):
         return g * 0.5
 
 
+AUTOCAST_CACHE = True  # autocast's weight casts once per step (and per graph replay), not per use: +1.3 %
+
+
 def muzero_loss(model, target_model, batch, is_weights, cfg, k=None, flip=None, amp=False, amp_dtype=None,
                 sync_logs=True, augmented=False):
     """loss.py:30-158.  ``batch`` = (obs [B,U+1,3,H,W], actions [B,U], rewards [B,U],
@@ -495,7 +541,7 @@ def muzero_loss(model, target_model, batch, is_weights, cfg, k=None, flip=None, 
     dev_type = obs.device.type
     zero = torch.zeros((), device=obs.device)
     with torch.autocast(dev_type, enabled=amp and dev_type == "cuda", dtype=amp_dtype or torch.float16,
-                        cache_enabled=False):
+                        cache_enabled=AUTOCAST_CACHE):
         h = model.representation(obs[:, 0])
         pl, vl = model.prediction(h)
         lp = F.cross_entropy(pl.float(), pi[:, 0], reduction="none")
@@ -623,7 +669,7 @@ class Trainer:
     distributed).  The batch is augmented eagerly into static input buffers before each replay.
     The first ``graph_warmup`` steps run eagerly (they are real steps)."""
 
-    def __init__(self, cfg=None, device="cuda", state_dict=None, amp=None, amp_dtype=None, channels_last=False,
+    def __init__(self, cfg=None, device="cuda", state_dict=None, amp=None, amp_dtype=None, channels_last=None,
                  graph=None, graph_warmup=3):
         c = cfg if isinstance(cfg, TrainConfig) else TrainConfig.from_any(cfg)
         self.cfg, self.device = c, torch.device(device)
@@ -634,11 +680,15 @@ class Trainer:
         self.target.load_state_dict(self.model.state_dict())
         self.amp = (self.device.type == "cuda") if amp is None else amp
         self.amp_dtype = amp_dtype  # None: float16 as the reference's torch.amp.autocast('cuda')
+        # default on the GPU: channels-last (18.8 vs 13.8 steps/s at config C4 with the same kernels)
+        channels_last = (self.device.type == "cuda") if channels_last is None else channels_last
         self.channels_last = channels_last
         if channels_last:  # NHWC activations: MIOpen's NHWC convolutions without layout transposes
             self.model = self.model.to(memory_format=torch.channels_last)
-            self.target = self.target.to(memory_format=torch.channels_last)
-            self.model.channels_last = self.target.channels_last = True
+            self.model.channels_last = True
+            # the target network's value (loss.py:54-55) runs in float32 like the reference's, outside
+            # autocast: MIOpen's NCHW fp32 Winograd kernels take 0.25 ms per conv, its NHWC fp32 path 0.51
+            # ms, so the target stays NCHW
         import torch.distributed as dist
         self.dist = dist if (dist.is_available() and dist.is_initialized()) else None
         if self.dist is not None:  # every rank starts from rank 0's weights
@@ -688,9 +738,13 @@ class Trainer:
         self.scaler.update()
         self.flat_grad.zero_()
         with torch.no_grad():  # utils.py:28-31 soft update (parameters only): tau * s + (1 - tau) * t
-            tp, sp = list(self.target.parameters()), list(self.model.parameters())
-            torch._foreach_mul_(tp, 1.0 - c.TARGET_MODEL_TAU)
-            torch._foreach_add_(tp, sp, alpha=c.TARGET_MODEL_TAU)
+            pairs = list(zip(self.target.parameters(), self.model.parameters()))
+            for same in (True, False):  # fused foreach kernels need equal strides (NCHW target, NHWC model)
+                tp = [t for t, p in pairs if (t.stride() == p.stride()) == same]
+                sp = [p for t, p in pairs if (t.stride() == p.stride()) == same]
+                if tp:
+                    torch._foreach_mul_(tp, 1.0 - c.TARGET_MODEL_TAU)
+                    torch._foreach_add_(tp, sp, alpha=c.TARGET_MODEL_TAU)
 
     def _augment_into_static(self, batch, is_weights, k, flip):
         obs, act, rew, pi, mval = batch

@@ -244,6 +244,12 @@ int gmz_bn_forward(int dtype, int layout, const void *x_dev, const void *res_dev
 int gmz_bn_backward(int dtype, int layout, const void *x_dev, const void *y_dev, const void *dy_dev, const uint8_t *mask_dev, int B,
                     int C, int S, const float *gamma_dev, const float *save_dev, int relu, void *dx_dev, void *dres_dev,
                     float *dgamma_dev, float *dbeta_dev, void *workspace_dev, void *stream);
+/* Eval-mode BatchNorm (running statistics) + residual + ReLU, same layouts/dtypes as gmz_bn_forward:
+ * y = relu?(gamma*(x-running_mean)/sqrt(running_var+eps) + beta (+ res)) — nn.BatchNorm2d/1d in eval()
+ * (the target network's value of loss.py:54-55).  workspace_dev: gmz_bn_workspace_bytes bytes. */
+int gmz_bn_eval(int dtype, int layout, const void *x_dev, const void *res_dev, int B, int C, int S, const float *gamma_dev,
+                const float *beta_dev, const float *running_mean_dev, const float *running_var_dev, float eps, int relu,
+                void *y_dev, void *workspace_dev, void *stream);
 
 #ifdef __cplusplus
 }

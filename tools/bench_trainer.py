@@ -26,10 +26,11 @@ ap.add_argument("--buffer", type=int, default=20000)
 ap.add_argument("--per", action="store_true")
 ap.add_argument("--no-amp", action="store_true")
 ap.add_argument("--bf16", action="store_true", help="autocast to bfloat16 instead of the reference's float16")
-ap.add_argument("--channels-last", action="store_true")
+ap.add_argument("--nchw", action="store_true", help="NCHW activations (default: channels-last, MIOpen's NHWC kernels)")
 ap.add_argument("--eager", action="store_true", help="no HIP-graph capture of the step")
-ap.add_argument("--benchmark", action="store_true", help="torch.backends.cudnn.benchmark (MIOpen Find per shape)")
+ap.add_argument("--no-benchmark", action="store_true", help="no torch.backends.cudnn.benchmark (MIOpen Find per shape)")
 a = ap.parse_args()
+a.channels_last, a.benchmark = not a.nchw, not a.no_benchmark
 torch.backends.cudnn.benchmark = a.benchmark
 
 world = int(os.environ.get("WORLD_SIZE", "1"))
