@@ -622,7 +622,10 @@ class ReplayBuffer:
         self.rew[idx] = st("reward_history", np.float32).to(self.device)
         self.pol[idx] = st("policy_history", np.float32).to(self.device)
         self.val[idx] = st("value_history", np.float32).to(self.device)
-        self.prio[idx.to(self.device)] = self.max_priority if self.cfg.ENABLE_PER else 1.0
+        if self.cfg.ENABLE_PER:
+            self.prio[idx.to(self.device)] = torch.as_tensor(self.max_priority, dtype=torch.float32, device=self.device)
+        else:
+            self.prio[idx.to(self.device)] = 1.0
         self.ptr = (self.ptr + n) % self.N
         self.count = min(self.N, self.count + n)
 
@@ -630,11 +633,13 @@ class ReplayBuffer:
         if self.count < B:
             return None
         if self.cfg.ENABLE_PER:
+            # no host synchronisation: the reference's per-segment draws uniform(seg*i, seg*(i+1))
+            # = seg * (i + random_sample()) take B host uniforms; the total stays on the device
             p = self.prio[: self.count].double()
             cum = torch.cumsum(p, 0)
-            total = float(cum[-1])
-            seg = total / B
-            u = torch.from_numpy(np.array([rng.uniform(seg * i, seg * (i + 1)) for i in range(B)])).to(self.device)
+            total = cum[-1]
+            r = torch.from_numpy(rng.random_sample(B)).to(self.device, non_blocking=True)
+            u = (torch.arange(B, device=self.device, dtype=torch.float64) + r) * (total / B)
             idx = torch.searchsorted(cum, u).clamp_max(self.count - 1)
             w = (self.count * (p[idx] / total)) ** (-self.cfg.PER_BETA)
             w = (w / w.max()).float()
@@ -648,7 +653,7 @@ class ReplayBuffer:
         if not self.cfg.ENABLE_PER:
             return
         p = td.abs().to(self.device).float() + self.cfg.PER_EPSILON
-        self.max_priority = max(self.max_priority, float(p.max()))
+        self.max_priority = torch.maximum(torch.as_tensor(self.max_priority, device=self.device), p.max())  # device
         self.prio[idx] = p
 
 
@@ -775,8 +780,10 @@ class Trainer:
         torch.cuda.current_stream(self.device).wait_stream(s)
         self._graphs = (g1, g2 if self.dist is not None else None)
 
-    def step(self, batch, is_weights, k=None, flip=None):
-        """One training step -> ((total, policy, value, reward, consistency) floats, td errors [B])."""
+    def step(self, batch, is_weights, k=None, flip=None, sync=True):
+        """One training step -> ((total, policy, value, reward, consistency) floats, td errors [B]).
+        ``sync=False``: the five losses stay a device tensor [5] (no host synchronisation, so the host
+        can prepare the next step while this one runs; read them with ``.tolist()`` later)."""
         c = self.cfg
         acc = max(1, c.GRADIENT_ACCUMULATION_STEPS)
         if self.graph and self.step_count >= self.graph_warmup:
@@ -798,6 +805,8 @@ class Trainer:
                 self._update()
                 self.sched.step()
         self.step_count += 1
+        if not sync:
+            return logs.detach().clone(), td
         return tuple(float(x) for x in logs.tolist()), td
 
     def state_dict_cpu(self):

@@ -27,6 +27,7 @@ ap.add_argument("--per", action="store_true")
 ap.add_argument("--no-amp", action="store_true")
 ap.add_argument("--bf16", action="store_true", help="autocast to bfloat16 instead of the reference's float16")
 ap.add_argument("--nchw", action="store_true", help="NCHW activations (default: channels-last, MIOpen's NHWC kernels)")
+ap.add_argument("--sync-logs", action="store_true", help="read each step's losses on the host before the next step")
 ap.add_argument("--eager", action="store_true", help="no HIP-graph capture of the step")
 ap.add_argument("--no-benchmark", action="store_true", help="no torch.backends.cudnn.benchmark (MIOpen Find per shape)")
 a = ap.parse_args()
@@ -65,11 +66,24 @@ for i in range(a.buffer):
 rb.add(chunk)
 
 
+pending = [None]
+
+
 def step():
+    """One step; its five losses reach the host one step later (read after the next step is queued,
+    so the GPU never waits for the host's sampling and launch work).  --sync-logs: read every
+    step's losses before the next step, like the reference's calculate_loss .item() calls."""
     batch, idx, w = rb.sample(a.batch, rs)
-    logs, td = tr.step(batch, w)
+    logs, td = tr.step(batch, w, sync=a.sync_logs)
     rb.update_priorities(idx, td)
-    return logs
+    if a.sync_logs:
+        return logs
+    prev, pending[0] = pending[0], logs
+    return tuple(prev.tolist()) if prev is not None else None
+
+
+def drain():
+    return tuple(pending[0].tolist()) if pending[0] is not None else None
 
 
 for _ in range(a.warmup):
@@ -80,6 +94,7 @@ torch.cuda.synchronize()
 t0 = time.perf_counter()
 for _ in range(a.steps):
     logs = step()
+logs = drain() or logs
 torch.cuda.synchronize()
 if dist:
     dist.barrier()
@@ -93,6 +108,6 @@ if rank == 0:
     print(json.dumps({"metric": "trainer steps/sec (config C4)", "value": a.steps / dt, "unit": "steps/s",
                       "n_gpus": world, "samples_per_s": a.steps * a.batch * world / dt, "ms_per_step": dt / a.steps * 1e3,
                       "batch_per_gpu": a.batch, "unroll": U, "board": a.size, "blocks": a.blocks, "amp": ("bf16" if a.bf16 else "fp16") if not a.no_amp else None, "channels_last": a.channels_last, "benchmark": a.benchmark, "graph": tr.graph,
-                      "per": a.per, "last_loss": logs[0], "data": "synthetic slices in a device ReplayBuffer"}))
+                      "per": a.per, "sync_logs": a.sync_logs, "last_loss": logs[0], "data": "synthetic slices in a device ReplayBuffer"}))
 if dist:
     dist.destroy_process_group()
