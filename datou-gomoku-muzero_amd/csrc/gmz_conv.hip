@@ -1,0 +1,264 @@
+// gmz_conv.hip — the trainer's 128 -> 128 3x3 convolutions (residual-block convs of GomokuNetEZ,
+// network.py:30-48) as implicit-GEMM MFMA kernels on channels-last (NHWC) f16/bf16 activations.
+//
+// Forward y = conv(x, W) and the input gradient dx = conv(dy, W') (W'[c][o][t] = W[o][c][8 - t]:
+// channels swapped, taps flipped) are the same kernel on differently packed weights; the weight
+// gradient stays MIOpen's.  Replaces, for these layers, MIOpen's NHWC kernels plus the zeroing pass
+// it runs before each of them (trainer.py, training step of loss.py:30-158).
+//
+// Work item = (board, half of the output channels): 2N items for N boards, so the 256 CUs see ~3
+// rounds at N = 360 instead of 1.4.  Two 512-thread workgroups per CU (one padded image each,
+// 78 KB at 15x15).  Per item: the board's NHWC activations are DMA'd (global_load_lds) into the
+// padded LDS image of k_tower3 (gmz_net.hip: cell (yy, xx) at yy*RS + xx*PS, conflict-free
+// ds_read_b128 B fragments, every tap / k-step offset an immediate), then 36 k-steps (9 taps x 4
+// k-steps of 32 input channels) of v_mfma_f32_16x16x32_{f16,bf16}: 8 waves = 2 groups of 2 n-tiles
+// x 4 position groups of 4|3 16-position tiles.  A fragments (weights) stream global -> VGPR
+// through a 3-deep register ring, shared by the waves of a channel group in L1.  Epilogue: f32 ->
+// activation dtype, 8-byte stores of 4 consecutive channels.
+#include <type_traits>
+
+#include "gmz_common.h"
+
+#include <hip/hip_bf16.h>
+#include <hip/hip_fp16.h>
+
+namespace gmz {
+namespace {
+
+typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+typedef __bf16 b16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef uint16_t u16x4_t __attribute__((ext_vector_type(4)));
+
+constexpr int CC = 128;         // channels in and out
+constexpr int CKSTEPS = 36;     // 9 taps x 4 k-steps of 32 input channels
+constexpr int FRAG_BYTES = 294912;  // 36 k-steps x 8 n-tiles x 64 lanes x 16 B
+
+__device__ __forceinline__ int csigma16(int j) { return j < 8 ? (j ^ 4) : j; }
+
+// padded board image (same geometry as Img3 in gmz_net.hip)
+template <int H>
+struct CImg {
+  static constexpr int HP = H + 2, PS = 272, RS = HP * PS - 32;
+  static constexpr int BYTES = ((HP - 1) * RS + HP * PS + 255) / 256 * 256;
+  static constexpr int RUN = (H - 1) * PS + 256;
+  static constexpr int RUN_DMA = (RUN + 1023) / 1024;
+};
+
+template <typename T> struct Mfma;
+template <> struct Mfma<__half> {
+  typedef f16x8_t V;
+  static __device__ __forceinline__ f32x4_t run(V a, V b, f32x4_t c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ uint16_t bits(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
+};
+template <> struct Mfma<__hip_bfloat16> {
+  typedef b16x8_t V;
+  static __device__ __forceinline__ f32x4_t run(V a, V b, f32x4_t c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ uint16_t bits(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
+};
+
+// lane group g of k-step s reads input-channel chunk 2s + {0, 8, 1, 9}[g] (8 channels per chunk)
+__device__ __forceinline__ int chunk_of(int ks, int g) { return 2 * ks + ((g & 1) * 8 + (g >> 1)); }
+
+// fragment (t, ks, nt, l, j) = Wx[n = nt*16 + (l & 15)][c = chunk_of(ks, l >> 4)*8 + j][t], with
+// Wx = W (transpose = 0) or W'[n][c][t] = W[c][n][8 - t] (transpose = 1, the input gradient)
+template <typename T>
+__global__ void __launch_bounds__(256) k_pack_conv(const float *__restrict__ w, long s0, long s1, long s2, long s3,
+                                                   int transpose, uint16_t *__restrict__ out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;  // (t, ks, nt, l)
+  if (i >= CKSTEPS * 8 * 64) return;
+  const int l = i & 63, nt = (i >> 6) & 7, st = i >> 9, t = st >> 2, ks = st & 3;
+  const int n = nt * 16 + (l & 15);
+  u16x4_t lo, hi;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = chunk_of(ks, l >> 4) * 8 + j;
+    const int o = transpose ? c : n, ci = transpose ? n : c, tt = transpose ? 8 - t : t;
+    const float v = w[o * s0 + ci * s1 + (tt / 3) * s2 + (tt % 3) * s3];
+    const uint16_t b = Mfma<T>::bits(v);
+    if (j < 4) lo[j] = b;
+    else hi[j - 4] = b;
+  }
+  uint4 r;
+  r.x = (uint32_t)lo[0] | ((uint32_t)lo[1] << 16);
+  r.y = (uint32_t)lo[2] | ((uint32_t)lo[3] << 16);
+  r.z = (uint32_t)hi[0] | ((uint32_t)hi[1] << 16);
+  r.w = (uint32_t)hi[2] | ((uint32_t)hi[3] << 16);
+  *(uint4 *)(out + (size_t)i * 8) = r;
+}
+
+template <int H, typename T>
+__global__ void __launch_bounds__(512, 2) k_conv3(const uint16_t *__restrict__ x, const uint16_t *__restrict__ wpk,
+                                                  uint16_t *__restrict__ y, int N) {
+  using I = CImg<H>;
+  using M = Mfma<T>;
+  typedef typename M::V V;
+  constexpr int A = H * H, NPT = (A + 15) / 16;
+  constexpr int PG = 4, NTW = 2, PTW = (NPT + PG - 1) / PG, RD = 3;
+  constexpr int PS = I::PS, RS = I::RS;
+  static_assert(CKSTEPS % RD == 0, "ring slots repeat per item");
+  __shared__ __attribute__((aligned(16))) uint8_t img[I::BYTES];
+
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int nq = w & 1, pg = w >> 1;  // waves w, w + 4 share a SIMD: position groups pg and pg + 2
+  const int g4 = lane >> 4;
+  const int cg = (g4 & 1) * 8 + (g4 >> 1);
+  const int half = blockIdx.x & 1;
+  const int ntile0 = half * 4 + nq * NTW;  // this wave's first n-tile (of 8)
+
+  for (int i = tid; i < I::BYTES / 16; i += 512) *(uint4 *)(img + i * 16) = make_uint4(0, 0, 0, 0);
+
+  int pos[PTW];
+#pragma unroll
+  for (int i = 0; i < PTW; ++i) {
+    const int pt = pg + PG * i;
+    const int p = pt * 16 + csigma16(lane & 15);
+    pos[i] = (pt < NPT && p < A) ? (p / H) * RS + (p % H) * PS : -1;
+  }
+  const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc((void *)wpk, (short)0, FRAG_BYTES, 0x00020000);
+  const int wvoff = ntile0 * 1024 + lane * 16;
+  V ar[RD][NTW];
+  auto loadA = [&](int slot, int st) {
+    const int soff = (st < CKSTEPS ? st : st - CKSTEPS) * 8192;
+#pragma unroll
+    for (int nt = 0; nt < NTW; ++nt)
+      ar[slot][nt] = __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(wrsrc, wvoff + nt * 1024, soff, 0));
+  };
+#pragma unroll
+  for (int k = 0; k < RD - 1; ++k) loadA(k, k);
+  __syncthreads();  // zeroed image before the first DMA
+
+  for (int b = blockIdx.x >> 1; b < N; b += gridDim.x >> 1) {
+    // ---- board b -> image interior: 1 KB pieces of each board row's run of cells
+    const uint8_t *src = (const uint8_t *)(x + (size_t)b * A * CC);
+    for (int j = w; j < H * I::RUN_DMA; j += 8) {
+      const int yy = j / I::RUN_DMA, piece = j % I::RUN_DMA;
+      const int o = piece * 1024 + lane * 16;
+      const int xx = o / PS, ch = (o % PS) >> 4;
+      if (o < I::RUN && ch < 16)
+        __builtin_amdgcn_global_load_lds((const void *)(src + (yy * H + xx) * 256 + ch * 16),
+                                         (__attribute__((address_space(3))) void *)(img + (yy + 1) * RS + PS + piece * 1024),
+                                         16, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    f32x4_t acc[NTW][PTW];
+    int bb[PTW];
+#pragma unroll
+    for (int i = 0; i < PTW; ++i) bb[i] = (pos[i] < 0 ? 0 : pos[i]) + cg * 16;
+    auto kloop = [&](auto ntl_c) {
+      constexpr int NTL = decltype(ntl_c)::value;
+      V bf[2][NTL];
+      auto readB = [&](int buf, int st) {
+        const int tap = st >> 2, ks = st & 3;
+        const int off = (tap / 3) * RS + (tap % 3) * PS + ks * 32;
+#pragma unroll
+        for (int i = 0; i < NTL; ++i) bf[buf][i] = *(const V *)(img + bb[i] + off);
+      };
+      readB(0, 0);
+#pragma unroll
+      for (int st = 0; st < CKSTEPS; ++st) {
+        loadA((st + RD - 1) % RD, st + RD - 1);
+        if (st + 1 < CKSTEPS) readB((st + 1) & 1, st + 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < NTL; ++i)
+#pragma unroll
+          for (int nt = 0; nt < NTW; ++nt)
+            acc[nt][i] = M::run(ar[st % RD][nt], bf[st & 1][i], st == 0 ? f32x4_t{0.f, 0.f, 0.f, 0.f} : acc[nt][i]);
+        if (st + 1 < CKSTEPS) __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int i = NTL; i < PTW; ++i)
+#pragma unroll
+        for (int nt = 0; nt < NTW; ++nt) acc[nt][i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    };
+    if constexpr (PTW * PG == NPT) kloop(std::integral_constant<int, PTW>{});
+    else if (pg + PG * (PTW - 1) < NPT) kloop(std::integral_constant<int, PTW>{});
+    else kloop(std::integral_constant<int, PTW - 1>{});
+
+    // ---- epilogue: 4 consecutive output channels of one position per lane -> 8-byte store
+    uint16_t *dst = y + (size_t)b * A * CC;
+#pragma unroll
+    for (int i = 0; i < PTW; ++i) {
+      const int pt = pg + PG * i;
+      const int p = pt * 16 + csigma16(lane & 15);
+      if (pt >= NPT || p >= A) continue;
+#pragma unroll
+      for (int nt = 0; nt < NTW; ++nt) {
+        const int n0 = (ntile0 + nt) * 16 + g4 * 4;
+        u16x4_t o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = M::bits(acc[nt][i][e]);
+        *(u16x4_t *)(dst + (size_t)p * CC + n0) = o;
+      }
+    }
+    __syncthreads();  // every wave is done reading the image before the next board's DMA
+  }
+}
+
+static int cu_count_conv() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    hipDeviceProp_t p;
+    n = hipGetDeviceProperties(&p, dev) == hipSuccess ? p.multiProcessorCount : 256;
+  }
+  return n;
+}
+
+template <int H, typename T>
+int launch_conv3(const void *x, const void *wpk, void *y, int N, hipStream_t st) {
+  long items = 2L * N, cap = 2L * 2 * cu_count_conv();
+  const int grid = (int)(items < cap ? items : cap);
+  hipLaunchKernelGGL((k_conv3<H, T>), dim3(grid), dim3(512), 0, st, (const uint16_t *)x, (const uint16_t *)wpk,
+                     (uint16_t *)y, N);
+  GMZ_LAUNCH_CHECK();
+  return 0;
+}
+
+template <typename T>
+int conv3_dispatch(int H, const void *x, const void *wpk, void *y, int N, hipStream_t st) {
+  switch (H) {
+    case 9: return launch_conv3<9, T>(x, wpk, y, N, st);
+    case 15: return launch_conv3<15, T>(x, wpk, y, N, st);
+  }
+  return fail("gmz_conv3x3: board size must be 9 or 15");
+}
+
+}  // namespace
+}  // namespace gmz
+
+using namespace gmz;
+
+GMZ_EXPORT int gmz_conv3x3_pack(int dtype, const float *w, int64_t s0, int64_t s1, int64_t s2, int64_t s3,
+                                int transpose, void *packed, void *stream) {
+  if (!w || !packed) return fail("gmz_conv3x3_pack: null operand");
+  if (dtype != 1 && dtype != 2) return fail("gmz_conv3x3_pack: dtype must be 1 (f16) or 2 (bf16)");
+  hipStream_t st = (hipStream_t)stream;
+  const int n = CKSTEPS * 8 * 64;
+  if (dtype == 1)
+    hipLaunchKernelGGL(k_pack_conv<__half>, dim3((n + 255) / 256), dim3(256), 0, st, w, (long)s0, (long)s1, (long)s2,
+                       (long)s3, transpose, (uint16_t *)packed);
+  else
+    hipLaunchKernelGGL(k_pack_conv<__hip_bfloat16>, dim3((n + 255) / 256), dim3(256), 0, st, w, (long)s0, (long)s1,
+                       (long)s2, (long)s3, transpose, (uint16_t *)packed);
+  GMZ_LAUNCH_CHECK();
+  return 0;
+}
+
+GMZ_EXPORT int gmz_conv3x3_forward(int dtype, int H, const void *x, const void *packed, void *y, int N, void *stream) {
+  if (!x || !packed || !y) return fail("gmz_conv3x3_forward: null operand");
+  if (N <= 0) return fail("gmz_conv3x3_forward: N must be positive");
+  if (((uintptr_t)x | (uintptr_t)packed | (uintptr_t)y) & 15) return fail("gmz_conv3x3_forward: operands must be 16-B aligned");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == 1) return conv3_dispatch<__half>(H, x, packed, y, N, st);
+  if (dtype == 2) return conv3_dispatch<__hip_bfloat16>(H, x, packed, y, N, st);
+  return fail("gmz_conv3x3_forward: dtype must be 1 (f16) or 2 (bf16)");
+}

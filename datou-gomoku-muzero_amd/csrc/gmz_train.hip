@@ -262,31 +262,43 @@ __global__ void __launch_bounds__(BN_THREADS) k_bnl_red(const T *__restrict__ x,
     }
   }
   if (grp < pl) {
-    for (long p = p0 + grp; p < p1; p += pl) {
-      if (mask && !mask[p / S]) continue;
-      const size_t k = (size_t)p * C + c;
-      float v[V];
-      if (!BWD) {
-        ldv<T, V>(x, k, v);
+    // U positions per thread per trip, every load of a trip issued before any arithmetic (the
+    // loop is latency-bound otherwise: one HBM round trip per position)
+    constexpr int U = BWD ? 4 : 8;
+    using VT = VecT<T, V>;
+    for (long p = p0 + grp; p < p1; p += (long)U * pl) {
+      VT rx[U], rd[U], ry[U];
+      bool ok[U];
 #pragma unroll
-        for (int j = 0; j < V; ++j) {
-          a[j] += v[j];
-          q[j] = fmaf(v[j], v[j], q[j]);
+      for (int u = 0; u < U; ++u) {
+        const long pp = p + (long)u * pl;
+        ok[u] = pp < p1;
+        const size_t k = (size_t)(ok[u] ? pp : p) * C + c;
+        rx[u] = *reinterpret_cast<const VT *>(x + k);
+        if (BWD) {
+          rd[u] = *reinterpret_cast<const VT *>(dy + k);
+          if (relu) ry[u] = *reinterpret_cast<const VT *>(y + k);
         }
-      } else {
-        float g[V], xv[V];
-        ldv<T, V>(dy, k, g);
-        if (relu) {
-          ldv<T, V>(y, k, v);
+        if (mask && ok[u]) ok[u] = mask[pp / S] != 0;
+      }
 #pragma unroll
-          for (int j = 0; j < V; ++j)
-            if (!(v[j] > 0.f)) g[j] = 0.f;
-        }
-        ldv<T, V>(x, k, xv);
+      for (int u = 0; u < U; ++u) {
+        if (!ok[u]) continue;
+        if (!BWD) {
 #pragma unroll
-        for (int j = 0; j < V; ++j) {
-          a[j] += g[j];
-          q[j] = fmaf(g[j], (xv[j] - m[j]) * is[j], q[j]);
+          for (int j = 0; j < V; ++j) {
+            const float v = ld(rx[u].v, j);
+            a[j] += v;
+            q[j] = fmaf(v, v, q[j]);
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < V; ++j) {
+            float g = ld(rd[u].v, j);
+            if (relu && !(ld(ry[u].v, j) > 0.f)) g = 0.f;
+            a[j] += g;
+            q[j] = fmaf(g, (ld(rx[u].v, j) - m[j]) * is[j], q[j]);
+          }
         }
       }
     }

@@ -100,10 +100,6 @@ def scalar_to_support(x, vmin, vmax, bins):
 
 
 # ------------------------------------------------------------------------------ network
-def _conv3(cin, cout):
-    return nn.Conv2d(cin, cout, 3, padding=1, bias=False)
-
-
 def _bn(mod, x, mask=None):
     """BatchNorm whose training-mode statistics (and running-stat update) cover only the rows
     where ``mask`` is set.  The reference runs the unrolled steps on the sub-batch of games still
@@ -318,6 +314,75 @@ class _Conv1x1NHWC(torch.autograd.Function):
         return gx, gw
 
 
+FUSED_CONV = True  # 128->128 3x3 convs of f16/bf16 channels-last activations run gmz_conv3x3 (HIP)
+_CONV_DTYPES = {torch.float16: 1, torch.bfloat16: 2}
+
+
+def _packed_conv_weight(w, dtype, transpose):
+    """gmz_conv3x3_pack of ``w`` (f32 [128,128,3,3], any memory format) for ``dtype``; cached on the
+    parameter per (dtype, transpose) and its version counter, so a weight used by several unroll
+    steps is packed once per optimiser step (also inside a captured step: first use packs)."""
+    from . import _lib
+    key = (dtype, transpose)
+    cache = w.__dict__.setdefault("_gmz_pack", {})
+    hit = cache.get(key)
+    if hit is not None and hit[0] == w._version:
+        return hit[1]
+    out = torch.empty(147456, dtype=torch.int16, device=w.device)
+    s = w.stride()
+    _lib.check(_lib.load().gmz_conv3x3_pack(_CONV_DTYPES[dtype], _lib.ptr(w.detach()), s[0], s[1], s[2], s[3],
+                                            int(transpose), _lib.ptr(out), _lib.stream_ptr()))
+    cache[key] = (w._version, out)
+    return out
+
+
+def _conv3x3_hip(x, packed):
+    from . import _lib
+    y = torch.empty_like(x, memory_format=torch.channels_last)
+    _lib.check(_lib.load().gmz_conv3x3_forward(_CONV_DTYPES[x.dtype], x.shape[2], _lib.ptr(x), _lib.ptr(packed),
+                                               _lib.ptr(y), x.shape[0], _lib.stream_ptr()))
+    return y
+
+
+class _Conv3x3NHWC(torch.autograd.Function):
+    """128 -> 128 3x3 convolution (padding 1, no bias) of channels-last f16/bf16 activations:
+    forward and input gradient on the HIP implicit-GEMM kernel (csrc/gmz_conv.hip; the input
+    gradient is the same kernel on the transposed, flipped weight), weight gradient by MIOpen
+    (aten.convolution_backward, weight only).  The weight stays the f32 parameter: the pack kernel
+    converts it (what autocast's cast would do)."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return _conv3x3_hip(x, _packed_conv_weight(w, x.dtype, 0))
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        gy = gy.to(x.dtype).contiguous(memory_format=torch.channels_last)
+        gx = _conv3x3_hip(gy, _packed_conv_weight(w, x.dtype, 1)) if ctx.needs_input_grad[0] else None
+        gw = None
+        if ctx.needs_input_grad[1]:
+            wd = torch.empty(w.shape, dtype=x.dtype, device=w.device).contiguous(memory_format=torch.channels_last)
+            gw = torch.ops.aten.convolution_backward(gy, x, wd, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
+                                                     [False, True, False])[1].to(w.dtype)
+        return gx, gw
+
+
+def _conv3(cin, cout):
+    return nn.Conv2d(cin, cout, 3, padding=1, bias=False)
+
+
+def _conv3_apply(conv, x):
+    """conv(x), on the HIP kernels when they cover the case (see ``_Conv3x3NHWC``)."""
+    if (FUSED_CONV and x.is_cuda and x.dim() == 4 and x.shape[1] == 128 and x.shape[2] == x.shape[3]
+            and x.shape[2] in (9, 15) and conv.weight.shape == (128, 128, 3, 3) and conv.bias is None):
+        dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x.dtype
+        if dt in _CONV_DTYPES and x.is_contiguous(memory_format=torch.channels_last):
+            return _Conv3x3NHWC.apply(x.to(dt), conv.weight)
+    return conv(x)
+
+
 class _Block(nn.Module):
     """Residual block (conv-BN-ReLU-conv-BN + identity, ReLU), parameter names of network.py:30-48."""
 
@@ -327,8 +392,8 @@ class _Block(nn.Module):
         self.conv2, self.bn2 = _conv3(c, c), nn.BatchNorm2d(c, eps=1e-4)
 
     def forward(self, x, mask=None):
-        y = _bn_act(self.bn1, self.conv1(x), mask)
-        return _bn_act(self.bn2, self.conv2(y), mask, res=x)
+        y = _bn_act(self.bn1, _conv3_apply(self.conv1, x), mask)
+        return _bn_act(self.bn2, _conv3_apply(self.conv2, y), mask, res=x)
 
 
 class _Trunk(nn.Module):

@@ -250,6 +250,17 @@ int gmz_bn_backward(int dtype, int layout, const void *x_dev, const void *y_dev,
 int gmz_bn_eval(int dtype, int layout, const void *x_dev, const void *res_dev, int B, int C, int S, const float *gamma_dev,
                 const float *beta_dev, const float *running_mean_dev, const float *running_var_dev, float eps, int relu,
                 void *y_dev, void *workspace_dev, void *stream);
+/* 3x3 convolution, 128 -> 128 channels, stride 1, padding 1, no bias (the residual-block convs of
+ * network.py:30-48), on channels-last activations x[N][H*H][128] -> y[N][H*H][128]; dtype 1 = f16,
+ * 2 = bf16 (activations and packed weights; f32 accumulation); H = 9 or 15.  The training step's
+ * forward convolution (loss.py:70-107 under autocast) and, with transposed packing, its input
+ * gradient dx = conv(dy, W') with W'[c][o][t] = W[o][c][8 - t].
+ * gmz_conv3x3_pack: f32 weight W[o][c][ky][kx] at element strides (s0, s1, s2, s3) -> packed_dev
+ *   (294,912 bytes, 16-B aligned) in MFMA fragment order; transpose = 1 packs W'.
+ * gmz_conv3x3_forward: x_dev, packed_dev and y_dev 16-B aligned, N >= 1. */
+int gmz_conv3x3_pack(int dtype, const float *w_dev, int64_t s0, int64_t s1, int64_t s2, int64_t s3, int transpose,
+                     void *packed_dev, void *stream);
+int gmz_conv3x3_forward(int dtype, int H, const void *x_dev, const void *packed_dev, void *y_dev, int N, void *stream);
 
 #ifdef __cplusplus
 }
