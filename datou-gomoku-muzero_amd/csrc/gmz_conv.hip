@@ -7,12 +7,13 @@
 // it runs before each of them (trainer.py, training step of loss.py:30-158).
 //
 // Work item = (board, half of the output channels): 2N items for N boards, so the 256 CUs see ~3
-// rounds at N = 360 instead of 1.4.  Two 512-thread workgroups per CU (one padded image each,
+// rounds at N = 360 instead of 1.4.  Two 256-thread workgroups per CU (one padded image each,
 // 78 KB at 15x15).  Per item: the board's NHWC activations are DMA'd (global_load_lds) into the
 // padded LDS image of k_tower3 (gmz_net.hip: cell (yy, xx) at yy*RS + xx*PS, conflict-free
 // ds_read_b128 B fragments, every tap / k-step offset an immediate), then 36 k-steps (9 taps x 4
-// k-steps of 32 input channels) of v_mfma_f32_16x16x32_{f16,bf16}: 8 waves = 2 groups of 2 n-tiles
-// x 4 position groups of 4|3 16-position tiles.  A fragments (weights) stream global -> VGPR
+// k-steps of 32 input channels) of v_mfma_f32_16x16x32_{f16,bf16}: 4 waves = 2 groups of 2 n-tiles
+// x 2 position groups of 8|7 16-position tiles (16 MFMAs per 2 weight-fragment loads per k-step:
+// 4 tiles per wave ran into the vector-L1 bandwidth, 256 B of weights per MFMA).  A fragments (weights) stream global -> VGPR
 // through a 3-deep register ring, shared by the waves of a channel group in L1.  Epilogue: f32 ->
 // activation dtype, 8-byte stores of 4 consecutive channels.
 #include <type_traits>
@@ -91,26 +92,26 @@ __global__ void __launch_bounds__(256) k_pack_conv(const float *__restrict__ w, 
   *(uint4 *)(out + (size_t)i * 8) = r;
 }
 
-template <int H, typename T>
-__global__ void __launch_bounds__(512, 2) k_conv3(const uint16_t *__restrict__ x, const uint16_t *__restrict__ wpk,
+template <int H, typename T, int PG>
+__global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restrict__ x, const uint16_t *__restrict__ wpk,
                                                   uint16_t *__restrict__ y, int N) {
   using I = CImg<H>;
   using M = Mfma<T>;
   typedef typename M::V V;
   constexpr int A = H * H, NPT = (A + 15) / 16;
-  constexpr int PG = 4, NTW = 2, PTW = (NPT + PG - 1) / PG, RD = 3;
+  constexpr int NTW = 2, PTW = (NPT + PG - 1) / PG, RD = 3, NW = 2 * PG, NTHR = 64 * NW;
   constexpr int PS = I::PS, RS = I::RS;
   static_assert(CKSTEPS % RD == 0, "ring slots repeat per item");
   __shared__ __attribute__((aligned(16))) uint8_t img[I::BYTES];
 
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  const int nq = w & 1, pg = w >> 1;  // waves w, w + 4 share a SIMD: position groups pg and pg + 2
+  const int nq = w & 1, pg = w >> 1;
   const int g4 = lane >> 4;
   const int cg = (g4 & 1) * 8 + (g4 >> 1);
   const int half = blockIdx.x & 1;
   const int ntile0 = half * 4 + nq * NTW;  // this wave's first n-tile (of 8)
 
-  for (int i = tid; i < I::BYTES / 16; i += 512) *(uint4 *)(img + i * 16) = make_uint4(0, 0, 0, 0);
+  for (int i = tid; i < I::BYTES / 16; i += NTHR) *(uint4 *)(img + i * 16) = make_uint4(0, 0, 0, 0);
 
   int pos[PTW];
 #pragma unroll
@@ -135,7 +136,7 @@ __global__ void __launch_bounds__(512, 2) k_conv3(const uint16_t *__restrict__ x
   for (int b = blockIdx.x >> 1; b < N; b += gridDim.x >> 1) {
     // ---- board b -> image interior: 1 KB pieces of each board row's run of cells
     const uint8_t *src = (const uint8_t *)(x + (size_t)b * A * CC);
-    for (int j = w; j < H * I::RUN_DMA; j += 8) {
+    for (int j = w; j < H * I::RUN_DMA; j += NW) {
       const int yy = j / I::RUN_DMA, piece = j % I::RUN_DMA;
       const int o = piece * 1024 + lane * 16;
       const int xx = o / PS, ch = (o % PS) >> 4;
@@ -213,12 +214,14 @@ static int cu_count_conv() {
   return n;
 }
 
+constexpr int CONV_PG = 2;  // position groups per workgroup: 2 -> 4 waves, 8|7 tiles per wave
+
 template <int H, typename T>
 int launch_conv3(const void *x, const void *wpk, void *y, int N, hipStream_t st) {
   long items = 2L * N, cap = 2L * 2 * cu_count_conv();
   const int grid = (int)(items < cap ? items : cap);
-  hipLaunchKernelGGL((k_conv3<H, T>), dim3(grid), dim3(512), 0, st, (const uint16_t *)x, (const uint16_t *)wpk,
-                     (uint16_t *)y, N);
+  hipLaunchKernelGGL((k_conv3<H, T, CONV_PG>), dim3(grid), dim3(128 * CONV_PG), 0, st, (const uint16_t *)x,
+                     (const uint16_t *)wpk, (uint16_t *)y, N);
   GMZ_LAUNCH_CHECK();
   return 0;
 }
