@@ -23,6 +23,7 @@ replay_buffer.py:58-94 (uniform without replacement, or stratified proportional 
 The convolutions run in PyTorch's kernels in this round; the fused HIP kernels cover inference.
 """
 import math
+import os as _os
 from dataclasses import dataclass, field, asdict
 
 import numpy as np
@@ -442,7 +443,45 @@ class _Dynamics(_Trunk):
         if h.is_contiguous(memory_format=torch.channels_last) and not h.is_contiguous():
             emb = emb.contiguous(memory_format=torch.channels_last)   # cat keeps channels-last
         nxt = super().forward(torch.cat((h, emb), dim=1), mask)
-        return nxt, self.reward_fc(nxt.reshape(n, -1))
+        fc0, act, fc2 = self.reward_fc
+        return nxt, fc2(act(_linear(fc0, nxt.reshape(n, -1))))
+
+
+class _BigKLinear(torch.autograd.Function):
+    """y = x W^T + b for the trainer's K = C*H*W = 28,800 Linears (projection fc1, reward_fc.0) under
+    fp16/bf16 autocast.  hipBLASLt runs x @ W^T at B = 360 on 24 workgroups (83 us for 28800->512);
+    here K is split in 16 chunks, one batched GEMM with float32 outputs summed in float32 (33 us),
+    rounded once to the autocast dtype like the single GEMM's output.  Backward: dx = dy W, and
+    dW = (x^T dy)^T (26 us vs 39 us for dy^T x at K = B = 360)."""
+    SPLIT = 16
+
+    @staticmethod
+    def forward(ctx, x, w, b, dt):
+        xs, ws = x.to(dt), w.to(dt)
+        n, K = xs.shape
+        S = _BigKLinear.SPLIT
+        y = torch.bmm(xs.view(n, S, K // S).transpose(0, 1), ws.view(-1, S, K // S).permute(1, 2, 0),
+                      out_dtype=torch.float32).sum(0)
+        ctx.save_for_backward(xs, ws)
+        ctx.wdtype = w.dtype
+        return (y + b).to(dt) if b is not None else y.to(dt)
+
+    @staticmethod
+    def backward(ctx, gy):
+        xs, ws = ctx.saved_tensors
+        gy = gy.to(xs.dtype)
+        gx = gy @ ws if ctx.needs_input_grad[0] else None
+        gw = (xs.t() @ gy).t().to(ctx.wdtype) if ctx.needs_input_grad[1] else None
+        gb = gy.sum(0, dtype=torch.float32) if ctx.needs_input_grad[2] else None
+        return gx, gw, gb, None
+
+
+def _linear(lin, x):
+    """lin(x), with K = 28,800 Linears under GPU autocast on ``_BigKLinear``."""
+    if (x.is_cuda and torch.is_autocast_enabled("cuda") and x.dim() == 2 and x.shape[1] >= 4096
+            and x.shape[1] % _BigKLinear.SPLIT == 0):
+        return _BigKLinear.apply(x, lin.weight, lin.bias, torch.get_autocast_dtype("cuda"))
+    return lin(x)
 
 
 class _Projection(nn.Module):
@@ -451,7 +490,7 @@ class _Projection(nn.Module):
         self.fc1, self.bn1, self.fc2 = nn.Linear(din, hidden), nn.BatchNorm1d(hidden, eps=1e-4), nn.Linear(hidden, out)
 
     def forward(self, h, mask=None):
-        return self.fc2(_bn_act(self.bn1, self.fc1(h.reshape(h.shape[0], -1)), mask))
+        return self.fc2(_bn_act(self.bn1, _linear(self.fc1, h.reshape(h.shape[0], -1)), mask))
 
 
 class TrainNet(nn.Module):
@@ -756,6 +795,9 @@ class Trainer:
         if channels_last:  # NHWC activations: MIOpen's NHWC convolutions without layout transposes
             self.model = self.model.to(memory_format=torch.channels_last)
             self.model.channels_last = True
+            if _os.environ.get("GMZ_TARGET_CL") == "1":  # A/B: channels-last float32 target
+                self.target = self.target.to(memory_format=torch.channels_last)
+                self.target.channels_last = True
             # the target network's value (loss.py:54-55) runs in float32 like the reference's, outside
             # autocast: MIOpen's NCHW fp32 Winograd kernels take 0.25 ms per conv, its NHWC fp32 path 0.51
             # ms, so the target stays NCHW
