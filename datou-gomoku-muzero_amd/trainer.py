@@ -23,7 +23,6 @@ replay_buffer.py:58-94 (uniform without replacement, or stratified proportional 
 The convolutions run in PyTorch's kernels in this round; the fused HIP kernels cover inference.
 """
 import math
-import os as _os
 from dataclasses import dataclass, field, asdict
 
 import numpy as np
@@ -799,8 +798,13 @@ class Trainer:
                 self.target = self.target.to(memory_format=torch.channels_last)
                 self.target.channels_last = True
             # the target network's value (loss.py:54-55) runs in float32 like the reference's, outside
-            # autocast: MIOpen's NCHW fp32 Winograd kernels take 0.25 ms per conv, its NHWC fp32 path 0.51
-            # ms, so the target stays NCHW
+            # autocast.  With MIOpen Find (torch.backends.cudnn.benchmark) its NHWC fp32 implicit GEMM
+            # takes 0.19 ms per 360-board conv (128 TFLOP/s, fp32 MFMA), so the target goes channels-last
+            # too; without Find MIOpen's immediate-mode NHWC fp32 pick takes 0.51 ms and its NCHW fp32
+            # Winograd 0.26 ms, so the target stays NCHW
+            if torch.backends.cudnn.benchmark:
+                self.target = self.target.to(memory_format=torch.channels_last)
+                self.target.channels_last = True
         import torch.distributed as dist
         self.dist = dist if (dist.is_available() and dist.is_initialized()) else None
         if self.dist is not None:  # every rank starts from rank 0's weights
