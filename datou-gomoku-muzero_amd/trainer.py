@@ -794,9 +794,6 @@ class Trainer:
         if channels_last:  # NHWC activations: MIOpen's NHWC convolutions without layout transposes
             self.model = self.model.to(memory_format=torch.channels_last)
             self.model.channels_last = True
-            if _os.environ.get("GMZ_TARGET_CL") == "1":  # A/B: channels-last float32 target
-                self.target = self.target.to(memory_format=torch.channels_last)
-                self.target.channels_last = True
             # the target network's value (loss.py:54-55) runs in float32 like the reference's, outside
             # autocast.  With MIOpen Find (torch.backends.cudnn.benchmark) its NHWC fp32 implicit GEMM
             # takes 0.19 ms per 360-board conv (128 TFLOP/s, fp32 MFMA), so the target goes channels-last
