@@ -58,6 +58,9 @@ _SIGS = {
     "gmz_bn_eval": ([I, I, P, P, I, I, I, P, P, P, P, ctypes.c_float, I, P, P, P], I),
     "gmz_conv3x3_pack": ([I, P, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, I, P, P], I),
     "gmz_conv3x3_forward": ([I, I, P, P, P, I, P], I),
+    "gmz_conv3x3_stats_slots": ([I, ctypes.POINTER(ctypes.c_int)], I),
+    "gmz_conv3x3_forward_stats": ([I, I, P, P, P, I, P, P, P], I),
+    "gmz_bn_forward_stats": ([I, P, P, I, I, I, P, P, ctypes.c_float, ctypes.c_float, P, P, P, I, P, P, P, I, P], I),
 }
 
 # symbols added by the network kernels (declared in include/gmz.h too)

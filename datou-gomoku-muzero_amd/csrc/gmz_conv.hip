@@ -53,6 +53,7 @@ template <> struct Mfma<__half> {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
   }
   static __device__ __forceinline__ uint16_t bits(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
+  static __device__ __forceinline__ float value(uint16_t u) { return (float)__builtin_bit_cast(_Float16, u); }
 };
 template <> struct Mfma<__hip_bfloat16> {
   typedef b16x8_t V;
@@ -60,6 +61,7 @@ template <> struct Mfma<__hip_bfloat16> {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
   }
   static __device__ __forceinline__ uint16_t bits(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
+  static __device__ __forceinline__ float value(uint16_t u) { return __uint_as_float(((uint32_t)u) << 16); }
 };
 
 // lane group g of k-step s reads input-channel chunk 2s + {0, 8, 1, 9}[g] (8 channels per chunk)
@@ -94,7 +96,8 @@ __global__ void __launch_bounds__(256) k_pack_conv(const float *__restrict__ w, 
 
 template <int H, typename T, int PG>
 __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restrict__ x, const uint16_t *__restrict__ wpk,
-                                                  uint16_t *__restrict__ y, int N) {
+                                                  uint16_t *__restrict__ y, int N, const uint8_t *__restrict__ mask,
+                                                  double *__restrict__ stats) {
   using I = CImg<H>;
   using M = Mfma<T>;
   typedef typename M::V V;
@@ -103,6 +106,7 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
   constexpr int PS = I::PS, RS = I::RS;
   static_assert(CKSTEPS % RD == 0, "ring slots repeat per item");
   __shared__ __attribute__((aligned(16))) uint8_t img[I::BYTES];
+  static_assert(I::BYTES >= PG * 64 * 2 * 4, "stats scratch fits in the image");
 
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int nq = w & 1, pg = w >> 1;
@@ -132,6 +136,14 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
 #pragma unroll
   for (int k = 0; k < RD - 1; ++k) loadA(k, k);
   __syncthreads();  // zeroed image before the first DMA
+  // BatchNorm statistics of the (rounded) output over the boards in the mask: per lane, its 4
+  // channels of each n-tile summed over its positions and boards
+  float s1[NTW][4], s2[NTW][4];
+#pragma unroll
+  for (int nt = 0; nt < NTW; ++nt)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s1[nt][e] = s2[nt][e] = 0.f;
+  int nvalid = 0;
 
   for (int b = blockIdx.x >> 1; b < N; b += gridDim.x >> 1) {
     // ---- board b -> image interior: 1 KB pieces of each board row's run of cells
@@ -185,6 +197,8 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
 
     // ---- epilogue: 4 consecutive output channels of one position per lane -> 8-byte store
     uint16_t *dst = y + (size_t)b * A * CC;
+    const bool counted = stats && (!mask || mask[b]);
+    nvalid += counted;
 #pragma unroll
     for (int i = 0; i < PTW; ++i) {
       const int pt = pg + PG * i;
@@ -197,9 +211,53 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
 #pragma unroll
         for (int e = 0; e < 4; ++e) o[e] = M::bits(acc[nt][i][e]);
         *(u16x4_t *)(dst + (size_t)p * CC + n0) = o;
+        if (counted) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float v = M::value(o[e]);
+            s1[nt][e] += v;
+            s2[nt][e] = fmaf(v, v, s2[nt][e]);
+          }
+        }
       }
     }
     __syncthreads();  // every wave is done reading the image before the next board's DMA
+  }
+  if (!stats) return;
+  // ---- per-workgroup partials: the 16 lanes of a lane group hold the same 4 channels at different
+  // positions; then the PG position-group waves of a channel group meet in LDS (the image is free)
+#pragma unroll
+  for (int nt = 0; nt < NTW; ++nt)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        s1[nt][e] += __shfl_xor(s1[nt][e], o, 64);
+        s2[nt][e] += __shfl_xor(s2[nt][e], o, 64);
+      }
+  float *red = (float *)img;  // [PG][64 channels of this half][2]
+  if ((lane & 15) == 0) {
+#pragma unroll
+    for (int nt = 0; nt < NTW; ++nt)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int cl = (nq * NTW + nt) * 16 + g4 * 4 + e;  // channel within this half
+        red[(pg * 64 + cl) * 2] = s1[nt][e];
+        red[(pg * 64 + cl) * 2 + 1] = s2[nt][e];
+      }
+  }
+  __syncthreads();
+  if (tid < 64) {
+    double a = 0.0, q = 0.0;
+#pragma unroll
+    for (int g = 0; g < PG; ++g) {
+      a += (double)red[(g * 64 + tid) * 2];
+      q += (double)red[(g * 64 + tid) * 2 + 1];
+    }
+    double *out = stats + ((size_t)(blockIdx.x >> 1) * CC + half * 64 + tid) * 3;
+    out[0] = a;
+    out[1] = q;
+    out[2] = (double)nvalid * A;
   }
 }
 
@@ -216,21 +274,25 @@ static int cu_count_conv() {
 
 constexpr int CONV_PG = 2;  // position groups per workgroup: 2 -> 4 waves, 8|7 tiles per wave
 
+int conv3_grid(int N) {
+  const long items = 2L * N, cap = 2L * 2 * cu_count_conv();
+  return (int)(items < cap ? items : cap);
+}
+
 template <int H, typename T>
-int launch_conv3(const void *x, const void *wpk, void *y, int N, hipStream_t st) {
-  long items = 2L * N, cap = 2L * 2 * cu_count_conv();
-  const int grid = (int)(items < cap ? items : cap);
-  hipLaunchKernelGGL((k_conv3<H, T, CONV_PG>), dim3(grid), dim3(128 * CONV_PG), 0, st, (const uint16_t *)x,
-                     (const uint16_t *)wpk, (uint16_t *)y, N);
+int launch_conv3(const void *x, const void *wpk, void *y, int N, const uint8_t *mask, double *stats, hipStream_t st) {
+  hipLaunchKernelGGL((k_conv3<H, T, CONV_PG>), dim3(conv3_grid(N)), dim3(128 * CONV_PG), 0, st, (const uint16_t *)x,
+                     (const uint16_t *)wpk, (uint16_t *)y, N, mask, stats);
   GMZ_LAUNCH_CHECK();
   return 0;
 }
 
 template <typename T>
-int conv3_dispatch(int H, const void *x, const void *wpk, void *y, int N, hipStream_t st) {
+int conv3_dispatch(int H, const void *x, const void *wpk, void *y, int N, const uint8_t *mask, double *stats,
+                   hipStream_t st) {
   switch (H) {
-    case 9: return launch_conv3<9, T>(x, wpk, y, N, st);
-    case 15: return launch_conv3<15, T>(x, wpk, y, N, st);
+    case 9: return launch_conv3<9, T>(x, wpk, y, N, mask, stats, st);
+    case 15: return launch_conv3<15, T>(x, wpk, y, N, mask, stats, st);
   }
   return fail("gmz_conv3x3: board size must be 9 or 15");
 }
@@ -256,12 +318,23 @@ GMZ_EXPORT int gmz_conv3x3_pack(int dtype, const float *w, int64_t s0, int64_t s
   return 0;
 }
 
-GMZ_EXPORT int gmz_conv3x3_forward(int dtype, int H, const void *x, const void *packed, void *y, int N, void *stream) {
+GMZ_EXPORT int gmz_conv3x3_stats_slots(int N, int *slots) {
+  if (N <= 0 || !slots) return fail("gmz_conv3x3_stats_slots: bad arguments");
+  *slots = conv3_grid(N) / 2;
+  return 0;
+}
+
+GMZ_EXPORT int gmz_conv3x3_forward_stats(int dtype, int H, const void *x, const void *packed, void *y, int N,
+                                         const uint8_t *mask, double *stats, void *stream) {
   if (!x || !packed || !y) return fail("gmz_conv3x3_forward: null operand");
   if (N <= 0) return fail("gmz_conv3x3_forward: N must be positive");
   if (((uintptr_t)x | (uintptr_t)packed | (uintptr_t)y) & 15) return fail("gmz_conv3x3_forward: operands must be 16-B aligned");
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == 1) return conv3_dispatch<__half>(H, x, packed, y, N, st);
-  if (dtype == 2) return conv3_dispatch<__hip_bfloat16>(H, x, packed, y, N, st);
+  if (dtype == 1) return conv3_dispatch<__half>(H, x, packed, y, N, mask, stats, st);
+  if (dtype == 2) return conv3_dispatch<__hip_bfloat16>(H, x, packed, y, N, mask, stats, st);
   return fail("gmz_conv3x3_forward: dtype must be 1 (f16) or 2 (bf16)");
+}
+
+GMZ_EXPORT int gmz_conv3x3_forward(int dtype, int H, const void *x, const void *packed, void *y, int N, void *stream) {
+  return gmz_conv3x3_forward_stats(dtype, H, x, packed, y, N, nullptr, nullptr, stream);
 }

@@ -528,6 +528,25 @@ int bn_backward(int nhwc, const void *x, const void *y, const void *dy, const ui
   return 0;
 }
 
+template <typename T>
+int bn_forward_stats(const void *x, const void *res, int B, int C, int S, const float *gamma, const float *beta,
+                     float eps, float momentum, float *rm, float *rv, int64_t *nb, int relu, void *y, float *save,
+                     const double *stats, int ns, hipStream_t st) {
+  hipLaunchKernelGGL(k_bn_finalize, dim3(C), dim3(WAVE), 0, st, stats, C, ns, 1, C, 0, eps, momentum, save, rm, rv, nb,
+                     (float *)nullptr, (float *)nullptr, (float *)nullptr);
+  GMZ_LAUNCH_CHECK();
+  const int V = nhwc_vec(C, sizeof(T), {x, res, y});
+  const long P = (long)B * S;
+  if (V == 8)
+    hipLaunchKernelGGL((k_bnl_apply<T, 8>), dim3(elementwise_blocks(P, C, 8)), dim3(BN_THREADS), 0, st, (const T *)x,
+                       (const T *)res, P, C, gamma, beta, relu, (T *)y, (const float *)save);
+  else
+    hipLaunchKernelGGL((k_bnl_apply<T, 2>), dim3(elementwise_blocks(P, C, 2)), dim3(BN_THREADS), 0, st, (const T *)x,
+                       (const T *)res, P, C, gamma, beta, relu, (T *)y, (const float *)save);
+  GMZ_LAUNCH_CHECK();
+  return 0;
+}
+
 // eval mode: save = (running_mean, 1/sqrt(running_var + eps))
 __global__ void k_bn_eval_save(const float *__restrict__ rm, const float *__restrict__ rv, int C, float eps,
                                float *__restrict__ save) {
@@ -632,4 +651,24 @@ GMZ_EXPORT int gmz_bn_eval(int dtype, int layout, const void *x, const void *res
                                      st);
   }
   return fail("gmz_bn_eval: dtype must be 0 (f32), 1 (f16) or 2 (bf16)");
+}
+
+GMZ_EXPORT int gmz_bn_forward_stats(int dtype, const void *x, const void *res, int B, int C, int S, const float *gamma,
+                                    const float *beta, float eps, float momentum, float *running_mean,
+                                    float *running_var, int64_t *num_batches, int relu, void *y, float *save,
+                                    const double *stats, int ns, void *stream) {
+  if (B <= 0 || C <= 0 || S <= 0 || ns <= 0 || (size_t)B * C * S >= (1ull << 31)) return fail("gmz_bn_forward_stats: bad shape");
+  if (check_layout(1, C)) return -1;
+  if (!x || !y || !gamma || !beta || !save || !stats) return fail("gmz_bn_forward_stats: null operand");
+  if ((running_mean == nullptr) != (running_var == nullptr)) return fail("gmz_bn_forward_stats: running stats pair");
+  hipStream_t st = (hipStream_t)stream;
+  switch (dtype) {
+    case 0: return bn_forward_stats<float>(x, res, B, C, S, gamma, beta, eps, momentum, running_mean, running_var,
+                                           num_batches, relu, y, save, stats, ns, st);
+    case 1: return bn_forward_stats<__half>(x, res, B, C, S, gamma, beta, eps, momentum, running_mean, running_var,
+                                            num_batches, relu, y, save, stats, ns, st);
+    case 2: return bn_forward_stats<__hip_bfloat16>(x, res, B, C, S, gamma, beta, eps, momentum, running_mean,
+                                                    running_var, num_batches, relu, y, save, stats, ns, st);
+  }
+  return fail("gmz_bn_forward_stats: dtype must be 0 (f32), 1 (f16) or 2 (bf16)");
 }

@@ -158,7 +158,8 @@ class _FusedMaskedBN(torch.autograd.Function):
     the reference's autocast)."""
 
     @staticmethod
-    def forward(ctx, x, gamma, beta, res, mask, running_mean, running_var, num_batches, eps, momentum, relu):
+    def forward(ctx, x, gamma, beta, res, mask, running_mean, running_var, num_batches, eps, momentum, relu,
+                stats=None):
         from . import _lib
         L = _lib.load()
         layout = _bn_layout(x)
@@ -170,11 +171,18 @@ class _FusedMaskedBN(torch.autograd.Function):
         S = x[0, 0].numel()
         y = torch.empty_like(x)
         save = torch.empty(2, C, dtype=torch.float32, device=x.device)
-        ws = _bn_workspace(layout, B, C, S, x.device)
-        _lib.check(L.gmz_bn_forward(_BN_DTYPES[x.dtype], layout, _lib.ptr(x), _lib.ptr(res), _lib.ptr(mask), B, C,
-                                    S, _lib.ptr(gamma), _lib.ptr(beta), float(eps), float(momentum),
-                                    _lib.ptr(running_mean), _lib.ptr(running_var), _lib.ptr(num_batches),
-                                    int(relu), _lib.ptr(y), _lib.ptr(save), _lib.ptr(ws), _lib.stream_ptr()))
+        if stats is not None and layout == 1:  # statistics reduced by the producing conv's epilogue
+            _lib.check(L.gmz_bn_forward_stats(_BN_DTYPES[x.dtype], _lib.ptr(x), _lib.ptr(res), B, C, S,
+                                              _lib.ptr(gamma), _lib.ptr(beta), float(eps), float(momentum),
+                                              _lib.ptr(running_mean), _lib.ptr(running_var), _lib.ptr(num_batches),
+                                              int(relu), _lib.ptr(y), _lib.ptr(save), _lib.ptr(stats[0]),
+                                              int(stats[1]), _lib.stream_ptr()))
+        else:
+            ws = _bn_workspace(layout, B, C, S, x.device)
+            _lib.check(L.gmz_bn_forward(_BN_DTYPES[x.dtype], layout, _lib.ptr(x), _lib.ptr(res), _lib.ptr(mask), B,
+                                        C, S, _lib.ptr(gamma), _lib.ptr(beta), float(eps), float(momentum),
+                                        _lib.ptr(running_mean), _lib.ptr(running_var), _lib.ptr(num_batches),
+                                        int(relu), _lib.ptr(y), _lib.ptr(save), _lib.ptr(ws), _lib.stream_ptr()))
         ctx.save_for_backward(x, y, mask, gamma, save)
         ctx.relu, ctx.has_res, ctx.layout = relu, res is not None, layout
         return y
@@ -197,7 +205,7 @@ class _FusedMaskedBN(torch.autograd.Function):
                                      _lib.ptr(mask), B, C, S, _lib.ptr(gamma), _lib.ptr(save), int(ctx.relu),
                                      _lib.ptr(dx), _lib.ptr(dres), _lib.ptr(dgamma), _lib.ptr(dbeta), _lib.ptr(ws),
                                      _lib.stream_ptr()))
-        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None
+        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None, None
 
 
 _WS_BYTES = {}
@@ -222,7 +230,8 @@ def _bn_act(mod, x, mask=None, res=None, relu=True):
             res = res.to(x.dtype)
         m = None if mask is None else mask.contiguous().view(torch.uint8)
         return _FusedMaskedBN.apply(x, mod.weight, mod.bias, res, m, mod.running_mean, mod.running_var,
-                                    mod.num_batches_tracked, mod.eps, mod.momentum, relu)
+                                    mod.num_batches_tracked, mod.eps, mod.momentum, relu,
+                                    getattr(x, "_gmz_bnstats", None))
     if (FUSED_BN and not mod.training and x.is_cuda and x.dtype in _BN_DTYPES and _bn_layout(x) is not None
             and not (torch.is_grad_enabled() and (x.requires_grad or mod.weight.requires_grad))):
         return _bn_eval(mod, x, res, relu)
@@ -336,12 +345,28 @@ def _packed_conv_weight(w, dtype, transpose):
     return out
 
 
-def _conv3x3_hip(x, packed):
+_STATS_SLOTS = {}
+
+
+def _conv3x3_hip(x, packed, mask=None, stats=None):
     from . import _lib
     y = torch.empty_like(x, memory_format=torch.channels_last)
-    _lib.check(_lib.load().gmz_conv3x3_forward(_CONV_DTYPES[x.dtype], x.shape[2], _lib.ptr(x), _lib.ptr(packed),
-                                               _lib.ptr(y), x.shape[0], _lib.stream_ptr()))
+    _lib.check(_lib.load().gmz_conv3x3_forward_stats(_CONV_DTYPES[x.dtype], x.shape[2], _lib.ptr(x), _lib.ptr(packed),
+                                                     _lib.ptr(y), x.shape[0], _lib.ptr(mask), _lib.ptr(stats),
+                                                     _lib.stream_ptr()))
     return y
+
+
+def _conv_stats_buffer(N, device):
+    """f64 [slots][128][3] partials for gmz_conv3x3_forward_stats -> (tensor, slots)."""
+    import ctypes
+    from . import _lib
+    if N not in _STATS_SLOTS:
+        n = ctypes.c_int()
+        _lib.check(_lib.load().gmz_conv3x3_stats_slots(N, ctypes.byref(n)))
+        _STATS_SLOTS[N] = n.value
+    ns = _STATS_SLOTS[N]
+    return torch.empty(ns * 128 * 3, dtype=torch.float64, device=device), ns
 
 
 class _Conv3x3NHWC(torch.autograd.Function):
@@ -352,9 +377,9 @@ class _Conv3x3NHWC(torch.autograd.Function):
     converts it (what autocast's cast would do)."""
 
     @staticmethod
-    def forward(ctx, x, w):
+    def forward(ctx, x, w, mask=None, stats=None):
         ctx.save_for_backward(x, w)
-        return _conv3x3_hip(x, _packed_conv_weight(w, x.dtype, 0))
+        return _conv3x3_hip(x, _packed_conv_weight(w, x.dtype, 0), mask, stats)
 
     @staticmethod
     def backward(ctx, gy):
@@ -366,20 +391,29 @@ class _Conv3x3NHWC(torch.autograd.Function):
             wd = torch.empty(w.shape, dtype=x.dtype, device=w.device).contiguous(memory_format=torch.channels_last)
             gw = torch.ops.aten.convolution_backward(gy, x, wd, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
                                                      [False, True, False])[1].to(w.dtype)
-        return gx, gw
+        return gx, gw, None, None
 
 
 def _conv3(cin, cout):
     return nn.Conv2d(cin, cout, 3, padding=1, bias=False)
 
 
-def _conv3_apply(conv, x):
-    """conv(x), on the HIP kernels when they cover the case (see ``_Conv3x3NHWC``)."""
+def _conv3_apply(conv, x, bn=None, mask=None):
+    """conv(x), on the HIP kernels when they cover the case (see ``_Conv3x3NHWC``).  ``bn``: the
+    training-mode BatchNorm that consumes the output — the kernel's epilogue then also reduces its
+    (row-masked) statistics, attached to the output for ``_bn_act`` (no separate reduction pass)."""
     if (FUSED_CONV and x.is_cuda and x.dim() == 4 and x.shape[1] == 128 and x.shape[2] == x.shape[3]
             and x.shape[2] in (9, 15) and conv.weight.shape == (128, 128, 3, 3) and conv.bias is None):
         dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x.dtype
         if dt in _CONV_DTYPES and x.is_contiguous(memory_format=torch.channels_last):
-            return _Conv3x3NHWC.apply(x.to(dt), conv.weight)
+            st = None
+            if bn is not None and bn.training and FUSED_BN:
+                st = _conv_stats_buffer(x.shape[0], x.device)
+            m = None if mask is None else mask.contiguous().view(torch.uint8)
+            y = _Conv3x3NHWC.apply(x.to(dt), conv.weight, m, None if st is None else st[0])
+            if st is not None:
+                y._gmz_bnstats = st
+            return y
     return conv(x)
 
 
@@ -392,8 +426,8 @@ class _Block(nn.Module):
         self.conv2, self.bn2 = _conv3(c, c), nn.BatchNorm2d(c, eps=1e-4)
 
     def forward(self, x, mask=None):
-        y = _bn_act(self.bn1, _conv3_apply(self.conv1, x), mask)
-        return _bn_act(self.bn2, _conv3_apply(self.conv2, y), mask, res=x)
+        y = _bn_act(self.bn1, _conv3_apply(self.conv1, x, self.bn1, mask), mask)
+        return _bn_act(self.bn2, _conv3_apply(self.conv2, y, self.bn2, mask), mask, res=x)
 
 
 class _Trunk(nn.Module):

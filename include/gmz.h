@@ -244,6 +244,12 @@ int gmz_bn_forward(int dtype, int layout, const void *x_dev, const void *res_dev
 int gmz_bn_backward(int dtype, int layout, const void *x_dev, const void *y_dev, const void *dy_dev, const uint8_t *mask_dev, int B,
                     int C, int S, const float *gamma_dev, const float *save_dev, int relu, void *dx_dev, void *dres_dev,
                     float *dgamma_dev, float *dbeta_dev, void *workspace_dev, void *stream);
+/* gmz_bn_forward with the statistics already reduced to partials (e.g. by gmz_conv3x3_forward_stats):
+ * stats_dev f64 [ns][C][3] (sum, sum of squares, counted elements); channels-last (layout 1) only. */
+int gmz_bn_forward_stats(int dtype, const void *x_dev, const void *res_dev, int B, int C, int S, const float *gamma_dev,
+                         const float *beta_dev, float eps, float momentum, float *running_mean_dev,
+                         float *running_var_dev, int64_t *num_batches_dev, int relu, void *y_dev, float *save_dev,
+                         const double *stats_dev, int ns, void *stream);
 /* Eval-mode BatchNorm (running statistics) + residual + ReLU, same layouts/dtypes as gmz_bn_forward:
  * y = relu?(gamma*(x-running_mean)/sqrt(running_var+eps) + beta (+ res)) — nn.BatchNorm2d/1d in eval()
  * (the target network's value of loss.py:54-55).  workspace_dev: gmz_bn_workspace_bytes bytes. */
@@ -261,6 +267,13 @@ int gmz_bn_eval(int dtype, int layout, const void *x_dev, const void *res_dev, i
 int gmz_conv3x3_pack(int dtype, const float *w_dev, int64_t s0, int64_t s1, int64_t s2, int64_t s3, int transpose,
                      void *packed_dev, void *stream);
 int gmz_conv3x3_forward(int dtype, int H, const void *x_dev, const void *packed_dev, void *y_dev, int N, void *stream);
+/* The same convolution, also writing the BatchNorm statistics of the (rounded) output over the boards
+ * whose mask_dev byte is nonzero (NULL: all): stats_dev f64 [slots][128][3] = (sum, sum of squares,
+ * counted positions) per slot, slots from gmz_conv3x3_stats_slots(N) — the partials layout
+ * gmz_bn_forward_stats consumes (channels-last, ns = slots). */
+int gmz_conv3x3_stats_slots(int N, int *slots);
+int gmz_conv3x3_forward_stats(int dtype, int H, const void *x_dev, const void *packed_dev, void *y_dev, int N,
+                              const uint8_t *mask_dev, double *stats_dev, void *stream);
 
 #ifdef __cplusplus
 }
