@@ -493,9 +493,17 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
   // ONE: this lane's residual tile values, [NTW][PTW][64 lanes] x 4 bf16 per wave (same lane writes
   // and reads back: program order suffices)
   u16x4 *xs = ONE ? (u16x4 *)t.xres + ((size_t)blockIdx.x * NW + w) * NTW * PTW * 64 + lane : nullptr;
-  auto store_out = [&](uint8_t *img, int nt, int i, const u16x4 &o) {
-    const int n0 = (nh * NTW + nt) * 16 + g4 * 4;
-    *(u16x4 *)(img + pos[i] + RS + PS + n0 * 2) = o;
+  static_assert(NTW % 2 == 0, "n-tiles pair up into 8-channel chunks");
+  // output channels of n-tile nt, lane group g4, element e: chan0(nt) + e (pack_conv3x3's row
+  // permutation): the n-tile pair (2u, 2u+1) gives a lane 8 consecutive channels = one 16-B chunk,
+  // so each tile pair is ONE conflict-free ds_write_b128 per lane (eight 16-B lanes cover the 64 banks)
+  auto chan0 = [&](int nt) {
+    const int ng = nh * NTW + nt;
+    return (ng >> 1) * 32 + 8 * g4 + 4 * (ng & 1);
+  };
+  auto store_pair = [&](uint8_t *img, int u, int i, const u16x4 &lo, const u16x4 &hi) {
+    const uint2 l2 = __builtin_bit_cast(uint2, lo), h2 = __builtin_bit_cast(uint2, hi);
+    *(uint4 *)(img + pos[i] + RS + PS + chan0(2 * u) * 2) = make_uint4(l2.x, l2.y, h2.x, h2.y);
   };
 
   // ---- weight fragment stream, per wave: k-step gs (modulo the whole set) of n-tile nt at
@@ -556,16 +564,19 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
         __builtin_amdgcn_sched_barrier(0);  // one tile's im2col loads at a time (VGPR budget)
       }
 #pragma unroll
-      for (int nt = 0; nt < NTW; ++nt) {
-        const int n0 = (nh * NTW + nt) * 16 + g4 * 4;
+      for (int u = 0; u < NTW / 2; ++u) {
 #pragma unroll
         for (int i = 0; i < PTW; ++i) {
           if (pos[i] < 0) continue;
-          u16x4 o;
+          u16x4 o[2];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] = f2bf(fmaxf(acc[nt][i][e] + t.stem_b[n0 + e], 0.f));
-          store_out(img0, nt, i, o);
-          if constexpr (ONE) xs[(nt * PTW + i) * 64] = o;
+          for (int h = 0; h < 2; ++h) {
+            const int n0 = chan0(2 * u + h);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[h][e] = f2bf(fmaxf(acc[2 * u + h][i][e] + t.stem_b[n0 + e], 0.f));
+            if constexpr (ONE) xs[((2 * u + h) * PTW + i) * 64] = o[h];
+          }
+          store_pair(img0, u, i, o[0], o[1]);
         }
       }
     } else {
@@ -583,7 +594,7 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
       const float *bias = sbias + (gl & 1) * C;
       f32x4 bv[NTW];
 #pragma unroll
-      for (int nt = 0; nt < NTW; ++nt) bv[nt] = *(const f32x4 *)(bias + (nh * NTW + nt) * 16 + g4 * 4);
+      for (int nt = 0; nt < NTW; ++nt) bv[nt] = *(const f32x4 *)(bias + chan0(nt));
       int bb[PTW];
 #pragma unroll
       for (int i = 0; i < PTW; ++i) {
@@ -641,10 +652,13 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
           // residual = this block's input, still in the image this epilogue overwrites, at the
           // very address this lane is about to store (read-then-write by the same lane)
 #pragma unroll
-          for (int nt = 0; nt < NTW; ++nt)
+          for (int u = 0; u < NTW / 2; ++u)
 #pragma unroll
-            for (int i = 0; i < PTW; ++i)
-              xr[nt][i] = *(const u16x4 *)(nimg + (pos[i] < 0 ? 0 : pos[i]) + RS + PS + ((nh * NTW + nt) * 16 + g4 * 4) * 2);
+            for (int i = 0; i < PTW; ++i) {
+              const uint4 v = *(const uint4 *)(nimg + (pos[i] < 0 ? 0 : pos[i]) + RS + PS + chan0(2 * u) * 2);
+              xr[2 * u][i] = __builtin_bit_cast(u16x4, make_uint2(v.x, v.y));
+              xr[2 * u + 1][i] = __builtin_bit_cast(u16x4, make_uint2(v.z, v.w));
+            }
         }
         int ay = 0, ax = 0;
         if constexpr (DYN && KIND == 0) {
@@ -652,9 +666,10 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
           ay = av / H;
           ax = av % H;
         }
+        u16x4 olo[PTW];  // even n-tile's outputs, stored with the odd one's as one 16-B chunk
 #pragma unroll
         for (int nt = 0; nt < NTW; ++nt) {
-          const int n0 = (nh * NTW + nt) * 16 + g4 * 4;
+          const int n0 = chan0(nt);
           if constexpr (KIND == 2 && ONE) {  // residual scratch, one n-tile at a time (VGPR budget)
 #pragma unroll
             for (int i = 0; i < PTW; ++i) xr[nt][i] = xs[(nt * PTW + i) * 64];
@@ -672,7 +687,11 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
               for (int e = 0; e < 4; ++e) v[e] += bf2f(xr[nt][i][e]);
             }
             const u16x4 o = __builtin_bit_cast(u16x4, make_uint2(relu_bf16x2(v[0], v[1]), relu_bf16x2(v[2], v[3])));
-            if ((PG * i + PG) * 16 <= A || pos[i] >= 0) store_out(nimg, nt, i, o);
+            if (nt & 1) {
+              if ((PG * i + PG) * 16 <= A || pos[i] >= 0) store_pair(nimg, nt >> 1, i, olo[i], o);
+            } else {
+              olo[i] = o;
+            }
             if constexpr (ONE && KIND != 1) xs[(nt * PTW + i) * 64] = o;  // the next block's input
           }
           if constexpr (ONE) __builtin_amdgcn_sched_barrier(0);

@@ -69,26 +69,34 @@ def conv_input_channel(ks, l, j):
     return (2 * ks + CHUNK_OF_GROUP[l >> 4]) * 8 + j
 
 
+def output_channel(nt, m):
+    """Output channel of MFMA row m (0..15) of n-tile nt in the tower kernels (k_tower3's chan0):
+    n-tiles pair up so that a lane's accumulators of tiles 2u and 2u+1 are 8 consecutive channels,
+    stored as one 16-byte chunk."""
+    return (nt >> 1) * 32 + 8 * (m >> 2) + 4 * (nt & 1) + (m & 3)
+
+
 def pack_conv3x3(wf):
     """[128(n), 128(c), 3, 3] f32 -> bf16 [9][4][8][64][8]: frag(t, ks, nt, l, j) =
-    W[n = nt*16 + (l&15)][c = conv_input_channel(ks, l, j)][t // 3][t % 3]."""
+    W[n = output_channel(nt, l&15)][c = conv_input_channel(ks, l, j)][t // 3][t % 3]."""
     Wt = wf.transpose(2, 3, 0, 1).reshape(9, C, C)  # [t][n][c]
     ks, nt, l, j = np.meshgrid(np.arange(4), np.arange(8), np.arange(64), np.arange(8), indexing="ij")
-    n = nt * 16 + (l & 15)
+    n = output_channel(nt, l & 15)
     c = conv_input_channel(ks, l, j)
     out = Wt[:, n, c]  # [9][4][8][64][8]
     return _bf16_bits(out)
 
 
 def pack_stem(wf):
-    """conv 3->128 [128, 3, 3, 3] -> bf16 [8][64][8] with k = tap*3 + c (27, zero-padded to 32)."""
+    """conv 3->128 [128, 3, 3, 3] -> bf16 [8][64][8] with k = tap*3 + c (27, zero-padded to 32), rows
+    in output_channel order."""
     Wk = np.zeros((C, 32), np.float32)
     for dy in range(3):
         for dx in range(3):
             for c in range(3):
                 Wk[:, (dy * 3 + dx) * 3 + c] = wf[:, c, dy, dx]
     nt, l, j = np.meshgrid(np.arange(8), np.arange(64), np.arange(8), indexing="ij")
-    return _bf16_bits(Wk[nt * 16 + (l & 15), 8 * (l >> 4) + j])
+    return _bf16_bits(Wk[output_channel(nt, l & 15), 8 * (l >> 4) + j])
 
 
 def r16(x):

@@ -17,7 +17,7 @@ def bf(u16):
 def unpack_conv(pk):  # [9][4][8][64][8] -> [9][n][c]
     out = np.zeros((9, 128, 128), np.float32)
     ks, nt, l, j = np.meshgrid(np.arange(4), np.arange(8), np.arange(64), np.arange(8), indexing="ij")
-    out[:, nt * 16 + (l & 15), N.conv_input_channel(ks, l, j)] = bf(pk)
+    out[:, N.output_channel(nt, l & 15), N.conv_input_channel(ks, l, j)] = bf(pk)
     return out
 
 
@@ -39,6 +39,17 @@ def small():
     return cfg, sd, N.pack_weights(sd, cfg)
 
 
+def test_output_channel_is_a_permutation_in_16_byte_chunks():
+    nt, m = np.meshgrid(np.arange(8), np.arange(16), indexing="ij")
+    ch = N.output_channel(nt, m)
+    assert sorted(ch.ravel()) == list(range(128))
+    # lane group g (rows 4g..4g+3) of tiles 2u, 2u+1: channels 32u + 8g + 0..7 (one 16-B chunk)
+    for u in range(4):
+        for g in range(4):
+            got = np.concatenate([ch[2 * u, 4 * g:4 * g + 4], ch[2 * u + 1, 4 * g:4 * g + 4]])
+            assert list(got) == list(range(32 * u + 8 * g, 32 * u + 8 * g + 8))
+
+
 def test_conv_pack_inverts(small):
     cfg, sd, pk = small
     s, _ = N.fold_bn(sd, "representation_net.resblocks.0.bn1")
@@ -56,7 +67,7 @@ def emulate(pk, cfg, obs=None, h=None, action=None):
     if obs is not None:
         Wk = np.zeros((128, 32), np.float32)
         nt, l, j = np.meshgrid(np.arange(8), np.arange(64), np.arange(8), indexing="ij")
-        Wk[nt * 16 + (l & 15), 8 * (l >> 4) + j] = bf(pk["repr_stem_w"])
+        Wk[N.output_channel(nt, l & 15), 8 * (l >> 4) + j] = bf(pk["repr_stem_w"])
         Wt = np.zeros((9, 128, 3), np.float32)
         for t in range(9):
             Wt[t] = Wk[:, t * 3:t * 3 + 3]

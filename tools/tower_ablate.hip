@@ -60,6 +60,21 @@ int main(int argc, char **argv) {
   uint16_t *dxres;  // residual scratch of single-image variants: 512 workgroups x up to 128 KB
   CK(hipMalloc(&dxres, (size_t)512 * 131072));
   TowerArgs a{dw, dbias, L, nullptr, nullptr, dact, nullptr, dpool, din, dac, dout, dhw, dhb, dpv, rows, dxres};
+  // k_tower3 reads MFMA row m of n-tile nt as output channel (nt>>1)*32 + 8*(m>>2) + 4*(nt&1) + (m&3)
+  // (network.output_channel), k_tower as nt*16 + m: the same weights for k_tower3 are row-permuted
+  std::vector<uint16_t> w3(w.size());
+  for (size_t blk = 0; blk < (size_t)L * 36; ++blk)
+    for (int nt3 = 0; nt3 < 8; ++nt3)
+      for (int l = 0; l < 64; ++l) {
+        const int m3 = l & 15, ch = (nt3 >> 1) * 32 + 8 * (m3 >> 2) + 4 * (nt3 & 1) + (m3 & 3);
+        const int nt = ch >> 4, lsrc = (l & 48) | (ch & 15);
+        memcpy(&w3[((blk * 8 + nt3) * 64 + l) * 8], &w[((blk * 8 + nt) * 64 + lsrc) * 8], 16);
+      }
+  uint16_t *dw3;
+  CK(hipMalloc(&dw3, w3.size() * 2));
+  CK(hipMemcpy(dw3, w3.data(), w3.size() * 2, hipMemcpyHostToDevice));
+  TowerArgs a3 = a;
+  a3.convs = dw3;
   const double flop = 1136505600.0 * rows;
   {  // k_tower3 must reproduce k_tower (LDS-staged weights, rotated image) bit for bit
     std::vector<uint16_t> o1((size_t)rows * A * 128), o2(o1.size());
@@ -69,7 +84,7 @@ int main(int argc, char **argv) {
     CK(hipMemcpy(p1.data(), dpv, p1.size() * 4, hipMemcpyDeviceToHost));
     CK(hipMemset(dpool + (size_t)rows * A * 128, 0, o1.size() * 2));
     CK(hipMemset(dpv, 0, p1.size() * 4));
-    hipLaunchKernelGGL((k_tower3<15, true, 0>), dim3(256), dim3(512), 0, 0, a);
+    hipLaunchKernelGGL((k_tower3<15, true, 0>), dim3(256), dim3(512), 0, 0, a3);
     CK(hipMemcpy(o2.data(), dpool + (size_t)rows * A * 128, o2.size() * 2, hipMemcpyDeviceToHost));
     CK(hipMemcpy(p2.data(), dpv, p2.size() * 4, hipMemcpyDeviceToHost));
     size_t dh = 0, dp = 0;
@@ -79,7 +94,7 @@ int main(int argc, char **argv) {
     printf("tower3 vs tower: hidden mismatches %zu / %zu (max |diff| %g), pv mismatches %zu / %zu\n", dh, o1.size(), mxd, dp, p1.size());
     CK(hipMemset(dpool + (size_t)rows * A * 128, 0, o1.size() * 2));
     CK(hipMemset(dpv, 0, p1.size() * 4));
-    hipLaunchKernelGGL((k_tower3<15, true, 0, 3, 4, 3>), dim3(256), dim3(768), 0, 0, a);
+    hipLaunchKernelGGL((k_tower3<15, true, 0, 3, 4, 3>), dim3(256), dim3(768), 0, 0, a3);
     CK(hipMemcpy(o2.data(), dpool + (size_t)rows * A * 128, o2.size() * 2, hipMemcpyDeviceToHost));
     CK(hipMemcpy(p2.data(), dpv, p2.size() * 4, hipMemcpyDeviceToHost));
     dh = dp = 0;
@@ -89,7 +104,7 @@ int main(int argc, char **argv) {
     printf("tower3 12w vs tower: hidden mismatches %zu / %zu (max |diff| %g), pv mismatches %zu / %zu\n", dh, o1.size(), mxd, dp, p1.size());
     CK(hipMemset(dpool + (size_t)rows * A * 128, 0, o1.size() * 2));
     CK(hipMemset(dpv, 0, p1.size() * 4));
-    hipLaunchKernelGGL((k_tower3<15, true, 0, 3, 4, 2>), dim3(256), dim3(512), 0, 0, a);
+    hipLaunchKernelGGL((k_tower3<15, true, 0, 3, 4, 2>), dim3(256), dim3(512), 0, 0, a3);
     CK(hipMemcpy(o2.data(), dpool + (size_t)rows * A * 128, o2.size() * 2, hipMemcpyDeviceToHost));
     CK(hipMemcpy(p2.data(), dpv, p2.size() * 4, hipMemcpyDeviceToHost));
     dh = dp = 0;
@@ -105,9 +120,9 @@ int main(int argc, char **argv) {
   float best[NV];
   for (int i = 0; i < NV; ++i) best[i] = 1e9f;
   for (int round = 0; round < 5; ++round) {
-    float t[NV] = {run<0>(a, 5), run<0, 3, 3, 4, 3>(a, 5), run<0, 3, 3, 4, 2>(a, 5), run<32, 3, 3, 4, 2>(a, 5),
-                   run<2, 3, 3, 4, 2>(a, 5), run<512, 3, 3, 4, 2>(a, 5), run<0, 3, 3, 4, 1>(a, 5),
-                   run<0, 3, 4, 4, 1>(a, 5), run<0, 3, 2, 4, 1>(a, 5)};
+    float t[NV] = {run<0>(a, 5), run<0, 3, 3, 4, 3>(a3, 5), run<0, 3, 3, 4, 2>(a3, 5), run<32, 3, 3, 4, 2>(a3, 5),
+                   run<2, 3, 3, 4, 2>(a3, 5), run<512, 3, 3, 4, 2>(a3, 5), run<0, 3, 3, 4, 1>(a3, 5),
+                   run<0, 3, 4, 4, 1>(a3, 5), run<0, 3, 2, 4, 1>(a3, 5)};
     for (int i = 0; i < NV; ++i) best[i] = t[i] < best[i] ? t[i] : best[i];
   }
   for (int i = 0; i < NV; ++i)
@@ -125,9 +140,9 @@ int main(int argc, char **argv) {
            sum[3] / (256 * NWV) / (ms_per_launch * 1e-3) / 1e9);
     return 0;
   };
-  stamps("12w (no io)", 12, run<128 | 32, 3, 3, 4, 3>(a, 5), [&] { run<128 | 32, 3, 3, 4, 3>(a, 1); });
-  stamps("8w product (no io)", 8, run<128 | 32, 3, 3, 4, 2>(a, 5), [&] { run<128 | 32, 3, 3, 4, 2>(a, 1); });
-  stamps("8w no-A-loads (no io)", 8, run<128 | 32 | 2, 3, 3, 4, 2>(a, 5), [&] { run<128 | 32 | 2, 3, 3, 4, 2>(a, 1); });
+  stamps("12w (no io)", 12, run<128 | 32, 3, 3, 4, 3>(a3, 5), [&] { run<128 | 32, 3, 3, 4, 3>(a3, 1); });
+  stamps("8w product (no io)", 8, run<128 | 32, 3, 3, 4, 2>(a3, 5), [&] { run<128 | 32, 3, 3, 4, 2>(a3, 1); });
+  stamps("8w no-A-loads (no io)", 8, run<128 | 32 | 2, 3, 3, 4, 2>(a3, 5), [&] { run<128 | 32 | 2, 3, 3, 4, 2>(a3, 1); });
   CK(hipDeviceSynchronize());
   return 0;
 }
