@@ -261,6 +261,151 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
   }
 }
 
+// ---- weight gradient: dW[o][c][t] = sum over boards n and positions p of dy[n][p][o] * x[n][p + d(t)][c]
+// (d(t) = (t/3 - 1, t%3 - 1), zero outside the board), the GEMM M = o, N = c, K = (n, p) per tap.
+// Workgroup = (tap row ty, chunk of boards): 8 waves = 4 (32 o) x 2 (64 c), accumulating the three taps
+// of row ty (3 x 2 m-tiles x 4 n-tiles, 96 f32 per lane).  Per board the dy tile and the x tile are
+// DMA'd into LDS as [position][128 channels] rows of 256 B (x: one extra zero row for neighbours off
+// the board) with the 16-B chunks of row r XOR-swizzled by ((r&3)<<2)|((r>>2)&3), applied on the DMA's
+// source side; both MFMA operands need 8 consecutive positions (K) per lane and come from
+// ds_read_b64_tr_b16 transposing reads (per 16-lane group a 4-position x 16-channel block, delivered
+// channel-major), conflict-free on this swizzle for rows 8 apart in the two groups of a 32-lane half.
+// Partials per chunk go to a scratch [chunk][9][128][128] that k_conv3_wgrad_reduce sums into the f32
+// weight gradient.
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+
+template <int H>
+struct WgLds {
+  static constexpr int A = H * H, KS = (A + 31) / 32, NPOS = KS * 32;
+  static constexpr int DY_BYTES = NPOS * 256, X_OFF = DY_BYTES, XROWS = A + 1;  // + zero row A
+  static constexpr int BYTES = DY_BYTES + (XROWS * 256 + 1023) / 1024 * 1024;
+  static constexpr int NPD = A * 256 / 1024 + ((A * 256) % 1024 != 0);  // DMA pieces per tile
+};
+
+__device__ __forceinline__ int wg_swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+
+__device__ __forceinline__ s16x4_t tr_read(const uint8_t *lds_base, int off) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t *)(
+      (__attribute__((address_space(3))) uint8_t *)lds_base + off));
+}
+
+// byte offset of channels [ch8 * 8 + 4 * (p & 1), +4) of row `row` in a swizzled [row][256 B] tile,
+// for transposing-read lane p (0..3) of a block starting at 16-B chunk ch8 (even)
+__device__ __forceinline__ int wg_off(int row, int ch8, int p) {
+  return row * 256 + (((ch8 + (p >> 1)) ^ wg_swz(row)) << 4) + 8 * (p & 1);
+}
+
+template <int H, typename T>
+__global__ void __launch_bounds__(512, 1) k_conv3_wgrad(const uint16_t *__restrict__ x, const uint16_t *__restrict__ dy,
+                                                        int N, int nch, float *__restrict__ part) {
+  using L = WgLds<H>;
+  using M = Mfma<T>;
+  typedef typename M::V V;
+  constexpr int A = H * H, KS = L::KS;
+  static_assert(L::BYTES <= 163840, "LDS budget");
+  __shared__ __attribute__((aligned(16))) uint8_t smem[L::BYTES];
+  uint8_t *xt = smem + L::X_OFF;
+
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int ty = blockIdx.x % 3, chunk = blockIdx.x / 3;
+  const int wo = w & 3, wc = w >> 2;
+  const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+
+  for (int i = tid; i < L::BYTES / 16; i += 512) *(uint4 *)(smem + i * 16) = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+
+  f32x4_t acc[3][2][4];
+#pragma unroll
+  for (int tx = 0; tx < 3; ++tx)
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) acc[tx][mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  for (int b = chunk; b < N; b += nch) {
+    // ---- dy and x rows 0..A-1: LDS-linear 1 KB pieces; lane l fills 16-B slot (row, l & 15), which
+    //      holds source chunk (l & 15) ^ swz(row)
+    const uint8_t *sd = (const uint8_t *)(dy + (size_t)b * A * CC);
+    const uint8_t *sx = (const uint8_t *)(x + (size_t)b * A * CC);
+    for (int j = w; j < 2 * L::NPD; j += 8) {
+      const int t = j >= L::NPD, jj = t ? j - L::NPD : j;
+      const int row = jj * 4 + (lane >> 4);
+      if (row < A) {
+        const int src = row * 256 + (((lane & 15) ^ wg_swz(row)) << 4);
+        __builtin_amdgcn_global_load_lds((const void *)((t ? sx : sd) + src),
+                                         (__attribute__((address_space(3))) void *)((t ? xt : smem) + jj * 1024),
+                                         16, 0, 0);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+#pragma unroll 2
+    for (int ks = 0; ks < KS; ++ks) {
+      // rows (positions) of this lane's two transposing reads: 8g + q and 8g + 4 + q of the k-step
+      const int p0 = ks * 32 + 8 * g + q, p1 = p0 + 4;
+      V af[2];
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        const int ch8 = (wo * 32 + mt * 16) >> 3;
+        const s16x4_t lo = tr_read(smem, wg_off(p0, ch8, pp)), hi = tr_read(smem, wg_off(p1, ch8, pp));
+        af[mt] = __builtin_bit_cast(V, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+      // x rows: the neighbour (y + ty - 1, x + tx - 1) of position p, the zero row A off the board
+      // (positions past the board read any row: their dy rows are zero)
+      const int y0 = p0 / H, x0 = p0 % H, y1 = p1 / H, x1 = p1 % H;
+#pragma unroll
+      for (int tx = 0; tx < 3; ++tx) {
+        const int ny0 = y0 + ty - 1, nx0 = x0 + tx - 1, ny1 = y1 + ty - 1, nx1 = x1 + tx - 1;
+        const int r0 = (p0 < A && ny0 >= 0 && ny0 < H && nx0 >= 0 && nx0 < H) ? ny0 * H + nx0 : A;
+        const int r1 = (p1 < A && ny1 >= 0 && ny1 < H && nx1 >= 0 && nx1 < H) ? ny1 * H + nx1 : A;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+          const int ch8 = (wc * 64 + nt * 16) >> 3;
+          const s16x4_t lo = tr_read(xt, wg_off(r0, ch8, pp)), hi = tr_read(xt, wg_off(r1, ch8, pp));
+          const V bf = __builtin_bit_cast(V, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+          for (int mt = 0; mt < 2; ++mt) acc[tx][mt][nt] = M::run(af[mt], bf, acc[tx][mt][nt]);
+        }
+      }
+    }
+    __syncthreads();  // every wave is done with this board's tiles before the next DMA
+  }
+  // ---- partials: acc[tx][mt][nt][e] = dW[o = 32 wo + 16 mt + 4 g + e][c = 64 wc + 16 nt + (lane & 15)][3 ty + tx]
+  float *pc = part + (size_t)chunk * 9 * CC * CC;
+#pragma unroll
+  for (int tx = 0; tx < 3; ++tx)
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int o = wo * 32 + 16 * mt + 4 * g + e, c = wc * 64 + 16 * nt + (lane & 15);
+          pc[((size_t)(ty * 3 + tx) * CC + o) * CC + c] = acc[tx][mt][nt][e];
+        }
+}
+
+// dW[o][c][ky][kx] (+)= sum over chunks of part[chunk][t][o][c], dW at element strides (s0, s1, s2, s3);
+// 8 independent partial sums per thread keep 8 loads in flight
+__global__ void __launch_bounds__(256) k_conv3_wgrad_reduce(const float *__restrict__ part, int nch, float *dw, long s0,
+                                                            long s1, long s2, long s3, int accumulate) {
+  const int i = blockIdx.x * 256 + threadIdx.x;  // (t, o, c)
+  if (i >= 9 * CC * CC) return;
+  const int c = i % CC, o = (i / CC) % CC, t = i / (CC * CC);
+  constexpr size_t STR = 9 * CC * CC;
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int k = 0;
+  for (; k + 8 <= nch; k += 8) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s[u] += part[(size_t)(k + u) * STR + i];
+  }
+  for (; k < nch; ++k) s[0] += part[(size_t)k * STR + i];
+  const float tot = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+  float *d = dw + o * s0 + c * s1 + (t / 3) * s2 + (t % 3) * s3;
+  *d = accumulate ? *d + tot : tot;
+}
+
 static int cu_count_conv() {
   static int n = 0;
   if (!n) {
@@ -295,6 +440,20 @@ int conv3_dispatch(int H, const void *x, const void *wpk, void *y, int N, const 
     case 15: return launch_conv3<15, T>(x, wpk, y, N, mask, stats, st);
   }
   return fail("gmz_conv3x3: board size must be 9 or 15");
+}
+
+int wgrad_chunks(int N) {
+  int n = cu_count_conv() / 3;
+  return n < N ? n : N;
+}
+
+template <int H, typename T>
+int launch_wgrad(const void *x, const void *dy, int N, float *part, hipStream_t st) {
+  const int nch = wgrad_chunks(N);
+  hipLaunchKernelGGL((k_conv3_wgrad<H, T>), dim3(3 * nch), dim3(512), 0, st, (const uint16_t *)x, (const uint16_t *)dy,
+                     N, nch, part);
+  GMZ_LAUNCH_CHECK();
+  return 0;
 }
 
 }  // namespace
@@ -337,4 +496,31 @@ GMZ_EXPORT int gmz_conv3x3_forward_stats(int dtype, int H, const void *x, const 
 
 GMZ_EXPORT int gmz_conv3x3_forward(int dtype, int H, const void *x, const void *packed, void *y, int N, void *stream) {
   return gmz_conv3x3_forward_stats(dtype, H, x, packed, y, N, nullptr, nullptr, stream);
+}
+
+GMZ_EXPORT int gmz_conv3x3_wgrad_workspace_bytes(int N, size_t *out) {
+  if (N <= 0 || !out) return fail("gmz_conv3x3_wgrad_workspace_bytes: bad arguments");
+  *out = (size_t)wgrad_chunks(N) * 9 * CC * CC * sizeof(float);
+  return 0;
+}
+
+GMZ_EXPORT int gmz_conv3x3_wgrad(int dtype, int H, const void *x, const void *dy, int N, float *dw, int64_t s0,
+                                 int64_t s1, int64_t s2, int64_t s3, int accumulate, void *workspace, void *stream) {
+  if (!x || !dy || !dw || !workspace) return fail("gmz_conv3x3_wgrad: null operand");
+  if (N <= 0) return fail("gmz_conv3x3_wgrad: N must be positive");
+  if (((uintptr_t)x | (uintptr_t)dy) & 15) return fail("gmz_conv3x3_wgrad: operands must be 16-B aligned");
+  hipStream_t st = (hipStream_t)stream;
+  float *part = (float *)workspace;
+  int rc;
+  if (dtype == 1) rc = H == 15 ? launch_wgrad<15, __half>(x, dy, N, part, st) : H == 9 ? launch_wgrad<9, __half>(x, dy, N, part, st) : -2;
+  else if (dtype == 2)
+    rc = H == 15 ? launch_wgrad<15, __hip_bfloat16>(x, dy, N, part, st)
+                 : H == 9 ? launch_wgrad<9, __hip_bfloat16>(x, dy, N, part, st) : -2;
+  else return fail("gmz_conv3x3_wgrad: dtype must be 1 (f16) or 2 (bf16)");
+  if (rc == -2) return fail("gmz_conv3x3_wgrad: board size must be 9 or 15");
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_conv3_wgrad_reduce, dim3((9 * CC * CC + 255) / 256), dim3(256), 0, st, (const float *)part,
+                     wgrad_chunks(N), dw, (long)s0, (long)s1, (long)s2, (long)s3, accumulate);
+  GMZ_LAUNCH_CHECK();
+  return 0;
 }

@@ -357,6 +357,28 @@ def _conv3x3_hip(x, packed, mask=None, stats=None):
     return y
 
 
+# the 128->128 convs' weight gradient on gmz_conv3x3_wgrad instead of MIOpen: exact (f32 accumulation,
+# tested) but not yet faster (52 + 10 us vs MIOpen's 55 us per 360-board layer), so off by default
+HIP_WGRAD = False
+_WGRAD_WS = {}
+
+
+def _conv3x3_wgrad_hip(x, gy, grad):
+    """grad (f32, any strides) += weight gradient of the 128->128 conv from channels-last x, gy."""
+    import ctypes
+    from . import _lib
+    L = _lib.load()
+    N = x.shape[0]
+    if N not in _WGRAD_WS:
+        n = ctypes.c_size_t()
+        _lib.check(L.gmz_conv3x3_wgrad_workspace_bytes(N, ctypes.byref(n)))
+        _WGRAD_WS[N] = n.value
+    ws = torch.empty(_WGRAD_WS[N] // 4, dtype=torch.float32, device=x.device)
+    s = grad.stride()
+    _lib.check(L.gmz_conv3x3_wgrad(_CONV_DTYPES[x.dtype], x.shape[2], _lib.ptr(x), _lib.ptr(gy), N, _lib.ptr(grad),
+                                   s[0], s[1], s[2], s[3], 1, _lib.ptr(ws), _lib.stream_ptr()))
+
+
 def _conv_stats_buffer(N, device):
     """f64 [slots][128][3] partials for gmz_conv3x3_forward_stats -> (tensor, slots)."""
     import ctypes
@@ -388,9 +410,16 @@ class _Conv3x3NHWC(torch.autograd.Function):
         gx = _conv3x3_hip(gy, _packed_conv_weight(w, x.dtype, 1)) if ctx.needs_input_grad[0] else None
         gw = None
         if ctx.needs_input_grad[1]:
-            wd = torch.empty(w.shape, dtype=x.dtype, device=w.device).contiguous(memory_format=torch.channels_last)
-            gw = torch.ops.aten.convolution_backward(gy, x, wd, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
-                                                     [False, True, False])[1].to(w.dtype)
+            if HIP_WGRAD:
+                # accumulated straight into the f32 .grad (the trainer's flat-bucket view; created when
+                # absent): no f16 gradient tensor, no cast, no AccumulateGrad add
+                if w.grad is None:
+                    w.grad = torch.zeros_like(w)
+                _conv3x3_wgrad_hip(x, gy, w.grad)
+            else:
+                wd = torch.empty(w.shape, dtype=x.dtype, device=w.device).contiguous(memory_format=torch.channels_last)
+                gw = torch.ops.aten.convolution_backward(gy, x, wd, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
+                                                         [False, True, False])[1].to(w.dtype)
         return gx, gw, None, None
 
 

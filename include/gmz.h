@@ -272,6 +272,13 @@ int gmz_conv3x3_forward(int dtype, int H, const void *x_dev, const void *packed_
  * counted positions) per slot, slots from gmz_conv3x3_stats_slots(N) — the partials layout
  * gmz_bn_forward_stats consumes (channels-last, ns = slots). */
 int gmz_conv3x3_stats_slots(int N, int *slots);
+/* Weight gradient of the same convolution (the reference's autocast backward of the residual-block
+ * convs): dw_dev f32 W[o][c][ky][kx] at element strides (s0..s3) = (accumulate ? dw + : ) sum over the
+ * N boards of dy x^T per tap; x_dev, dy_dev channels-last [N][H*H][128] f16/bf16, 16-B aligned.
+ * workspace_dev: gmz_conv3x3_wgrad_workspace_bytes(N) bytes (per-chunk partials). */
+int gmz_conv3x3_wgrad_workspace_bytes(int N, size_t *out);
+int gmz_conv3x3_wgrad(int dtype, int H, const void *x_dev, const void *dy_dev, int N, float *dw_dev, int64_t s0,
+                      int64_t s1, int64_t s2, int64_t s3, int accumulate, void *workspace_dev, void *stream);
 int gmz_conv3x3_forward_stats(int dtype, int H, const void *x_dev, const void *packed_dev, void *y_dev, int N,
                               const uint8_t *mask_dev, double *stats_dev, void *stream);
 

@@ -16,6 +16,7 @@ w = (torch.randn(128, 128, 3, 3, device="cuda") / 34).contiguous(memory_format=t
 wh = w.half()
 pk, pkt = T._packed_conv_weight(w, torch.float16, 0), T._packed_conv_weight(w, torch.float16, 1)
 fl = 2.0 * N * H * H * 128 * 128 * 9
+gacc = torch.zeros_like(w)
 
 
 def tm(fn, n=50):
@@ -38,10 +39,15 @@ res = {
     "miopen dgrad": tm(lambda: torch.ops.aten.convolution_backward(x, x, wh, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [True, False, False])),
     "miopen wgrad": tm(lambda: torch.ops.aten.convolution_backward(x, x, wh, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False])),
     "pack": tm(lambda: T._packed_conv_weight(w.add_(0), torch.float16, 0)),
+    "hip wgrad": tm(lambda: T._conv3x3_wgrad_hip(x, x, gacc)),
 }
 y = T._conv3x3_hip(x, pk).float()
 yr = torch.nn.functional.conv2d(x.float(), wh.float(), padding=1)
 err = float((y - yr).abs().max() / yr.abs().max())
-print("N=%d H=%d  rel err %.2e" % (N, H, err))
+gw = torch.zeros_like(w)
+T._conv3x3_wgrad_hip(x, x, gw)
+gwr = torch.ops.aten.convolution_backward(x.float(), x.float(), wh.float(), None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False])[1]
+werr = float((gw - gwr).abs().max() / gwr.abs().max())
+print("N=%d H=%d  rel err %.2e  wgrad rel err %.2e" % (N, H, err, werr))
 for k, v in res.items():
     print("%-14s %8.1f us  %6.0f TFLOP/s" % (k, v, fl / v / 1e6))
