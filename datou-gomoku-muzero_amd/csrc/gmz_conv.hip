@@ -264,52 +264,54 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
 // ---- weight gradient: dW[o][c][t] = sum over boards n and positions p of dy[n][p][o] * x[n][p + d(t)][c]
 // (d(t) = (t/3 - 1, t%3 - 1), zero outside the board), the GEMM M = o, N = c, K = (n, p) per tap.
 // Workgroup = (tap row ty, chunk of boards): 8 waves = 4 (32 o) x 2 (64 c), accumulating the three taps
-// of row ty (3 x 2 m-tiles x 4 n-tiles, 96 f32 per lane).  Per board the dy tile and the x tile are
-// DMA'd into LDS as [position][128 channels] rows of 256 B (x: one extra zero row for neighbours off
-// the board) with the 16-B chunks of row r XOR-swizzled by ((r&3)<<2)|((r>>2)&3), applied on the DMA's
-// source side; both MFMA operands need 8 consecutive positions (K) per lane and come from
-// ds_read_b64_tr_b16 transposing reads (per 16-lane group a 4-position x 16-channel block, delivered
-// channel-major), conflict-free on this swizzle for rows 8 apart in the two groups of a 32-lane half.
+// of row ty (3 x 2 m-tiles x 4 n-tiles, 96 f32 per lane).  Per board the dy tile [position][128 o]
+// and the zero-padded x image [(H+2) x (H+2) cells][128 c] are DMA'd into LDS in their HBM (NHWC)
+// order with 288-byte rows; both MFMA operands need 8 consecutive positions (K) per lane and come from
+// ds_read_b64_tr_b16 transposing reads (per 16-lane group a 4-row x 16-channel block, delivered
+// channel-major).  K order inside a k-step: lane group g takes positions 4g..4g+3 (first read) and
+// 16+4g..16+4g+3 (second), so the two groups of a 32-lane half read rows 4 apart = 1152 B = 32 banks
+// apart, and the 288-B stride puts a group's 4 rows 8 banks apart: conflict-free.  With padded x the
+// three taps of the row and the four n-tiles are immediate offsets from two base addresses per k-step.
 // Partials per chunk go to a scratch [chunk][9][128][128] that k_conv3_wgrad_reduce sums into the f32
 // weight gradient.
 typedef short s16x4_t __attribute__((ext_vector_type(4)));
 
 template <int H>
 struct WgLds {
-  static constexpr int A = H * H, KS = (A + 31) / 32, NPOS = KS * 32;
-  static constexpr int DY_BYTES = NPOS * 256, X_OFF = DY_BYTES, XROWS = A + 1;  // + zero row A
-  static constexpr int BYTES = DY_BYTES + (XROWS * 256 + 1023) / 1024 * 1024;
-  static constexpr int NPD = A * 256 / 1024 + ((A * 256) % 1024 != 0);  // DMA pieces per tile
+  static constexpr int A = H * H, KS = (A + 31) / 32, NPOS = KS * 32, RB = 288, HP = H + 2;
+  static constexpr int DY_BYTES = NPOS * RB, X_OFF = DY_BYTES, X_BYTES = HP * HP * RB;
+  static constexpr int BYTES = DY_BYTES + X_BYTES;
+  static constexpr int NPD = (A * RB + 1023) / 1024;        // dy DMA pieces
+  static constexpr int RUN = (H - 1) * RB + 256, RUN_DMA = (RUN + 1023) / 1024;  // one board row of x
 };
-
-__device__ __forceinline__ int wg_swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
 
 __device__ __forceinline__ s16x4_t tr_read(const uint8_t *lds_base, int off) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t *)(
       (__attribute__((address_space(3))) uint8_t *)lds_base + off));
 }
 
-// byte offset of channels [ch8 * 8 + 4 * (p & 1), +4) of row `row` in a swizzled [row][256 B] tile,
-// for transposing-read lane p (0..3) of a block starting at 16-B chunk ch8 (even)
-__device__ __forceinline__ int wg_off(int row, int ch8, int p) {
-  return row * 256 + (((ch8 + (p >> 1)) ^ wg_swz(row)) << 4) + 8 * (p & 1);
-}
-
+#ifndef WGRAD_ABL
+#define WGRAD_ABL 0  // timing ablations (tools only): 1 = no DMA, 2 = k-loop twice per board
+#endif
 template <int H, typename T>
 __global__ void __launch_bounds__(512, 1) k_conv3_wgrad(const uint16_t *__restrict__ x, const uint16_t *__restrict__ dy,
                                                         int N, int nch, float *__restrict__ part) {
   using L = WgLds<H>;
   using M = Mfma<T>;
   typedef typename M::V V;
-  constexpr int A = H * H, KS = L::KS;
+  constexpr int A = H * H, KS = L::KS, RB = L::RB, HP = L::HP;
   static_assert(L::BYTES <= 163840, "LDS budget");
   __shared__ __attribute__((aligned(16))) uint8_t smem[L::BYTES];
   uint8_t *xt = smem + L::X_OFF;
 
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  const int ty = blockIdx.x % 3, chunk = blockIdx.x / 3;
+  // XCD-aware: workgroups are dealt to the 8 XCDs round-robin by index, so the three tap rows of a
+  // chunk get indices 8 apart (same XCD, same L2): each board is fetched from HBM once, not 3 times
+  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+  const int ty = slot % 3, chunk = (slot / 3) * 8 + xcd;
   const int wo = w & 3, wc = w >> 2;
   const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+  const int ocol = (wo * 32 + 4 * pp) * 2, ccol = (wc * 64 + 4 * pp) * 2;  // this lane's column bytes
 
   for (int i = tid; i < L::BYTES / 16; i += 512) *(uint4 *)(smem + i * 16) = make_uint4(0, 0, 0, 0);
   __syncthreads();
@@ -323,46 +325,49 @@ __global__ void __launch_bounds__(512, 1) k_conv3_wgrad(const uint16_t *__restri
       for (int nt = 0; nt < 4; ++nt) acc[tx][mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   for (int b = chunk; b < N; b += nch) {
-    // ---- dy and x rows 0..A-1: LDS-linear 1 KB pieces; lane l fills 16-B slot (row, l & 15), which
-    //      holds source chunk (l & 15) ^ swz(row)
+    // ---- dy rows 0..A-1 and the x image interior: LDS-linear 1 KB pieces, row pads skipped
     const uint8_t *sd = (const uint8_t *)(dy + (size_t)b * A * CC);
     const uint8_t *sx = (const uint8_t *)(x + (size_t)b * A * CC);
-    for (int j = w; j < 2 * L::NPD; j += 8) {
-      const int t = j >= L::NPD, jj = t ? j - L::NPD : j;
-      const int row = jj * 4 + (lane >> 4);
-      if (row < A) {
-        const int src = row * 256 + (((lane & 15) ^ wg_swz(row)) << 4);
-        __builtin_amdgcn_global_load_lds((const void *)((t ? sx : sd) + src),
-                                         (__attribute__((address_space(3))) void *)((t ? xt : smem) + jj * 1024),
-                                         16, 0, 0);
+    for (int j = w; j < ((WGRAD_ABL & 1) ? 0 : L::NPD + H * L::RUN_DMA); j += 8) {
+      if (j < L::NPD) {
+        const int o = j * 1024 + lane * 16;
+        const int row = o / RB, ch = (o % RB) >> 4;
+        if (row < A && ch < 16)
+          __builtin_amdgcn_global_load_lds((const void *)(sd + row * 256 + ch * 16),
+                                           (__attribute__((address_space(3))) void *)(smem + j * 1024), 16, 0, 0);
+      } else {
+        const int jj = j - L::NPD, yy = jj / L::RUN_DMA, piece = jj % L::RUN_DMA;
+        const int o = piece * 1024 + lane * 16;
+        const int xx = o / RB, ch = (o % RB) >> 4;
+        if (o < L::RUN && ch < 16)
+          __builtin_amdgcn_global_load_lds((const void *)(sx + (yy * H + xx) * 256 + ch * 16),
+                                           (__attribute__((address_space(3))) void *)(xt + ((yy + 1) * HP + 1) * RB + piece * 1024),
+                                           16, 0, 0);
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 
 #pragma unroll 2
-    for (int ks = 0; ks < KS; ++ks) {
-      // rows (positions) of this lane's two transposing reads: 8g + q and 8g + 4 + q of the k-step
-      const int p0 = ks * 32 + 8 * g + q, p1 = p0 + 4;
+    for (int kk = 0; kk < ((WGRAD_ABL & 2) ? 2 * KS : KS); ++kk) {
+      const int ks = kk % KS;
+      const int p0 = ks * 32 + 4 * g + q, p1 = p0 + 16;
+      // x rows: cell (y + ty, x) of the padded image for tap column 0; columns 1, 2 are +RB, +2 RB.
+      // Positions past the board (zero dy rows) read the last position's cells
+      const int c0 = p0 < A ? p0 : A - 1, c1 = p1 < A ? p1 : A - 1;
+      const int xb0 = ((c0 / H + ty) * HP + c0 % H) * RB + ccol, xb1 = ((c1 / H + ty) * HP + c1 % H) * RB + ccol;
+      const int ab0 = p0 * RB + ocol, ab1 = p1 * RB + ocol;
       V af[2];
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) {
-        const int ch8 = (wo * 32 + mt * 16) >> 3;
-        const s16x4_t lo = tr_read(smem, wg_off(p0, ch8, pp)), hi = tr_read(smem, wg_off(p1, ch8, pp));
+        const s16x4_t lo = tr_read(smem, ab0 + mt * 32), hi = tr_read(smem, ab1 + mt * 32);
         af[mt] = __builtin_bit_cast(V, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
       }
-      // x rows: the neighbour (y + ty - 1, x + tx - 1) of position p, the zero row A off the board
-      // (positions past the board read any row: their dy rows are zero)
-      const int y0 = p0 / H, x0 = p0 % H, y1 = p1 / H, x1 = p1 % H;
 #pragma unroll
       for (int tx = 0; tx < 3; ++tx) {
-        const int ny0 = y0 + ty - 1, nx0 = x0 + tx - 1, ny1 = y1 + ty - 1, nx1 = x1 + tx - 1;
-        const int r0 = (p0 < A && ny0 >= 0 && ny0 < H && nx0 >= 0 && nx0 < H) ? ny0 * H + nx0 : A;
-        const int r1 = (p1 < A && ny1 >= 0 && ny1 < H && nx1 >= 0 && nx1 < H) ? ny1 * H + nx1 : A;
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) {
-          const int ch8 = (wc * 64 + nt * 16) >> 3;
-          const s16x4_t lo = tr_read(xt, wg_off(r0, ch8, pp)), hi = tr_read(xt, wg_off(r1, ch8, pp));
+          const s16x4_t lo = tr_read(xt, xb0 + tx * RB + nt * 32), hi = tr_read(xt, xb1 + tx * RB + nt * 32);
           const V bf = __builtin_bit_cast(V, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
 #pragma unroll
           for (int mt = 0; mt < 2; ++mt) acc[tx][mt][nt] = M::run(af[mt], bf, acc[tx][mt][nt]);
@@ -371,7 +376,7 @@ __global__ void __launch_bounds__(512, 1) k_conv3_wgrad(const uint16_t *__restri
     }
     __syncthreads();  // every wave is done with this board's tiles before the next DMA
   }
-  // ---- partials: acc[tx][mt][nt][e] = dW[o = 32 wo + 16 mt + 4 g + e][c = 64 wc + 16 nt + (lane & 15)][3 ty + tx]
+  // ---- acc[tx][mt][nt][e] = dW[o = 32 wo + 16 mt + 4 g + e][c = 64 wc + 16 nt + (lane & 15)][3 ty + tx]
   float *pc = part + (size_t)chunk * 9 * CC * CC;
 #pragma unroll
   for (int tx = 0; tx < 3; ++tx)
@@ -442,9 +447,12 @@ int conv3_dispatch(int H, const void *x, const void *wpk, void *y, int N, const 
   return fail("gmz_conv3x3: board size must be 9 or 15");
 }
 
+// chunks of boards: a multiple of 8 (one per XCD in each group of 24 workgroups), at most one
+// workgroup per CU
 int wgrad_chunks(int N) {
-  int n = cu_count_conv() / 3;
-  return n < N ? n : N;
+  int n = cu_count_conv() / 24 * 8;
+  const int cap = (N + 7) / 8 * 8;
+  return n < cap ? n : cap;
 }
 
 template <int H, typename T>
@@ -512,7 +520,8 @@ GMZ_EXPORT int gmz_conv3x3_wgrad(int dtype, int H, const void *x, const void *dy
   hipStream_t st = (hipStream_t)stream;
   float *part = (float *)workspace;
   int rc;
-  if (dtype == 1) rc = H == 15 ? launch_wgrad<15, __half>(x, dy, N, part, st) : H == 9 ? launch_wgrad<9, __half>(x, dy, N, part, st) : -2;
+  if (dtype == 1)
+    rc = H == 15 ? launch_wgrad<15, __half>(x, dy, N, part, st) : H == 9 ? launch_wgrad<9, __half>(x, dy, N, part, st) : -2;
   else if (dtype == 2)
     rc = H == 15 ? launch_wgrad<15, __hip_bfloat16>(x, dy, N, part, st)
                  : H == 9 ? launch_wgrad<9, __hip_bfloat16>(x, dy, N, part, st) : -2;

@@ -358,7 +358,8 @@ def _conv3x3_hip(x, packed, mask=None, stats=None):
 
 
 # the 128->128 convs' weight gradient on gmz_conv3x3_wgrad instead of MIOpen: exact (f32 accumulation,
-# tested) but not yet faster (52 + 10 us vs MIOpen's 55 us per 360-board layer), so off by default
+# tested) but not yet faster (47 + 9 us vs MIOpen's 55 us per 360-board layer: the per-board LDS DMA is
+# not overlapped with the k-loop, which itself runs at ~40 % MFMA busy), so off by default
 HIP_WGRAD = False
 _WGRAD_WS = {}
 
