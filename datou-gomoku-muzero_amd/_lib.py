@@ -55,6 +55,7 @@ _SIGS = {
     "gmz_bn_workspace_bytes": ([I, I, I, I, ctypes.POINTER(ctypes.c_size_t)], I),
     "gmz_bn_forward": ([I, I, P, P, P, I, I, I, P, P, ctypes.c_float, ctypes.c_float, P, P, P, I, P, P, P, P], I),
     "gmz_bn_backward": ([I, I, P, P, P, P, I, I, I, P, P, I, P, P, P, P, P, P], I),
+    "gmz_bn_backward_acc": ([I, I, P, P, P, P, I, I, I, P, P, I, P, P, P, P, P, P, I], I),
     "gmz_bn_eval": ([I, I, P, P, I, I, I, P, P, P, P, ctypes.c_float, I, P, P, P], I),
     "gmz_conv3x3_pack": ([I, P, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, I, P, P], I),
     "gmz_conv3x3_forward": ([I, I, P, P, P, I, P], I),

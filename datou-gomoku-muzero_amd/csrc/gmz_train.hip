@@ -124,8 +124,13 @@ __global__ void __launch_bounds__(WAVE) k_bn_finalize(const double *__restrict__
       if (c == 0 && num_batches) num_batches[0] += 1;
     }
   } else {
-    dgamma[c] = (float)b;
-    dbeta[c] = (float)a;
+    if (backward == 2) {  // accumulate into the parameters' f32 gradients
+      dgamma[c] += (float)b;
+      dbeta[c] += (float)a;
+    } else {
+      dgamma[c] = (float)b;
+      dbeta[c] = (float)a;
+    }
     coef[c] = n > 0.0 ? (float)(a / n) : 0.0f;
     coef[C + c] = n > 0.0 ? (float)(b / n) : 0.0f;
   }
@@ -490,7 +495,7 @@ int bn_forward(int nhwc, const void *x, const void *res, const uint8_t *mask, in
 template <typename T>
 int bn_backward(int nhwc, const void *x, const void *y, const void *dy, const uint8_t *mask, int B, int C, int S,
                 const float *gamma, const float *save, int relu, void *dx, void *dres, float *dgamma, float *dbeta,
-                void *ws, hipStream_t st) {
+                void *ws, hipStream_t st, int accumulate) {
   const int ns = splits_for(B, C, S, nhwc);
   const int V = nhwc ? nhwc_vec(C, sizeof(T), {x, y, dy, dx, dres}) : 0;
   float *coef = (float *)((double *)ws + ws_doubles(B, C, S, nhwc));  // f32 [2][C] after the partials
@@ -507,7 +512,7 @@ int bn_backward(int nhwc, const void *x, const void *y, const void *dy, const ui
   }
   GMZ_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_bn_finalize, dim3(C), dim3(WAVE), 0, st, (const double *)ws, C, ns, nhwc ? 1 : ns,
-                     nhwc ? C : 1, 1, 0.f, 0.f, (float *)nullptr, (float *)nullptr, (float *)nullptr,
+                     nhwc ? C : 1, accumulate ? 2 : 1, 0.f, 0.f, (float *)nullptr, (float *)nullptr, (float *)nullptr,
                      (int64_t *)nullptr, dgamma, dbeta, coef);
   GMZ_LAUNCH_CHECK();
   if (nhwc) {
@@ -617,9 +622,10 @@ GMZ_EXPORT int gmz_bn_forward(int dtype, int layout, const void *x, const void *
   return fail("gmz_bn_forward: dtype must be 0 (f32), 1 (f16) or 2 (bf16)");
 }
 
-GMZ_EXPORT int gmz_bn_backward(int dtype, int layout, const void *x, const void *y, const void *dy,
-                               const uint8_t *mask, int B, int C, int S, const float *gamma, const float *save,
-                               int relu, void *dx, void *dres, float *dgamma, float *dbeta, void *ws, void *stream) {
+GMZ_EXPORT int gmz_bn_backward_acc(int dtype, int layout, const void *x, const void *y, const void *dy,
+                                   const uint8_t *mask, int B, int C, int S, const float *gamma, const float *save,
+                                   int relu, void *dx, void *dres, float *dgamma, float *dbeta, void *ws, void *stream,
+                                   int accumulate) {
   if (B <= 0 || C <= 0 || S <= 0 || (size_t)B * C * S >= (1ull << 31)) return fail("gmz_bn_backward: bad shape");
   if (check_layout(layout, C)) return -1;
   if (!x || !dy || !dx || !gamma || !save || !dgamma || !dbeta || !ws || (relu && !y))
@@ -627,13 +633,20 @@ GMZ_EXPORT int gmz_bn_backward(int dtype, int layout, const void *x, const void 
   hipStream_t st = (hipStream_t)stream;
   switch (dtype) {
     case 0: return bn_backward<float>(layout, x, y, dy, mask, B, C, S, gamma, save, relu, dx, dres, dgamma, dbeta, ws,
-                                      st);
+                                      st, accumulate);
     case 1: return bn_backward<__half>(layout, x, y, dy, mask, B, C, S, gamma, save, relu, dx, dres, dgamma, dbeta,
-                                       ws, st);
+                                       ws, st, accumulate);
     case 2: return bn_backward<__hip_bfloat16>(layout, x, y, dy, mask, B, C, S, gamma, save, relu, dx, dres, dgamma,
-                                               dbeta, ws, st);
+                                               dbeta, ws, st, accumulate);
   }
   return fail("gmz_bn_backward: dtype must be 0 (f32), 1 (f16) or 2 (bf16)");
+}
+
+GMZ_EXPORT int gmz_bn_backward(int dtype, int layout, const void *x, const void *y, const void *dy,
+                               const uint8_t *mask, int B, int C, int S, const float *gamma, const float *save,
+                               int relu, void *dx, void *dres, float *dgamma, float *dbeta, void *ws, void *stream) {
+  return gmz_bn_backward_acc(dtype, layout, x, y, dy, mask, B, C, S, gamma, save, relu, dx, dres, dgamma, dbeta, ws,
+                             stream, 0);
 }
 
 GMZ_EXPORT int gmz_bn_eval(int dtype, int layout, const void *x, const void *res, int B, int C, int S,

@@ -185,6 +185,7 @@ class _FusedMaskedBN(torch.autograd.Function):
                                         int(relu), _lib.ptr(y), _lib.ptr(save), _lib.ptr(ws), _lib.stream_ptr()))
         ctx.save_for_backward(x, y, mask, gamma, save)
         ctx.relu, ctx.has_res, ctx.layout = relu, res is not None, layout
+        ctx.beta = beta
         return y
 
     @staticmethod
@@ -198,13 +199,23 @@ class _FusedMaskedBN(torch.autograd.Function):
         S = x[0, 0].numel()
         dx = torch.empty_like(x)
         dres = torch.empty_like(x) if ctx.has_res else None
-        dgamma = torch.empty(C, dtype=torch.float32, device=x.device)
-        dbeta = torch.empty(C, dtype=torch.float32, device=x.device)
+        beta = ctx.beta
+        # the parameters' f32 .grad (the trainer's flat-bucket views) take the gradients in place:
+        # no gradient tensors, no AccumulateGrad adds (one per BatchNorm use and parameter)
+        acc = (gamma.grad is not None and beta.grad is not None and gamma.grad.dtype == torch.float32
+               and beta.grad.dtype == torch.float32 and gamma.grad.is_contiguous() and beta.grad.is_contiguous())
+        if acc:
+            dgamma, dbeta = gamma.grad, beta.grad
+        else:
+            dgamma = torch.empty(C, dtype=torch.float32, device=x.device)
+            dbeta = torch.empty(C, dtype=torch.float32, device=x.device)
         ws = _bn_workspace(layout, B, C, S, x.device)
-        _lib.check(L.gmz_bn_backward(_BN_DTYPES[x.dtype], layout, _lib.ptr(x), _lib.ptr(y), _lib.ptr(dy),
-                                     _lib.ptr(mask), B, C, S, _lib.ptr(gamma), _lib.ptr(save), int(ctx.relu),
-                                     _lib.ptr(dx), _lib.ptr(dres), _lib.ptr(dgamma), _lib.ptr(dbeta), _lib.ptr(ws),
-                                     _lib.stream_ptr()))
+        _lib.check(L.gmz_bn_backward_acc(_BN_DTYPES[x.dtype], layout, _lib.ptr(x), _lib.ptr(y), _lib.ptr(dy),
+                                         _lib.ptr(mask), B, C, S, _lib.ptr(gamma), _lib.ptr(save), int(ctx.relu),
+                                         _lib.ptr(dx), _lib.ptr(dres), _lib.ptr(dgamma), _lib.ptr(dbeta),
+                                         _lib.ptr(ws), _lib.stream_ptr(), int(acc)))
+        if acc:
+            return dx, None, None, dres, None, None, None, None, None, None, None, None
         return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None, None
 
 
@@ -420,7 +431,12 @@ class _Conv3x3NHWC(torch.autograd.Function):
             else:
                 wd = torch.empty(w.shape, dtype=x.dtype, device=w.device).contiguous(memory_format=torch.channels_last)
                 gw = torch.ops.aten.convolution_backward(gy, x, wd, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
-                                                         [False, True, False])[1].to(w.dtype)
+                                                         [False, True, False])[1]
+                if w.grad is not None and w.grad.dtype == torch.float32:
+                    w.grad.add_(gw)  # one mixed-dtype add into the f32 .grad instead of a cast + AccumulateGrad
+                    gw = None
+                else:
+                    gw = gw.to(w.dtype)
         return gx, gw, None, None
 
 

@@ -244,6 +244,12 @@ int gmz_bn_forward(int dtype, int layout, const void *x_dev, const void *res_dev
 int gmz_bn_backward(int dtype, int layout, const void *x_dev, const void *y_dev, const void *dy_dev, const uint8_t *mask_dev, int B,
                     int C, int S, const float *gamma_dev, const float *save_dev, int relu, void *dx_dev, void *dres_dev,
                     float *dgamma_dev, float *dbeta_dev, void *workspace_dev, void *stream);
+/* gmz_bn_backward with accumulate = 1: dgamma_dev/dbeta_dev += the gradients (the parameters' f32 .grad,
+ * no separate gradient tensors or adds); accumulate = 0 is gmz_bn_backward. */
+int gmz_bn_backward_acc(int dtype, int layout, const void *x_dev, const void *y_dev, const void *dy_dev,
+                        const uint8_t *mask_dev, int B, int C, int S, const float *gamma_dev, const float *save_dev,
+                        int relu, void *dx_dev, void *dres_dev, float *dgamma_dev, float *dbeta_dev,
+                        void *workspace_dev, void *stream, int accumulate);
 /* gmz_bn_forward with the statistics already reduced to partials (e.g. by gmz_conv3x3_forward_stats):
  * stats_dev f64 [ns][C][3] (sum, sum of squares, counted elements); channels-last (layout 1) only. */
 int gmz_bn_forward_stats(int dtype, const void *x_dev, const void *res_dev, int B, int C, int S, const float *gamma_dev,
