@@ -429,7 +429,7 @@ class _Conv3x3NHWC(torch.autograd.Function):
                     w.grad = torch.zeros_like(w)
                 _conv3x3_wgrad_hip(x, gy, w.grad)
             else:
-                wd = torch.empty(w.shape, dtype=x.dtype, device=w.device).contiguous(memory_format=torch.channels_last)
+                wd = torch.empty(w.shape, dtype=x.dtype, device=w.device, memory_format=torch.channels_last)  # shape only
                 gw = torch.ops.aten.convolution_backward(gy, x, wd, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
                                                          [False, True, False])[1]
                 if w.grad is not None and w.grad.dtype == torch.float32:
