@@ -416,32 +416,44 @@ struct Img3 {
 // 1 = A fragments from one k-step (L1-resident), 2 = no weight loads, 32 = no per-board I/O,
 // 128 = s_memtime phase stamps -> pv_feat, 256 = pin the last k-step, 512 = no epilogue,
 // 1024 = no per-layer barrier
-template <int H, bool DYN, int ABL = 0, int RD = 4, int NQ = 2, int PG = 4>
+template <int H, bool DYN, int ABL = 0, int RD = 4, int NQ = 2, int PG = 4, int NB = 1>
 __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
   using G = Geo<H>;
   using I = Img3<H>;
-  constexpr int A = G::A, NPT = G::NPT;
+  // NB boards per workgroup at once (small boards): their NB x NPT position tiles form one tile
+  // space, so each weight fragment a wave loads feeds NB times the MFMAs
+  constexpr int A = G::A, NPT = G::NPT, NPTB = NB * NPT;
   constexpr int NW = NQ * PG, NTHR = 64 * NW;       // waves: NQ channel groups x PG position groups
-  constexpr int NTW = 8 / NQ, PTW = (NPT + PG - 1) / PG;  // n-tiles / position tiles per wave
+  constexpr int NTW = 8 / NQ, PTW = (NPTB + PG - 1) / PG;  // n-tiles / position tiles per wave
   static_assert(8 % NQ == 0, "channel groups");
   constexpr int PS = I::PS, RS = I::RS, IMG = I::BYTES;
   constexpr int KSTEPS = 36;  // 9 taps x 4 k-steps of 32 input channels
   // two images when they fit (15x15: 2 x 78 KB); otherwise (19x19: 119 KB) ONE image, an extra
   // barrier per layer before the in-place epilogue, and the residual kept in a global scratch
   constexpr bool ONE = 2 * IMG + 2 * C * 4 + 9 * C * 4 > 163840;
-  constexpr int NIMG = ONE ? 1 : 2;
-  static_assert(NIMG * IMG + 2 * C * 4 + 9 * C * 4 <= 163840, "LDS budget");
-  __shared__ __attribute__((aligned(16))) uint8_t smem[NIMG * IMG + 2 * C * 4 + 9 * C * 4];
-  float *sbias = (float *)(smem + NIMG * IMG);  // [2][128] per-layer double buffer
+  constexpr int NIMG = ONE ? 1 : 2, BB = NIMG * IMG;  // BB: LDS bytes per board (its images)
+  static_assert(!ONE || NB == 1, "single-image boards run one board per workgroup");
+  static_assert(NB * BB + 2 * C * 4 + 9 * C * 4 <= 163840, "LDS budget");
+  __shared__ __attribute__((aligned(16))) uint8_t smem[NB * BB + 2 * C * 4 + 9 * C * 4];
+  float *sbias = (float *)(smem + NB * BB);  // [2][128] per-layer double buffer
   float *saction = sbias + 2 * C;             // DYN: [9][128]
-  uint8_t *img0 = smem;
 
   auto next_row = [&](int from) {
     while (from < t.rows && t.out_slot[from] < 0) from += gridDim.x;
     return from;
   };
-  int r = next_row(blockIdx.x);
-  if (r >= t.rows) return;
+  // the workgroup's current boards rr[0..NB): rows blockIdx.x, + gridDim.x, ...; a missing partner
+  // repeats the last row (identical values computed and stored twice)
+  int rr[NB];
+  auto take_rows = [&](int from) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const int nx = next_row(b == 0 ? from : rr[b - 1] + gridDim.x);
+      rr[b] = (b > 0 && nx >= t.rows) ? rr[b - 1] : nx;
+    }
+  };
+  take_rows(blockIdx.x);
+  if (rr[0] >= t.rows) return;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   // wave w -> (channel group nh, position group pg) = (w % NQ, w / NQ): the waves sharing a SIMD
   // (w, w+4, ...) get different position groups, so a short last group does not load one SIMD less
@@ -453,8 +465,9 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
   // ---- DYN input DMA: 1 KB pieces of each board row's interior run; lane l of piece j covers run
   //      bytes j*1024 + 16*l (chunk (o % PS)/16 of position o / PS); pad chunks and bytes past the
   //      run are masked off
-  auto issue_input = [&](int row) {
+  auto issue_input = [&](int row, int bsl) {
     const uint8_t *src = (const uint8_t *)(t.pool + (size_t)t.in_slot[row] * A * C);
+    uint8_t *img0 = smem + bsl * BB;
     for (int j = w; j < H * I::RUN_DMA; j += NW) {
       const int y = j / I::RUN_DMA, piece = j % I::RUN_DMA;
       const int o = piece * 1024 + lane * 16;
@@ -473,21 +486,23 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
   };
 
   // ---- zero both images (borders and pads), biases of layer 0, action term
-  for (int i = tid; i < NIMG * IMG / 16; i += NTHR) *(uint4 *)(smem + i * 16) = make_uint4(0, 0, 0, 0);
+  for (int i = tid; i < NB * BB / 16; i += NTHR) *(uint4 *)(smem + i * 16) = make_uint4(0, 0, 0, 0);
   if (tid < C) sbias[tid] = t.bias[tid];
   if (DYN)
     for (int i = tid; i < 9 * C; i += NTHR) saction[i] = t.action_term[i];
   __syncthreads();  // zeroing done before the DMA writes the interior
-  if constexpr (DYN && !(ABL & 32)) issue_input(r);
+  if constexpr (DYN && !(ABL & 32))
+#pragma unroll
+    for (int b = 0; b < NB; ++b) issue_input(rr[b], b);
 
   // per tile: LDS byte offset of the top-left neighbour of this lane's column position (+ its
   // k-chunk for B reads); -1 marks positions past the board
   int pos[PTW];
 #pragma unroll
   for (int i = 0; i < PTW; ++i) {
-    const int pt = pg + PG * i;
-    const int p = pt * 16 + sigma16(lane & 15);
-    pos[i] = (pt < NPT && p < A) ? (p / H) * RS + (p % H) * PS : -1;
+    const int pt = pg + PG * i, bsl = pt / NPT, lt = pt - bsl * NPT;
+    const int p = lt * 16 + sigma16(lane & 15);
+    pos[i] = (pt < NPTB && p < A) ? bsl * BB + (p / H) * RS + (p % H) * PS : -1;
   }
   f32x4 acc[NTW][PTW];
   // ONE: this lane's residual tile values, [NTW][PTW][64 lanes] x 4 bf16 per wave (same lane writes
@@ -529,10 +544,8 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
   uint64_t st_loop = 0, st_epi = 0, st_bar = 0, st_t0 = 0, st_t1 = 0, st_t2 = 0;  // ABL & 128 stamps
   const uint64_t st_start = (ABL & 128) ? __builtin_amdgcn_s_memtime() : 0;
 
-  while (r < t.rows) {
-    const int os = t.out_slot[r];
+  while (rr[0] < t.rows) {
     if constexpr (!DYN) {  // ---- REPR stem (one MFMA k-step on an im2col operand) -> img0
-      const float *ob = t.obs + (size_t)r * 3 * A;
       // opaque per-board copy of the lane id: keeps the compiler from hoisting the PTW x 8 im2col
       // offsets and masks out of the board loop (they would live across the whole tower and spill)
       int ln = lane;
@@ -544,8 +557,10 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
       for (int i = 0; i < PTW; ++i) {
 #pragma unroll
         for (int nt = 0; nt < NTW; ++nt) acc[nt][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (pg + PG * i >= NPT) continue;
-        const int p = (pg + PG * i) * 16 + sigma16(ln & 15);
+        if (pg + PG * i >= NPTB) continue;
+        const int pt = pg + PG * i, bsl = pt / NPT;
+        const float *ob = t.obs + (size_t)rr[bsl] * 3 * A;
+        const int p = (pt - bsl * NPT) * 16 + sigma16(ln & 15);
         const int y = p / H, x = p % H;
         bf16x8_t b;
 #pragma unroll
@@ -576,7 +591,7 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
             for (int e = 0; e < 4; ++e) o[h][e] = f2bf(fmaxf(acc[2 * u + h][i][e] + t.stem_b[n0 + e], 0.f));
             if constexpr (ONE) xs[((2 * u + h) * PTW + i) * 64] = o[h];
           }
-          store_pair(img0, u, i, o[0], o[1]);
+          store_pair(smem, u, i, o[0], o[1]);
         }
       }
     } else {
@@ -636,8 +651,8 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
           if ((ABL & 256) || st + 1 < KSTEPS) __builtin_amdgcn_sched_barrier(0);
         }
       };
-      if constexpr (PTW * PG == NPT) kloop(std::integral_constant<int, PTW>{});
-      else if (pg + PG * (PTW - 1) < NPT) kloop(std::integral_constant<int, PTW>{});
+      if constexpr (PTW * PG == NPTB) kloop(std::integral_constant<int, PTW>{});
+      else if (pg + PG * (PTW - 1) < NPTB) kloop(std::integral_constant<int, PTW>{});
       else kloop(std::integral_constant<int, PTW - 1>{});
       if (ABL & 128) { st_t1 = __builtin_amdgcn_s_memtime(); st_loop += st_t1 - st_t0; }
       // epilogue: (action term) (+ residual) + ReLU -> bf16 -> the other image.  One straight-line
@@ -660,11 +675,16 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
               xr[2 * u + 1][i] = __builtin_bit_cast(u16x4, make_uint2(v.z, v.w));
             }
         }
-        int ay = 0, ax = 0;
+        int ay[NB], ax[NB];
+#pragma unroll
+        for (int b = 0; b < NB; ++b) ay[b] = ax[b] = 0;
         if constexpr (DYN && KIND == 0) {
-          const int av = t.action[r];
-          ay = av / H;
-          ax = av % H;
+#pragma unroll
+          for (int b = 0; b < NB; ++b) {
+            const int av = t.action[rr[b]];
+            ay[b] = av / H;
+            ax[b] = av % H;
+          }
         }
         u16x4 olo[PTW];  // even n-tile's outputs, stored with the odd one's as one 16-B chunk
 #pragma unroll
@@ -678,8 +698,9 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
           for (int i = 0; i < PTW; ++i) {
             f32x4 v = acc[nt][i];
             if constexpr (DYN && KIND == 0) {
-              const int p = (pg + PG * i) * 16 + sigma16(lane & 15);
-              const int ddy = ay - p / H + 1, ddx = ax - p % H + 1;
+              const int pt = pg + PG * i, bsl = pt / NPT;
+              const int p = (pt - bsl * NPT) * 16 + sigma16(lane & 15);
+              const int ddy = ay[bsl] - p / H + 1, ddx = ax[bsl] - p % H + 1;
               if (ddy >= 0 && ddy <= 2 && ddx >= 0 && ddx <= 2) v += *(const f32x4 *)(saction + (ddy * 3 + ddx) * C + n0);
             }
             if constexpr (KIND == 2) {
@@ -688,7 +709,7 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
             }
             const u16x4 o = __builtin_bit_cast(u16x4, make_uint2(relu_bf16x2(v[0], v[1]), relu_bf16x2(v[2], v[3])));
             if (nt & 1) {
-              if ((PG * i + PG) * 16 <= A || pos[i] >= 0) store_pair(nimg, nt >> 1, i, olo[i], o);
+              if ((NB == 1 && (PG * i + PG) * 16 <= A) || pos[i] >= 0) store_pair(nimg, nt >> 1, i, olo[i], o);
             } else {
               olo[i] = o;
             }
@@ -713,12 +734,21 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
       if (ABL & 128) st_bar += __builtin_amdgcn_s_memtime() - st_t2;
     }
 
-    // ---- next board's input -> the free image, overlapped with this board's output stage
-    const int nr = next_row(r + gridDim.x);
+    // ---- next boards' input -> the free images, overlapped with these boards' output stage
+    int nrr[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) nrr[b] = rr[b];
+    take_rows(rr[NB - 1] + gridDim.x);
     if constexpr (DYN && !ONE && !(ABL & 32)) {
-      if (nr < t.rows) issue_input(nr);  // DYN has 1 + 2*blocks (odd) layers: the result is in img[1]
+      if (rr[0] < t.rows)  // DYN has 1 + 2*blocks (odd) layers: the result is in img[1]
+#pragma unroll
+        for (int b = 0; b < NB; ++b) issue_input(rr[b], b);
     }
-    const uint8_t *fin = smem + (ONE ? 0 : (t.n_layers & 1) * IMG);
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+    if (b > 0 && nrr[b] == nrr[b - 1]) break;  // a repeated row: already stored
+    const int r = nrr[b], os = t.out_slot[r];
+    const uint8_t *fin = smem + b * BB + (ONE ? 0 : (t.n_layers & 1) * IMG);
     if (!(ABL & 32)) {
       uint4 *dst = (uint4 *)(t.pool + (size_t)os * A * C);
       for (int i = tid; i < A * 16; i += NTHR) dst[i] = *(const uint4 *)(fin + cell(i >> 4) + (i & 15) * 16);
@@ -742,11 +772,11 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
         t.pv_feat[(size_t)r * pv_stride(A) + i] = fmaxf(sum, 0.f);
       }
     }
+    }
     __syncthreads();  // the next board's layer 0 overwrites img[1]
     if constexpr (DYN && ONE && !(ABL & 32)) {
-      if (nr < t.rows) issue_input(nr);  // single image: only now is it free
+      if (rr[0] < t.rows) issue_input(rr[0], 0);  // single image: only now is it free
     }
-    r = nr;
   }
   if ((ABL & 128) && lane == 0) {  // diagnostic build only: per-wave phase cycles -> pv_feat
     float *o = t.pv_feat + (blockIdx.x * NW + w) * 4;
@@ -950,9 +980,11 @@ static int cu_count() {
 // wave decomposition per board size.  Default: 12 waves = 4 channel quarters x 3 position groups
 // (15 tiles of 16 positions at 15x15: no idle tile, 3 waves per SIMD; RD 3 keeps it within 168
 // VGPRs).  19x19 (single LDS image, 23 tiles): 8 waves = 2 channel halves x 4 position groups.
-template <int H> struct TowerCfg { static constexpr int NQ = 4, PG = 3, RD = 3; };
-template <> struct TowerCfg<15> { static constexpr int NQ = 4, PG = 2, RD = 3; };  // 8 tiles | 7 tiles
-template <> struct TowerCfg<19> { static constexpr int NQ = 2, PG = 4, RD = 2; };
+// NB: boards per workgroup at once — small boards (6x6, 9x9: 3 and 6 position tiles) pair up so a
+// wave's weight fragments feed 2x the MFMAs
+template <int H> struct TowerCfg { static constexpr int NQ = 4, PG = 3, RD = 3, NB = 2; };
+template <> struct TowerCfg<15> { static constexpr int NQ = 4, PG = 2, RD = 3, NB = 1; };  // 8 tiles | 7 tiles
+template <> struct TowerCfg<19> { static constexpr int NQ = 2, PG = 4, RD = 2, NB = 1; };
 
 // bytes of k_tower3's per-workgroup residual scratch (single-image boards only)
 template <int H>
@@ -977,8 +1009,9 @@ static int launch_tower(const TowerArgs &a, hipStream_t s) {
   if (a.rows <= 0) return 0;
   using T = TowerCfg<H>;
   if (tower_xres_bytes<H>() && !a.xres) return fail("gmz_net: missing residual scratch");
-  const int grid = a.rows < cu_count() ? a.rows : cu_count();
-  hipLaunchKernelGGL((k_tower3<H, DYN, 0, T::RD, T::NQ, T::PG>), dim3(grid), dim3(64 * T::NQ * T::PG), 0, s, a);
+  const int need = (a.rows + T::NB - 1) / T::NB;
+  const int grid = need < cu_count() ? need : cu_count();
+  hipLaunchKernelGGL((k_tower3<H, DYN, 0, T::RD, T::NQ, T::PG, T::NB>), dim3(grid), dim3(64 * T::NQ * T::PG), 0, s, a);
   GMZ_LAUNCH_CHECK();
   return 0;
 }
