@@ -983,6 +983,8 @@ static int cu_count() {
 // NB: boards per workgroup at once — small boards (6x6, 9x9: 3 and 6 position tiles) pair up so a
 // wave's weight fragments feed 2x the MFMAs
 template <int H> struct TowerCfg { static constexpr int NQ = 4, PG = 3, RD = 3, NB = 2; };
+// 9x9, two boards: 8 waves x 6 tiles beat 12 x 4 (0.340 vs 0.365 ms per 1024 rows, measured)
+template <> struct TowerCfg<9> { static constexpr int NQ = 4, PG = 2, RD = 3, NB = 2; };
 template <> struct TowerCfg<15> { static constexpr int NQ = 4, PG = 2, RD = 3, NB = 1; };  // 8 tiles | 7 tiles
 template <> struct TowerCfg<19> { static constexpr int NQ = 2, PG = 4, RD = 2, NB = 1; };
 
