@@ -108,6 +108,37 @@ def test_hip_net_matches_reference_fixture(mods, golden):
     assert np.allclose(h2.sum(axis=(1, 2, 3)), d["h2_sum"], rtol=HID_REL)
 
 
+@pytest.mark.parametrize("size", [6, 9])
+def test_two_board_workgroups_are_batch_invariant(mods, size):
+    """Small boards run two rows per tower workgroup (gmz_net.hip TowerCfg NB = 2): an odd row count
+    (the last row has no partner), a skipped partner (slot -1) and every pairing must give each row
+    bit-for-bit the output it gets alone."""
+    N, W, GmzConfig = mods
+    cfg = GmzConfig(BOARD_SIZE=size, NUM_RES_BLOCKS=2)
+    sd = W.synthetic_state_dict(cfg, seed=7 + size, with_projection=False)
+    n = 7
+    obs = _positions(size, n, np.random.RandomState(size + 1))
+    acts = np.random.RandomState(size + 2).randint(0, size * size, n)
+    net = N.GomokuNetHip(sd, cfg, num_slots=4 * n, max_rows=n)
+    slots = np.arange(n)
+    slots[3] = -1  # rows 2 and 3 share a workgroup; row 3 is skipped
+    lg, v, _ = net.initial_inference(obs, slots=slots)
+    lg2, v2, r2 = net.recurrent_inference(np.where(slots < 0, 0, slots), acts, np.where(slots < 0, -1, slots + n))
+    torch.cuda.synchronize()
+    batch = [t.cpu().numpy().copy() for t in (lg, v, lg2, v2, r2)]
+    hb = net.hidden(np.arange(n, 2 * n)).cpu().numpy()
+    for i in range(n):
+        if slots[i] < 0:
+            continue
+        o = 2 * n + i
+        a, b, _ = net.initial_inference(obs[i:i + 1], slots=[o])
+        c, d, e = net.recurrent_inference([o], acts[i:i + 1], [3 * n + i])
+        torch.cuda.synchronize()
+        for got, want in zip((a, b, c, d, e), batch):
+            assert np.array_equal(got.cpu().numpy()[0], want[i]), i
+        assert np.array_equal(net.hidden([3 * n + i]).cpu().numpy()[0], hb[i])
+
+
 def test_skipped_rows_untouched(mods):
     N, W, GmzConfig = mods
     cfg = GmzConfig(BOARD_SIZE=9, NUM_RES_BLOCKS=1)
