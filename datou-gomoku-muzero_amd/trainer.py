@@ -369,9 +369,10 @@ def _conv3x3_hip(x, packed, mask=None, stats=None):
 
 
 # the 128->128 convs' weight gradient on gmz_conv3x3_wgrad instead of MIOpen: exact (f32 accumulation,
-# tested) but not yet faster (47 + 9 us vs MIOpen's 55 us per 360-board layer: the per-board LDS DMA is
-# not overlapped with the k-loop, which itself runs at ~40 % MFMA busy), so off by default
-HIP_WGRAD = False
+# tested), 47 + 9 us vs MIOpen's 55 us + the add into the f32 .grad per 360-board layer; the whole step
+# 26.4-26.5 -> 26.8-27.0 steps/s (same-box A/B, tools/bench_trainer.py --hip-wgrad).  The kernel's
+# per-board LDS DMA is not yet overlapped with its k-loop (~40 % MFMA busy)
+HIP_WGRAD = True
 _WGRAD_WS = {}
 
 
