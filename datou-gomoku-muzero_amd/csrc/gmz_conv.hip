@@ -3,8 +3,9 @@
 //
 // Forward y = conv(x, W) and the input gradient dx = conv(dy, W') (W'[c][o][t] = W[o][c][8 - t]:
 // channels swapped, taps flipped) are the same kernel on differently packed weights; the weight
-// gradient stays MIOpen's.  Replaces, for these layers, MIOpen's NHWC kernels plus the zeroing pass
-// it runs before each of them (trainer.py, training step of loss.py:30-158).
+// gradient is k_conv3_wgrad + k_conv3_wgrad_reduce (below).  Replaces, for these layers, MIOpen's NHWC
+// kernels plus the zeroing pass it runs before each of them (trainer.py, training step of
+// loss.py:30-158).
 //
 // Work item = (board, half of the output channels): 2N items for N boards, so the 256 CUs see ~3
 // rounds at N = 360 instead of 1.4.  Two 256-thread workgroups per CU (one padded image each,
