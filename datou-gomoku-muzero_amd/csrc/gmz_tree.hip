@@ -51,6 +51,7 @@ struct Dev {
   Edge *edges;
   float *logits;
   int32_t *node_parent, *node_action, *path_u, *path_a, *sel;
+  int32_t *node_last;  // [G][S] action last selected at the node: prefetch hint only (select_game)
   GameState *gs;
   uint64_t *legal;  // [G][NJ]
   int16_t *set_rank;
@@ -240,19 +241,63 @@ __device__ __forceinline__ void load_legal(const Dev &D, int g, uint64_t (&lg)[N
   for (int j = 0; j < NJ; ++j) lg[j] = D.legal[(size_t)g * gmz::NJ + j];
 }
 
-// _select_action at a non-root node (mcts.py:106-117).  Returns the action; *child = its child id
-// (taken from the already-loaded edge row: no second dependent memory round trip per level).
+// one non-root node's edge row, logits and selection hint in registers (index clamped, unconditional
+// loads: one memory round trip)
+template <int NJ>
+struct RowRegs {
+  int4 e[NJ];
+  float lv[NJ];
+  int last;
+};
+template <int NJ>
+__device__ __forceinline__ void row_fetch(const Dev &D, int g, int u, int lane, RowRegs<NJ> &r) {
+  const Edge *row = edge_row(D, g, u);
+  const float *lr = D.logits + ((size_t)g * D.S + u) * D.A;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int a = lane + WAVE * j, ac = a < D.A ? a : D.A - 1;
+    r.e[j] = *(const int4 *)(row + ac);
+    r.lv[j] = lr[ac];
+  }
+  r.last = D.node_last[(size_t)g * D.S + u];
+}
+
+// _select_action at a non-root node (mcts.py:106-117) on the fetched row `cur`.  Returns the action;
+// *child = its child id (from the row: no second dependent round trip per level).  The descent is one
+// dependent row fetch per level, so while this level's selection computes, the row of the child of the
+// hinted action (node_last: the predicted choice of this node's next visit, set at its last visit) is
+// fetched into `nxt` (*nxt_u = that child, -1 if none): the caller uses it when the prediction holds
+// and fetches afresh otherwise.  Results never depend on the hint.
 template <int NJ>
 __device__ int select_nonroot(const Dev &D, const uint64_t (&lg)[NJ], int g, int u, int lane, float mm_max,
-                              float mm_min, int *child) {
+                              float mm_min, int *child, const RowRegs<NJ> &cur, RowRegs<NJ> &nxt, int *nxt_u) {
   int n[NJ], ch[NJ];
   float q[NJ];
   double p[NJ];
-  float lv[NJ];
-  logits_load<NJ>(D, D.logits + ((size_t)g * D.S + u) * D.A, lane, lv);  // in flight with the edge row
-  row_load<NJ>(D, edge_row(D, g, u), lane, n, q, ch);
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {  // get_qsa (mcts.py:35-38), as row_load
+    const bool ok = lane + WAVE * j < D.A;
+    const int4 e = cur.e[j];
+    n[j] = ok ? e.y : 0;
+    ch[j] = ok ? e.x : -1;
+    q[j] = 0.f;
+    if (ok && n[j] > 0) {
+      const float v = __int_as_float(e.z) / (float)n[j];
+      const float dv = D.disc_f * v;
+      q[j] = __int_as_float(e.w) + dv;
+    }
+  }
+  *nxt_u = -1;
+  const int al = __builtin_amdgcn_readfirstlane(cur.last);
+  if (al >= 0 && al < D.A) {
+    const int cp = bcast_slot<NJ>(ch, al);
+    if (cp > 0 && cp < D.S) {
+      row_fetch<NJ>(D, g, cp, lane, nxt);
+      *nxt_u = cp;
+    }
+  }
   int max_n;
-  improved_policy<NJ>(D, lg, lane, lv, n, q, mm_max, mm_min, p, max_n);
+  improved_policy<NJ>(D, lg, lane, cur.lv, n, q, mm_max, mm_min, p, max_n);
   int tot = 0;
 #pragma unroll
   for (int j = 0; j < NJ; ++j) tot += n[j];
@@ -275,6 +320,25 @@ __device__ int select_nonroot(const Dev &D, const uint64_t (&lg)[NJ], int g, int
     if (m) a = WAVE * j + __builtin_ctzll(m);
   }
   *child = bcast_slot<NJ>(ch, a);
+  // hint for the next visit: the argmax once this visit is counted (N_a + 1, sum N + 1), the same
+  // policy otherwise — the deterministic selection spreads visits, so it often moves on from a
+  double best2 = -INFINITY;
+  const double inv_tot2 = 1.0 / (double)(2 + tot);
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int aj = lane + WAVE * j;
+    sc[j] = -INFINITY;
+    if (aj < D.A && ((lg[j] >> lane) & 1ull)) sc[j] = p[j] - (double)(n[j] + (aj == a)) * inv_tot2;
+    best2 = fmax(best2, sc[j]);
+  }
+  best2 = dred_max_d(best2);
+  int a2 = a;
+#pragma unroll
+  for (int j = NJ - 1; j >= 0; --j) {
+    const uint64_t m = __ballot(sc[j] == best2 && best2 != -INFINITY);
+    if (m) a2 = WAVE * j + __builtin_ctzll(m);
+  }
+  if (lane == 0) D.node_last[(size_t)g * D.S + u] = a2;
   return a;
 }
 
@@ -407,6 +471,7 @@ __global__ void __launch_bounds__(256) k_begin_move(Dev D, const double *__restr
     D.gs[g] = st;
     D.node_parent[(size_t)g * D.S] = -1;
     D.node_action[(size_t)g * D.S] = -1;
+    D.node_last[(size_t)g * D.S] = -1;
   }
 }
 
@@ -517,9 +582,17 @@ __device__ __forceinline__ void select_game(const Dev &D, int g, int lane, int32
   int32_t *pu = D.path_u + (size_t)g * S, *pa = D.path_a + (size_t)g * S;
   uint64_t lg[NJ];
   load_legal<NJ>(D, g, lg);
+  RowRegs<NJ> cur, nxt;
+  int nxt_u = -1;
   for (;;) {
     int c;
-    a = (u == 0) ? select_root(D, g, lane, st.n_sel, &c) : select_nonroot<NJ>(D, lg, g, u, lane, st.mm_max, st.mm_min, &c);
+    if (u == 0) {
+      a = select_root(D, g, lane, st.n_sel, &c);
+    } else {
+      if (u == nxt_u) cur = nxt;  // the hinted row is this node's
+      else row_fetch<NJ>(D, g, u, lane, cur);
+      a = select_nonroot<NJ>(D, lg, g, u, lane, st.mm_max, st.mm_min, &c, cur, nxt, &nxt_u);
+    }
     if (lane == 0) {
       pu[d] = u;
       pa[d] = a;
@@ -581,6 +654,7 @@ __device__ __forceinline__ void expand_backup_game(const Dev &D, int g, int lane
   if (lane == 0) {
     D.node_parent[(size_t)g * S + leaf] = pu[d - 1];
     D.node_action[(size_t)g * S + leaf] = pa[d - 1];
+    D.node_last[(size_t)g * S + leaf] = -1;
   }
   const float r_leaf = reward_in ? reward_in[g] : 0.f;
   // _backpropagate (mcts.py:119-138), k duplicate leaves (mcts.py:326-345): the value chain is the
@@ -849,6 +923,7 @@ GMZ_EXPORT int gmz_engine_create(const gmz_engine_cfg *cfg, gmz_engine **out) {
   rc |= dalloc(e, &D.logits, G * S * A);
   rc |= dalloc(e, &D.node_parent, G * S);
   rc |= dalloc(e, &D.node_action, G * S);
+  rc |= dalloc(e, &D.node_last, G * S);
   rc |= dalloc(e, &D.path_u, G * S);
   rc |= dalloc(e, &D.path_a, G * S);
   rc |= dalloc(e, &D.sel, G * MAX_TOP);
