@@ -15,7 +15,8 @@
 //   Edge edges[G][S][A]   {child, N, W, R} 16 B per (node, action): one dwordx4 per lane per
 //                         action, coalesced across the wave when a node's children are scanned
 //   float logits[G][S][A] node policy logits (network output)
-//   int path_u/path_a[G][S], node_parent/node_action[G][S], per-game scalars GameState[G]
+//   int path_u/path_a[G][S], node_parent/node_action[G][S], node_last[G][S] (descent prefetch hint),
+//   per-game scalars GameState[G]
 // S = num_simulations + 2 node slots per game (root + <= 1 new node per wave + 1 scratch slot).
 //
 // Numerics: float32 statistics with -ffp-contract=off and IEEE division reproduce the reference's
