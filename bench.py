@@ -1,4 +1,5 @@
-"""Self-play throughput benchmark (BASELINE.json metric: self-play moves/sec, 15x15, 400 sims).
+"""Self-play throughput benchmark (BASELINE.json metric: self-play moves/sec, 15x15, 400 sims;
+trainer steps/sec).
 
 One *step* = one move of every game on this GPU: the full Gumbel-MuZero search (1 initial +
 ~100 waves of select -> GomokuNetEZ recurrent inference -> expand/backup, mcts.py:288-362) and the
@@ -6,18 +7,34 @@ move itself (do_move + get_game_ended, workers.py:178-181), G games at once (con
 Finished games restart immediately.  Data: synthetic — empty boards, random-init GomokuNetEZ
 (8 blocks x 128 channels, numpy-seeded), Gumbel noise from the device RNG.
 
-  python bench.py [--gpus N --steps K --warmup W]              (N > 1: launched by torch.distributed.run)
+  python bench.py [--gpus N --steps K --warmup W]
+
+N > 1: one process per GPU.  Under torch.distributed.run (WORLD_SIZE set) the ranks are the
+launcher's; with WORLD_SIZE unset, ``--gpus N`` starts the N rank processes itself (before anything
+touches the GPU) with RANK/LOCAL_RANK/WORLD_SIZE/MASTER_ADDR=127.0.0.1 set.  Games shard by rank
+with no data-path collective (main.py:100-101: independent workers), rank 0's weights are broadcast
+once (RCCL), timing is the max over ranks.  GMZ_DIST_BACKEND=gloo rehearses the N > 1 path with
+several ranks sharing one GPU.
 
 Prints ONE JSON line on rank 0 (schema: the driver contract) including
-  roofline     : the dominant kernel (dynamics tower k_tower3<15,true>) timed with HIP events on its
-                 launch stream inside the timed region; achieved = algorithmic FLOP per launch /
-                 mean launch duration vs the 2.5 PFLOP/s dense bf16 MFMA peak;
-  cpu_baseline : the C oracle's search (oracle/gmz_oracle.c) with the float32 numpy network
-                 (oracle/netref.py) on the same weights, rank 0 / N=1 only, bounded sample.
+  roofline      : the dominant kernel (dynamics tower k_tower3<15,DYN>) timed with HIP events on its
+                  launch stream inside the timed region; achieved = algorithmic FLOP of the rows the
+                  searches actually requested / mean launch duration vs the 2.5 PFLOP/s dense f16/bf16
+                  MFMA peak;
+  roofline_tree : the fused expand/backup + select kernel (k_expand_select), same timing; achieved =
+                  algorithmic bytes counted from the per-game work counters (gmz_engine_tree_counters,
+                  byte model in DESIGN.md §5) / mean launch duration vs 8 TB/s HBM;
+  trainer       : config C4's trainer (B = 360 per GPU, 5 unroll steps, PER, fp16 autocast, HIP convs),
+                  steps/s after the self-play region, on every rank (DDP: one RCCL gradient all-reduce +
+                  the sharded-PER syncs per step), plus the MFMA fraction of its dominant HIP conv;
+  cpu_baseline  : the C oracle's search (oracle/gmz_oracle.c) with the float32 numpy network
+                  (oracle/netref.py) on the same weights, rank 0 / N=1 only, bounded sample.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -26,7 +43,6 @@ sys.path.insert(0, REPO)
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
-
 
 
 def repr_flop_per_row(size, blocks):
@@ -42,7 +58,19 @@ def tower_flop_per_row(size, blocks):
     15x15, 8 blocks: 1,136,505,600."""
     A = size * size
     return 2 * A * 128 * 144 * 9 + 2 * blocks * 2 * A * 128 * 128 * 9 + 2 * A * 128 * 3
-PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, no sparsity)
+
+
+def tree_bytes(ctr, A):
+    """Algorithmic HBM bytes of the fused expand/backup + select launches (SURVEY §8d model):
+      expand, per game-wave : read the leaf's logits (4A) + store them (4A) + its empty child row (16A)
+      backup, per game-wave : 24 B per level (parent index, R, N r+w, W r+w) + 16 B (min/max, value, k)
+      select, per level     : 20A B per non-root level (child N, W, R, child index, logits) + 8 B (path)
+    ``ctr``: engine.tree_counters().  (The root level's <= 16 selected edges are not counted.)"""
+    return (ctr["backups"] * (24 * A + 16) + 24 * ctr["backup_levels"]
+            + 20 * A * (ctr["select_levels"] - ctr["selects"]) + 8 * ctr["select_levels"])
+
+
+PEAK_MFMA_TFLOPS = 2500.0   # MI355X dense f16 / bf16 MFMA (MI355X_MICROARCH.md, no sparsity)
 PEAK_HBM_GBS = 8000.0
 
 
@@ -50,7 +78,7 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -61,11 +89,54 @@ def parse():
     ap.add_argument("--blocks", type=int, default=8)
     ap.add_argument("--mode", default="MuZero")
     ap.add_argument("--net", default="hip", choices=["hip", "hash"])
+    ap.add_argument("--precision", default="fp16", choices=["fp16", "bf16"],
+                    help="MFMA operand type of the network towers (f32 accumulation either way)")
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--cpu-baseline-sec", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--trainer-steps", type=int, default=20, help="timed trainer steps (0: no trainer leg)")
+    ap.add_argument("--trainer-warmup", type=int, default=6)
+    ap.add_argument("--trainer-batch", type=int, default=360)
+    ap.add_argument("--trainer-buffer", type=int, default=4096, help="synthetic slices per rank's PER shard")
     ap.add_argument("--pmc-file", default=os.path.join(REPO, "profiles", "pmc_tower_latest.json"))
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n, argv, script=None):
+    """Start ``n`` rank processes of ``script`` (default: this file) with the torch.distributed env
+    contract (RANK, LOCAL_RANK, WORLD_SIZE, LOCAL_WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT) and
+    wait for them.  Called before anything initialises the GPU.  If one rank fails, the others are
+    terminated (their exact PIDs).  Returns the first non-zero exit code, else 0."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", script or os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:
+                    q.terminate()
+        time.sleep(0.2)
+    for p in procs:
+        p.wait()
+    return rc
 
 
 def collective_max(x, dist, backend="nccl"):
@@ -78,20 +149,30 @@ def collective_max(x, dist, backend="nccl"):
     return float(t.item())
 
 
-def result_line(args, world, dt, waves, G):
-    """The JSON object rank 0 prints (without roofline / cpu_baseline)."""
+def collective_sum(x, dist, backend="nccl"):
+    if dist is None:
+        return x
+    dev = "cuda" if backend == "nccl" else "cpu"
+    t = torch.tensor([x], device=dev, dtype=torch.float64)
+    dist.all_reduce(t)
+    return float(t.item())
+
+
+def result_line(args, world, dt, waves, G, backend=None):
+    """The JSON object rank 0 prints (without roofline / cpu_baseline / trainer)."""
     total_moves = G * args.steps * world
     return {
         "metric": "self-play moves/sec (15x15, 400 sims)" if (args.size, args.sims) == (15, 400)
         else "self-play moves/sec (%dx%d, %d sims)" % (args.size, args.size, args.sims),
         "value": total_moves / dt, "unit": "moves/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+        "scaling": "weak", "vs_baseline": None, "dtype": getattr(args, "precision", "fp16"), "data": "synthetic",
         "config": {"workload": "%dx%d Gumbel %s, %d sims/move, %d concurrent games per GPU, GomokuNetEZ %d blocks x "
                                "128 ch (numpy-seeded random init), empty-board starts, device Gumbel RNG"
                                % (args.size, args.size, args.mode, args.sims, G, args.blocks),
                    "games_per_gpu": G, "global_games": G * world, "board_size": args.size,
                    "num_simulations": args.sims, "mcts": args.mode, "waves_per_move": waves / max(1, args.steps),
+                   "ranks": world, "dist_backend": backend,
                    "parallelism": "dp%d (independent games per GPU, no collective)" % world},
     }
 
@@ -138,23 +219,120 @@ def cpu_baseline(args, sd, cfg):
         if dt >= args.cpu_baseline_sec or moves >= 64:
             break
     return {"value": moves / dt, "unit": "moves/s", "cores": int(cores), "kind": "port",
-            "sample": "%d move(s) of one 15x15 game from the empty board, %d sims, %d NN rows (the reference's "
+            "sample": "%d move(s) of one %dx%d game from the empty board, %d sims (%s), %d NN rows (the reference's "
                       "duplicate-leaf batches kept), %.1f s; C oracle search + numpy fp32 GomokuNetEZ"
-                      % (moves, args.sims, rows, dt)}
+                      % (moves, H, H, args.sims, args.mode, rows, dt)}
+
+
+def synthetic_slices(n, size, unroll, rs):
+    """n TrainingSlice-shaped arrays (replay_buffer.py payload) of random content: sparse 0/1 planes,
+    actions with a random game end (-1 after it), rewards in {-1,0,1}, normalised random policies,
+    values in [-1, 1]."""
+    A = size * size
+    obs = (rs.rand(n, unroll + 1, 3, size, size) < 0.2).astype(np.uint8)
+    act = rs.randint(0, A, (n, unroll)).astype(np.int32)
+    ends = rs.randint(1, unroll + 1, n)
+    act[np.arange(unroll)[None, :] >= ends[:, None]] = -1
+    rew = rs.choice(np.array([-1.0, 0.0, 1.0], np.float32), (n, unroll))
+    pol = rs.exponential(1.0, (n, unroll + 1, A)).astype(np.float32)
+    pol /= pol.sum(-1, keepdims=True)
+    val = rs.uniform(-1, 1, (n, unroll + 1)).astype(np.float32)
+    return obs, act, rew, pol, val
+
+
+def trainer_leg(args, world, rank, dist, backend):
+    """Config C4's training step on every rank (DDP when world > 1), timed like the self-play region."""
+    from datou_gomoku_muzero_amd import trainer as T
+    torch.backends.cudnn.benchmark = True  # MIOpen Find for the convolutions left on MIOpen
+    cfg = T.TrainConfig(BOARD_SIZE=args.size, NUM_RES_BLOCKS=args.blocks, PHYSICAL_BATCH_SIZE=args.trainer_batch,
+                        TRAIN_BUFFER_SIZE=args.trainer_buffer, ENABLE_PER=True)
+    tr = T.Trainer(cfg, device="cuda")
+    rb = T.ReplayBuffer(cfg, device="cuda")
+    rs = np.random.RandomState(args.seed + 31 * rank)
+    rb.add_arrays(*synthetic_slices(args.trainer_buffer, args.size, cfg.NUM_UNROLL_STEPS, rs))
+    group = dist if dist is not None else None
+    pending = [None]
+
+    def step():
+        batch, idx, w = rb.sample(args.trainer_batch, rs, dist=group)
+        logs, td = tr.step(batch, w, sync=False)
+        rb.update_priorities(idx, td, dist=group)
+        prev, pending[0] = pending[0], logs
+        return prev
+
+    t_w = time.perf_counter()
+    for _ in range(args.trainer_warmup):
+        step()
+    torch.cuda.synchronize()
+    log("rank %d: trainer warm-up %.1f s (MIOpen Find, graph capture)" % (rank, time.perf_counter() - t_w))
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.trainer_steps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    dt = collective_max(time.perf_counter() - t0, dist, backend)
+    loss = float(pending[0][0]) if pending[0] is not None else None
+    # the dominant HIP kernel of the step: the 128->128 residual-block conv (forward and input gradient),
+    # timed standalone at the step's shape (B boards, f16 NHWC) with HIP events
+    B, H = args.trainer_batch, args.size
+    x = torch.randn(B, 128, H, H, device="cuda").half().contiguous(memory_format=torch.channels_last)
+    wt = (torch.randn(128, 128, 3, 3, device="cuda") / 34).contiguous(memory_format=torch.channels_last)
+    pk = T._packed_conv_weight(wt, torch.float16, 0)
+    for _ in range(3):
+        T._conv3x3_hip(x, pk)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    n = 20
+    for _ in range(n):
+        T._conv3x3_hip(x, pk)
+    e.record()
+    torch.cuda.synchronize()
+    ms = s.elapsed_time(e) / n
+    flop = 2.0 * B * H * H * 128 * 128 * 9
+    ach = flop / (ms * 1e-3) / 1e12
+    return {"metric": "trainer steps/sec (C4: B=%d per GPU, %d unroll steps, %dx%d, %d blocks, PER)"
+                      % (B, cfg.NUM_UNROLL_STEPS, H, H, args.blocks),
+            "value": args.trainer_steps / dt, "unit": "steps/s", "n_gpus": world, "steps": args.trainer_steps,
+            "warmup": args.trainer_warmup, "ms_per_step": dt / args.trainer_steps * 1e3,
+            "samples_per_s": args.trainer_steps * B * world / dt, "higher_is_better": True, "scaling": "weak",
+            "dtype": "fp16 autocast (f32 master weights; f32 target network, as the reference)",
+            "data": "synthetic slices in a device PER shard per rank (%d each)" % args.trainer_buffer,
+            "parallelism": "ddp%d: one flat-bucket gradient all-reduce + sharded-PER syncs per step" % world
+            if world > 1 else "single GPU",
+            "last_loss": loss,
+            "roofline": {"bound": "mfma", "kernel": "gmz_conv3x3 (128->128 3x3 conv, f16 NHWC, B=%d)" % B,
+                         "achieved": ach, "peak": PEAK_MFMA_TFLOPS, "unit": "TFLOP/s", "frac": ach / PEAK_MFMA_TFLOPS,
+                         "mean_launch_ms": ms, "timed": "standalone at the step's shape, %d launches" % n,
+                         "traffic": None}}
 
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # no external launcher: one process per GPU, started here before any GPU call
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+    world = int(env_world or "1")
+    if world != args.gpus:
+        log("bench.py: --gpus %d disagrees with WORLD_SIZE=%d" % (args.gpus, world))
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    backend = None
     if world > 1:
         import torch.distributed as dist
         # GMZ_DIST_BACKEND=gloo rehearses the N>1 path with several ranks sharing one GPU
         backend = os.environ.get("GMZ_DIST_BACKEND", "nccl")
         torch.cuda.set_device(local % torch.cuda.device_count())
         dist.init_process_group(backend, init_method="env://")
+        if rank == 0:
+            log("torch.distributed: world_size=%d backend=%s (%s)" % (dist.get_world_size(), dist.get_backend(),
+                                                                      "RCCL" if backend == "nccl" else backend))
     else:
         torch.cuda.set_device(0)
     import datou_gomoku_muzero_amd.engine as E
@@ -167,11 +345,11 @@ def main():
     sd = W.synthetic_state_dict(cfg, seed=args.seed, with_projection=False)
     if dist is not None:  # the self-play tier's one exchange: rank 0's weights -> all ranks (RCCL)
         from datou_gomoku_muzero_amd.weight_sync import broadcast_state_dict
-        dev = "cuda" if os.environ.get("GMZ_DIST_BACKEND", "nccl") == "nccl" else "cpu"
+        dev = "cuda" if backend == "nccl" else "cpu"
         sd = {k: v.cpu().numpy() for k, v in broadcast_state_dict(sd, src=0, device=dev).items()}
     slots = G * (cfg.NUM_SIMULATIONS + 2)
     if args.net == "hip":
-        net = N.GomokuNetHip(sd, cfg, num_slots=slots, max_rows=G)
+        net = N.GomokuNetHip(sd, cfg, num_slots=slots, max_rows=G, precision=args.precision)
     else:
         net = E.HashNetBackend(slots, cfg.ACTION_SPACE_SIZE)
     eng = E.BatchedSelfPlayEngine(cfg, num_games=G, net=net, seed=args.seed + 7919 * rank)
@@ -194,6 +372,8 @@ def main():
             net.repr_timer = timer
         else:
             net.tower_timer = timer
+    eng.tree_timer = N.KernelTimer()
+    eng.tree_counters(reset=True)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -208,26 +388,48 @@ def main():
     if dist:
         dist.barrier()
     dt = time.perf_counter() - t0
-    dt = collective_max(dt, dist, os.environ.get("GMZ_DIST_BACKEND", "nccl"))
-    out = result_line(args, world, dt, waves, G)
+    dt = collective_max(dt, dist, backend)
+    out = result_line(args, world, dt, waves, G, backend)
+    ctr = eng.tree_counters()
     if timer is not None:
-        n_launch, ms, rows = timer.summary()
+        n_launch, ms, _ = timer.summary()
+        # rows the searches requested (finished games' rows are skipped by the tower): every selected
+        # game-wave is one row; AlphaZero's representation tower also runs each move's G root rows
+        rows = (ctr["selects"] + (G * args.steps if az else 0)) / max(1, n_launch)
         fpr = (repr_flop_per_row if az else tower_flop_per_row)(args.size, args.blocks)
         flop = fpr * rows
         achieved = flop / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
         traffic = None
         if os.path.exists(args.pmc_file) and (args.size, args.blocks) == (15, 8) and not az:  # the PMC pass's config
             try:
-                traffic = json.load(open(args.pmc_file)).get("hbm_bytes_per_launch")
+                pm = json.load(open(args.pmc_file))
+                if pm.get("precision", "bf16") == args.precision:
+                    traffic = pm.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
         kname = ("k_tower3<%d,REPR> (representation tower, stem + %d fused convs + head 1x1 convs)" % (args.size, 2 * args.blocks)
                  if az else "k_tower3<%d,DYN> (dynamics tower, %d fused convs + head 1x1 convs)" % (args.size, 1 + 2 * args.blocks))
-        out["roofline"] = {"bound": "mfma", "kernel": kname,
-                           "achieved": achieved, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                           "frac": achieved / PEAK_BF16_TFLOPS, "traffic": traffic,
+        out["roofline"] = {"bound": "mfma", "kernel": kname + ", " + args.precision,
+                           "achieved": achieved, "peak": PEAK_MFMA_TFLOPS, "unit": "TFLOP/s",
+                           "frac": achieved / PEAK_MFMA_TFLOPS, "traffic": traffic,
                            "launches": n_launch, "mean_launch_ms": ms, "rows_per_launch": rows,
                            "flop_per_row": fpr}
+    n_tree, ms_tree, _ = eng.tree_timer.summary()
+    if n_tree:
+        A = args.size * args.size
+        bpl = tree_bytes(ctr, A) / n_tree
+        gbs = bpl / (ms_tree * 1e-3) / 1e9
+        out["roofline_tree"] = {
+            "bound": "hbm", "kernel": "k_expand_select<%d> (backup of wave i + selection of wave i+1)" % ((A + 63) // 64),
+            "achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS, "traffic": None,
+            "launches": n_tree, "mean_launch_ms": ms_tree, "bytes_per_launch": bpl,
+            "mean_backup_levels": ctr["backup_levels"] / max(1, ctr["backups"]),
+            "mean_select_levels": ctr["select_levels"] / max(1, ctr["selects"]),
+            "games_per_launch": ctr["backups"] / n_tree}
+    if args.trainer_steps > 0 and args.net == "hip":
+        del eng, net
+        torch.cuda.empty_cache()
+        out["trainer"] = trainer_leg(args, world, rank, dist, backend)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.net == "hip":
         log("cpu baseline (bounded sample ~%.0f s)..." % args.cpu_baseline_sec)
         out["cpu_baseline"] = cpu_baseline(args, sd, cfg)

@@ -20,7 +20,6 @@
 
 namespace gmz {
 
-typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
 
@@ -62,22 +61,55 @@ struct TowerArgs {
   uint16_t *xres;          // single-image boards (19x19): per-workgroup residual scratch (k_tower3)
 };
 
-__device__ __forceinline__ uint16_t f2bf(float f) {
-  __bf16 b = (__bf16)f;
-  return __builtin_bit_cast(uint16_t, b);
-}
-__device__ __forceinline__ float bf2f(uint16_t u) { return __uint_as_float(((uint32_t)u) << 16); }
-// ReLU(bf16(a)), ReLU(bf16(b)) packed: round first, then max(., 0) on the bf16 bit patterns as
-// signed 16-bit integers (negative bf16 <=> sign bit set; -0 -> +0): one v_pk_max_i16 for two
-// values, and round(relu(x)) == relu(round(x)) since rounding keeps the sign
+// MFMA operand element types of the towers and the reward GEMM (f32 accumulation either way).
+// Activations (LDS images, the HBM hidden-state pool) and packed weights are 16-bit patterns of E.
+//   F16  (default): v_mfma_f32_16x16x32_f16, 10-bit mantissa; stores saturate at +65504 (no inf)
+//   Bf16          : v_mfma_f32_16x16x32_bf16, 7-bit mantissa, f32 range
+// gfx950 runs both at the same dense rate.  relu2 packs ReLU(E(a)), ReLU(E(b)): round first, then
+// max(., 0) on the bit patterns as signed 16-bit integers (negative <=> sign bit set; -0 -> +0):
+// one v_cvt_pk + one v_pk_max_i16 for two values, and round(relu(x)) == relu(round(x)) since
+// rounding keeps the sign.
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ uint32_t relu_bf16x2(float a, float b) {
-  const bf16x2_t h = __builtin_convertvector((f32x2){a, b}, bf16x2_t);  // one v_cvt_pk_bf16_f32
-  const s16x2 v = __builtin_elementwise_max(__builtin_bit_cast(s16x2, h), (s16x2){0, 0});
-  return __builtin_bit_cast(uint32_t, v);
-}
+struct Bf16 {
+  static constexpr int id = GMZ_NET_BF16;
+  typedef __bf16 s;
+  typedef __bf16 v8 __attribute__((ext_vector_type(8)));
+  typedef __bf16 v2 __attribute__((ext_vector_type(2)));
+  static __device__ __forceinline__ f32x4 mfma(v8 a, v8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ float to_f(uint16_t u) { return __uint_as_float(((uint32_t)u) << 16); }
+  static __device__ __forceinline__ float lo(uint32_t w) { return __uint_as_float(w << 16); }
+  static __device__ __forceinline__ float hi(uint32_t w) { return __uint_as_float(w & 0xFFFF0000u); }
+  static __device__ __forceinline__ uint16_t relu1(float f) { return __builtin_bit_cast(uint16_t, (__bf16)fmaxf(f, 0.f)); }
+  static __device__ __forceinline__ uint32_t relu2(float a, float b) {
+    const v2 h = __builtin_convertvector((f32x2){a, b}, v2);  // one v_cvt_pk_bf16_f32
+    const s16x2 v = __builtin_elementwise_max(__builtin_bit_cast(s16x2, h), (s16x2){0, 0});
+    return __builtin_bit_cast(uint32_t, v);
+  }
+};
+struct F16 {
+  static constexpr int id = GMZ_NET_F16;
+  typedef _Float16 s;
+  typedef _Float16 v8 __attribute__((ext_vector_type(8)));
+  typedef _Float16 v2 __attribute__((ext_vector_type(2)));
+  static __device__ __forceinline__ f32x4 mfma(v8 a, v8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ float to_f(uint16_t u) { return (float)__builtin_bit_cast(_Float16, u); }
+  static __device__ __forceinline__ float lo(uint32_t w) { return to_f((uint16_t)(w & 0xFFFFu)); }
+  static __device__ __forceinline__ float hi(uint32_t w) { return to_f((uint16_t)(w >> 16)); }
+  static __device__ __forceinline__ uint16_t relu1(float f) {
+    return __builtin_bit_cast(uint16_t, (_Float16)fminf(fmaxf(f, 0.f), 65504.f));
+  }
+  static __device__ __forceinline__ uint32_t relu2(float a, float b) {
+    const v2 h = __builtin_convertvector((f32x2){a, b}, v2);  // one v_cvt_pk_f16_f32 (RNE)
+    s16x2 v = __builtin_elementwise_max(__builtin_bit_cast(s16x2, h), (s16x2){0, 0});
+    v = __builtin_elementwise_min(v, (s16x2){0x7BFF, 0x7BFF});  // +inf / overflow -> 65504
+    return __builtin_bit_cast(uint32_t, v);
+  }
+};
 
 // LDS image of the padded board: position q = (y+1)*HP + (x+1) owns 256 B = 16 chunks of 8 channels.
 // Chunk c of position q lives in 16-B slot (c + key(q)) & 15 with key(q) = (y*H + x) & 15 computed
@@ -87,301 +119,6 @@ __device__ __forceinline__ uint32_t relu_bf16x2(float a, float b) {
 // column permutation sigma(j) = j < 8 ? j ^ 4 : j, every ds_read_b128 lane group (4 x 16 lanes)
 // touches 16 distinct slots: conflict-free B-operand reads.
 __device__ __forceinline__ int sigma16(int j) { return j < 8 ? (j ^ 4) : j; }
-
-constexpr int TAP_BYTES = 32768;  // one tap of one conv: 4 k-steps x 8 n-tiles x 64 lanes x 16 B
-
-// ABL (ablation bits, 0 in the product; tools/tower_ablate.hip times variants): 1 = no weight
-// stream (LDS-DMA + vmcnt wait), 2 = no per-tap barrier, 4 = no MFMA, 8 = no B-fragment LDS reads,
-// 16 = no per-layer epilogue (bias/residual/ReLU/LDS store), 32 = no per-board I/O (input staging,
-// hidden-state store, head 1x1 convs), 64 = s_setprio(1) around each MFMA burst (experiment)
-template <int H, bool DYN, int ABL = 0>
-__global__ void __launch_bounds__(512) k_tower(TowerArgs t) {
-  using G = Geo<H>;
-  constexpr int A = G::A, HP = G::HP, AP = G::AP, NPT = G::NPT, PTW = G::PTW;
-  constexpr int ACT_BYTES = AP * C * 2;
-  constexpr int MAX_LAYERS = 17;
-  constexpr int BIAS_BYTES = (MAX_LAYERS + 9) * C * 4;  // per-layer bias + DYN action term, LDS-resident
-  // ONE shared arena (a second __shared__ object next to LDS-DMA targets can make hipcc drain vmcnt)
-  __shared__ __attribute__((aligned(16))) uint8_t smem[ACT_BYTES + 2 * TAP_BYTES + BIAS_BYTES];
-  uint8_t *act = smem;
-  uint8_t *wst = smem + ACT_BYTES;
-  float *sbias = (float *)(smem + ACT_BYTES + 2 * TAP_BYTES);
-  float *saction = sbias + MAX_LAYERS * C;
-
-  const int r = blockIdx.x;
-  const int os = t.out_slot[r];
-  if (os < 0) return;
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  const int nh = w >> 2, pg = w & 3;
-  const int g4 = lane >> 4;
-  const int cg = (g4 & 1) * 8 + (g4 >> 1);  // {0, 8, 1, 9}
-
-  auto chunk_addr = [&](int q, int key, int c) -> int { return q * 256 + (((c + key) & 15) << 4); };
-  auto key_of_q = [&](int q) -> int { return ((q / HP - 1) * H + (q % HP - 1)) & 15; };
-
-  // ---- border of the padded board = zero padding of every conv
-  for (int i = tid; i < (4 * HP - 4) * 16; i += 512) {
-    const int b = i >> 4, ch = i & 15;
-    int q;
-    if (b < HP) q = b;
-    else if (b < 2 * HP) q = (HP - 1) * HP + (b - HP);
-    else {
-      const int k = b - 2 * HP;
-      q = (1 + (k >> 1)) * HP + ((k & 1) ? HP - 1 : 0);
-    }
-    *(uint4 *)(act + q * 256 + ch * 16) = make_uint4(0, 0, 0, 0);
-  }
-  // ---- LDS-DMA weight stream: tap-stage s -> wst[s & 1]; wave w moves KB chunks w, w+8, w+16, w+24
-  const uint8_t *wsrc = (const uint8_t *)t.convs;
-  const int total_stages = t.n_layers * 9;
-  auto issue_stage = [&](int st) {
-    const uint8_t *src = wsrc + (size_t)st * TAP_BYTES + lane * 16;
-    uint8_t *dst = wst + (st & 1) * TAP_BYTES;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int kb = w + 8 * i;
-      __builtin_amdgcn_global_load_lds((const void *)(src + kb * 1024),
-                                       (__attribute__((address_space(3))) void *)(dst + kb * 1024), 16, 0, 0);
-    }
-  };
-  if (!(ABL & 1)) issue_stage(0);
-  for (int i = tid; i < t.n_layers * C; i += 512) sbias[i] = t.bias[i];
-  if (DYN)
-    for (int i = tid; i < 9 * C; i += 512) saction[i] = t.action_term[i];
-  // ---- DYN input: parent hidden state (network.py:89-93 input `state`)
-  if constexpr (DYN && !(ABL & 32)) {
-    const uint4 *src = (const uint4 *)(t.pool + (size_t)t.in_slot[r] * A * C);
-    for (int i = tid; i < A * 16; i += 512) {
-      const int p = i >> 4, ch = i & 15;
-      const int q = (p / H + 1) * HP + (p % H + 1);
-      *(uint4 *)(act + chunk_addr(q, p & 15, ch)) = src[i];
-    }
-  }
-  // ---- per-wave position tiles (column j of tile i = position pt*16 + sigma(j))
-  int qc[PTW];
-#pragma unroll
-  for (int i = 0; i < PTW; ++i) {
-    const int pt = pg + 4 * i;
-    const int p = pt * 16 + sigma16(lane & 15);
-    qc[i] = (pt < NPT && p < A) ? (p / H + 1) * HP + (p % H + 1) : -1;
-  }
-  f32x4 acc[4][PTW];
-  u16x4 xres[4][PTW];  // residual stream = the bf16 layer output already stored in the LDS image
-
-  auto epilogue_store = [&](int nt, int i, const u16x4 &o) {
-    const int q = qc[i];
-    const int p = (pg + 4 * i) * 16 + sigma16(lane & 15);
-    const int n0 = (nh * 4 + nt) * 16 + g4 * 4;
-    *(u16x4 *)(act + chunk_addr(q, p & 15, n0 >> 3) + (n0 & 4) * 2) = o;
-  };
-
-  // ---- REPR stem: conv3x3(3 -> 128) as one MFMA k-step on an im2col operand (k = tap*3 + c)
-  if constexpr (!DYN) {
-    const float *ob = t.obs + (size_t)r * 3 * A;
-    bf16x8_t a[4];
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) a[nt] = ((const bf16x8_t *)t.stem_w)[(nh * 4 + nt) * 64 + lane];
-#pragma unroll
-    for (int i = 0; i < PTW; ++i) {
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) acc[nt][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (pg + 4 * i >= NPT) continue;
-      const int p = (pg + 4 * i) * 16 + sigma16(lane & 15);
-      const int y = p / H, x = p % H;
-      bf16x8_t b;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int k = 8 * g4 + j;
-        float v = 0.f;
-        if (k < 27 && p < A) {
-          const int tap = k / 3, c = k % 3;
-          const int yy = y + tap / 3 - 1, xx = x + tap % 3 - 1;
-          if (yy >= 0 && yy < H && xx >= 0 && xx < H) v = ob[c * A + yy * H + xx];
-        }
-        b[j] = (__bf16)v;
-      }
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) acc[nt][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[nt], b, acc[nt][i], 0, 0, 0);
-    }
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      const int n0 = (nh * 4 + nt) * 16 + g4 * 4;
-#pragma unroll
-      for (int i = 0; i < PTW; ++i) {
-        if (qc[i] < 0) continue;
-        u16x4 o;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = f2bf(fmaxf(acc[nt][i][e] + t.stem_b[n0 + e], 0.f));
-        xres[nt][i] = o;
-        epilogue_store(nt, i, o);
-      }
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  // ---- the conv stream: one tap (4 k-steps of 32 channels) per stage, one barrier per stage
-  int s = 0;
-  for (int L = 0; L < t.n_layers; ++L) {
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-      for (int i = 0; i < PTW; ++i) acc[nt][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // B fragments of k-step 0 of the current tap; prefetched before the previous tap's barrier
-    // (they only depend on the layer's input image, not on the weights that barrier publishes)
-    bf16x8_t bpre[PTW];
-    auto tap_addr = [&](int tap, int (&base)[PTW], int (&rot)[PTW]) {
-      const int dy = tap / 3 - 1, dx = tap % 3 - 1;
-      const int offq = dy * HP + dx, offv = dy * H + dx;
-#pragma unroll
-      for (int i = 0; i < PTW; ++i) {
-        const bool ok = qc[i] >= 0;
-        const int p = (pg + 4 * i) * 16 + sigma16(lane & 15);
-        base[i] = ok ? (qc[i] + offq) * 256 : 0;
-        rot[i] = ok ? (p + offv + cg) : 0;
-      }
-    };
-    auto readB = [&](bf16x8_t (&dst)[PTW], const int (&base)[PTW], const int (&rot)[PTW], int ks) {
-#pragma unroll
-      for (int i = 0; i < PTW; ++i) {
-        if (ABL & 8) dst[i] = bf16x8_t{};
-        else dst[i] = *(const bf16x8_t *)(act + base[i] + (((rot[i] + 2 * ks) & 15) << 4));
-      }
-    };
-    {
-      int base0[PTW], rot0[PTW];
-      tap_addr(0, base0, rot0);
-      readB(bpre, base0, rot0, 0);
-    }
-    for (int tap = 0; tap < 9; ++tap, ++s) {
-      if (!(ABL & 1) && s + 1 < total_stages) issue_stage(s + 1);
-      int base[PTW], rot[PTW];
-      tap_addr(tap, base, rot);
-      const uint8_t *wb = wst + (s & 1) * TAP_BYTES + (nh * 4 * 64 + lane) * 16;
-      // every wave computes PTW tiles unconditionally (tiles past the board read the zero row and
-      // are never stored): branch-free code lets hipcc count lgkmcnt waits per k-step
-      bf16x8_t a[2][4], b[2][PTW];
-      auto readA = [&](int buf, int ks) {
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) a[buf][nt] = *(const bf16x8_t *)(wb + (ks * 8 + nt) * 1024);
-      };
-      readA(0, 0);
-#pragma unroll
-      for (int i = 0; i < PTW; ++i) b[0][i] = bpre[i];
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        // pin the schedule: next k-step's fragment reads are issued before this k-step's 16 MFMAs
-        // (hipcc otherwise recycles one fragment register and waits lgkmcnt(0) every 4 MFMAs)
-        if (ks < 3) {
-          readA((ks + 1) & 1, ks + 1);
-          readB(b[(ks + 1) & 1], base, rot, ks + 1);
-        } else if (tap < 8) {
-          int nbase[PTW], nrot[PTW];
-          tap_addr(tap + 1, nbase, nrot);
-          readB(bpre, nbase, nrot, 0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        if (ABL & 64) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int i = 0; i < PTW; ++i)
-#pragma unroll
-          for (int nt = 0; nt < 4; ++nt) {
-            if (ABL & 4) {
-              asm volatile("" ::"v"(a[ks & 1][nt]), "v"(b[ks & 1][i]));
-            } else {
-              acc[nt][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks & 1][nt], b[ks & 1][i], acc[nt][i], 0, 0, 0);
-            }
-          }
-        if (ABL & 64) __builtin_amdgcn_s_setprio(0);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      if (tap < 8) {
-        if (!(ABL & 1)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (!(ABL & 2)) __syncthreads();
-      }
-    }
-    if (ABL & 16) {  // keep the accumulators live (guide rule 17) so the MFMAs are not DCE'd
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-        for (int i = 0; i < PTW; ++i) asm volatile("" ::"v"(acc[nt][i]));
-      if (!(ABL & 1)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (!(ABL & 2)) __syncthreads();
-      continue;
-    }
-    // epilogue, part 1 (before the barrier, overlapping the partner wave's MFMA tail):
-    // bias (+ action term) (+ residual) + ReLU in registers, packed to bf16
-    const int kind = DYN ? (L == 0 ? 0 : ((L - 1) & 1) + 1) : ((L & 1) + 1);  // 0 stem, 1 conv1, 2 conv2
-    const float *bias = sbias + L * C;
-    int ay = 0, ax = 0;
-    if (DYN && kind == 0) {
-      const int av = t.action[r];
-      ay = av / H;
-      ax = av % H;
-    }
-    u16x4 outv[4][PTW];
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      const int n0 = (nh * 4 + nt) * 16 + g4 * 4;
-      const f32x4 bv = *(const f32x4 *)(bias + n0);
-#pragma unroll
-      for (int i = 0; i < PTW; ++i) {
-        const int p = (pg + 4 * i) * 16 + sigma16(lane & 15);
-        f32x4 v = acc[nt][i] + bv;
-        if (DYN && kind == 0) {
-          const int ddy = ay - p / H + 1, ddx = ax - p % H + 1;
-          if (ddy >= 0 && ddy <= 2 && ddx >= 0 && ddx <= 2) v += *(const f32x4 *)(saction + (ddy * 3 + ddx) * C + n0);
-        }
-        if (kind == 2) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] += bf2f(xres[nt][i][e]);
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) outv[nt][i][e] = f2bf(fmaxf(v[e], 0.f));
-        if (kind != 1) xres[nt][i] = outv[nt][i];
-      }
-    }
-    if (!(ABL & 1)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // every wave is done reading this layer's input
-    // epilogue, part 2: store the layer output into the LDS image
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-      for (int i = 0; i < PTW; ++i)
-        if (qc[i] >= 0) epilogue_store(nt, i, outv[nt][i]);
-    __syncthreads();
-  }
-
-  if (ABL & 32) return;
-  // ---- hidden state -> slot pool (NHWC bf16)
-  uint4 *dst = (uint4 *)(t.pool + (size_t)os * A * C);
-  for (int i = tid; i < A * 16; i += 512) {
-    const int p = i >> 4, ch = i & 15;
-    const int q = (p / H + 1) * HP + (p % H + 1);
-    dst[i] = *(const uint4 *)(act + chunk_addr(q, p & 15, ch));
-  }
-  // ---- prediction-head 1x1 convs + BN + ReLU (network.py:69,71), flattened NCHW (pv row layout)
-  for (int i = tid; i < pv_stride(A); i += 512) {
-    int o, p;
-    pv_split(i, A, o, p);
-    if (o == 3) { t.pv_feat[(size_t)r * pv_stride(A) + i] = 0.f; continue; }
-    const int q = (p / H + 1) * HP + (p % H + 1);
-    const float *hw = t.head_w + o * C;
-    float sum = t.head_b[o];
-#pragma unroll 4
-    for (int ch = 0; ch < 16; ++ch) {
-      const uint4 v = *(const uint4 *)(act + chunk_addr(q, p & 15, ch));
-      const uint32_t wds[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        sum += hw[ch * 8 + 2 * e] * __uint_as_float(wds[e] << 16);
-        sum += hw[ch * 8 + 2 * e + 1] * __uint_as_float(wds[e] & 0xFFFF0000u);
-      }
-    }
-    t.pv_feat[(size_t)r * pv_stride(A) + i] = fmaxf(sum, 0.f);
-  }
-  (void)key_of_q;
-}
 
 // ------------------------------------------------------------------------------------------------
 // k_tower3: the tower kernel the library launches.  Persistent (one 512-thread workgroup per CU,
@@ -416,10 +153,11 @@ struct Img3 {
 // 1 = A fragments from one k-step (L1-resident), 2 = no weight loads, 32 = no per-board I/O,
 // 128 = s_memtime phase stamps -> pv_feat, 256 = pin the last k-step, 512 = no epilogue,
 // 1024 = no per-layer barrier
-template <int H, bool DYN, int ABL = 0, int RD = 4, int NQ = 2, int PG = 4, int NB = 1>
+template <int H, bool DYN, int ABL = 0, int RD = 4, int NQ = 2, int PG = 4, int NB = 1, typename E = F16>
 __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
   using G = Geo<H>;
   using I = Img3<H>;
+  using V8 = typename E::v8;
   // NB boards per workgroup at once (small boards): their NB x NPT position tiles form one tile
   // space, so each weight fragment a wave loads feeds NB times the MFMAs
   constexpr int A = G::A, NPT = G::NPT, NPTB = NB * NPT;
@@ -505,7 +243,7 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
     pos[i] = (pt < NPTB && p < A) ? bsl * BB + (p / H) * RS + (p % H) * PS : -1;
   }
   f32x4 acc[NTW][PTW];
-  // ONE: this lane's residual tile values, [NTW][PTW][64 lanes] x 4 bf16 per wave (same lane writes
+  // ONE: this lane's residual tile values, [NTW][PTW][64 lanes] x 4 16-bit values per wave (same lane writes
   // and reads back: program order suffices)
   u16x4 *xs = ONE ? (u16x4 *)t.xres + ((size_t)blockIdx.x * NW + w) * NTW * PTW * 64 + lane : nullptr;
   static_assert(NTW % 2 == 0, "n-tiles pair up into 8-channel chunks");
@@ -528,14 +266,14 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
       __builtin_amdgcn_make_buffer_rsrc((void *)t.convs, (short)0, total_ks * 8192, 0x00020000);
   const int wvoff = (nh * NTW) * 1024 + lane * 16;
   static_assert(KSTEPS % RD == 0, "ring slots must repeat per layer");
-  bf16x8_t ar[RD][NTW];
+  V8 ar[RD][NTW];
   auto loadA = [&](int slot, int gs) {
     if constexpr ((ABL & 2) != 0) if (gs >= 2) return;  // ablation: no weight stream in the loop
     const int soff = (ABL & 1) ? 0 : (gs < total_ks ? gs : gs - total_ks) * 8192;  // ablation: L1-resident
 #pragma unroll
     for (int nt = 0; nt < NTW; ++nt) {
       const auto v = __builtin_amdgcn_raw_buffer_load_b128(wrsrc, wvoff + nt * 1024, soff, 0);
-      ar[slot][nt] = __builtin_bit_cast(bf16x8_t, v);
+      ar[slot][nt] = __builtin_bit_cast(V8, v);
     }
   };
 #pragma unroll
@@ -550,9 +288,9 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
       // offsets and masks out of the board loop (they would live across the whole tower and spill)
       int ln = lane;
       asm volatile("" : "+v"(ln));
-      bf16x8_t a[NTW];
+      V8 a[NTW];
 #pragma unroll
-      for (int nt = 0; nt < NTW; ++nt) a[nt] = ((const bf16x8_t *)t.stem_w)[(nh * NTW + nt) * 64 + lane];
+      for (int nt = 0; nt < NTW; ++nt) a[nt] = ((const V8 *)t.stem_w)[(nh * NTW + nt) * 64 + lane];
 #pragma unroll
       for (int i = 0; i < PTW; ++i) {
 #pragma unroll
@@ -562,7 +300,7 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
         const float *ob = t.obs + (size_t)rr[bsl] * 3 * A;
         const int p = (pt - bsl * NPT) * 16 + sigma16(ln & 15);
         const int y = p / H, x = p % H;
-        bf16x8_t b;
+        V8 b;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int k = 8 * (ln >> 4) + j;
@@ -572,10 +310,10 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
             const int yy = y + tap / 3 - 1, xx = x + tap % 3 - 1;
             if (yy >= 0 && yy < H && xx >= 0 && xx < H) v = ob[c * A + yy * H + xx];
           }
-          b[j] = (__bf16)v;
+          b[j] = (typename E::s)v;
         }
 #pragma unroll
-        for (int nt = 0; nt < NTW; ++nt) acc[nt][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[nt], b, acc[nt][i], 0, 0, 0);
+        for (int nt = 0; nt < NTW; ++nt) acc[nt][i] = E::mfma(a[nt], b, acc[nt][i]);
         __builtin_amdgcn_sched_barrier(0);  // one tile's im2col loads at a time (VGPR budget)
       }
 #pragma unroll
@@ -588,7 +326,7 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
           for (int h = 0; h < 2; ++h) {
             const int n0 = chan0(2 * u + h);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) o[h][e] = f2bf(fmaxf(acc[2 * u + h][i][e] + t.stem_b[n0 + e], 0.f));
+            for (int e = 0; e < 4; ++e) o[h][e] = E::relu1(acc[2 * u + h][i][e] + t.stem_b[n0 + e]);
             if constexpr (ONE) xs[((2 * u + h) * PTW + i) * 64] = o[h];
           }
           store_pair(smem, u, i, o[0], o[1]);
@@ -624,12 +362,12 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
         for (int i = NTL; i < PTW; ++i)
 #pragma unroll
           for (int nt = 0; nt < NTW; ++nt) acc[nt][i] = bv[nt];  // the empty slot (never stored)
-        bf16x8_t b[2][NTL];
+        V8 b[2][NTL];
         auto readB = [&](int buf, int st) {
           const int tap = st >> 2, ks = st & 3;
           const int off = (tap / 3) * RS + (tap % 3) * PS + ks * 32;
 #pragma unroll
-          for (int i = 0; i < NTL; ++i) b[buf][i] = *(const bf16x8_t *)(smem + bb[i] + off);
+          for (int i = 0; i < NTL; ++i) b[buf][i] = *(const V8 *)(smem + bb[i] + off);
         };
         readB(0, 0);
         if (ABL & 128) st_t0 = __builtin_amdgcn_s_memtime();
@@ -644,8 +382,7 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
           for (int i = 0; i < NTL; ++i)
 #pragma unroll
             for (int nt = 0; nt < NTW; ++nt)
-              acc[nt][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ar[st % RD][nt], b[st & 1][i],
-                                                                   st == 0 ? bv[nt] : acc[nt][i], 0, 0, 0);
+              acc[nt][i] = E::mfma(ar[st % RD][nt], b[st & 1][i], st == 0 ? bv[nt] : acc[nt][i]);
           // the last k-step stays open: the scheduler may start the epilogue of the tiles whose final
           // MFMA has issued while the remaining ones run (ABL & 256 pins it, for comparison)
           if ((ABL & 256) || st + 1 < KSTEPS) __builtin_amdgcn_sched_barrier(0);
@@ -655,7 +392,7 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
       else if (pg + PG * (PTW - 1) < NPTB) kloop(std::integral_constant<int, PTW>{});
       else kloop(std::integral_constant<int, PTW - 1>{});
       if (ABL & 128) { st_t1 = __builtin_amdgcn_s_memtime(); st_loop += st_t1 - st_t0; }
-      // epilogue: (action term) (+ residual) + ReLU -> bf16 -> the other image.  One straight-line
+      // epilogue: (action term) (+ residual) + ReLU -> E -> the other image.  One straight-line
       // copy per layer kind; every LDS operand (residual) is read in one batch before any
       // arithmetic, so the epilogue pays one LDS latency, not one per tile.
       const int kind = DYN ? (L == 0 ? 0 : ((L - 1) & 1) + 1) : ((L & 1) + 1);
@@ -705,9 +442,9 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
             }
             if constexpr (KIND == 2) {
 #pragma unroll
-              for (int e = 0; e < 4; ++e) v[e] += bf2f(xr[nt][i][e]);
+              for (int e = 0; e < 4; ++e) v[e] += E::to_f(xr[nt][i][e]);
             }
-            const u16x4 o = __builtin_bit_cast(u16x4, make_uint2(relu_bf16x2(v[0], v[1]), relu_bf16x2(v[2], v[3])));
+            const u16x4 o = __builtin_bit_cast(u16x4, make_uint2(E::relu2(v[0], v[1]), E::relu2(v[2], v[3])));
             if (nt & 1) {
               if ((NB == 1 && (PG * i + PG) * 16 <= A) || pos[i] >= 0) store_pair(nimg, nt >> 1, i, olo[i], o);
             } else {
@@ -765,8 +502,8 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
           const uint32_t wds[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            sum += hw[ch * 8 + 2 * e] * __uint_as_float(wds[e] << 16);
-            sum += hw[ch * 8 + 2 * e + 1] * __uint_as_float(wds[e] & 0xFFFF0000u);
+            sum += hw[ch * 8 + 2 * e] * E::lo(wds[e]);
+            sum += hw[ch * 8 + 2 * e + 1] * E::hi(wds[e]);
           }
         }
         t.pv_feat[(size_t)r * pv_stride(A) + i] = fmaxf(sum, 0.f);
@@ -812,6 +549,7 @@ struct HeadGemmArgs {
   int nR, nP;
 };
 
+template <typename E>
 __device__ __forceinline__ void reward_fc1_block(const HeadGemmArgs &h, int bx, int ks) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int rbase = bx * 64 + w * 16;
@@ -820,25 +558,25 @@ __device__ __forceinline__ void reward_fc1_block(const HeadGemmArgs &h, int bx, 
   const uint16_t *hrow = h.pool + (size_t)(slot >= 0 ? slot : 0) * h.K + 8 * (lane >> 4);
   const int k0 = (int)((long long)h.nks * ks / h.ksplit), k1 = (int)((long long)h.nks * (ks + 1) / h.ksplit);
   f32x4 acc[4] = {};
-  const bf16x8_t *wv = (const bf16x8_t *)h.rw + lane;
+  const typename E::v8 *wv = (const typename E::v8 *)h.rw + lane;
   int kk = k0;
   for (; kk + RFC_UNROLL <= k1; kk += RFC_UNROLL) {
-    bf16x8_t a[RFC_UNROLL], b[RFC_UNROLL][4];
+    typename E::v8 a[RFC_UNROLL], b[RFC_UNROLL][4];
 #pragma unroll
     for (int u = 0; u < RFC_UNROLL; ++u) {
-      a[u] = *(const bf16x8_t *)(hrow + (kk + u) * 32);
+      a[u] = *(const typename E::v8 *)(hrow + (kk + u) * 32);
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) b[u][nt] = wv[((kk + u) * 4 + nt) * 64];
     }
 #pragma unroll
     for (int u = 0; u < RFC_UNROLL; ++u)
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u], b[u][nt], acc[nt], 0, 0, 0);
+      for (int nt = 0; nt < 4; ++nt) acc[nt] = E::mfma(a[u], b[u][nt], acc[nt]);
   }
   for (; kk < k1; ++kk) {
-    const bf16x8_t a = *(const bf16x8_t *)(hrow + kk * 32);
+    const typename E::v8 a = *(const typename E::v8 *)(hrow + kk * 32);
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wv[(kk * 4 + nt) * 64], acc[nt], 0, 0, 0);
+    for (int nt = 0; nt < 4; ++nt) acc[nt] = E::mfma(a, wv[(kk * 4 + nt) * 64], acc[nt]);
   }
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt)
@@ -883,11 +621,12 @@ __device__ __forceinline__ f32x4 f32_tile(const float *__restrict__ pv, int pvs,
   return acc0 + acc1;
 }
 
+template <typename E>
 __global__ void __launch_bounds__(256) k_head_gemm(HeadGemmArgs h) {
   int b = blockIdx.x;
   if (b < h.nR) {
     const int nbx = (h.rows + 63) / 64;
-    reward_fc1_block(h, b % nbx, b / nbx);
+    reward_fc1_block<E>(h, b % nbx, b / nbx);
     return;
   }
   b -= h.nR;
@@ -1006,26 +745,30 @@ static size_t xres_bytes(int H) {
   }
 }
 
-template <int H, bool DYN>
+template <int H, bool DYN, typename E>
 static int launch_tower(const TowerArgs &a, hipStream_t s) {
   if (a.rows <= 0) return 0;
   using T = TowerCfg<H>;
   if (tower_xres_bytes<H>() && !a.xres) return fail("gmz_net: missing residual scratch");
   const int need = (a.rows + T::NB - 1) / T::NB;
   const int grid = need < cu_count() ? need : cu_count();
-  hipLaunchKernelGGL((k_tower3<H, DYN, 0, T::RD, T::NQ, T::PG, T::NB>), dim3(grid), dim3(64 * T::NQ * T::PG), 0, s, a);
+  hipLaunchKernelGGL((k_tower3<H, DYN, 0, T::RD, T::NQ, T::PG, T::NB, E>), dim3(grid), dim3(64 * T::NQ * T::PG), 0, s, a);
   GMZ_LAUNCH_CHECK();
   return 0;
 }
 
-static int tower(int H, bool dyn, const TowerArgs &a, hipStream_t s) {
+template <typename E>
+static int tower_e(int H, bool dyn, const TowerArgs &a, hipStream_t s) {
   switch (H) {
-    case 6: return dyn ? launch_tower<6, true>(a, s) : launch_tower<6, false>(a, s);
-    case 9: return dyn ? launch_tower<9, true>(a, s) : launch_tower<9, false>(a, s);
-    case 15: return dyn ? launch_tower<15, true>(a, s) : launch_tower<15, false>(a, s);
-    case 19: return dyn ? launch_tower<19, true>(a, s) : launch_tower<19, false>(a, s);
+    case 6: return dyn ? launch_tower<6, true, E>(a, s) : launch_tower<6, false, E>(a, s);
+    case 9: return dyn ? launch_tower<9, true, E>(a, s) : launch_tower<9, false, E>(a, s);
+    case 15: return dyn ? launch_tower<15, true, E>(a, s) : launch_tower<15, false, E>(a, s);
+    case 19: return dyn ? launch_tower<19, true, E>(a, s) : launch_tower<19, false, E>(a, s);
     default: return fail("gmz_net: board_size must be one of 6, 9, 15, 19");
   }
+}
+static int tower(const gmz_net_weights *w, bool dyn, const TowerArgs &a, hipStream_t s) {
+  return w->dtype == GMZ_NET_BF16 ? tower_e<Bf16>(w->board_size, dyn, a, s) : tower_e<F16>(w->board_size, dyn, a, s);
 }
 
 // split-K factor of the reward GEMM: 32 -> (rows/64) x 32 blocks keep ~64 KB of hidden-state reads
@@ -1053,6 +796,7 @@ static int check_w(const gmz_net_weights *w) {
   if (w->head_hidden != 64) return fail("gmz_net: head_hidden must be 64");
   if (w->board_size != 6 && w->board_size != 9 && w->board_size != 15 && w->board_size != 19)
     return fail("gmz_net: board_size must be 6, 9, 15 or 19");
+  if (w->dtype != GMZ_NET_F16 && w->dtype != GMZ_NET_BF16) return fail("gmz_net: dtype must be GMZ_NET_F16 or GMZ_NET_BF16");
   return 0;
 }
 
@@ -1074,7 +818,8 @@ static int heads(const gmz_net_weights *w, const uint16_t *pool, const int32_t *
   const int nR = reward ? ((rows + 63) / 64) * KSPLIT : 0, nP = nrt * ncg, nV = nrt;
   HeadGemmArgs g{pool, out_slot, rows, K, K / 32, KSPLIT, w->reward_fc1_w, rpart, pv, A, nrt, ncg,
                  w->policy_fc_w, w->policy_fc_b, logits, w->value_fc1_w, vpre, nR, nP};
-  hipLaunchKernelGGL(k_head_gemm, dim3(nR + nP + nV), dim3(256), 0, s, g);
+  if (w->dtype == GMZ_NET_BF16) hipLaunchKernelGGL(k_head_gemm<Bf16>, dim3(nR + nP + nV), dim3(256), 0, s, g);
+  else hipLaunchKernelGGL(k_head_gemm<F16>, dim3(nR + nP + nV), dim3(256), 0, s, g);
   GMZ_LAUNCH_CHECK();
   HeadFinishArgs f{out_slot, rows, w->head_hidden, KSPLIT, vpre, w->value_fc1_b, w->value_fc2_w, w->value_fc2_b,
                    reward ? rpart : nullptr, w->reward_fc1_b, w->reward_fc2_w, w->reward_fc2_b, value, reward};
@@ -1091,7 +836,7 @@ GMZ_EXPORT int gmz_net_initial_tower(const gmz_net_weights *w, const float *obs,
   TowerArgs a{w->repr_convs, w->repr_bias, 2 * w->blocks, w->repr_stem_w, w->repr_stem_b, nullptr, obs, pool,
               nullptr, nullptr, out_slot, w->head_conv_w, w->head_conv_b, (float *)workspace, rows,
               ws_xres(workspace, A, rows)};
-  return tower(H, false, a, (hipStream_t)stream);
+  return tower(w, false, a, (hipStream_t)stream);
 }
 
 GMZ_EXPORT int gmz_net_initial_heads(const gmz_net_weights *w, const uint16_t *pool, const int32_t *out_slot, int rows,
@@ -1116,7 +861,7 @@ GMZ_EXPORT int gmz_net_recurrent_tower(const gmz_net_weights *w, uint16_t *pool,
   TowerArgs a{w->dyn_convs, w->dyn_bias, 1 + 2 * w->blocks, nullptr, nullptr, w->dyn_action, nullptr, pool,
               in_slot, action, out_slot, w->head_conv_w, w->head_conv_b, (float *)workspace, rows,
               ws_xres(workspace, A, rows)};
-  return tower(w->board_size, true, a, (hipStream_t)stream);
+  return tower(w, true, a, (hipStream_t)stream);
 }
 
 GMZ_EXPORT int gmz_net_recurrent_heads(const gmz_net_weights *w, const uint16_t *pool, const int32_t *out_slot, int rows,

@@ -53,6 +53,7 @@ struct Dev {
   float *logits;
   int32_t *node_parent, *node_action, *path_u, *path_a, *sel;
   int32_t *node_last;  // [G][S] action last selected at the node: prefetch hint only (select_game)
+  int32_t *ctr;        // [G][4] k_expand_select work counters (gmz_engine_tree_counters)
   GameState *gs;
   uint64_t *legal;  // [G][NJ]
   int16_t *set_rank;
@@ -134,14 +135,15 @@ __device__ int transformed_q(const Dev &D, int lane, const int (&n)[NJ], const f
   const bool have_range = mm_max > mm_min;
   const float den_f = (mm_max - mm_min) + D.delta_f;
   if (!allv) {
-    // one wave-uniform reciprocal instead of a correctly rounded division per child (<= 1 ulp, the
-    // same order as the reduction-order differences already present; exact ties stay exact)
-    const double inv_den = 1.0 / (double)den_f;
+    // correctly rounded float64 division per child, as the reference's (q - min) / (max - min + delta)
+    // on a python float (utils.py:19-25): a reciprocal-multiply can differ by 1 ulp and merge two
+    // distinct normalised Qs into a tie that changes the first-index argmax
+    const double den = (double)den_f;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       double nq = 0.0;
       if (have_range) {
-        double x = ((double)q[j] - (double)mm_min) * inv_den;
+        double x = ((double)q[j] - (double)mm_min) / den;
         x = (x < 1.0) ? x : 1.0;
         nq = (x > 0.0) ? x : 0.0;
       }
@@ -747,8 +749,18 @@ __device__ __forceinline__ void expand_backup_game(const Dev &D, int g, int lane
 template <int NJ>
 __global__ void __launch_bounds__(256) k_select(Dev D, int32_t *__restrict__ in_slot, int32_t *__restrict__ act_out,
                                                 int32_t *__restrict__ out_slot, float *__restrict__ obs) {
-  const int g = blockIdx.x * 4 + threadIdx.x / WAVE;
-  if (g < D.G) select_game<NJ>(D, g, threadIdx.x & (WAVE - 1), in_slot, act_out, out_slot, obs);
+  const int g = blockIdx.x * 4 + threadIdx.x / WAVE, lane = threadIdx.x & (WAVE - 1);
+  if (g >= D.G) return;
+  select_game<NJ>(D, g, lane, in_slot, act_out, out_slot, obs);
+  if (lane == 0) {  // selection counters (see k_expand_select): every selected game-wave is one network row
+    const GameState s1 = D.gs[g];
+    if (s1.active) {
+      int4 c = ((int4 *)D.ctr)[g];
+      c.z += 1;
+      c.w += s1.depth;
+      ((int4 *)D.ctr)[g] = c;
+    }
+  }
 }
 
 template <int NJ>
@@ -770,10 +782,22 @@ __global__ void __launch_bounds__(256) k_expand_select(Dev D, const float *__res
                                                        int32_t *__restrict__ out_slot, float *__restrict__ obs) {
   const int g = blockIdx.x * 4 + threadIdx.x / WAVE, lane = threadIdx.x & (WAVE - 1);
   if (g >= D.G) return;
+  const int active0 = D.gs[g].active, depth0 = D.gs[g].depth;
   expand_backup_game<NJ>(D, g, lane, logits_in, value_in, reward_in);
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_s_waitcnt(0);
   select_game<NJ>(D, g, lane, in_slot, act_out, out_slot, obs);
+  // work counters (the algorithmic-byte model of bench.py's tree roofline): game-waves backed up,
+  // levels backed up, game-waves selected, levels walked by the selection (incl. the root level).
+  // Lane 0 wrote the GameState in select_game, so its own read sees the new depth.
+  if (lane == 0 && active0) {
+    const GameState s1 = D.gs[g];
+    int4 c = ((int4 *)D.ctr)[g];
+    c.x += 1;
+    c.y += depth0;
+    if (s1.active) { c.z += 1; c.w += s1.depth; }
+    ((int4 *)D.ctr)[g] = c;
+  }
 }
 
 template <int NJ>
@@ -925,6 +949,7 @@ GMZ_EXPORT int gmz_engine_create(const gmz_engine_cfg *cfg, gmz_engine **out) {
   rc |= dalloc(e, &D.node_parent, G * S);
   rc |= dalloc(e, &D.node_action, G * S);
   rc |= dalloc(e, &D.node_last, G * S);
+  rc |= dalloc(e, &D.ctr, G * 4);
   rc |= dalloc(e, &D.path_u, G * S);
   rc |= dalloc(e, &D.path_a, G * S);
   rc |= dalloc(e, &D.sel, G * MAX_TOP);
@@ -940,7 +965,7 @@ GMZ_EXPORT int gmz_engine_create(const gmz_engine_cfg *cfg, gmz_engine **out) {
     gmz_engine_destroy(e);
     return -1;
   }
-  if (hipMemset(D.gs, 0, G * sizeof(GameState)) != hipSuccess) {
+  if (hipMemset(D.gs, 0, G * sizeof(GameState)) != hipSuccess || hipMemset(D.ctr, 0, G * 16) != hipSuccess) {
     gmz_engine_destroy(e);
     return fail("gmz_engine_create: hipMemset failed");
   }
@@ -1118,6 +1143,14 @@ GMZ_EXPORT int gmz_engine_wave_depth(gmz_engine *e, int32_t *depth_dev, void *st
   if (!e || !depth_dev) return fail("gmz_engine_wave_depth: null argument");
   hipLaunchKernelGGL(k_wave_depth, dim3((e->D.G + 255) / 256), dim3(256), 0, (hipStream_t)stream, e->D, depth_dev);
   GMZ_LAUNCH_CHECK();
+  return 0;
+}
+
+GMZ_EXPORT int gmz_engine_tree_counters(gmz_engine *e, int32_t *ctr_dev, int reset, void *stream) {
+  if (!e) return fail("null engine");
+  hipStream_t s = (hipStream_t)stream;
+  if (ctr_dev) GMZ_HIP(hipMemcpyAsync(ctr_dev, e->D.ctr, (size_t)e->D.G * 16, hipMemcpyDeviceToDevice, s));
+  if (reset) GMZ_HIP(hipMemsetAsync(e->D.ctr, 0, (size_t)e->D.G * 16, s));
   return 0;
 }
 

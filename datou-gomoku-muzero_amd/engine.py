@@ -80,6 +80,7 @@ class BatchedSelfPlayEngine:
         self._n_legal = np.full(G, A, dtype=np.int32)
         self._last_reset = True
         self.waves_last = 0
+        self.tree_timer = None  # optional network.KernelTimer around the fused expand/backup+select launches
 
     # ------------------------------------------------------------------ lifecycle
     def close(self):
@@ -177,9 +178,13 @@ class BatchedSelfPlayEngine:
             else:
                 self.net.initial(self.obs, self.out_slot, self.logits, self.value, s)
             if w + 1 < waves and self.fuse_waves:  # backup of this wave + selection of the next in one launch
+                if self.tree_timer is not None:
+                    self.tree_timer.start()
                 check(L.gmz_engine_expand_backup_select(self.handle, ptr(self.logits), ptr(self.value), rw,
                                                         ptr(self.in_slot), ptr(self.act_req), ptr(self.out_slot),
                                                         ptr(self.obs), s))
+                if self.tree_timer is not None:
+                    self.tree_timer.stop(0)
             else:
                 check(L.gmz_engine_expand_backup(self.handle, ptr(self.logits), ptr(self.value), rw, s))
                 if w + 1 < waves:
@@ -205,6 +210,14 @@ class BatchedSelfPlayEngine:
         """workers.py:49-123 find_winning_moves_rebuilt on the device for G positions (see
         ``winning_scan``); ``counters`` = (missed_fives, missed_totals) int32[G] accumulated in place."""
         return winning_scan(boards, players, action, self.cfg.N_IN_ROW, counters, stream, self.lib)
+
+    def tree_counters(self, reset=False):
+        """Work done by the fused expand/backup + select launches since the last reset, summed over
+        games: dict(backups, backup_levels, selects, select_levels) (gmz_engine_tree_counters)."""
+        c = torch.zeros(self.G, 4, dtype=torch.int32, device=self.device)
+        check(self.lib.gmz_engine_tree_counters(self.handle, ptr(c), 1 if reset else 0, self._stream()))
+        t = c.to(torch.int64).sum(0).tolist()
+        return dict(backups=t[0], backup_levels=t[1], selects=t[2], select_levels=t[3])
 
     def root_stats(self):
         G, A, dev = self.G, self.A, self.device

@@ -16,7 +16,8 @@ Gumbel noise is drawn from the global numpy RandomState (``np.random.gumbel(0, 1
 mcts.py:312) so a seeded run reproduces the reference's search.
 
 Returns (policy float64[A], value np.float32, action int); on an inference timeout at the root:
-(zeros(A), 0.0, -1) as the reference (mcts.py:298-302).
+(zeros(A), 0.0, -1) as the reference (mcts.py:298-302); a timed-out 'recurrent_batch' is logged and
+the same wave is requested again, as the reference's ``continue`` does (mcts.py:82-85, 337).
 """
 import logging
 from queue import Empty
@@ -65,8 +66,13 @@ class _QueueNet:
                 continue
             h = self.hidden[int(ins[r])]
             hb = np.concatenate([h] * k, axis=0)
-            o.request_queue.put((o.worker_id, "recurrent_batch", (hb, np.array([acts[r]] * k, dtype=np.int32))))
-            p, v, hn, rw = o.result_queue.get(timeout=_TIMEOUT)
+            while True:
+                o.request_queue.put((o.worker_id, "recurrent_batch", (hb, np.array([acts[r]] * k, dtype=np.int32))))
+                try:
+                    p, v, hn, rw = o.result_queue.get(timeout=_TIMEOUT)
+                    break
+                except Empty:  # mcts.py:82-85 + 337: warn, then the same wave (same leaves) is re-requested
+                    o.logger.warning("Worker %s timed out waiting for recurrent inference." % o.worker_id)
             self.hidden[int(outs[r])] = hn[0:1]
             logits[r].copy_(torch.as_tensor(np.asarray(p, dtype=np.float32)[0].reshape(-1)))
             value[r] = float(np.asarray(v, dtype=np.float32).reshape(-1)[0])

@@ -4,14 +4,18 @@
 ``ModelWeightsUpdate.weights`` the trainer sends, workers.py:332-335) into the kernel layouts of
 csrc/gmz_net.hip:
   * eval-mode BatchNorm (eps 1e-4, network.py:34,37,53,62,65,82) folded into conv weight/bias;
-  * 3x3 conv weights as bf16 in v_mfma_f32_16x16x32_bf16 A-operand fragment order
+  * 3x3 conv weights as f16 (default) or bf16 in v_mfma_f32_16x16x32_{f16,bf16} A-operand fragment order
     [tap][k-step][n-tile][lane][8] (rows = output channels), so a 16 KB weight stage is a
     linear copy and every fragment read is one conflict-free ds_read_b128;
   * the dynamics action embedding (one-hot plane -> 1x1 conv, network.py:90-92) folded into a
     [9][C] per-tap additive term of the dynamics conv (exact algebra: the plane has one 1);
-  * reward_fc.0 permuted from NCHW-flatten to the NHWC hidden-state order, bf16 B-fragment order.
+  * reward_fc.0 permuted from NCHW-flatten to the NHWC hidden-state order, B-fragment order.
 
-``GomokuNetHip`` owns the bf16 hidden-state slot pool (HBM) and launches the kernels through the
+``precision``: "fp16" (default; 10-bit mantissa, the type of the reference trainer's own autocast)
+or "bf16" (7-bit mantissa) — the 16-bit type of the packed weights, the activations and the
+hidden-state pool; MFMA accumulation is float32 either way and gfx950 runs both at the same rate.
+
+``GomokuNetHip`` owns the 16-bit hidden-state slot pool (HBM) and launches the kernels through the
 C ABI (include/gmz.h gmz_net_*).  It is the ``net`` backend of engine.BatchedSelfPlayEngine.
 """
 import ctypes
@@ -32,7 +36,12 @@ class NetWeights(ctypes.Structure):
                 ("head_hidden", ctypes.c_int32)] + [(n, ctypes.c_void_p) for n in (
                     "repr_stem_w", "repr_stem_b", "repr_convs", "repr_bias", "dyn_convs", "dyn_bias", "dyn_action",
                     "head_conv_w", "head_conv_b", "policy_fc_w", "policy_fc_b", "value_fc1_w", "value_fc1_b",
-                    "value_fc2_w", "value_fc2_b", "reward_fc1_w", "reward_fc1_b", "reward_fc2_w", "reward_fc2_b")]
+                    "value_fc2_w", "value_fc2_b", "reward_fc1_w", "reward_fc1_b", "reward_fc2_w", "reward_fc2_b")] + [
+                    ("dtype", ctypes.c_int32)]
+
+
+PRECISIONS = {"fp16": 0, "bf16": 1}  # include/gmz.h GMZ_NET_F16 / GMZ_NET_BF16
+_TORCH16 = {"fp16": torch.float16, "bf16": torch.bfloat16}
 
 
 _lib.register({
@@ -56,8 +65,13 @@ def fold_bn(sd, prefix):
     return s.astype(np.float32), (b - m * s).astype(np.float32)
 
 
-def _bf16_bits(x):
-    t = torch.from_numpy(np.ascontiguousarray(x, dtype=np.float32)).to(torch.bfloat16)
+def _e16_bits(x, precision="fp16"):
+    """float32 array -> uint16 bit patterns of the 16-bit type (round to nearest even; f16 saturates
+    at +-65504 instead of overflowing to inf)."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    if precision == "fp16":
+        x = np.clip(x, -65504.0, 65504.0)
+    t = torch.from_numpy(x).to(_TORCH16[precision])
     return t.view(torch.int16).numpy().view(np.uint16)
 
 
@@ -76,19 +90,19 @@ def output_channel(nt, m):
     return (nt >> 1) * 32 + 8 * (m >> 2) + 4 * (nt & 1) + (m & 3)
 
 
-def pack_conv3x3(wf):
-    """[128(n), 128(c), 3, 3] f32 -> bf16 [9][4][8][64][8]: frag(t, ks, nt, l, j) =
+def pack_conv3x3(wf, precision="fp16"):
+    """[128(n), 128(c), 3, 3] f32 -> 16-bit [9][4][8][64][8]: frag(t, ks, nt, l, j) =
     W[n = output_channel(nt, l&15)][c = conv_input_channel(ks, l, j)][t // 3][t % 3]."""
     Wt = wf.transpose(2, 3, 0, 1).reshape(9, C, C)  # [t][n][c]
     ks, nt, l, j = np.meshgrid(np.arange(4), np.arange(8), np.arange(64), np.arange(8), indexing="ij")
     n = output_channel(nt, l & 15)
     c = conv_input_channel(ks, l, j)
     out = Wt[:, n, c]  # [9][4][8][64][8]
-    return _bf16_bits(out)
+    return _e16_bits(out, precision)
 
 
-def pack_stem(wf):
-    """conv 3->128 [128, 3, 3, 3] -> bf16 [8][64][8] with k = tap*3 + c (27, zero-padded to 32), rows
+def pack_stem(wf, precision="fp16"):
+    """conv 3->128 [128, 3, 3, 3] -> 16-bit [8][64][8] with k = tap*3 + c (27, zero-padded to 32), rows
     in output_channel order."""
     Wk = np.zeros((C, 32), np.float32)
     for dy in range(3):
@@ -96,7 +110,7 @@ def pack_stem(wf):
             for c in range(3):
                 Wk[:, (dy * 3 + dx) * 3 + c] = wf[:, c, dy, dx]
     nt, l, j = np.meshgrid(np.arange(8), np.arange(64), np.arange(8), indexing="ij")
-    return _bf16_bits(Wk[output_channel(nt, l & 15), 8 * (l >> 4) + j])
+    return _e16_bits(Wk[output_channel(nt, l & 15), 8 * (l >> 4) + j], precision)
 
 
 def r16(x):
@@ -111,16 +125,16 @@ def pad_fc(w, rows, cols):
     return out
 
 
-def pack_reward_fc1(w, A):
-    """reward_fc.0.weight [hd, C*A] (NCHW-flatten input) -> bf16 B fragments [K/32][hd/16][64][8]
+def pack_reward_fc1(w, A, precision="fp16"):
+    """reward_fc.0.weight [hd, C*A] (NCHW-flatten input) -> 16-bit B fragments [K/32][hd/16][64][8]
     over the NHWC hidden order k = p*C + c."""
     hd = w.shape[0]
     Wn = w.reshape(hd, C, A).transpose(2, 1, 0).reshape(A * C, hd)  # [k = p*C + c][n]
     kk, nt, l, j = np.meshgrid(np.arange(A * C // 32), np.arange(hd // 16), np.arange(64), np.arange(8), indexing="ij")
-    return _bf16_bits(Wn[kk * 32 + 8 * (l >> 4) + j, nt * 16 + (l & 15)])
+    return _e16_bits(Wn[kk * 32 + 8 * (l >> 4) + j, nt * 16 + (l & 15)], precision)
 
 
-def pack_weights(sd, cfg):
+def pack_weights(sd, cfg, precision="fp16"):
     """Reference state_dict (numpy or torch tensors) -> dict of packed numpy arrays."""
     sd = {k: (v.detach().cpu().numpy() if hasattr(v, "detach") else np.asarray(v)) for k, v in sd.items()}
     H = cfg.BOARD_SIZE
@@ -128,7 +142,7 @@ def pack_weights(sd, cfg):
     nb = cfg.NUM_RES_BLOCKS
     out = {}
     s, b = fold_bn(sd, "representation_net.bn")
-    out["repr_stem_w"] = pack_stem(_f32(sd["representation_net.conv.weight"]) * s[:, None, None, None])
+    out["repr_stem_w"] = pack_stem(_f32(sd["representation_net.conv.weight"]) * s[:, None, None, None], precision)
     out["repr_stem_b"] = b
 
     def tower(prefix):
@@ -137,7 +151,7 @@ def pack_weights(sd, cfg):
             for k in (1, 2):
                 p = "%s.resblocks.%d." % (prefix, i)
                 s, b = fold_bn(sd, p + "bn%d" % k)
-                convs.append(pack_conv3x3(_f32(sd[p + "conv%d.weight" % k]) * s[:, None, None, None]))
+                convs.append(pack_conv3x3(_f32(sd[p + "conv%d.weight" % k]) * s[:, None, None, None], precision))
                 biases.append(b)
         return convs, biases
 
@@ -149,7 +163,7 @@ def pack_weights(sd, cfg):
     emb = _f32(sd["dynamics_net.action_embed_conv.weight"]).reshape(16)
     act = np.einsum("ncyx,c->yxn", wd[:, C:], emb).reshape(9, C)
     convs, biases = tower("dynamics_net")
-    out["dyn_convs"] = np.stack([pack_conv3x3(wd[:, :C])] + convs)
+    out["dyn_convs"] = np.stack([pack_conv3x3(wd[:, :C], precision)] + convs)
     out["dyn_bias"] = np.stack([b] + biases)
     out["dyn_action"] = act.astype(np.float32)
     sp, bp = fold_bn(sd, "prediction_net.policy_bn")
@@ -165,7 +179,7 @@ def pack_weights(sd, cfg):
     out["value_fc1_b"] = _f32(sd["prediction_net.value_fc1.bias"])
     out["value_fc2_w"] = np.ascontiguousarray(_f32(sd["prediction_net.value_fc2.weight"]).T)
     out["value_fc2_b"] = _f32(sd["prediction_net.value_fc2.bias"])
-    out["reward_fc1_w"] = pack_reward_fc1(_f32(sd["dynamics_net.reward_fc.0.weight"]), A)
+    out["reward_fc1_w"] = pack_reward_fc1(_f32(sd["dynamics_net.reward_fc.0.weight"]), A, precision)
     out["reward_fc1_b"] = _f32(sd["dynamics_net.reward_fc.0.bias"])
     out["reward_fc2_w"] = np.ascontiguousarray(_f32(sd["dynamics_net.reward_fc.2.weight"]).T)
     out["reward_fc2_b"] = _f32(sd["dynamics_net.reward_fc.2.bias"])
@@ -204,11 +218,14 @@ class KernelTimer:
 class GomokuNetHip:
     """GomokuNetEZ initial/recurrent inference on the device (engine ``net`` backend).
 
-    ``num_slots`` hidden-state slots of bf16 [A][128] live in ``self.pool`` (HBM); the engine
-    addresses them as ``game * slots_per_game + node``.
+    ``num_slots`` hidden-state slots of 16-bit [A][128] (``precision``: "fp16" default, or "bf16")
+    live in ``self.pool`` (HBM); the engine addresses them as ``game * slots_per_game + node``.
     """
 
-    def __init__(self, state_dict, cfg=None, num_slots=1, max_rows=1, device="cuda", **overrides):
+    def __init__(self, state_dict, cfg=None, num_slots=1, max_rows=1, device="cuda", precision="fp16", **overrides):
+        if precision not in PRECISIONS:
+            raise ValueError("GomokuNetHip: precision must be 'fp16' or 'bf16'")
+        self.precision = precision
         self.cfg = from_any(cfg, **overrides)
         c = self.cfg
         if c.NUM_FILTERS != C or c.HEAD_HIDDEN_DIM != 64 or c.BOARD_SIZE not in (6, 9, 15, 19):
@@ -224,10 +241,11 @@ class GomokuNetHip:
 
     def load_state_dict(self, state_dict):
         """Hot-swap weights (ModelWeightsUpdate, workers.py:332-335)."""
-        packed = pack_weights(state_dict, self.cfg)
+        packed = pack_weights(state_dict, self.cfg, self.precision)
         self._tensors = {k: torch.from_numpy(np.ascontiguousarray(v)).to(self.device) for k, v in packed.items()}
         c = self.cfg
         w = NetWeights(c.BOARD_SIZE, C, c.NUM_RES_BLOCKS, c.HEAD_HIDDEN_DIM)
+        w.dtype = PRECISIONS[self.precision]
         for k, t in self._tensors.items():
             setattr(w, k, t.data_ptr())
         self.w = w
@@ -272,11 +290,11 @@ class GomokuNetHip:
 
     # ---- convenience (tests / single-game adapters): slots 0..rows-1 are used as scratch
     def hidden(self, slots):
-        """bf16 hidden states of the given slots as float32 [n, C, H, W] (NCHW, like the reference)."""
+        """The hidden states of the given slots as float32 [n, C, H, W] (NCHW, like the reference)."""
         H = self.cfg.BOARD_SIZE
         idx = torch.as_tensor(np.asarray(slots, dtype=np.int64), device=self.device)
-        hv = self.pool.view(-1, self.A, C)[idx]  # [n][A][C] bf16 bits
-        f = hv.view(torch.bfloat16).float()
+        hv = self.pool.view(-1, self.A, C)[idx]  # [n][A][C] 16-bit patterns
+        f = hv.view(_TORCH16[self.precision]).float()
         return f.permute(0, 2, 1).reshape(len(slots), C, H, H)
 
     def initial_inference(self, obs, slots=None):

@@ -20,7 +20,9 @@ torch.distributed is initialised, data parallelism with one flat-bucket gradient
 (RCCL over xGMI);
 ``ReplayBuffer`` keeps the slices resident in device memory and samples like
 replay_buffer.py:58-94 (uniform without replacement, or stratified proportional PER).
-The convolutions run in PyTorch's kernels in this round; the fused HIP kernels cover inference.
+The 128->128 residual-block convolutions (forward, input and weight gradients) and every
+training-mode BatchNorm run on the HIP kernels of csrc/gmz_conv.hip / csrc/gmz_train.hip; the
+trunks' first convolutions, 1x1 convolutions and Linears run on MIOpen / hipBLASLt.
 """
 import math
 from dataclasses import dataclass, field, asdict
@@ -813,7 +815,36 @@ class ReplayBuffer:
         self.ptr = (self.ptr + n) % self.N
         self.count = min(self.N, self.count + n)
 
-    def sample(self, B, rng=np.random):
+    def add_arrays(self, obs, act, rew, pol, val):
+        """Append n slices given as stacked arrays/tensors (obs [n,U+1,3,H,W] 0/1, act [n,U] int,
+        rew [n,U], pol [n,U+1,A], val [n,U+1]); same ring semantics as :meth:`add`."""
+        n = int(obs.shape[0])
+        if n == 0:
+            return
+        if n > self.N:  # only the newest N survive the ring
+            obs, act, rew, pol, val = obs[-self.N:], act[-self.N:], rew[-self.N:], pol[-self.N:], val[-self.N:]
+            n = self.N
+        idx = ((torch.arange(n) + self.ptr) % self.N).to(self.device)
+        dv = lambda x, dt: torch.as_tensor(x).to(self.device, dt)  # noqa: E731
+        self.obs[idx] = dv(obs, torch.uint8)
+        self.act[idx] = dv(act, torch.int32)
+        self.rew[idx] = dv(rew, torch.float32)
+        self.pol[idx] = dv(pol, torch.float32)
+        self.val[idx] = dv(val, torch.float32)
+        if self.cfg.ENABLE_PER:
+            self.prio[idx] = torch.as_tensor(self.max_priority, dtype=torch.float32, device=self.device)
+        else:
+            self.prio[idx] = 1.0
+        self.ptr = (self.ptr + n) % self.N
+        self.count = min(self.N, self.count + n)
+
+    def sample(self, B, rng=np.random, dist=None):
+        """replay_buffer.py:58-94.  ``dist``: torch.distributed when this buffer is one rank's shard of
+        a data-parallel trainer (sharded PER): each rank samples its B slices from its
+        own shard (rank chosen uniformly, then proportional within the shard, so a slice's sampling
+        probability is p_i / (N * T_rank)); the IS weights use the GLOBAL slice count (one all-reduce
+        SUM) and are normalised by the max over the global batch (one all-reduce MAX).  With one rank
+        this is exactly the reference's (count * p_i / T)^-beta / max."""
         if self.count < B:
             return None
         if self.cfg.ENABLE_PER:
@@ -825,20 +856,47 @@ class ReplayBuffer:
             r = torch.from_numpy(rng.random_sample(B)).to(self.device, non_blocking=True)
             u = (torch.arange(B, device=self.device, dtype=torch.float64) + r) * (total / B)
             idx = torch.searchsorted(cum, u).clamp_max(self.count - 1)
-            w = (self.count * (p[idx] / total)) ** (-self.cfg.PER_BETA)
-            w = (w / w.max()).float()
+            prob = p[idx] / total
+            count = float(self.count)
+            if dist is not None and dist.get_world_size() > 1:
+                count = _allreduce(torch.tensor([count], dtype=torch.float64, device=self.device), dist)
+                prob = prob / dist.get_world_size()
+            w = (count * prob) ** (-self.cfg.PER_BETA)
+            wmax = w.max()
+            if dist is not None and dist.get_world_size() > 1:
+                wmax = _allreduce(wmax.reshape(1), dist, max_op=True)[0]
+            w = (w / wmax).float()
         else:
             idx = torch.from_numpy(rng.choice(self.count, B, replace=False)).to(self.device)
             w = torch.ones(B, device=self.device)
         batch = (self.obs[idx].float(), self.act[idx], self.rew[idx], self.pol[idx], self.val[idx])
         return batch, idx, w
 
-    def update_priorities(self, idx, td):
+    def update_priorities(self, idx, td, dist=None):
+        """replay_buffer.py:96-101; with ``dist`` the running max priority (the priority of newly added
+        slices) is kept global by an all-reduce MAX, so every shard admits new slices alike."""
         if not self.cfg.ENABLE_PER:
             return
         p = td.abs().to(self.device).float() + self.cfg.PER_EPSILON
-        self.max_priority = torch.maximum(torch.as_tensor(self.max_priority, device=self.device), p.max())  # device
+        m = torch.maximum(torch.as_tensor(self.max_priority, device=self.device, dtype=torch.float32), p.max())
+        if dist is not None and dist.get_world_size() > 1:
+            m = _allreduce(m.reshape(1), dist, max_op=True)[0]
+        self.max_priority = m  # device scalar
         self.prio[idx] = p
+
+
+def _allreduce(t, dist, max_op=False):
+    """All-reduce a small tensor (SUM or MAX) on any backend: RCCL takes device tensors, gloo host
+    tensors.  Returns the reduced tensor on ``t``'s device."""
+    op = dist.ReduceOp.MAX if max_op else dist.ReduceOp.SUM
+    if dist.get_backend() == "gloo" and t.is_cuda:
+        h = t.cpu()
+        dist.all_reduce(h, op=op)
+        out = h.to(t.device)
+    else:
+        dist.all_reduce(t, op=op)
+        out = t
+    return out
 
 
 # ------------------------------------------------------------------------------ trainer

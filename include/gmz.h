@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define GMZ_ABI_VERSION 2
+#define GMZ_ABI_VERSION 3
 
 /* ------------------------------------------------------------------ misc */
 const char *gmz_last_error(void);
@@ -148,6 +148,13 @@ int gmz_engine_wave_k(gmz_engine *e, int32_t *k_dev, void *stream);
  * games whose search is finished): the input of the tree kernels' algorithmic-byte count
  * (tools/tree_microbench.py). */
 int gmz_engine_wave_depth(gmz_engine *e, int32_t *depth_dev, void *stream);
+/* Work counters since the last reset, per game: ctr_dev int32[G][4] = {game-waves backed up and
+ * tree levels backed up by the fused expand/backup + select launches (gmz_engine_expand_backup_select),
+ * game-waves selected and tree levels walked by those selections incl. the root level (fused launches
+ * and gmz_engine_select; every selected game-wave is one network row)}.  ctr_dev may be
+ * NULL (reset only); reset != 0 zeroes the engine's counters after the copy.  Stream-ordered.
+ * Input of bench.py's algorithmic-byte count for the tree kernel's HBM roofline. */
+int gmz_engine_tree_counters(gmz_engine *e, int32_t *ctr_dev, int reset, void *stream);
 /* Diagnostics (device pointers into engine pools, for tests): root child visit counts
  * int32[G][A], root (N, W) and MinMaxStats (max, min) per game. */
 int gmz_engine_root_stats(gmz_engine *e, int32_t *visits_dev, int32_t *root_n_dev, float *root_w_dev,
@@ -168,16 +175,16 @@ int gmz_hashnet_recurrent(uint32_t *hid_pool_dev, const int32_t *in_slot_dev, co
 
 /* ------------------------------------------------------------------ GomokuNetEZ (network.py) */
 /* Device pointers to the packed inference weights (datou-gomoku-muzero_amd/network.py:pack_weights
- * builds them from a reference state_dict: BatchNorm folded, bf16 conv weights in MFMA fragment
+ * builds them from a reference state_dict: BatchNorm folded, 16-bit (`dtype`) conv weights in MFMA fragment
  * order).  Kernels are specialised for channels == 128, head_hidden == 64, 3 support bins,
- * board_size in {6, 9, 15}. */
+ * board_size in {6, 9, 15, 19}. */
 typedef struct gmz_net_weights {
   int32_t board_size, channels, blocks, head_hidden;
-  const uint16_t *repr_stem_w;  /* bf16 [8][64][8]       conv 3->C, k = tap*3 + c (27 -> 32)      */
+  const uint16_t *repr_stem_w;  /* e16  [8][64][8]       conv 3->C, k = tap*3 + c (27 -> 32)      */
   const float *repr_stem_b;     /* [C]                                                             */
-  const uint16_t *repr_convs;   /* bf16 [2*blocks][9][4][8][64][8] ResBlock convs                 */
+  const uint16_t *repr_convs;   /* e16  [2*blocks][9][4][8][64][8] ResBlock convs                 */
   const float *repr_bias;       /* [2*blocks][C]                                                   */
-  const uint16_t *dyn_convs;    /* bf16 [1+2*blocks][9][4][8][64][8] (layer 0 = dynamics conv,     */
+  const uint16_t *dyn_convs;    /* e16  [1+2*blocks][9][4][8][64][8] (layer 0 = dynamics conv,     */
   const float *dyn_bias;        /*      hidden-state channels only)  [1+2*blocks][C]              */
   const float *dyn_action;      /* [9][C] action-embedding contribution per tap (BN folded)        */
   const float *head_conv_w;     /* [3][C] policy (2) + value (1) 1x1 convs, BN folded              */
@@ -188,16 +195,21 @@ typedef struct gmz_net_weights {
   const float *value_fc1_b;     /* [hd]                                                            */
   const float *value_fc2_w;     /* [hd][3]                                                         */
   const float *value_fc2_b;     /* [3]                                                             */
-  const uint16_t *reward_fc1_w; /* bf16 [A*C/32][hd/16][64][8] fragment order, NHWC input order    */
+  const uint16_t *reward_fc1_w; /* e16  [A*C/32][hd/16][64][8] fragment order, NHWC input order    */
   const float *reward_fc1_b;    /* [hd]                                                            */
   const float *reward_fc2_w;    /* [hd][3]                                                         */
   const float *reward_fc2_b;    /* [3]                                                             */
+  int32_t dtype;                /* GMZ_NET_F16 (default) or GMZ_NET_BF16: the type of the 16-bit     */
+                                /* arrays above (conv / stem / reward_fc1 weights), of the hidden-   */
+                                /* state pool and of the towers' MFMA operands (f32 accumulation)    */
 } gmz_net_weights;
+#define GMZ_NET_F16 0
+#define GMZ_NET_BF16 1
 
 /* Scratch needed by gmz_net_initial / gmz_net_recurrent for `rows` rows (caller allocates). */
 int gmz_net_workspace_bytes(const gmz_net_weights *w, int rows, size_t *out);
 /* network.py:137-143 initial_inference: obs_dev f32[rows][3][A] -> logits f32[rows][A],
- * value f32[rows] (support_to_scalar), hidden state -> hid_pool_dev[out_slot[r]] (bf16 [A][C]).
+ * value f32[rows] (support_to_scalar), hidden state -> hid_pool_dev[out_slot[r]] (dtype [A][C]).
  * Rows with out_slot[r] < 0 are skipped. */
 int gmz_net_initial(const gmz_net_weights *w, const float *obs_dev, int rows, const int32_t *out_slot_dev,
                     uint16_t *hid_pool_dev, float *logits_dev, float *value_dev, void *workspace_dev,

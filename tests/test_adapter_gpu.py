@@ -147,3 +147,36 @@ def test_search_batch_equals_per_game_search(M, golden, fname):
         assert np.abs(pol[i] - p).max() <= 1e-12
     # and the reference's own outputs
     assert act.tolist() == d["action"].tolist()
+
+
+class _DropOnce(ServerQueue):
+    """ServerQueue whose reply to the n-th 'recurrent_batch' request is lost (a timeout)."""
+
+    def __init__(self, A, drop_at):
+        super().__init__(A)
+        self.n_rec, self.drop_at = 0, drop_at
+
+    def put(self, item):
+        super().put(item)
+        if item[1] == "recurrent_batch":
+            self.n_rec += 1
+            if self.n_rec == self.drop_at:
+                self.results.pop()  # the server never answers this one
+
+
+def test_recurrent_timeout_retries_the_wave(M):
+    """mcts.py:82-85 + 337: a timed-out recurrent request returns [] and the loop `continue`s, so
+    the same wave is requested again and the search result is unchanged."""
+    mcts, GmzConfig = M
+    cfg = GmzConfig(BOARD_SIZE=6, NUM_SIMULATIONS=40)
+    rs_state = np.random.get_state()
+    outs, logs = [], []
+    for q in (ServerQueue(36), _DropOnce(36, drop_at=3)):
+        np.random.set_state(rs_state)
+        eng = mcts.HipMuZeroMCTS(0, q, q, cfg=cfg)
+        pol, val, act = eng.search(Game(np.zeros((6, 6)), 1, None))
+        outs.append((pol, val, act))
+        logs.append(q.log)
+    assert outs[0][2] == outs[1][2] >= 0 and outs[0][1] == outs[1][1]
+    assert np.array_equal(outs[0][0], outs[1][0])
+    assert len(logs[1]) == len(logs[0]) + 1 and logs[1][4] == logs[1][3]  # the dropped request, re-sent

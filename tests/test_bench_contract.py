@@ -47,3 +47,37 @@ def test_result_line_schema():
         assert k in line
     assert line["value"] == 8 * 1024 * 10 / 2.0 and line["scaling"] == "weak" and line["n_gpus"] == 8
     assert "workload" in line["config"] and "model" not in line["config"]
+
+
+def test_spawn_ranks_sets_the_distributed_env(tmp_path):
+    """bench.py --gpus N without an external launcher: spawn_ranks starts N processes with the
+    torch.distributed env contract; they rendezvous (gloo here) and see world_size N."""
+    import bench
+    script = tmp_path / "rank.py"
+    script.write_text(
+        "import os, sys, torch, torch.distributed as dist\n"
+        "dist.init_process_group('gloo', init_method='env://')\n"
+        "t = torch.ones(1)\n"
+        "dist.all_reduce(t)\n"
+        "open(os.path.join(sys.argv[1], 'r%s' % os.environ['RANK']), 'w').write(\n"
+        "    '%d %d %s %d' % (dist.get_rank(), dist.get_world_size(), os.environ['LOCAL_RANK'], int(t.item())))\n"
+        "dist.destroy_process_group()\n")
+    assert bench.spawn_ranks(2, [str(tmp_path)], script=str(script)) == 0
+    for r in range(2):
+        assert (tmp_path / ("r%d" % r)).read_text() == "%d 2 %d 2" % (r, r)
+
+
+def test_spawn_ranks_reports_a_failing_rank(tmp_path):
+    import bench
+    script = tmp_path / "fail.py"
+    script.write_text("import os, sys, time\n"
+                      "sys.exit(3) if os.environ['RANK'] == '1' else time.sleep(30)\n")
+    assert bench.spawn_ranks(2, [], script=str(script)) == 3  # rank 0 is terminated, not waited for
+
+
+def test_gpus_must_match_world_size():
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "4"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 2 and "disagrees" in p.stderr

@@ -1,6 +1,6 @@
 """CPU checks of the HIP network's weight packing (network.py): fragment layouts invert exactly,
-and a float32 emulation of the kernels' algebra on the packed (BN-folded, bf16) weights matches
-the oracle forward (oracle/netref.py) within bf16 weight-rounding tolerance."""
+and a float32 emulation of the kernels' algebra on the packed (BN-folded, f16 or bf16) weights matches
+the oracle forward (oracle/netref.py) within the 16-bit weight-rounding tolerance."""
 import numpy as np
 import pytest
 
@@ -10,8 +10,15 @@ from datou_gomoku_muzero_amd import weights as W
 from datou_gomoku_muzero_amd.config import GmzConfig
 
 
-def bf(u16):
-    return (np.asarray(u16, np.uint16).astype(np.uint32) << 16).view(np.float32)
+PREC = "fp16"  # set by the `small` fixture
+
+
+def bf(u16, prec=None):
+    """16-bit patterns of the packing precision -> float32."""
+    u = np.asarray(u16, np.uint16)
+    if (prec or PREC) == "fp16":
+        return u.view(np.float16).astype(np.float32)
+    return (u.astype(np.uint32) << 16).view(np.float32)
 
 
 def unpack_conv(pk):  # [9][4][8][64][8] -> [9][n][c]
@@ -32,11 +39,13 @@ def conv_from_taps(x, Wt, bias):  # x [B, C, H, W], Wt [9][n][c]
     return out + bias.reshape(1, -1, 1, 1)
 
 
-@pytest.fixture(scope="module")
-def small():
+@pytest.fixture(scope="module", params=["fp16", "bf16"])
+def small(request):
+    global PREC
+    PREC = request.param
     cfg = GmzConfig(BOARD_SIZE=6, NUM_RES_BLOCKS=2)
     sd = W.synthetic_state_dict(cfg, seed=9, with_projection=False)
-    return cfg, sd, N.pack_weights(sd, cfg)
+    return cfg, sd, N.pack_weights(sd, cfg, request.param)
 
 
 def test_output_channel_is_a_permutation_in_16_byte_chunks():
@@ -55,7 +64,7 @@ def test_conv_pack_inverts(small):
     s, _ = N.fold_bn(sd, "representation_net.resblocks.0.bn1")
     wf = sd["representation_net.resblocks.0.conv1.weight"] * s[:, None, None, None]
     got = unpack_conv(pk["repr_convs"][0])
-    want = bf(N._bf16_bits(wf.transpose(2, 3, 0, 1).reshape(9, 128, 128)))
+    want = bf(N._e16_bits(wf.transpose(2, 3, 0, 1).reshape(9, 128, 128), PREC))
     assert (got == want).all()
 
 
@@ -113,11 +122,12 @@ def test_packed_emulation_matches_oracle(small):
     p, v, h = netref.initial_inference(sd, obs)
     ep, ev, eh, _ = emulate(pk, cfg, obs=obs)
     scale = np.abs(p).max()
-    assert np.abs(ep - p).max() <= 0.02 * scale + 1e-3
-    assert np.abs(ev - v).max() <= 0.02
+    tol = 0.003 if PREC == "fp16" else 0.02  # weight rounding only: 2^-11 vs 2^-8 relative
+    assert np.abs(ep - p).max() <= tol * scale + 1e-3
+    assert np.abs(ev - v).max() <= tol
     acts = np.array([0, 17, 35])
     p2, v2, h2, r2 = netref.recurrent_inference(sd, h, acts)
     ep2, ev2, eh2, er2 = emulate(pk, cfg, h=h, action=acts)
-    assert np.abs(ep2 - p2).max() <= 0.02 * np.abs(p2).max() + 1e-3
-    assert np.abs(ev2 - v2).max() <= 0.02 and np.abs(er2 - r2).max() <= 0.02
-    assert np.abs(eh2 - h2).max() <= 0.02 * np.abs(h2).max()
+    assert np.abs(ep2 - p2).max() <= tol * np.abs(p2).max() + 1e-3
+    assert np.abs(ev2 - v2).max() <= tol and np.abs(er2 - r2).max() <= tol
+    assert np.abs(eh2 - h2).max() <= tol * np.abs(h2).max()

@@ -2,6 +2,7 @@
 process): gpu_selfplay_worker -> (GameRecord, [TrainingSlice]) on data_queue -> RecordStore (the
 reference's SQLite format) -> trainer ReplayBuffer -> Trainer steps -> ModelWeightsUpdate on the
 model-update queue -> the worker hot-swaps the new weights between moves."""
+import os
 import queue
 
 import numpy as np
@@ -74,3 +75,23 @@ def test_selfplay_records_train_and_hot_swap(tmp_path):
     gpu_selfplay_worker(0, 0, dq2, queue.Queue(), queue.Queue(), _Ev(), num_games=16, cfg=cfg, max_moves=12,
                         state_dict=sd0, model_update_queue=mq, emit_move_notices=False)
     assert mq.empty(), "the worker did not consume the ModelWeightsUpdate"
+
+
+def test_bench_spawns_its_own_ranks_gloo_rehearsal():
+    """`python bench.py --gpus 2` with no external launcher starts 2 rank processes (here sharing the
+    one GPU over gloo) and rank 0 prints ONE line with n_gpus 2 and the global game count."""
+    import json
+    import subprocess
+    import sys
+    from conftest import REPO
+    env = dict(os.environ, GMZ_DIST_BACKEND="gloo")
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--net", "hash", "--games", "64",
+                        "--size", "9", "--sims", "50", "--steps", "2", "--warmup", "1", "--trainer-steps", "0"],
+                       env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [l for l in p.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, p.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["global_games"] == 128 and d["config"]["ranks"] == 2
+    assert "world_size=2" in p.stderr

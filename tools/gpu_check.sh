@@ -4,7 +4,7 @@
 TAG=${1:-x}
 OUT=gpurun_out/check_$TAG
 mkdir -p $OUT
-timeout -k 10 900 python -m pytest tests -m gpu -x -q > $OUT/pytest.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1
 echo "pytest rc=$? $(tail -1 $OUT/pytest.log)"
 timeout -k 10 300 python bench.py --steps 4 --warmup 1 --no-cpu-baseline > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail -5 $OUT/bench.err; exit 1; }
 python -c "import json; d=json.load(open('$OUT/bench.json')); r=d['roofline']; print('moves/s %.1f  ms/step %.1f  tower %.3f ms  frac %.3f' % (d['value'], d['ms_per_step'], r['mean_launch_ms'], r['frac']))"
