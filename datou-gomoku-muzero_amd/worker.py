@@ -36,21 +36,108 @@ from . import records as R
 from .config import from_any
 
 
-def _board_state(board, player, last_move):
-    """game.py:12-17 on the host (records keep the observation the search saw)."""
-    obs = np.zeros((3,) + board.shape, dtype=np.float32)
-    obs[0] = board == player
-    obs[1] = board == -player
-    if last_move is not None:
-        obs[2, last_move[0], last_move[1]] = 1
+def board_states_to_obs(boards, players, last_moves, H):
+    """game.py:12-17 for a whole game at once: boards int8[n, A], players int8[n], last_moves int32[n]
+    (-1 = none) -> float32 [n, 3, H, H] (the observation the search saw at each move)."""
+    n = boards.shape[0]
+    b = boards.reshape(n, H, H)
+    p = players.reshape(n, 1, 1)
+    obs = np.zeros((n, 3, H, H), dtype=np.float32)
+    obs[:, 0] = b == p
+    obs[:, 1] = b == -p
+    has = last_moves >= 0
+    obs[np.nonzero(has)[0], 2, last_moves[has] // H, last_moves[has] % H] = 1
     return obs
 
 
-class _Game:
-    __slots__ = ("obs", "actions", "policies", "values", "boards")
+class GameHistory:
+    """Per-game move history kept on the device, harvested one move behind (no per-move host sync).
 
-    def __init__(self):
-        self.obs, self.actions, self.policies, self.values, self.boards = [], [], [], [], []
+    Every move appends, for each game, the position the search saw (board, player to move, last
+    move), the search's improved policy (f64), root value and action at index move_count of the game's
+    row in one of two banks.  ``after_play`` snapshots the move's status / move counts / missed-win
+    counters / banks into pinned host buffers (async copies + an event) and flips the bank of every
+    game that just ended, so the next game of that slot writes the other bank.  ``harvest`` (called
+    after the NEXT move has been queued) waits for that event — already passed by then — and copies
+    each finished game's rows to the host with DMA copies on a side stream.  A bank is rewritten only
+    when its slot's next game ends too, at least 2*N_IN_ROW-1 moves later, long after the harvest."""
+
+    def __init__(self, G, A, device, min_game_len=9):
+        assert min_game_len >= 2, "a bank must survive one move after its game ended"
+        L = A  # a game has at most A moves
+        self.G, self.A, self.L, self.dev = G, A, L, device
+        z = lambda *sh, dt: torch.zeros(*sh, dtype=dt, device=device)  # noqa: E731
+        self.board = z(2, G, L, A, dt=torch.int8)
+        self.pol = z(2, G, L, A, dt=torch.float64)
+        self.val = z(2, G, L, dt=torch.float32)
+        self.act = z(2, G, L, dt=torch.int32)
+        self.player = z(2, G, L, dt=torch.int8)
+        self.last = z(2, G, L, dt=torch.int32)
+        self.bank = z(G, dt=torch.int64)
+        self.gidx = torch.arange(G, device=device)
+        self.side = torch.cuda.Stream(device)
+        self.k = 0
+        pin = lambda dt: torch.zeros(G, dtype=dt).pin_memory()  # noqa: E731
+        self.snaps = [dict(status=pin(torch.int8), mc=pin(torch.int32), bank=pin(torch.int64), mf=pin(torch.int32),
+                           mt=pin(torch.int32), act=pin(torch.int32), ev=None) for _ in range(2)]
+
+    def record(self, boards, players, last_moves, move_counts, policy, value, action):
+        """Append this move's search inputs/outputs (all device tensors, before the move is played)."""
+        i = (self.bank, self.gidx, move_counts.long().clamp(0, self.L - 1))
+        self.board[i] = boards.reshape(self.G, self.A)
+        self.player[i] = players
+        self.last[i] = last_moves
+        self.pol[i] = policy
+        self.val[i] = value
+        self.act[i] = action
+
+    def after_play(self, status, move_counts, action, missed_f, missed_t):
+        """Snapshot the move's results (async) and start the next game of every finished slot in the
+        other bank; the missed-win counters of finished games restart from zero."""
+        sn = self.snaps[self.k & 1]
+        self.k += 1
+        for key, t in (("status", status), ("mc", move_counts), ("bank", self.bank), ("mf", missed_f),
+                       ("mt", missed_t), ("act", action)):
+            sn[key].copy_(t, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        sn["ev"] = ev
+        ended = (status != 2) & (status != 3)
+        missed_f.masked_fill_(ended, 0)
+        missed_t.masked_fill_(ended, 0)
+        self.bank ^= ended.long()
+        return sn
+
+    def harvest(self, sn):
+        """Finished games of snapshot ``sn`` -> list of (game index, winner, n_moves, missed_fives,
+        missed_totals, boards int8[n,A], players int8[n], last_moves int32[n], policies f64[n,A],
+        values f32[n], actions int32[n]) on the host.  Games whose search found no legal move
+        (action -1, workers.py:169-170) are abandoned without a record, as the reference does."""
+        if sn is None or sn["ev"] is None:
+            return []
+        sn["ev"].synchronize()
+        st = sn["status"].numpy()
+        fin = np.nonzero((st != 2) & (st != 3))[0]
+        out = []
+        if len(fin) == 0:
+            return out
+        mc, bank, act = sn["mc"].numpy(), sn["bank"].numpy(), sn["act"].numpy()
+        jobs = []
+        with torch.cuda.stream(self.side):
+            self.side.wait_event(sn["ev"])
+            for g in fin:
+                if act[g] < 0:
+                    continue
+                n, bk = int(mc[g]) + 1, int(bank[g])
+                host = [torch.empty((n,) + tuple(t.shape[3:]), dtype=t.dtype, pin_memory=True)
+                        for t in (self.board, self.player, self.last, self.pol, self.val, self.act)]
+                for h, t in zip(host, (self.board, self.player, self.last, self.pol, self.val, self.act)):
+                    h.copy_(t[bk, g, :n], non_blocking=True)
+                jobs.append((int(g), int(st[g]), n, int(sn["mf"][g]), int(sn["mt"][g]), host))
+        self.side.synchronize()
+        for g, winner, n, mf, mt, host in jobs:
+            out.append((g, winner, n, mf, mt) + tuple(h.numpy() for h in host))
+        return out
 
 
 def gpu_selfplay_worker(worker_id, worker_mode, data_queue, log_status_queue, ui_queue, shutdown_event,
@@ -58,7 +145,7 @@ def gpu_selfplay_worker(worker_id, worker_mode, data_queue, log_status_queue, ui
                         latest_model_step=None, log_queue=None, pause_event=None, *, device=0, num_games=1024,
                         model_update_queue=None, initial_model_requests_queue=None, state_dict=None, cfg=None,
                         seed=0, max_moves=None, emit_move_notices=True, db_path="outputs/training_state.db",
-                        reanalysis_games=64):
+                        reanalysis_games=64, precision="fp16", move_times=None):
     logger = logging.getLogger("GpuSelfPlay-%s" % worker_id)
     if log_queue is not None:
         try:
@@ -86,11 +173,11 @@ def gpu_selfplay_worker(worker_id, worker_mode, data_queue, log_status_queue, ui
     if state_dict is None:
         state_dict = W.synthetic_state_dict(c, seed=seed, with_projection=False)
     G = int(num_games)
-    net = N.GomokuNetHip(state_dict, c, num_slots=G * (c.NUM_SIMULATIONS + 2), max_rows=G)
+    net = N.GomokuNetHip(state_dict, c, num_slots=G * (c.NUM_SIMULATIONS + 2), max_rows=G, precision=precision)
     eng = E.BatchedSelfPlayEngine(c, num_games=G, net=net, seed=seed + 7919 * int(worker_id))
     eng.reset_games()
     H, A = c.BOARD_SIZE, c.ACTION_SPACE_SIZE
-    games = [_Game() for _ in range(G)]
+    hist = GameHistory(G, A, eng.device, min_game_len=2 * c.N_IN_ROW - 1)
     pool = ThreadPoolExecutor(max_workers=4)
     moves_done = 0
     # missed-win counters of workers.py:191-203, accumulated on the device move by move by the batched
@@ -98,13 +185,15 @@ def gpu_selfplay_worker(worker_id, worker_mode, data_queue, log_status_queue, ui
     missed_f = torch.zeros(G, dtype=torch.int32, device=eng.device)
     missed_t = torch.zeros(G, dtype=torch.int32, device=eng.device)
 
-    def finish_game(g, winner, move_count, mf, mt):
-        record, slices = R.build_game_record(g.obs, g.actions, g.policies, g.values, g.boards, winner,
-                                             c.DISCOUNT, c.N_STEPS, c.NUM_UNROLL_STEPS)
+    def finish_game(winner, n, mf, mt, boards, players, lasts, pols, vals, acts):
+        obs = board_states_to_obs(boards, players, lasts, H)
+        record, slices = R.build_game_record(list(obs), [int(x) for x in acts], list(pols), list(vals),
+                                             list(boards.reshape(n, H, H)), winner, c.DISCOUNT, c.N_STEPS,
+                                             c.NUM_UNROLL_STEPS)
         version = latest_model_step.value if latest_model_step is not None else 0
         if slices:
             data_queue.put((record, slices, version))
-        status = R.SelfPlayStatus(move_count, mf, mt)
+        status = R.SelfPlayStatus(n, mf, mt)
         if log_status_queue is not None:
             log_status_queue.put(status)
         if ui_queue is not None:
@@ -113,7 +202,23 @@ def gpu_selfplay_worker(worker_id, worker_mode, data_queue, log_status_queue, ui
         if trainer_event_queue is not None:
             trainer_event_queue.put(R.GameCompletedNotice())
 
+    def move_notices(n):
+        for _ in range(n):
+            if ui_queue.full():
+                break
+            ui_queue.put(R.SelfPlayMove())
+
+    def drain(sn):
+        """Host side of a played move (one move behind the device): per-move UI notices, finished games."""
+        if sn is None:
+            return
+        for item in hist.harvest(sn):
+            pool.submit(finish_game, *item[1:])
+        if emit_move_notices and ui_queue is not None:
+            pool.submit(move_notices, int((sn["act"].numpy() >= 0).sum()))
+
     reanalyser, store = None, None
+    pending = None  # snapshot of the last played move, harvested after the next move is queued
 
     logger.info("GPU self-play worker %s: %d games on cuda:%d" % (worker_id, G, device))
     while not shutdown_event.is_set():
@@ -149,36 +254,21 @@ def gpu_selfplay_worker(worker_id, worker_mode, data_queue, log_status_queue, ui
         b, p, lm, mc = eng.game_state()
         pol, val, act = eng.search()
         eng.winning_scan(b, p, act, counters=(missed_f, missed_t))  # position before the move
+        hist.record(b, p, lm, mc, pol, val, act)
         status = eng.play(reset_finished=True)
-        torch.cuda.synchronize()
-        mf_all, mt_all = missed_f.cpu().numpy(), missed_t.cpu().numpy()
-        b, p, lm, mc = b.cpu().numpy(), p.cpu().numpy(), lm.cpu().numpy(), mc.cpu().numpy()
-        pol, val, act, status = pol.cpu().numpy(), val.cpu().numpy(), act.cpu().numpy(), status.cpu().numpy()
-        ended = torch.from_numpy((status != 2) & (status != 3)).to(eng.device)
-        missed_f.masked_fill_(ended, 0)
-        missed_t.masked_fill_(ended, 0)
-        for i in range(G):
-            a = int(act[i])
-            if a < 0:  # workers.py:169-170 (no legal move)
-                games[i] = _Game()
-                continue
-            gm = games[i]
-            last = None if lm[i] < 0 else (int(lm[i]) // H, int(lm[i]) % H)
-            gm.obs.append(_board_state(b[i], int(p[i]), last))
-            gm.policies.append(pol[i].copy())
-            gm.values.append(np.float32(val[i]))
-            gm.actions.append(a)
-            gm.boards.append(b[i].copy())
-            if emit_move_notices and ui_queue is not None and not ui_queue.full():
-                ui_queue.put(R.SelfPlayMove())
-            st = int(status[i])
-            if st != 2:
-                pool.submit(finish_game, gm, st, int(mc[i]) + 1, int(mf_all[i]), int(mt_all[i]))
-                games[i] = _Game()
+        sn = hist.after_play(status, mc, act, missed_f, missed_t)
+        drain(pending)  # the previous move's host work runs while this move is on the device
+        pending = sn
         moves_done += 1
+        if move_times is not None:  # tools/worker_bench.py: host clock after each move was queued
+            move_times.append(time.perf_counter())
         if max_moves is not None and moves_done >= max_moves:
             break
+    drain(pending)
     pool.shutdown(wait=True)
+    if move_times is not None:
+        torch.cuda.synchronize()
+        move_times.append(time.perf_counter())  # every move played and every record posted
     eng.close()
     if reanalyser is not None:
         reanalyser.eng.close()

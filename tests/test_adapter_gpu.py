@@ -180,3 +180,64 @@ def test_recurrent_timeout_retries_the_wave(M):
     assert outs[0][2] == outs[1][2] >= 0 and outs[0][1] == outs[1][1]
     assert np.array_equal(outs[0][0], outs[1][0])
     assert len(logs[1]) == len(logs[0]) + 1 and logs[1][4] == logs[1][3]  # the dropped request, re-sent
+
+
+def test_worker_records_equal_a_synchronous_loop(M):
+    """The worker's device-side history harvested one move behind (worker.GameHistory) yields exactly
+    the records of a plain synchronous loop over the same engine (same seed, same weights) that copies
+    every move's position / policy / value / action to the host before the next move."""
+    from datou_gomoku_muzero_amd import engine as E, network as N, records as R, weights as W
+    from datou_gomoku_muzero_amd.worker import gpu_selfplay_worker
+    mcts, GmzConfig = M
+    cfg = GmzConfig(BOARD_SIZE=6, NUM_SIMULATIONS=16, NUM_RES_BLOCKS=1)
+    G, moves, seed = 8, 45, 5
+
+    class Ev:
+        def is_set(self):
+            return False
+
+    dq = queue.Queue()
+    gpu_selfplay_worker(0, None, dq, None, None, Ev(), num_games=G, cfg=cfg, max_moves=moves, seed=seed)
+    got = []
+    while not dq.empty():
+        got.append(dq.get())
+    # the synchronous reference loop
+    sd = W.synthetic_state_dict(cfg, seed=seed, with_projection=False)
+    net = N.GomokuNetHip(sd, cfg, num_slots=G * 18, max_rows=G)
+    eng = E.BatchedSelfPlayEngine(cfg, num_games=G, net=net, seed=seed)
+    eng.reset_games()
+    hist = [dict(obs=[], act=[], pol=[], val=[], brd=[]) for _ in range(G)]
+    want = []
+    for _ in range(moves):
+        b, p, lm, mc = eng.game_state()
+        pol, val, act = eng.search()
+        st = eng.play(reset_finished=True)
+        torch.cuda.synchronize()
+        b, p, lm = b.cpu().numpy(), p.cpu().numpy(), lm.cpu().numpy()
+        pol, val, act, st = pol.cpu().numpy(), val.cpu().numpy(), act.cpu().numpy(), st.cpu().numpy()
+        for g in range(G):
+            h = hist[g]
+            o = np.zeros((3, 6, 6), np.float32)
+            o[0], o[1] = b[g] == p[g], b[g] == -p[g]
+            if lm[g] >= 0:
+                o[2, lm[g] // 6, lm[g] % 6] = 1
+            h["obs"].append(o), h["act"].append(int(act[g])), h["pol"].append(pol[g].copy())
+            h["val"].append(np.float32(val[g])), h["brd"].append(b[g].copy())
+            if st[g] != 2:
+                want.append(R.build_game_record(h["obs"], h["act"], h["pol"], h["val"], h["brd"], int(st[g]),
+                                                cfg.DISCOUNT, cfg.N_STEPS, cfg.NUM_UNROLL_STEPS))
+                hist[g] = dict(obs=[], act=[], pol=[], val=[], brd=[])
+    eng.close()
+    assert len(got) == len(want) > 0
+
+    def key(rec):
+        return (len(rec.actions), tuple(rec.actions))
+    got = sorted(((r, s) for r, s, _ in got), key=lambda x: key(x[0]))
+    want = sorted(want, key=lambda x: key(x[0]))
+    for (r1, s1), (r2, s2) in zip(got, want):
+        assert r1.actions == r2.actions and r1.rewards == r2.rewards and r1.values == r2.values
+        for f in ("observations", "policies", "board_states"):
+            assert all(np.array_equal(x, y) for x, y in zip(getattr(r1, f), getattr(r2, f))), f
+        for a, b in zip(s1, s2):
+            for x, y in zip(a, b):
+                assert np.array_equal(np.asarray(x), np.asarray(y))
