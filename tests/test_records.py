@@ -4,7 +4,7 @@ winning-move scanner (workers.py:49-123, fixture winmoves.npz)."""
 import numpy as np
 
 from datou_gomoku_muzero_amd import records as R
-from datou_gomoku_muzero_amd.worker import _board_state
+from datou_gomoku_muzero_amd.worker import board_states_to_obs
 
 
 def test_game_record_and_slices_match_reference_worker(golden):
@@ -12,13 +12,16 @@ def test_game_record_and_slices_match_reference_worker(golden):
     seq = d["in_seq"].tolist()
     H = 6
     board = np.zeros((H, H), np.int8)
-    player, last = 1, None
-    obs, boards = [], []
-    for a in seq:
-        obs.append(_board_state(board, player, last))
+    player, last = 1, -1
+    boards, players, lasts = [], [], []
+    for a in seq:  # the positions the worker's device history holds (worker.GameHistory)
         boards.append(board.copy())
+        players.append(player)
+        lasts.append(last)
         board[a // H, a % H] = player
-        last, player = (a // H, a % H), -player
+        last, player = a, -player
+    obs = list(board_states_to_obs(np.array(boards).reshape(len(seq), -1), np.array(players, np.int8),
+                                   np.array(lasts, np.int32), H))
     pols = [p for p in d["in_pols"]]
     vals = [np.float32(v) for v in d["in_vals"]]
     record, slices = R.build_game_record(obs, seq, pols, vals, boards, winner=1)
