@@ -16,26 +16,29 @@ import torch  # noqa: E402
 import torch.multiprocessing as mp  # noqa: E402
 
 
-def consumer(qs, stop, counts):
-    """Drain every queue (unpickling the payloads) until told to stop and the queues are empty."""
-    import queue as Q
-    n = {k: 0 for k in qs}
-    slices = 0
-    while True:
-        busy = False
-        for k, q in qs.items():
-            try:
-                item = q.get(timeout=0.01)
-            except Q.Empty:
-                continue
-            busy = True
-            n[k] += 1
+def consumer(qs, counts):
+    """One reader thread per queue (blocking get, unpickling every payload) until its None sentinel."""
+    import threading
+    n, slices = {}, {}
+
+    def read(k, q):
+        c = s = 0
+        while True:
+            item = q.get()
+            if item is None:
+                break
+            c += 1
             if k == "data":
-                slices += len(item[1])
-        if not busy and stop.is_set():
-            break
+                s += len(item[1])
+        n[k], slices[k] = c, s
+
+    th = [threading.Thread(target=read, args=kq) for kq in qs.items()]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
     counts.update(n)
-    counts["slices"] = slices
+    counts["slices"] = slices.get("data", 0)
 
 
 class Ev:
@@ -47,6 +50,9 @@ class Ev:
 
 
 def main():
+    import faulthandler
+    import threading
+    faulthandler.dump_traceback_later(90, repeat=True)  # a stuck run names where it waits
     ap = argparse.ArgumentParser()
     ap.add_argument("--games", type=int, default=1024)
     ap.add_argument("--moves", type=int, default=24)
@@ -60,24 +66,51 @@ def main():
     stop = ctx.Event()
     mgr = ctx.Manager()
     counts = mgr.dict()
-    cons = ctx.Process(target=consumer, args=(qs, stop, counts))
+    cons = ctx.Process(target=consumer, args=(qs, counts))
     cons.start()
     from datou_gomoku_muzero_amd.worker import gpu_selfplay_worker
     from datou_gomoku_muzero_amd.config import GmzConfig
     cfg = GmzConfig(BOARD_SIZE=a.size, NUM_SIMULATIONS=a.sims)
     times = []
     t0 = time.perf_counter()
+
+    def progress():
+        while not stop.is_set():
+            time.sleep(10)
+            print("worker_bench: %d moves after %.0f s" % (len(times), time.perf_counter() - t0), file=sys.stderr, flush=True)
+    threading.Thread(target=progress, daemon=True).start()
     gpu_selfplay_worker(0, None, qs["data"], qs["log"], qs["ui"], Ev(), trainer_event_queue=qs["trainer"],
                         num_games=a.games, cfg=cfg, max_moves=a.warmup + a.moves,
                         emit_move_notices=not a.no_move_notices, move_times=times)
+    print("worker_bench: worker done after %.1f s, waiting for the consumer" % (time.perf_counter() - t0), file=sys.stderr,
+          flush=True)
     stop.set()
+    for q in qs.values():
+        q.put(None)
     cons.join(timeout=300)
+    t_cons = time.perf_counter() - t0
     steady = times[-1] - times[a.warmup - 1]
+    # the bare engine on the same box and workload (bench.py's step: search + play), for the ratio
+    from datou_gomoku_muzero_amd import engine as E, network as N, weights as W
+    sd = W.synthetic_state_dict(cfg, seed=0, with_projection=False)
+    net = N.GomokuNetHip(sd, cfg, num_slots=a.games * (a.sims + 2), max_rows=a.games)
+    eng = E.BatchedSelfPlayEngine(cfg, num_games=a.games, net=net, seed=0)
+    eng.reset_games()
+    for i in range(a.warmup + a.moves):
+        if i == a.warmup:
+            torch.cuda.synchronize()
+            te = time.perf_counter()
+        eng.search()
+        eng.play(reset_finished=True)
+    torch.cuda.synchronize()
+    engine_rate = a.games * a.moves / (time.perf_counter() - te)
     print(json.dumps({"metric": "drop-in worker self-play moves/sec (%dx%d, %d sims)" % (a.size, a.size, a.sims),
                       "value": a.games * a.moves / steady, "unit": "moves/s", "games": a.games, "moves": a.moves,
                       "warmup_moves": a.warmup, "steady_s": steady, "setup_and_warmup_s": times[a.warmup - 1] - t0,
                       "queues": "torch.multiprocessing (spawn) Queues, main.py sizes; consumer process unpickles",
-                      "move_notices": not a.no_move_notices, "messages": dict(counts)}))
+                      "move_notices": not a.no_move_notices, "messages": dict(counts),
+                      "consumer_done_s": t_cons, "engine_only_moves_per_s": engine_rate,
+                      "worker_over_engine": a.games * a.moves / steady / engine_rate}))
 
 
 if __name__ == "__main__":
