@@ -27,6 +27,10 @@ Prints ONE JSON line on rank 0 (schema: the driver contract) including
   trainer       : config C4's trainer (B = 360 per GPU, 5 unroll steps, PER, fp16 autocast, HIP convs),
                   steps/s after the self-play region, on every rank (DDP: one RCCL gradient all-reduce +
                   the sharded-PER syncs per step), plus the MFMA fraction of its dominant HIP conv;
+  loop_c4       : config C4 composed on every rank (datou-gomoku-muzero_amd/loop.py): self-play moves of
+                  G games -> finished games' slices into the rank's PER shard -> DDP trainer steps ->
+                  periodic weight push (RCCL broadcast) into the self-play network; moves/s and trainer
+                  steps/s of the whole job over the timed iterations;
   cpu_baseline  : the C oracle's search (oracle/gmz_oracle.c) with the float32 numpy network
                   (oracle/netref.py) on the same weights, rank 0 / N=1 only, bounded sample.
 """
@@ -98,6 +102,16 @@ def parse(argv=None):
     ap.add_argument("--trainer-warmup", type=int, default=6)
     ap.add_argument("--trainer-batch", type=int, default=360)
     ap.add_argument("--trainer-buffer", type=int, default=4096, help="synthetic slices per rank's PER shard")
+    ap.add_argument("--loop-iters", type=int, default=20, help="timed iterations of the C4 loop (0: no loop leg)")
+    ap.add_argument("--loop-warmup", type=int, default=6)
+    ap.add_argument("--loop-games", type=int, default=1024, help="self-play games per GPU inside the C4 loop")
+    ap.add_argument("--loop-moves-per-iter", type=int, default=1)
+    ap.add_argument("--loop-train-per-iter", type=int, default=1)
+    ap.add_argument("--loop-update-interval", type=int, default=10,
+                    help="trainer steps between weight pushes (reference MODEL_UPDATE_INTERVAL = 1000; shortened "
+                         "so the timed window contains pushes)")
+    ap.add_argument("--loop-buffer", type=int, default=65536, help="replay shard capacity per rank")
+    ap.add_argument("--loop-prefill", type=int, default=4096, help="synthetic slices in each shard before the loop")
     ap.add_argument("--pmc-file", default=os.path.join(REPO, "profiles", "pmc_tower_latest.json"))
     return ap.parse_args(argv)
 
@@ -224,32 +238,16 @@ def cpu_baseline(args, sd, cfg):
                       % (moves, H, H, args.sims, args.mode, rows, dt)}
 
 
-def synthetic_slices(n, size, unroll, rs):
-    """n TrainingSlice-shaped arrays (replay_buffer.py payload) of random content: sparse 0/1 planes,
-    actions with a random game end (-1 after it), rewards in {-1,0,1}, normalised random policies,
-    values in [-1, 1]."""
-    A = size * size
-    obs = (rs.rand(n, unroll + 1, 3, size, size) < 0.2).astype(np.uint8)
-    act = rs.randint(0, A, (n, unroll)).astype(np.int32)
-    ends = rs.randint(1, unroll + 1, n)
-    act[np.arange(unroll)[None, :] >= ends[:, None]] = -1
-    rew = rs.choice(np.array([-1.0, 0.0, 1.0], np.float32), (n, unroll))
-    pol = rs.exponential(1.0, (n, unroll + 1, A)).astype(np.float32)
-    pol /= pol.sum(-1, keepdims=True)
-    val = rs.uniform(-1, 1, (n, unroll + 1)).astype(np.float32)
-    return obs, act, rew, pol, val
-
-
 def trainer_leg(args, world, rank, dist, backend):
     """Config C4's training step on every rank (DDP when world > 1), timed like the self-play region."""
-    from datou_gomoku_muzero_amd import trainer as T
+    from datou_gomoku_muzero_amd import trainer as T, weights as W
     torch.backends.cudnn.benchmark = True  # MIOpen Find for the convolutions left on MIOpen
     cfg = T.TrainConfig(BOARD_SIZE=args.size, NUM_RES_BLOCKS=args.blocks, PHYSICAL_BATCH_SIZE=args.trainer_batch,
                         TRAIN_BUFFER_SIZE=args.trainer_buffer, ENABLE_PER=True)
     tr = T.Trainer(cfg, device="cuda")
     rb = T.ReplayBuffer(cfg, device="cuda")
     rs = np.random.RandomState(args.seed + 31 * rank)
-    rb.add_arrays(*synthetic_slices(args.trainer_buffer, args.size, cfg.NUM_UNROLL_STEPS, rs))
+    rb.add_arrays(*W.synthetic_slices(args.trainer_buffer, args.size, cfg.NUM_UNROLL_STEPS, rs))
     group = dist if dist is not None else None
     pending = [None]
 
@@ -430,6 +428,24 @@ def main():
         del eng, net
         torch.cuda.empty_cache()
         out["trainer"] = trainer_leg(args, world, rank, dist, backend)
+    if args.loop_iters > 0 and args.net == "hip":
+        from datou_gomoku_muzero_amd.loop import run_c4
+        torch.cuda.empty_cache()
+        d, dt_loop = run_c4(args, rank, world, dist, backend, log=log)
+        dt_loop = collective_max(dt_loop, dist, backend)
+        tot = {k: collective_sum(float(v), dist, backend) for k, v in d.items()}
+        out["loop_c4"] = {
+            "metric": "C4 loop: self-play moves/sec and trainer steps/sec with both running on every GPU",
+            "moves_per_s": tot["moves"] * args.loop_games / dt_loop, "trainer_steps_per_s": d["train_steps"] / dt_loop,
+            "unit": "moves/s, steps/s", "n_gpus": world, "iterations": args.loop_iters, "seconds": dt_loop,
+            "games_per_gpu": args.loop_games, "moves_per_iter": args.loop_moves_per_iter,
+            "train_steps_per_iter": args.loop_train_per_iter, "batch_per_gpu": args.trainer_batch,
+            "finished_games": int(tot["games"]), "slices_added": int(tot["slices"]),
+            "weight_pushes": d["weight_pushes"], "model_update_interval": args.loop_update_interval,
+            "data": "self-play from the trainer's initial weights; each PER shard pre-filled with %d synthetic "
+                    "slices so training starts at once" % args.loop_prefill,
+            "parallelism": "dp%d: self-play + replay shard per GPU; one gradient all-reduce + sharded-PER syncs "
+                           "per step; rank 0 weight broadcast per push" % world}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.net == "hip":
         log("cpu baseline (bounded sample ~%.0f s)..." % args.cpu_baseline_sec)
         out["cpu_baseline"] = cpu_baseline(args, sd, cfg)

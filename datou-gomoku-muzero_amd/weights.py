@@ -111,3 +111,19 @@ def from_torch(sd):
         a = v.detach().cpu().numpy() if hasattr(v, "detach") else np.asarray(v)
         out[k] = a if a.dtype == np.int64 else a.astype(np.float32)
     return out
+
+
+def synthetic_slices(n, size, unroll, rs):
+    """n TrainingSlice-shaped arrays (replay_buffer.py payload) of random content: sparse 0/1 planes,
+    actions with a random game end (-1 after it), rewards in {-1,0,1}, normalised random policies,
+    values in [-1, 1]."""
+    A = size * size
+    obs = (rs.rand(n, unroll + 1, 3, size, size) < 0.2).astype(np.uint8)
+    act = rs.randint(0, A, (n, unroll)).astype(np.int32)
+    ends = rs.randint(1, unroll + 1, n)
+    act[np.arange(unroll)[None, :] >= ends[:, None]] = -1
+    rew = rs.choice(np.array([-1.0, 0.0, 1.0], np.float32), (n, unroll))
+    pol = rs.exponential(1.0, (n, unroll + 1, A)).astype(np.float32)
+    pol /= pol.sum(-1, keepdims=True)
+    val = rs.uniform(-1, 1, (n, unroll + 1)).astype(np.float32)
+    return obs, act, rew, pol, val

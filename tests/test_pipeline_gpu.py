@@ -86,12 +86,41 @@ def test_bench_spawns_its_own_ranks_gloo_rehearsal():
     from conftest import REPO
     env = dict(os.environ, GMZ_DIST_BACKEND="gloo")
     env.pop("WORLD_SIZE", None)
-    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--net", "hash", "--games", "64",
-                        "--size", "9", "--sims", "50", "--steps", "2", "--warmup", "1", "--trainer-steps", "0"],
-                       env=env, capture_output=True, text=True, timeout=240)
-    assert p.returncode == 0, p.stderr[-2000:]
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--games", "64",
+                        "--size", "9", "--sims", "50", "--blocks", "1", "--steps", "2", "--warmup", "1",
+                        "--trainer-steps", "2", "--trainer-warmup", "4", "--trainer-batch", "16", "--trainer-buffer", "64",
+                        "--loop-iters", "4", "--loop-warmup", "4", "--loop-games", "64", "--loop-update-interval", "2",
+                        "--loop-prefill", "64", "--loop-buffer", "4096"],
+                       env=env, capture_output=True, text=True, timeout=280)
+    assert p.returncode == 0, p.stderr[-3000:]
     lines = [l for l in p.stdout.splitlines() if l.startswith("{")]  # (gloo itself prints connection notes)
     assert len(lines) == 1, p.stdout
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["config"]["global_games"] == 128 and d["config"]["ranks"] == 2
     assert "world_size=2" in p.stderr
+    assert d["trainer"]["n_gpus"] == 2 and d["trainer"]["value"] > 0
+    lc = d["loop_c4"]
+    assert lc["n_gpus"] == 2 and lc["trainer_steps_per_s"] > 0 and lc["moves_per_s"] > 0 and lc["weight_pushes"] == 2
+
+
+def test_c4_loop_on_the_gpu_pushes_trained_weights_into_self_play():
+    """loop.C4Loop with the real HIP self-play (single rank): finished games fill the replay shard,
+    the trainer steps, and every push hot-swaps exactly the trainer's weights into the engine's
+    network (its packed tensors equal a fresh packing of the trainer's state_dict)."""
+    from datou_gomoku_muzero_amd import loop as LP, network as N, trainer as T
+    from datou_gomoku_muzero_amd.config import GmzConfig
+    cfg = GmzConfig(BOARD_SIZE=6, NUM_SIMULATIONS=16, NUM_RES_BLOCKS=1)
+    tcfg = T.TrainConfig(BOARD_SIZE=6, NUM_RES_BLOCKS=1, PHYSICAL_BATCH_SIZE=16, TRAIN_BUFFER_SIZE=4096, ENABLE_PER=True)
+    tr = T.Trainer(tcfg, device="cuda", graph=False)
+    sp = LP.SelfPlay(cfg, 32, tr.state_dict_cpu(), seed=3)
+    rb = T.ReplayBuffer(tcfg, device="cuda")
+    lp = LP.C4Loop(sp, tr, rb, tcfg, 16, moves_per_iter=2, train_steps_per_iter=1, model_update_interval=2)
+    st = lp.run(40)
+    torch.cuda.synchronize()
+    assert st["games"] > 0 and st["slices"] == len(rb) and st["train_steps"] > 0
+    assert st["weight_pushes"] == st["train_steps"] // 2 >= 1
+    if st["train_steps"] % 2 == 0:  # the last push is the current trainer state
+        want = N.pack_weights(tr.state_dict_cpu(), cfg, "fp16")
+        for k, v in want.items():
+            assert np.array_equal(sp.net._tensors[k].cpu().numpy(), v), k
+    sp.close()
