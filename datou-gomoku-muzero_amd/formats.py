@@ -9,9 +9,13 @@ Blobs are written exactly as the reference writes them (``pickle.dumps(obj, HIGH
 ``data_structures.GameRecord`` / ``TrainingSlice`` namedtuples holding numpy arrays), and read with a
 RESTRICTED unpickler that resolves only those two classes and numpy's array / dtype / scalar
 constructors: a blob naming anything else is rejected, never executed.  The ``trainer_state`` blob
-(a pickled dict of torch state_dicts and optimiser state, db_manager.py:229-242) is not read: it
-cannot be decoded without executing arbitrary pickled callables, and checkpoints travel as
-state_dicts (weights.py) instead.
+(a pickled dict of torch state_dicts and optimiser / scheduler state, db_manager.py:231-243) is read
+by ``load_trainer_state`` with a second restricted unpickler: only ``collections.OrderedDict``,
+torch's tensor rebuild function and its storage constructor resolve, and the storage bytes are
+decoded by ``torch.load(weights_only=True)`` (the reference's pickled storages otherwise go through
+``torch.storage._load_from_bytes``, an unrestricted ``torch.load``); the result must be the
+reference's dict of tensors, numbers, strings and containers.  ``save_trainer_state`` writes the
+reference's own blob (``pickle.dumps`` of that dict).
 
 Re-analysis bookkeeping (db_manager.py:151-227): eligible-game count, lock of the oldest eligible
 game(s), the sliding-window rewrite of a re-analysed game's slices (same blobs as the reference's
@@ -117,6 +121,58 @@ def dumps(obj):
     elif type(obj).__name__ == "TrainingSlice" and not isinstance(obj, T):
         obj = T(*obj)
     return pickle.dumps(obj, protocol=pickle.HIGHEST_PROTOCOL)
+
+
+def _storage_from_bytes(b):
+    """torch.storage._load_from_bytes restated with the weights-only loader."""
+    import torch
+    return torch.load(io.BytesIO(b), weights_only=True)
+
+
+class _TrainerStateUnpickler(pickle.Unpickler):
+    def find_class(self, module, name):
+        import collections
+        import torch
+        if (module, name) == ("collections", "OrderedDict"):
+            return collections.OrderedDict
+        if (module, name) == ("torch._utils", "_rebuild_tensor_v2"):
+            return torch._utils._rebuild_tensor_v2
+        if (module, name) == ("torch.storage", "_load_from_bytes"):
+            return _storage_from_bytes
+        raise UnsafeBlobError("trainer_state blob references %s.%s: only tensors, OrderedDict and plain "
+                              "containers are decoded" % (module, name))
+
+    def persistent_load(self, pid):
+        raise UnsafeBlobError("trainer_state blob uses persistent ids (not a plain pickle of a dict)")
+
+
+def _check_plain(obj, depth=0):
+    import torch
+    if depth > 16:
+        raise UnsafeBlobError("trainer_state nests too deep")
+    if isinstance(obj, dict):
+        for k, v in obj.items():
+            _check_plain(k, depth + 1)
+            _check_plain(v, depth + 1)
+    elif isinstance(obj, (list, tuple)):
+        for v in obj:
+            _check_plain(v, depth + 1)
+    elif not (obj is None or isinstance(obj, (bool, int, float, str, bytes, torch.Tensor))):
+        raise UnsafeBlobError("trainer_state holds a %s" % type(obj).__name__)
+
+
+def loads_trainer_state(blob):
+    """Decode a trainer_state blob (db_manager.py:238-243) without executing anything it names."""
+    obj = _TrainerStateUnpickler(io.BytesIO(bytes(blob))).load()
+    if not isinstance(obj, dict) or "model_state_dict" not in obj:
+        raise UnsafeBlobError("trainer_state blob is not the reference's state dict")
+    _check_plain(obj)
+    return obj
+
+
+def dumps_trainer_state(state):
+    """Encode as db_manager.py:233 does: pickle.dumps(state_dict, HIGHEST_PROTOCOL)."""
+    return pickle.dumps(state, protocol=pickle.HIGHEST_PROTOCOL)
 
 
 class RecordStore:
@@ -240,6 +296,17 @@ class RecordStore:
             with self.conn:
                 self.conn.execute("UPDATE games SET status = 'PENDING' WHERE game_id = ?", (game_id,))
             return False
+
+    def save_trainer_state(self, state):
+        """db_manager.py:231-236: the whole trainer state as one blob (INSERT OR REPLACE)."""
+        self.conn.execute("INSERT OR REPLACE INTO trainer_state (key, state_blob) VALUES (?, ?)",
+                          ("singleton_state", dumps_trainer_state(state)))
+        self.conn.commit()
+
+    def load_trainer_state(self):
+        """db_manager.py:238-243 (restricted decoding: ``loads_trainer_state``); None when absent."""
+        row = self.conn.execute("SELECT state_blob FROM trainer_state WHERE key = ?", ("singleton_state",)).fetchone()
+        return loads_trainer_state(row[0]) if row else None
 
     def unlock_game_on_error(self, game_id):
         """db_manager.py:223-227."""

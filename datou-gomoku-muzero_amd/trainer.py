@@ -484,6 +484,9 @@ class _Trunk(nn.Module):
 
     def __init__(self, cin, c, blocks):
         super().__init__()
+        self._build(cin, c, blocks)
+
+    def _build(self, cin, c, blocks):
         self.conv, self.bn = _conv3(cin, c), nn.BatchNorm2d(c, eps=1e-4)
         self.resblocks = nn.Sequential(*[_Block(c) for _ in range(blocks)])
 
@@ -514,8 +517,11 @@ class _Dynamics(_Trunk):
     EMB = 16  # network.py:81 action embedding planes
 
     def __init__(self, c, H, blocks, hd, rbins):
-        super().__init__(c + self.EMB, c, blocks)
+        nn.Module.__init__(self)
+        # registration order of network.py:79-87 (action_embed_conv, conv, bn, resblocks, reward_fc):
+        # parameters() order is the index order of a reference optimiser checkpoint
         self.action_embed_conv = nn.Conv2d(1, self.EMB, 1, bias=False)
+        self._build(c + self.EMB, c, blocks)
         self.reward_fc = nn.Sequential(nn.Linear(c * H * H, hd), nn.ReLU(), nn.Linear(hd, rbins))
 
     def forward(self, h, a, mask=None):
@@ -1055,6 +1061,43 @@ class Trainer:
         if not sync:
             return logs.detach().clone(), td
         return tuple(float(x) for x in logs.tolist()), td
+
+    def load_trainer_state(self, state):
+        """Resume from the reference's trainer checkpoint (workers.py:469-475; the dict
+        formats.RecordStore.load_trainer_state decodes): model, optimiser moments and step counts,
+        scheduler position, train_step_count.  The target network restarts as a copy of the model
+        (workers.py:491).  Execution flags stay this trainer's (fused, capturable, device lr)."""
+        self.model.load_state_dict(state["model_state_dict"])
+        self.target.load_state_dict(self.model.state_dict())
+        self.opt.load_state_dict(state["optimizer_state_dict"])
+        cuda = self.device.type == "cuda"
+        for g in self.opt.param_groups:
+            lr = float(g["lr"])
+            g["lr"] = torch.tensor(lr, device=self.device) if cuda else lr
+            g["fused"], g["capturable"], g["foreach"] = (True, True, None) if cuda else (None, False, None)
+        for st in self.opt.state.values():
+            if "step" in st:
+                st["step"] = torch.as_tensor(float(st["step"]), dtype=torch.float32,
+                                             device=self.device if cuda else "cpu")
+        self.sched.load_state_dict(state["scheduler_state_dict"])
+        self.step_count = int(state.get("train_step_count", 0))
+        self.games_completed = int(state.get("games_completed_count", 0))
+        self._graphs, self._static = None, None  # re-captured on the next step
+
+    def trainer_state(self, games_completed_count=None):
+        """The reference's checkpoint dict (workers.py:594-597), CPU tensors, optimiser state in the
+        reference's form (float lr, CPU step counts, no fused/capturable flags) so either side can
+        resume from it; store with formats.RecordStore.save_trainer_state."""
+        opt = self.opt.state_dict()
+        opt = {"state": {i: {k: (v.detach().cpu().reshape(()) if k == "step" else v.detach().cpu())
+                             for k, v in st.items()} for i, st in opt["state"].items()},
+               "param_groups": [dict(g, lr=float(g["lr"]), fused=None, capturable=False, foreach=None)
+                                for g in opt["param_groups"]]}
+        sch = self.sched.state_dict()
+        return {"model_state_dict": self.state_dict_cpu(), "optimizer_state_dict": opt, "scheduler_state_dict": sch,
+                "train_step_count": self.step_count,
+                "games_completed_count": getattr(self, "games_completed", 0) if games_completed_count is None
+                else int(games_completed_count)}
 
     def state_dict_cpu(self):
         """ModelWeightsUpdate payload (workers.py:587-593) for the self-play engines."""

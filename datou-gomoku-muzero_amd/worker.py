@@ -13,9 +13,10 @@ hot-swap between moves (workers.py:332-335); otherwise ``state_dict`` (or seeded
 ``worker_mode`` 1 (re-analysis, workers.py:243-305; off by default, config.py:85): the worker locks up to
 ``reanalysis_games`` stored games of the reference's SQLite database at a time (``db_path``), searches all
 their positions in batches of ``num_games`` on a second engine that shares the network, rewrites their
-slices and posts ``ReAnalysisStatus`` (reanalysis.py).  The current trainer step is
-``latest_model_step.value`` (the reference reads it from the pickled trainer_state blob, which is not
-decoded here; formats.py).  Self-play games in progress are kept and resume in mode 0.
+slices and posts ``ReAnalysisStatus`` (reanalysis.py).  The current trainer step is the stored
+checkpoint's ``train_step_count``, as the reference reads it (workers.py:247-249; decoded by
+formats.RecordStore.load_trainer_state's restricted loader); no checkpoint yet -> wait 5 s.  Self-play
+games in progress are kept and resume in mode 0.
 
 Launch from main.py's ``process_definitions`` in place of the workers + server, e.g.
     mp.Process(target=gpu_selfplay_worker, args=(0, worker_mode, data_queue, log_status_queue,
@@ -238,7 +239,15 @@ def gpu_selfplay_worker(worker_id, worker_mode, data_queue, log_status_queue, ui
                 reanalyser = RA.Reanalyser(E.BatchedSelfPlayEngine(c, num_games=G, net=net,
                                                                    seed=seed + 104729 * (int(worker_id) + 1)))
                 store = F.RecordStore(db_path)
-            step = latest_model_step.value if latest_model_step is not None else 0
+            try:  # workers.py:247-249: the trainer step comes from the stored checkpoint
+                ts = store.load_trainer_state()
+            except Exception as e:
+                logger.error("Worker %s: unreadable trainer_state: %s" % (worker_id, e))
+                ts = None
+            if not ts:
+                time.sleep(5)
+                continue
+            step = int(ts.get("train_step_count", 0))
             try:
                 n = RA.reanalysis_step(reanalyser, store, step, c, reanalysis_games, ui_queue)
             except Exception as e:  # workers.py:297-299

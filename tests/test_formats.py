@@ -119,3 +119,59 @@ def test_replay_warmup_from_reference_database(ref_copy):
     assert np.array_equal(rb.act[:len(slices)].numpy(), np.stack([s.action_history for s in slices]))
     assert np.array_equal(rb.pol[:len(slices)].numpy(), np.stack([s.policy_history for s in slices]).astype(np.float32))
     st.close(checkpoint=False)
+
+
+def test_reference_trainer_state_resumes(golden, tmp_path):
+    """The reference's trainer checkpoint (tests/golden/ref_trainer_state.db, written by its own
+    DatabaseManager.save_trainer_state after 3 Adam steps; make_golden_trainer_state.py) decodes with
+    the restricted loader and resumes a Trainer exactly: weights, Adam moments and steps, scheduler
+    position (lr), train_step_count; our checkpoint round-trips through the same blob format."""
+    import torch
+    from datou_gomoku_muzero_amd import trainer as T
+    d = golden("ref_trainer_state.npz")
+    st = F.RecordStore(os.path.join(GOLDEN, "ref_trainer_state.db"))
+    state = st.load_trainer_state()
+    st.close(checkpoint=False)
+    assert state["train_step_count"] == 1234 and state["games_completed_count"] == 56
+    cfg = T.TrainConfig(BOARD_SIZE=6, NUM_RES_BLOCKS=1, NUM_FILTERS=8)
+    tr = T.Trainer(cfg, device="cpu")
+    assert [n for n, _ in tr.model.named_parameters()] == d["param_names"].tolist()  # optimiser index order
+    tr.load_trainer_state(state)
+    sd = tr.model.state_dict()
+    for k in sd:
+        a = sd[k].numpy()
+        if "m/" + k in d.files:
+            assert np.array_equal(a, d["m/" + k]), k
+        else:
+            f = a.astype(np.float64).ravel()
+            want = d["ms/" + k]
+            assert np.array_equal(f[:16], want[2:]) and np.isclose(f.sum(), want[0]) and np.isclose(np.square(f).sum(), want[1])
+    ost = tr.opt.state_dict()["state"]
+    for i in range(len(tr.params)):
+        if "exp_avg/%d" % i in d.files:
+            assert np.array_equal(ost[i]["exp_avg"].numpy(), d["exp_avg/%d" % i])
+            assert np.array_equal(ost[i]["exp_avg_sq"].numpy(), d["exp_avg_sq/%d" % i])
+            assert float(ost[i]["step"]) == float(d["step/%d" % i])
+    assert tr.step_count == 1234 and abs(tr.opt.param_groups[0]["lr"] - float(d["lr"])) < 1e-15
+    # our checkpoint in the reference's blob format round-trips
+    st2 = F.RecordStore(str(tmp_path / "ours.db"))
+    st2.save_trainer_state(tr.trainer_state())
+    back = st2.load_trainer_state()
+    st2.close()
+    assert back["train_step_count"] == 1234
+    for k, v in tr.model.state_dict().items():
+        assert torch.equal(back["model_state_dict"][k], v)
+    tr2 = T.Trainer(cfg, device="cpu")
+    tr2.load_trainer_state(back)
+    assert tr2.opt.param_groups[0]["lr"] == tr.opt.param_groups[0]["lr"]
+
+
+def test_trainer_state_loader_rejects_other_globals():
+    import pickle
+
+    class Evil:
+        def __reduce__(self):
+            return (os.system, ("true",))
+    blob = pickle.dumps({"model_state_dict": {}, "x": Evil()})
+    with pytest.raises(F.UnsafeBlobError):
+        F.loads_trainer_state(blob)
