@@ -21,7 +21,7 @@ U64 = ctypes.c_uint64
 class EngineCfg(ctypes.Structure):
     _fields_ = [("num_games", ctypes.c_int32), ("board_size", ctypes.c_int32), ("n_in_row", ctypes.c_int32),
                 ("num_simulations", ctypes.c_int32), ("num_top_actions", ctypes.c_int32), ("mode", ctypes.c_int32),
-                ("c_visit", ctypes.c_int32), ("reserved", ctypes.c_int32), ("c_scale", ctypes.c_double),
+                ("c_visit", ctypes.c_int32), ("flags", ctypes.c_int32), ("c_scale", ctypes.c_double),
                 ("minmax_delta", ctypes.c_double), ("discount", ctypes.c_double)]
 
 

@@ -61,6 +61,7 @@ struct Dev {
   int8_t *boards, *players;
   int32_t *last_moves, *move_counts;
   int G, A, S, size, n_sims, m_top, c_visit, mode;
+  int no_hint;  // gmz_engine_cfg.flags bit 0: descent prefetch hint off (timing A/B; results identical)
   double c_scale;
   float disc_f, delta_f;
 };
@@ -292,7 +293,7 @@ __device__ int select_nonroot(const Dev &D, const uint64_t (&lg)[NJ], int g, int
   }
   *nxt_u = -1;
   const int al = __builtin_amdgcn_readfirstlane(cur.last);
-  if (al >= 0 && al < D.A) {
+  if (!D.no_hint && al >= 0 && al < D.A) {
     const int cp = bcast_slot<NJ>(ch, al);
     if (cp > 0 && cp < D.S) {
       row_fetch<NJ>(D, g, cp, lane, nxt);
@@ -323,6 +324,7 @@ __device__ int select_nonroot(const Dev &D, const uint64_t (&lg)[NJ], int g, int
     if (m) a = WAVE * j + __builtin_ctzll(m);
   }
   *child = bcast_slot<NJ>(ch, a);
+  if (D.no_hint) return a;
   // hint for the next visit: the argmax once this visit is counted (N_a + 1, sum N + 1), the same
   // policy otherwise — the deterministic selection spreads visits, so it often moves on from a
   double best2 = -INFINITY;
@@ -939,6 +941,7 @@ GMZ_EXPORT int gmz_engine_create(const gmz_engine_cfg *cfg, gmz_engine **out) {
   D.m_top = cfg->num_top_actions;
   D.c_visit = cfg->c_visit;
   D.mode = cfg->mode;
+  D.no_hint = cfg->flags & 1;
   D.c_scale = cfg->c_scale;
   D.disc_f = (float)cfg->discount;
   D.delta_f = (float)cfg->minmax_delta;

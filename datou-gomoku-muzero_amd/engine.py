@@ -43,7 +43,7 @@ class HashNetBackend:
 class BatchedSelfPlayEngine:
     """G games per GPU.  ``cfg``: any object with the reference config attribute names."""
 
-    def __init__(self, cfg=None, num_games=1, net=None, device="cuda", seed=0, **overrides):
+    def __init__(self, cfg=None, num_games=1, net=None, device="cuda", seed=0, descent_hint=True, **overrides):
         self.cfg = from_any(cfg, **overrides)
         c = self.cfg
         if c.MCTS_IMPLEMENTATION not in ("AlphaZero", "MuZero"):
@@ -54,7 +54,8 @@ class BatchedSelfPlayEngine:
         self.mode = 1 if c.MCTS_IMPLEMENTATION == "MuZero" else 0
         self.slots_per_game = c.NUM_SIMULATIONS + 2
         self.ecfg = _lib.EngineCfg(self.G, c.BOARD_SIZE, c.N_IN_ROW, c.NUM_SIMULATIONS, c.NUM_TOP_ACTIONS, self.mode,
-                                   int(c.C_VISIT), 0, float(c.C_SCALE), float(c.VALUE_MINMAX_DELTA), float(c.DISCOUNT))
+                                   int(c.C_VISIT), 0 if descent_hint else 1, float(c.C_SCALE),
+                                   float(c.VALUE_MINMAX_DELTA), float(c.DISCOUNT))
         h = ctypes.c_void_p()
         check(self.lib.gmz_engine_create(ctypes.byref(self.ecfg), ctypes.byref(h)))
         self.handle = h
