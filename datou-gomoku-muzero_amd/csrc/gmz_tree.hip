@@ -66,6 +66,18 @@ struct Dev {
   float disc_f, delta_f;
 };
 
+#ifdef GMZ_TREE_PROF
+// phase-cycle instrumentation (tools/tree_prof.py builds a separate library with -DGMZ_TREE_PROF)
+// per-wave accumulators in LDS (no global atomics inside the timed phases), flushed once per wave
+__device__ unsigned long long g_tree_prof[16];
+__shared__ unsigned long long tp_lds[4][16];
+#define TP_STAMP(var) const long long var = (long long)__builtin_amdgcn_s_memtime()
+#define TP_ADD(i, v) do { if (lane == 0) tp_lds[threadIdx.x / WAVE][i] += (unsigned long long)(v); } while (0)
+#else
+#define TP_STAMP(var) do {} while (0)
+#define TP_ADD(i, v) do {} while (0)
+#endif
+
 __device__ __forceinline__ float clip1(float v) { return v < -1.f ? -1.f : (v > 1.f ? 1.f : v); }
 
 __device__ __forceinline__ const Edge *edge_row(const Dev &D, int g, int u) {
@@ -278,6 +290,7 @@ __device__ int select_nonroot(const Dev &D, const uint64_t (&lg)[NJ], int g, int
   int n[NJ], ch[NJ];
   float q[NJ];
   double p[NJ];
+  TP_STAMP(tp0);
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {  // get_qsa (mcts.py:35-38), as row_load
     const bool ok = lane + WAVE * j < D.A;
@@ -301,7 +314,9 @@ __device__ int select_nonroot(const Dev &D, const uint64_t (&lg)[NJ], int g, int
     }
   }
   int max_n;
+  TP_STAMP(tp1);
   improved_policy<NJ>(D, lg, lane, cur.lv, n, q, mm_max, mm_min, p, max_n);
+  TP_STAMP(tp2);
   int tot = 0;
 #pragma unroll
   for (int j = 0; j < NJ; ++j) tot += n[j];
@@ -324,6 +339,12 @@ __device__ int select_nonroot(const Dev &D, const uint64_t (&lg)[NJ], int g, int
     if (m) a = WAVE * j + __builtin_ctzll(m);
   }
   *child = bcast_slot<NJ>(ch, a);
+  TP_STAMP(tp3);
+#ifdef GMZ_TREE_PROF
+  TP_ADD(1, tp1 - tp0);
+  TP_ADD(2, tp2 - tp1);
+  TP_ADD(3, tp3 - tp2);
+#endif
   if (D.no_hint) return a;
   // hint for the next visit: the argmax once this visit is counted (N_a + 1, sum N + 1), the same
   // policy otherwise — the deterministic selection spreads visits, so it often moves on from a
@@ -344,6 +365,10 @@ __device__ int select_nonroot(const Dev &D, const uint64_t (&lg)[NJ], int g, int
     if (m) a2 = WAVE * j + __builtin_ctzll(m);
   }
   if (lane == 0) D.node_last[(size_t)g * D.S + u] = a2;
+  TP_STAMP(tp4);
+#ifdef GMZ_TREE_PROF
+  TP_ADD(4, tp4 - tp3);
+#endif
   return a;
 }
 
@@ -592,10 +617,24 @@ __device__ __forceinline__ void select_game(const Dev &D, int g, int lane, int32
   for (;;) {
     int c;
     if (u == 0) {
+      TP_STAMP(tr0);
       a = select_root(D, g, lane, st.n_sel, &c);
+#ifdef GMZ_TREE_PROF
+      __builtin_amdgcn_s_waitcnt(0);
+      TP_STAMP(tr1);
+      TP_ADD(5, tr1 - tr0);
+#endif
     } else {
+      TP_STAMP(tf0);
       if (u == nxt_u) cur = nxt;  // the hinted row is this node's
       else row_fetch<NJ>(D, g, u, lane, cur);
+#ifdef GMZ_TREE_PROF
+      __builtin_amdgcn_s_waitcnt(0);
+      TP_STAMP(tf1);
+      TP_ADD(0, tf1 - tf0);
+      TP_ADD(7, 1);
+      TP_ADD(11, u == nxt_u ? 1 : 0);
+#endif
       a = select_nonroot<NJ>(D, lg, g, u, lane, st.mm_max, st.mm_min, &c, cur, nxt, &nxt_u);
     }
     if (lane == 0) {
@@ -784,11 +823,26 @@ __global__ void __launch_bounds__(256) k_expand_select(Dev D, const float *__res
                                                        int32_t *__restrict__ out_slot, float *__restrict__ obs) {
   const int g = blockIdx.x * 4 + threadIdx.x / WAVE, lane = threadIdx.x & (WAVE - 1);
   if (g >= D.G) return;
+#ifdef GMZ_TREE_PROF
+  if (lane < 16) tp_lds[threadIdx.x / WAVE][lane] = 0;
+#endif
+  TP_STAMP(tk0);
   const int active0 = D.gs[g].active, depth0 = D.gs[g].depth;
   expand_backup_game<NJ>(D, g, lane, logits_in, value_in, reward_in);
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_s_waitcnt(0);
+  TP_STAMP(tk1);
   select_game<NJ>(D, g, lane, in_slot, act_out, out_slot, obs);
+#ifdef GMZ_TREE_PROF
+  __builtin_amdgcn_s_waitcnt(0);
+  TP_STAMP(tk2);
+  TP_ADD(6, tk1 - tk0);
+  TP_ADD(8, 1);
+  TP_ADD(9, tk2 - tk0);
+  TP_ADD(10, tk2 - tk1);
+  __builtin_amdgcn_s_waitcnt(0);
+  if (lane < 16) atomicAdd(&g_tree_prof[lane], tp_lds[threadIdx.x / WAVE][lane]);
+#endif
   // work counters (the algorithmic-byte model of bench.py's tree roofline): game-waves backed up,
   // levels backed up, game-waves selected, levels walked by the selection (incl. the root level).
   // Lane 0 wrote the GameState in select_game, so its own read sees the new depth.
@@ -1156,6 +1210,18 @@ GMZ_EXPORT int gmz_engine_tree_counters(gmz_engine *e, int32_t *ctr_dev, int res
   if (reset) GMZ_HIP(hipMemsetAsync(e->D.ctr, 0, (size_t)e->D.G * 16, s));
   return 0;
 }
+
+#ifdef GMZ_TREE_PROF
+GMZ_EXPORT int gmz_tree_prof_read(unsigned long long *out16, int reset) {
+  GMZ_HIP(hipDeviceSynchronize());
+  GMZ_HIP(hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_tree_prof), sizeof(unsigned long long) * 16));
+  if (reset) {
+    unsigned long long z[16] = {0};
+    GMZ_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_tree_prof), z, sizeof(z)));
+  }
+  return 0;
+}
+#endif
 
 GMZ_EXPORT int gmz_engine_root_stats(gmz_engine *e, int32_t *visits, int32_t *root_n, float *root_w, float *mm_max,
                                      float *mm_min, void *stream) {
