@@ -15,7 +15,10 @@
 //   Edge edges[G][S][A]   {child, N, W, R} 16 B per (node, action): one dwordx4 per lane per
 //                         action, coalesced across the wave when a node's children are scanned
 //   float logits[G][S][A] node policy logits (network output)
-//   int path_u/path_a[G][S], node_parent/node_action[G][S], node_last[G][S] (descent prefetch hint),
+//   int path_u/path_a[G][S], node_parent/node_action[G][S]
+//   int4 hdr[G][S]        per-node header {sum of child N, max child N, visited children, next-visit
+//                         hint}: maintained by the backup so that a selection step needs no integer
+//                         wave reductions; the hint is the predicted choice of the node's next visit
 //   per-game scalars GameState[G]
 // S = num_simulations + 2 node slots per game (root + <= 1 new node per wave + 1 scratch slot).
 //
@@ -52,7 +55,7 @@ struct Dev {
   Edge *edges;
   float *logits;
   int32_t *node_parent, *node_action, *path_u, *path_a, *sel;
-  int32_t *node_last;  // [G][S] action last selected at the node: prefetch hint only (select_game)
+  int4 *hdr;           // [G][S] NodeHdr {tot = sum N_child, maxn = max N_child, nvis = #children N > 0, last}
   int32_t *ctr;        // [G][4] k_expand_select work counters (gmz_engine_tree_counters)
   GameState *gs;
   uint64_t *legal;  // [G][NJ]
@@ -263,7 +266,7 @@ template <int NJ>
 struct RowRegs {
   int4 e[NJ];
   float lv[NJ];
-  int last;
+  int4 hdr;  // the node's header {tot, maxn, nvis, last}
 };
 template <int NJ>
 __device__ __forceinline__ void row_fetch(const Dev &D, int g, int u, int lane, RowRegs<NJ> &r) {
@@ -275,18 +278,44 @@ __device__ __forceinline__ void row_fetch(const Dev &D, int g, int u, int lane, 
     r.e[j] = *(const int4 *)(row + ac);
     r.lv[j] = lr[ac];
   }
-  r.last = D.node_last[(size_t)g * D.S + u];
+  r.hdr = D.hdr[(size_t)g * D.S + u];
+}
+
+// Per-descent constants of the completed-Q normalisation (mm_max / mm_min do not change during a
+// selection): the denominator and the normalised Q of an unvisited child (q = 0.0, mcts.py:35-38).
+struct NormQ {
+  float mm_max, mm_min, den_f;
+  bool have_range;
+  double nq0;
+};
+__device__ __forceinline__ NormQ norm_q_consts(const Dev &D, float mm_max, float mm_min) {
+  NormQ z;
+  z.mm_max = mm_max;
+  z.mm_min = mm_min;
+  z.have_range = mm_max > mm_min;
+  z.den_f = (mm_max - mm_min) + D.delta_f;
+  z.nq0 = 0.0;
+  if (z.have_range) {
+    double x = (0.0 - (double)mm_min) / (double)z.den_f;
+    x = (x < 1.0) ? x : 1.0;
+    z.nq0 = (x > 0.0) ? x : 0.0;
+  }
+  return z;
 }
 
 // _select_action at a non-root node (mcts.py:106-117) on the fetched row `cur`.  Returns the action;
 // *child = its child id (from the row: no second dependent round trip per level).  The descent is one
 // dependent row fetch per level, so while this level's selection computes, the row of the child of the
-// hinted action (node_last: the predicted choice of this node's next visit, set at its last visit) is
+// hinted action (hdr.last: the predicted choice of this node's next visit, set at its last visit) is
 // fetched into `nxt` (*nxt_u = that child, -1 if none): the caller uses it when the prediction holds
 // and fetches afresh otherwise.  Results never depend on the hint.
+// The node header supplies sum N, max N and "every child visited" (the integer reductions of
+// _get_transformed_completed_Qs and of the score denominator, exact); the float64 normalisation
+// (q - min) / den runs only for visited children, an unvisited one takes the per-descent constant nq0
+// (its q is 0.0): the same correctly rounded quotient either way.
 template <int NJ>
-__device__ int select_nonroot(const Dev &D, const uint64_t (&lg)[NJ], int g, int u, int lane, float mm_max,
-                              float mm_min, int *child, const RowRegs<NJ> &cur, RowRegs<NJ> &nxt, int *nxt_u) {
+__device__ int select_nonroot(const Dev &D, const uint64_t (&lg)[NJ], int g, int u, int lane, const NormQ &nz,
+                              int *child, const RowRegs<NJ> &cur, RowRegs<NJ> &nxt, int *nxt_u) {
   int n[NJ], ch[NJ];
   float q[NJ];
   double p[NJ];
@@ -304,8 +333,11 @@ __device__ int select_nonroot(const Dev &D, const uint64_t (&lg)[NJ], int g, int
       q[j] = __int_as_float(e.w) + dv;
     }
   }
+  const int tot = __builtin_amdgcn_readfirstlane(cur.hdr.x);
+  const int max_n = __builtin_amdgcn_readfirstlane(cur.hdr.y);
+  const int nvis = __builtin_amdgcn_readfirstlane(cur.hdr.z);
   *nxt_u = -1;
-  const int al = __builtin_amdgcn_readfirstlane(cur.last);
+  const int al = __builtin_amdgcn_readfirstlane(cur.hdr.w);
   if (!D.no_hint && al >= 0 && al < D.A) {
     const int cp = bcast_slot<NJ>(ch, al);
     if (cp > 0 && cp < D.S) {
@@ -313,14 +345,42 @@ __device__ int select_nonroot(const Dev &D, const uint64_t (&lg)[NJ], int g, int
       *nxt_u = cp;
     }
   }
-  int max_n;
   TP_STAMP(tp1);
-  improved_policy<NJ>(D, lg, lane, cur.lv, n, q, mm_max, mm_min, p, max_n);
-  TP_STAMP(tp2);
-  int tot = 0;
+  if (nvis < D.A) {
+    // _get_transformed_completed_Qs, some child unvisited: float64 array (mcts.py:141-149)
+    const double scale = (double)(D.c_visit + max_n) * D.c_scale;
+    const double den = (double)nz.den_f;
+    double x[NJ], m = -INFINITY;
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) tot += n[j];
-  tot = dred_sum_i(tot);
+    for (int j = 0; j < NJ; ++j) {
+      double nq = nz.nq0;
+      if (n[j] > 0 && nz.have_range) {
+        double y = ((double)q[j] - (double)nz.mm_min) / den;
+        y = (y < 1.0) ? y : 1.0;
+        nq = (y > 0.0) ? y : 0.0;
+      }
+      const double t = scale * nq;
+      const int a = lane + WAVE * j;
+      const bool ok = a < D.A && ((lg[j] >> lane) & 1ull);
+      x[j] = ok ? (double)cur.lv[j] + t : -INFINITY;  // _get_improved_policy (mcts.py:151-156)
+      m = fmax(m, x[j]);
+    }
+    m = dred_max_d(m);
+    double sum = 0.0;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      x[j] = (x[j] == -INFINITY) ? 0.0 : exp(x[j] - m);
+      sum += x[j];
+    }
+    sum = dred_sum_d(sum);
+    const double inv_s = 1.0 / sum;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) p[j] = x[j] * inv_s;
+  } else {
+    int mx_unused;
+    improved_policy<NJ>(D, lg, lane, cur.lv, n, q, nz.mm_max, nz.mm_min, p, mx_unused);
+  }
+  TP_STAMP(tp2);
   double sc[NJ], best = -INFINITY;
   const double inv_tot = 1.0 / (double)(1 + tot);
 #pragma unroll
@@ -335,8 +395,8 @@ __device__ int select_nonroot(const Dev &D, const uint64_t (&lg)[NJ], int g, int
   int a = 0;
 #pragma unroll
   for (int j = NJ - 1; j >= 0; --j) {
-    const uint64_t m = __ballot(sc[j] == best && best != -INFINITY);
-    if (m) a = WAVE * j + __builtin_ctzll(m);
+    const uint64_t mk = __ballot(sc[j] == best && best != -INFINITY);
+    if (mk) a = WAVE * j + __builtin_ctzll(mk);
   }
   *child = bcast_slot<NJ>(ch, a);
   TP_STAMP(tp3);
@@ -347,24 +407,25 @@ __device__ int select_nonroot(const Dev &D, const uint64_t (&lg)[NJ], int g, int
 #endif
   if (D.no_hint) return a;
   // hint for the next visit: the argmax once this visit is counted (N_a + 1, sum N + 1), the same
-  // policy otherwise — the deterministic selection spreads visits, so it often moves on from a
-  double best2 = -INFINITY;
-  const double inv_tot2 = 1.0 / (double)(2 + tot);
+  // policy otherwise — the deterministic selection spreads visits, so it often moves on from a.
+  // A prediction only (the row it names is fetched early), so float32 scores suffice.
+  float best2 = -INFINITY, sc2[NJ];
+  const float inv_tot2 = 1.0f / (float)(2 + tot);
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int aj = lane + WAVE * j;
-    sc[j] = -INFINITY;
-    if (aj < D.A && ((lg[j] >> lane) & 1ull)) sc[j] = p[j] - (double)(n[j] + (aj == a)) * inv_tot2;
-    best2 = fmax(best2, sc[j]);
+    sc2[j] = -INFINITY;
+    if (aj < D.A && ((lg[j] >> lane) & 1ull)) sc2[j] = (float)p[j] - (float)(n[j] + (aj == a)) * inv_tot2;
+    best2 = fmaxf(best2, sc2[j]);
   }
-  best2 = dred_max_d(best2);
+  best2 = dred_max_f(best2);
   int a2 = a;
 #pragma unroll
   for (int j = NJ - 1; j >= 0; --j) {
-    const uint64_t m = __ballot(sc[j] == best2 && best2 != -INFINITY);
-    if (m) a2 = WAVE * j + __builtin_ctzll(m);
+    const uint64_t mk = __ballot(sc2[j] == best2 && best2 != -INFINITY);
+    if (mk) a2 = WAVE * j + __builtin_ctzll(mk);
   }
-  if (lane == 0) D.node_last[(size_t)g * D.S + u] = a2;
+  if (lane == 0) D.hdr[(size_t)g * D.S + u].w = a2;
   TP_STAMP(tp4);
 #ifdef GMZ_TREE_PROF
   TP_ADD(4, tp4 - tp3);
@@ -501,7 +562,7 @@ __global__ void __launch_bounds__(256) k_begin_move(Dev D, const double *__restr
     D.gs[g] = st;
     D.node_parent[(size_t)g * D.S] = -1;
     D.node_action[(size_t)g * D.S] = -1;
-    D.node_last[(size_t)g * D.S] = -1;
+    D.hdr[(size_t)g * D.S] = make_int4(0, 0, 0, -1);
   }
 }
 
@@ -614,6 +675,7 @@ __device__ __forceinline__ void select_game(const Dev &D, int g, int lane, int32
   load_legal<NJ>(D, g, lg);
   RowRegs<NJ> cur, nxt;
   int nxt_u = -1;
+  const NormQ nz = norm_q_consts(D, st.mm_max, st.mm_min);
   for (;;) {
     int c;
     if (u == 0) {
@@ -635,7 +697,7 @@ __device__ __forceinline__ void select_game(const Dev &D, int g, int lane, int32
       TP_ADD(7, 1);
       TP_ADD(11, u == nxt_u ? 1 : 0);
 #endif
-      a = select_nonroot<NJ>(D, lg, g, u, lane, st.mm_max, st.mm_min, &c, cur, nxt, &nxt_u);
+      a = select_nonroot<NJ>(D, lg, g, u, lane, nz, &c, cur, nxt, &nxt_u);
     }
     if (lane == 0) {
       pu[d] = u;
@@ -684,10 +746,14 @@ __device__ __forceinline__ void expand_backup_game(const Dev &D, int g, int lane
                                                    const float *__restrict__ value_in,
                                                    const float *__restrict__ reward_in) {
   const int A = D.A, S = D.S;
+  const int32_t *pu = D.path_u + (size_t)g * S, *pa = D.path_a + (size_t)g * S;
+  // the first 64 path entries by lane, loaded beside the GameState (not after it): a level's node and
+  // action then come from a lane permute instead of a dependent memory round trip
+  const int pl = lane < S ? lane : S - 1;
+  const int pu_l = pu[pl], pa_l = pa[pl];
   GameState st = D.gs[g];
   if (!st.active) return;
   const int d = st.depth, leaf = st.leaf, k = st.k;
-  const int32_t *pu = D.path_u + (size_t)g * S, *pa = D.path_a + (size_t)g * S;
   // Node.expand (mcts.py:24-25): logits, reward; children row starts empty
   float *nl = D.logits + ((size_t)g * S + leaf) * A;
   Edge *nrow = edge_row_w(D, g, leaf);
@@ -698,7 +764,7 @@ __device__ __forceinline__ void expand_backup_game(const Dev &D, int g, int lane
   if (lane == 0) {
     D.node_parent[(size_t)g * S + leaf] = pu[d - 1];
     D.node_action[(size_t)g * S + leaf] = pa[d - 1];
-    D.node_last[(size_t)g * S + leaf] = -1;
+    D.hdr[(size_t)g * S + leaf] = make_int4(0, 0, 0, -1);
   }
   const float r_leaf = reward_in ? reward_in[g] : 0.f;
   // _backpropagate (mcts.py:119-138), k duplicate leaves (mcts.py:326-345): the value chain is the
@@ -709,9 +775,16 @@ __device__ __forceinline__ void expand_backup_game(const Dev &D, int g, int lane
     const int j = base + lane;
     Edge e = Edge{0, 0, 0.f, 0.f};
     Edge *ep = nullptr;
+    int4 *hp = nullptr;
+    int4 h = make_int4(0, 0, 0, 0);
+    const int lvl = d - 1 - j;  // path index of this lane's edge
+    const int pu_j = __shfl(pu_l, lvl & (WAVE - 1), 64), pa_j = __shfl(pa_l, lvl & (WAVE - 1), 64);
     if (j < d) {
-      ep = edge_row_w(D, g, pu[d - 1 - j]) + pa[d - 1 - j];
+      const int nu = lvl < WAVE ? pu_j : pu[lvl], na = lvl < WAVE ? pa_j : pa[lvl];
+      ep = edge_row_w(D, g, nu) + na;
+      hp = D.hdr + (size_t)g * S + nu;
       e = *ep;
+      h = *hp;
       if (j == 0) { e.child = leaf; e.r = r_leaf; }
     }
     const float rj = e.r;
@@ -737,9 +810,14 @@ __device__ __forceinline__ void expand_backup_game(const Dev &D, int g, int lane
         mx = fmaxf(mx, q);
         mn = fminf(mn, q);
       }
+      // the parent's header (sum N, max N, visited children), as the k updates above
+      h.x += k;
+      h.y = max(h.y, N);
+      h.z += (e.n == 0);
       e.w = W;
       e.n = N;
       *ep = e;
+      *hp = h;
     } else if (j == d) {
       float W = st.root_w;
       for (int t = 0; t < k; ++t) W = W + myv;
@@ -1005,7 +1083,7 @@ GMZ_EXPORT int gmz_engine_create(const gmz_engine_cfg *cfg, gmz_engine **out) {
   rc |= dalloc(e, &D.logits, G * S * A);
   rc |= dalloc(e, &D.node_parent, G * S);
   rc |= dalloc(e, &D.node_action, G * S);
-  rc |= dalloc(e, &D.node_last, G * S);
+  rc |= dalloc(e, &D.hdr, G * S);
   rc |= dalloc(e, &D.ctr, G * 4);
   rc |= dalloc(e, &D.path_u, G * S);
   rc |= dalloc(e, &D.path_a, G * S);
