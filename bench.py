@@ -5,7 +5,9 @@ One *step* = one move of every game on this GPU: the full Gumbel-MuZero search (
 ~100 waves of select -> GomokuNetEZ recurrent inference -> expand/backup, mcts.py:288-362) and the
 move itself (do_move + get_game_ended, workers.py:178-181), G games at once (config 2: G = 1024).
 Finished games restart immediately.  Data: synthetic — empty boards, random-init GomokuNetEZ
-(8 blocks x 128 channels, numpy-seeded), Gumbel noise from the device RNG.
+(8 blocks x 128 channels, numpy-seeded), Gumbel noise from the device RNG.  The G games run as two
+half-size engines on two HIP streams (--streams 2, engine.SplitSelfPlayEngine: the same games as
+one engine, bit for bit; one half's tree/head kernels overlap the other half's tower).
 
   python bench.py [--gpus N --steps K --warmup W]
 
@@ -18,12 +20,13 @@ several ranks sharing one GPU.
 
 Prints ONE JSON line on rank 0 (schema: the driver contract) including
   roofline      : the dominant kernel (dynamics tower k_tower3<15,DYN>) timed with HIP events on its
-                  launch stream inside the timed region; achieved = algorithmic FLOP of the rows the
-                  searches actually requested / mean launch duration vs the 2.5 PFLOP/s dense f16/bf16
-                  MFMA peak;
+                  launch stream(s) inside the timed region; achieved = algorithmic FLOP of the rows the
+                  searches actually requested / the kernel's busy time (union of its launch intervals
+                  over both streams; = launches x mean duration with one stream) vs the 2.5 PFLOP/s
+                  dense f16/bf16 MFMA peak; per-launch figures beside it;
   roofline_tree : the fused expand/backup + select kernel (k_expand_select), same timing; achieved =
                   algorithmic bytes counted from the per-game work counters (gmz_engine_tree_counters,
-                  byte model in DESIGN.md §5) / mean launch duration vs 8 TB/s HBM;
+                  byte model in DESIGN.md §5) / its busy time vs 8 TB/s HBM;
   trainer       : config C4's trainer (B = 360 per GPU, 5 unroll steps, PER, fp16 autocast, HIP convs),
                   steps/s after the self-play region, on every rank (DDP: one RCCL gradient all-reduce +
                   the sharded-PER syncs per step), plus the MFMA fraction of its dominant HIP conv;
@@ -93,6 +96,12 @@ def parse(argv=None):
     ap.add_argument("--blocks", type=int, default=8)
     ap.add_argument("--mode", default="MuZero")
     ap.add_argument("--net", default="hip", choices=["hip", "hash"])
+    ap.add_argument("--streams", type=int, default=2,
+                    help="HIP streams per GPU: the G games as this many half-size engines whose waves interleave "
+                         "(engine.SplitSelfPlayEngine; 1 = one BatchedSelfPlayEngine)")
+    ap.add_argument("--single-stream-moves", type=int, default=2,
+                    help="with --streams > 1: moves of ONE engine on one stream after the timed region, for the two "
+                         "kernels' single-stream launch times (0: skip)")
     ap.add_argument("--precision", default="fp16", choices=["fp16", "bf16"],
                     help="MFMA operand type of the network towers (f32 accumulation either way)")
     ap.add_argument("--seed", type=int, default=1234)
@@ -186,9 +195,32 @@ def result_line(args, world, dt, waves, G, backend=None):
                                % (args.size, args.size, args.mode, args.sims, G, args.blocks),
                    "games_per_gpu": G, "global_games": G * world, "board_size": args.size,
                    "num_simulations": args.sims, "mcts": args.mode, "waves_per_move": waves / max(1, args.steps),
-                   "ranks": world, "dist_backend": backend,
+                   "ranks": world, "dist_backend": backend, "streams_per_gpu": getattr(args, "streams", 1),
                    "parallelism": "dp%d (independent games per GPU, no collective)" % world},
     }
+
+
+def timer_stats(timers, base):
+    """Launch statistics of KernelTimers (one per stream): (launches, mean launch ms, busy ms) where
+    busy = the union of the launch intervals over all streams (ms, from HIP events against ``base``)."""
+    iv = []
+    for t in timers:
+        for a, b, _ in t.pairs:
+            iv.append((base.elapsed_time(a), base.elapsed_time(b)))
+    if not iv:
+        return 0, 0.0, 0.0
+    n = len(iv)
+    mean = sum(b - a for a, b in iv) / n
+    iv.sort()
+    busy, cur0, cur1 = 0.0, iv[0][0], iv[0][1]
+    for a, b in iv[1:]:
+        if a > cur1:
+            busy += cur1 - cur0
+            cur0, cur1 = a, b
+        else:
+            cur1 = max(cur1, b)
+    busy += cur1 - cur0
+    return n, mean, busy
 
 
 def cpu_baseline(args, sd, cfg):
@@ -350,9 +382,12 @@ def main():
         net = N.GomokuNetHip(sd, cfg, num_slots=slots, max_rows=G, precision=args.precision)
     else:
         net = E.HashNetBackend(slots, cfg.ACTION_SPACE_SIZE)
-    eng = E.BatchedSelfPlayEngine(cfg, num_games=G, net=net, seed=args.seed + 7919 * rank)
+    eng = E.make_engine(cfg, num_games=G, net=net, seed=args.seed + 7919 * rank, streams=args.streams)
     eng.reset_games()
-    log("rank %d: engine G=%d %dx%d %s/%d, net=%s" % (rank, G, args.size, args.size, args.mode, args.sims, args.net))
+    parts = eng.engines if args.streams > 1 else [eng]
+    pstreams = eng.streams if args.streams > 1 else [torch.cuda.current_stream()]
+    log("rank %d: engine G=%d %dx%d %s/%d, net=%s, %d stream(s)" % (rank, G, args.size, args.size, args.mode, args.sims,
+                                                                     args.net, args.streams))
 
     def step():
         eng.search()
@@ -362,19 +397,24 @@ def main():
         step()
         torch.cuda.synchronize()
         log("warmup %d/%d done" % (i + 1, args.warmup))
-    timer = None
     az = args.mode == "AlphaZero"  # AlphaZero searches run the representation tower per wave
-    if args.net == "hip":
-        timer = N.KernelTimer()
-        if az:
-            net.repr_timer = timer
-        else:
-            net.tower_timer = timer
-    eng.tree_timer = N.KernelTimer()
+    timers, tree_timers = [], []
+    for e, st in zip(parts, pstreams):  # HIP events on each part's launch stream
+        if args.net == "hip":
+            t = N.KernelTimer(st)
+            timers.append(t)
+            if az:
+                e.net.repr_timer = t
+            else:
+                e.net.tower_timer = t
+        e.tree_timer = N.KernelTimer(st)
+        tree_timers.append(e.tree_timer)
     eng.tree_counters(reset=True)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
+    base = torch.cuda.Event(enable_timing=True)
+    base.record()
     t0 = time.perf_counter()
     waves = 0
     for i in range(args.steps):
@@ -389,14 +429,17 @@ def main():
     dt = collective_max(dt, dist, backend)
     out = result_line(args, world, dt, waves, G, backend)
     ctr = eng.tree_counters()
-    if timer is not None:
-        n_launch, ms, _ = timer.summary()
+    if timers:
+        n_launch, ms, busy = timer_stats(timers, base)
         # rows the searches requested (finished games' rows are skipped by the tower): every selected
         # game-wave is one row; AlphaZero's representation tower also runs each move's G root rows
         rows = (ctr["selects"] + (G * args.steps if az else 0)) / max(1, n_launch)
         fpr = (repr_flop_per_row if az else tower_flop_per_row)(args.size, args.blocks)
         flop = fpr * rows
-        achieved = flop / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
+        per_launch = flop / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
+        # delivered rate while the kernel runs: all launches' FLOP over the union of their intervals
+        # (with one stream = the per-launch figure; with two, launches of the two streams overlap)
+        achieved = flop * n_launch / (busy * 1e-3) / 1e12 if busy > 0 else 0.0
         traffic = None
         if os.path.exists(args.pmc_file) and (args.size, args.blocks) == (15, 8) and not az:  # the PMC pass's config
             try:
@@ -411,19 +454,60 @@ def main():
                            "achieved": achieved, "peak": PEAK_MFMA_TFLOPS, "unit": "TFLOP/s",
                            "frac": achieved / PEAK_MFMA_TFLOPS, "traffic": traffic,
                            "launches": n_launch, "mean_launch_ms": ms, "rows_per_launch": rows,
-                           "flop_per_row": fpr}
-    n_tree, ms_tree, _ = eng.tree_timer.summary()
+                           "flop_per_row": fpr, "streams": args.streams, "busy_ms": busy,
+                           "achieved_per_launch": per_launch,
+                           "timing": "HIP events around every launch on its stream; achieved = algorithmic FLOP of all "
+                                     "launches / busy_ms (union of the launch intervals of all streams)"}
+    n_tree, ms_tree, busy_tree = timer_stats(tree_timers, base)
     if n_tree:
         A = args.size * args.size
         bpl = tree_bytes(ctr, A) / n_tree
-        gbs = bpl / (ms_tree * 1e-3) / 1e9
+        gbs = bpl * n_tree / (busy_tree * 1e-3) / 1e9 if busy_tree > 0 else 0.0
         out["roofline_tree"] = {
             "bound": "hbm", "kernel": "k_expand_select<%d> (backup of wave i + selection of wave i+1)" % ((A + 63) // 64),
             "achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS, "traffic": None,
             "launches": n_tree, "mean_launch_ms": ms_tree, "bytes_per_launch": bpl,
             "mean_backup_levels": ctr["backup_levels"] / max(1, ctr["backups"]),
             "mean_select_levels": ctr["select_levels"] / max(1, ctr["selects"]),
-            "games_per_launch": ctr["backups"] / n_tree}
+            "games_per_launch": ctr["backups"] / n_tree, "streams": args.streams, "busy_ms": busy_tree,
+            "achieved_per_launch": bpl / (ms_tree * 1e-3) / 1e9}
+    if args.streams > 1 and args.single_stream_moves > 0:
+        # the same G games as ONE engine on one stream (every CU per launch): the kernels' launch times
+        # without the other stream beside them (not the headline: the two-stream step above is)
+        e1 = E.BatchedSelfPlayEngine(cfg, num_games=G, net=net, seed=args.seed + 7919 * rank + 1)
+        e1.reset_games()
+        e1.search()
+        e1.play(reset_finished=True)
+        t1, tt1 = (N.KernelTimer() if args.net == "hip" else None), N.KernelTimer()
+        if t1 is not None:
+            if az:
+                net.repr_timer = t1
+            else:
+                net.tower_timer = t1
+        e1.tree_timer = tt1
+        e1.tree_counters(reset=True)
+        torch.cuda.synchronize()
+        b1 = torch.cuda.Event(enable_timing=True)
+        b1.record()
+        for _ in range(args.single_stream_moves):
+            e1.search()
+            e1.play(reset_finished=True)
+        torch.cuda.synchronize()
+        c1 = e1.tree_counters()
+        ss = {"moves": args.single_stream_moves, "games": G}
+        if t1 is not None:
+            n1, m1, _ = timer_stats([t1], b1)
+            r1 = (c1["selects"] + (G * args.single_stream_moves if az else 0)) / max(1, n1)
+            a1 = fpr * r1 / (m1 * 1e-3) / 1e12
+            ss["tower"] = {"mean_launch_ms": m1, "rows_per_launch": r1, "achieved": a1, "frac": a1 / PEAK_MFMA_TFLOPS}
+        n2, m2, _ = timer_stats([tt1], b1)
+        if n2:
+            g2 = tree_bytes(c1, args.size * args.size) / n2 / (m2 * 1e-3) / 1e9
+            ss["tree"] = {"mean_launch_ms": m2, "achieved_gbs": g2, "frac": g2 / PEAK_HBM_GBS}
+        out["single_stream_kernels"] = ss
+        net.tower_timer = net.repr_timer = None
+        e1.close()
+        del e1
     if args.trainer_steps > 0 and args.net == "hip":
         del eng, net
         torch.cuda.empty_cache()

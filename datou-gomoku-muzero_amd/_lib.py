@@ -11,7 +11,7 @@ import torch  # noqa: F401  (must precede the CDLL load: shared HIP runtime)
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GMZ_LIB") or os.path.join(PKG_DIR, "libgmz.so")  # GMZ_LIB: A/B builds (tools)
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -22,7 +22,7 @@ class EngineCfg(ctypes.Structure):
     _fields_ = [("num_games", ctypes.c_int32), ("board_size", ctypes.c_int32), ("n_in_row", ctypes.c_int32),
                 ("num_simulations", ctypes.c_int32), ("num_top_actions", ctypes.c_int32), ("mode", ctypes.c_int32),
                 ("c_visit", ctypes.c_int32), ("flags", ctypes.c_int32), ("c_scale", ctypes.c_double),
-                ("minmax_delta", ctypes.c_double), ("discount", ctypes.c_double)]
+                ("minmax_delta", ctypes.c_double), ("discount", ctypes.c_double), ("game_offset", ctypes.c_int32)]
 
 
 _SIGS = {

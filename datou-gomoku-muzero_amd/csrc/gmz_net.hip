@@ -59,6 +59,7 @@ struct TowerArgs {
   float *pv_feat;          // [rows][pv_stride(A)]: policy planes at [0, 2A), value plane at pv_kpol(A) + p
   int rows;
   uint16_t *xres;          // single-image boards (19x19): per-workgroup residual scratch (k_tower3)
+  int max_grid;            // cap on the persistent grid (gmz_net_weights.max_grid; 0 = every CU)
 };
 
 // MFMA operand element types of the towers and the reward GEMM (f32 accumulation either way).
@@ -751,7 +752,8 @@ static int launch_tower(const TowerArgs &a, hipStream_t s) {
   using T = TowerCfg<H>;
   if (tower_xres_bytes<H>() && !a.xres) return fail("gmz_net: missing residual scratch");
   const int need = (a.rows + T::NB - 1) / T::NB;
-  const int grid = need < cu_count() ? need : cu_count();
+  const int cus = (a.max_grid > 0 && a.max_grid < cu_count()) ? a.max_grid : cu_count();
+  const int grid = need < cus ? need : cus;
   hipLaunchKernelGGL((k_tower3<H, DYN, 0, T::RD, T::NQ, T::PG, T::NB, E>), dim3(grid), dim3(64 * T::NQ * T::PG), 0, s, a);
   GMZ_LAUNCH_CHECK();
   return 0;
@@ -767,7 +769,9 @@ static int tower_e(int H, bool dyn, const TowerArgs &a, hipStream_t s) {
     default: return fail("gmz_net: board_size must be one of 6, 9, 15, 19");
   }
 }
-static int tower(const gmz_net_weights *w, bool dyn, const TowerArgs &a, hipStream_t s) {
+static int tower(const gmz_net_weights *w, bool dyn, const TowerArgs &a0, hipStream_t s) {
+  TowerArgs a = a0;
+  a.max_grid = w->max_grid;
   return w->dtype == GMZ_NET_BF16 ? tower_e<Bf16>(w->board_size, dyn, a, s) : tower_e<F16>(w->board_size, dyn, a, s);
 }
 

@@ -64,6 +64,7 @@ struct Dev {
   int8_t *boards, *players;
   int32_t *last_moves, *move_counts;
   int G, A, S, size, n_sims, m_top, c_visit, mode;
+  int game_offset;  // gmz_engine_cfg.game_offset: global index of game 0 (device Gumbel noise)
   int no_hint;  // gmz_engine_cfg.flags bit 0: descent prefetch hint off (timing A/B; results identical)
   double c_scale;
   float disc_f, delta_f;
@@ -492,7 +493,7 @@ __global__ void __launch_bounds__(256) k_begin_move(Dev D, const double *__restr
     if (gumbel_in) {
       gv = gumbel_in[(size_t)g * A + a];
     } else {
-      const uint32_t h1 = mix32((uint32_t)seed ^ mix32(counter * 0x9E3779B1u + (uint32_t)g * 0x85EBCA77u));
+      const uint32_t h1 = mix32((uint32_t)seed ^ mix32(counter * 0x9E3779B1u + (uint32_t)(g + D.game_offset) * 0x85EBCA77u));
       const uint32_t h2 = mix32(h1 ^ mix32((uint32_t)a + 0x68E31DA4u) ^ (uint32_t)(seed >> 32));
       const uint32_t h3 = mix32(h2 + 0x1B873593u);
       const uint64_t bits = ((uint64_t)h2 << 21) ^ (uint64_t)h3;  // 53 random bits
@@ -1074,6 +1075,7 @@ GMZ_EXPORT int gmz_engine_create(const gmz_engine_cfg *cfg, gmz_engine **out) {
   D.c_visit = cfg->c_visit;
   D.mode = cfg->mode;
   D.no_hint = cfg->flags & 1;
+  D.game_offset = cfg->game_offset;
   D.c_scale = cfg->c_scale;
   D.disc_f = (float)cfg->discount;
   D.delta_f = (float)cfg->minmax_delta;

@@ -30,6 +30,16 @@ class HashNetBackend:
         self.A = action_space
         self.pool = torch.zeros(num_slots, dtype=torch.int32, device=device)  # uint32 ids
 
+    def split(self, parts, max_grid=0):
+        """Backends over disjoint equal slices of the pool (SplitSelfPlayEngine)."""
+        n = self.pool.numel() // parts
+        out = []
+        for i in range(parts):
+            q = HashNetBackend.__new__(HashNetBackend)
+            q.A, q.pool = self.A, self.pool[i * n:(i + 1) * n]
+            out.append(q)
+        return out
+
     def initial(self, obs, out_slot, logits, value, stream):
         check(_lib.load().gmz_hashnet_initial(ptr(obs), obs.shape[0], self.A, ptr(out_slot), ptr(self.pool),
                                               ptr(logits), ptr(value), stream))
@@ -43,7 +53,8 @@ class HashNetBackend:
 class BatchedSelfPlayEngine:
     """G games per GPU.  ``cfg``: any object with the reference config attribute names."""
 
-    def __init__(self, cfg=None, num_games=1, net=None, device="cuda", seed=0, descent_hint=True, **overrides):
+    def __init__(self, cfg=None, num_games=1, net=None, device="cuda", seed=0, descent_hint=True, game_offset=0,
+                 **overrides):
         self.cfg = from_any(cfg, **overrides)
         c = self.cfg
         if c.MCTS_IMPLEMENTATION not in ("AlphaZero", "MuZero"):
@@ -55,7 +66,7 @@ class BatchedSelfPlayEngine:
         self.slots_per_game = c.NUM_SIMULATIONS + 2
         self.ecfg = _lib.EngineCfg(self.G, c.BOARD_SIZE, c.N_IN_ROW, c.NUM_SIMULATIONS, c.NUM_TOP_ACTIONS, self.mode,
                                    int(c.C_VISIT), 0 if descent_hint else 1, float(c.C_SCALE),
-                                   float(c.VALUE_MINMAX_DELTA), float(c.DISCOUNT))
+                                   float(c.VALUE_MINMAX_DELTA), float(c.DISCOUNT), int(game_offset))
         h = ctypes.c_void_p()
         check(self.lib.gmz_engine_create(ctypes.byref(self.ecfg), ctypes.byref(h)))
         self.handle = h
@@ -158,6 +169,13 @@ class BatchedSelfPlayEngine:
         """One search for every game (mcts.py:288-362 / 197-280).  ``gumbel``: optional f64[G,A]
         noise (host or device); default = device noise from (seed, move counter).
         Returns device tensors (policy f64[G,A], value f32[G], action int32[G])."""
+        for _ in self.search_steps(gumbel, stream):
+            pass
+        return self.policy, self.root_value, self.action
+
+    def search_steps(self, gumbel=None, stream=None):
+        """:meth:`search` as a generator that yields after each simulation wave has been enqueued
+        (SplitSelfPlayEngine interleaves the waves of engines on different streams)."""
         s = self._stream(stream)
         L = self.lib
         g = None
@@ -191,8 +209,8 @@ class BatchedSelfPlayEngine:
                 if w + 1 < waves:
                     check(L.gmz_engine_select(self.handle, ptr(self.in_slot), ptr(self.act_req), ptr(self.out_slot),
                                               ptr(self.obs), s))
+            yield w
         check(L.gmz_engine_finish_move(self.handle, ptr(self.policy), ptr(self.root_value), ptr(self.action), s))
-        return self.policy, self.root_value, self.action
 
     def play(self, action=None, reset_finished=True, stream=None):
         """do_move + get_game_ended for all games.  Returns the device status tensor
@@ -230,6 +248,148 @@ class BatchedSelfPlayEngine:
         check(self.lib.gmz_engine_root_stats(self.handle, ptr(visits), ptr(rn), ptr(rw), ptr(mx), ptr(mn),
                                              self._stream()))
         return visits, rn, rw, mx, mn
+
+
+class SplitSelfPlayEngine:
+    """G games as ``parts`` BatchedSelfPlayEngines of G/parts games, each on its own HIP stream, with
+    their simulation waves interleaved on the host (same public interface as BatchedSelfPlayEngine).
+
+    Why: one tower launch fills every CU (a persistent workgroup per CU), and the tree / head kernels
+    between two towers are short and latency-bound.  With two halves on two streams and each half's
+    tower grid capped at 3/4 of the CUs (``max_grid``), one half's tree and head kernels run on the
+    CUs the other half's tower leaves free, and each tower's ramp-up and tail overlap the other
+    half's work (measured with tools/dual_stream_probe.py).  Every game's search is
+    exactly the unsplit engine's: part i plays games [i*G/parts, (i+1)*G/parts) with ``game_offset``
+    so the device Gumbel noise per game is unchanged, and its outputs are row views of the full
+    tensors.  Calls fork from the caller's stream and join back to it."""
+
+    def __init__(self, cfg=None, num_games=2, net=None, device="cuda", seed=0, parts=2, max_grid=None,
+                 descent_hint=True, **overrides):
+        self.cfg = from_any(cfg, **overrides)
+        c = self.cfg
+        G = int(num_games)
+        if parts < 1 or G % parts:
+            raise ValueError("SplitSelfPlayEngine: num_games must be a multiple of parts")
+        self.lib = _lib.load()
+        self.device = torch.device(device)
+        self.G, self.A, self.size, self.parts = G, c.ACTION_SPACE_SIZE, c.BOARD_SIZE, int(parts)
+        self.mode = 1 if c.MCTS_IMPLEMENTATION == "MuZero" else 0
+        self.slots_per_game = c.NUM_SIMULATIONS + 2
+        g = self.g = G // parts
+        if max_grid is None:
+            max_grid = torch.cuda.get_device_properties(self.device).multi_processor_count * 3 // 4 if parts > 1 else 0
+        if net is None:
+            net = HashNetBackend(G * self.slots_per_game, self.A, device)
+        self.net = net
+        nets = net.split(parts, max_grid) if parts > 1 else [net]
+        self.engines = [BatchedSelfPlayEngine(c, g, nets[i], device, seed, descent_hint, game_offset=i * g)
+                        for i in range(parts)]
+        self.streams = [torch.cuda.Stream(self.device) for _ in range(parts)]
+        dev = self.device
+        self.policy = torch.zeros(G, self.A, dtype=torch.float64, device=dev)
+        self.root_value = torch.zeros(G, dtype=torch.float32, device=dev)
+        self.action = torch.zeros(G, dtype=torch.int32, device=dev)
+        self.status = torch.zeros(G, dtype=torch.int8, device=dev)
+        for i, e in enumerate(self.engines):  # the parts write straight into row slices
+            sl = slice(i * g, (i + 1) * g)
+            e.policy, e.root_value, e.action, e.status = self.policy[sl], self.root_value[sl], self.action[sl], self.status[sl]
+        self.waves_last = 0
+
+    # ------------------------------------------------------------------ streams
+    def _fork(self, stream=None):
+        main = stream if stream is not None else torch.cuda.current_stream(self.device)
+        ev = torch.cuda.Event()
+        ev.record(main)
+        for st in self.streams:
+            st.wait_event(ev)
+        return main
+
+    def _join(self, main):
+        for st in self.streams:
+            ev = torch.cuda.Event()
+            ev.record(st)
+            main.wait_event(ev)
+
+    def _rows(self, x, i):
+        return None if x is None else x[i * self.g:(i + 1) * self.g]
+
+    # ------------------------------------------------------------------ interface of BatchedSelfPlayEngine
+    def close(self):
+        for e in self.engines:
+            e.close()
+
+    def search(self, gumbel=None, stream=None):
+        g = None
+        if gumbel is not None:  # to the device on the caller's stream, before the fork
+            g = torch.as_tensor(gumbel, dtype=torch.float64).to(self.device).contiguous()
+        main = self._fork(stream)
+        gens = [e.search_steps(self._rows(g, i), st) for i, (e, st) in enumerate(zip(self.engines, self.streams))]
+        live = list(zip(gens, self.streams))
+        while live:  # one wave of each part in turn
+            for item in list(live):
+                gen, st = item
+                with torch.cuda.stream(st):
+                    try:
+                        next(gen)
+                    except StopIteration:
+                        live.remove(item)
+        self._join(main)
+        self.waves_last = max(e.waves_last for e in self.engines)
+        return self.policy, self.root_value, self.action
+
+    def play(self, action=None, reset_finished=True, stream=None):
+        a = None if action is None else torch.as_tensor(action, dtype=torch.int32).to(self.device)
+        main = self._fork(stream)
+        for i, (e, st) in enumerate(zip(self.engines, self.streams)):
+            with torch.cuda.stream(st):
+                e.play(self._rows(a, i), reset_finished)
+        self._join(main)
+        return self.status
+
+    def reset_games(self, mask=None):
+        for i, e in enumerate(self.engines):
+            e.reset_games(None if mask is None else np.asarray(mask)[i * self.g:(i + 1) * self.g])
+
+    def game_state(self):
+        parts = [e.game_state() for e in self.engines]
+        return tuple(torch.cat([p[k] for p in parts]) for k in range(4))
+
+    def set_positions(self, boards, players, last_moves, move_counts=None):
+        b = np.asarray(boards).reshape(self.G, -1)
+        p, lm = np.asarray(players).reshape(self.G), np.asarray(last_moves).reshape(self.G)
+        mc = None if move_counts is None else np.asarray(move_counts).reshape(self.G)
+        for i, e in enumerate(self.engines):
+            e.set_positions(self._rows(b, i), self._rows(p, i), self._rows(lm, i), self._rows(mc, i))
+
+    def winning_scan(self, boards, players, action=None, counters=None, stream=None):
+        return winning_scan(boards, players, action, self.cfg.N_IN_ROW, counters, stream, self.lib)
+
+    def tree_counters(self, reset=False):
+        out = dict(backups=0, backup_levels=0, selects=0, select_levels=0)
+        for e in self.engines:
+            for k, v in e.tree_counters(reset).items():
+                out[k] += v
+        return out
+
+    def root_stats(self):
+        parts = [e.root_stats() for e in self.engines]
+        return tuple(torch.cat([p[k] for p in parts]) for k in range(5))
+
+
+def default_streams(num_games):
+    """HIP streams for G games: two half-size engines from 256 games up (the measured gain of
+    SplitSelfPlayEngine needs each half's tower to fill a good share of the CUs), else one."""
+    return 2 if num_games >= 256 and num_games % 2 == 0 else 1
+
+
+def make_engine(cfg=None, num_games=1, net=None, device="cuda", seed=0, streams=None, **kw):
+    """BatchedSelfPlayEngine, or SplitSelfPlayEngine over ``streams`` HIP streams when streams > 1
+    (None: default_streams(num_games))."""
+    if streams is None:
+        streams = default_streams(num_games)
+    if streams > 1:
+        return SplitSelfPlayEngine(cfg, num_games, net, device, seed, parts=streams, **kw)
+    return BatchedSelfPlayEngine(cfg, num_games, net, device, seed, **kw)
 
 
 def winning_scan(boards, players, actions=None, n_in_row=5, counters=None, stream=None, lib=None):

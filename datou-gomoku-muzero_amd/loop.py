@@ -58,14 +58,14 @@ def slices_from_game(boards, players, lasts, pols, vals, acts, winner, H, discou
 class SelfPlay:
     """G games on this rank's GPU (the self-play half of the worker loop, worker.py)."""
 
-    def __init__(self, cfg, num_games, state_dict, seed=0, precision="fp16"):
+    def __init__(self, cfg, num_games, state_dict, seed=0, precision="fp16", streams=None):
         from . import engine as E, network as N
         from .worker import GameHistory
         c = cfg
         self.cfg, self.G = c, int(num_games)
         self.net = N.GomokuNetHip(state_dict, c, num_slots=self.G * (c.NUM_SIMULATIONS + 2), max_rows=self.G,
                                   precision=precision)
-        self.eng = E.BatchedSelfPlayEngine(c, num_games=self.G, net=self.net, seed=seed)
+        self.eng = E.make_engine(c, num_games=self.G, net=self.net, seed=seed, streams=streams)
         self.eng.reset_games()
         self.hist = GameHistory(self.G, c.ACTION_SPACE_SIZE, self.eng.device, min_game_len=2 * c.N_IN_ROW - 1)
         dev = self.eng.device

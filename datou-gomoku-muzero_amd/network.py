@@ -18,6 +18,7 @@ hidden-state pool; MFMA accumulation is float32 either way and gfx950 runs both 
 ``GomokuNetHip`` owns the 16-bit hidden-state slot pool (HBM) and launches the kernels through the
 C ABI (include/gmz.h gmz_net_*).  It is the ``net`` backend of engine.BatchedSelfPlayEngine.
 """
+import copy
 import ctypes
 
 import numpy as np
@@ -37,7 +38,7 @@ class NetWeights(ctypes.Structure):
                     "repr_stem_w", "repr_stem_b", "repr_convs", "repr_bias", "dyn_convs", "dyn_bias", "dyn_action",
                     "head_conv_w", "head_conv_b", "policy_fc_w", "policy_fc_b", "value_fc1_w", "value_fc1_b",
                     "value_fc2_w", "value_fc2_b", "reward_fc1_w", "reward_fc1_b", "reward_fc2_w", "reward_fc2_b")] + [
-                    ("dtype", ctypes.c_int32)]
+                    ("dtype", ctypes.c_int32), ("max_grid", ctypes.c_int32)]
 
 
 PRECISIONS = {"fp16": 0, "bf16": 1}  # include/gmz.h GMZ_NET_F16 / GMZ_NET_BF16
@@ -252,6 +253,32 @@ class GomokuNetHip:
         nbytes = ctypes.c_size_t()
         check(self.lib.gmz_net_workspace_bytes(ctypes.byref(w), self.max_rows, ctypes.byref(nbytes)))
         self.workspace = torch.empty(nbytes.value, dtype=torch.uint8, device=self.device)
+        for q in getattr(self, "_children", []):  # split() views follow the hot swap
+            keep = q.w.max_grid
+            q.w = NetWeights.from_buffer_copy(w)
+            q.w.max_grid = keep
+            q._tensors = self._tensors
+
+    def split(self, parts, max_grid=0):
+        """``parts`` backends over disjoint, equal slices of this hidden-state pool that share the
+        packed weights, each with its own workspace (engine.SplitSelfPlayEngine: one per HIP stream,
+        so their launches may run concurrently).  ``max_grid`` caps their persistent tower grid."""
+        n = self.pool.numel() // parts
+        out = []
+        for i in range(parts):
+            q = copy.copy(self)
+            q.pool = self.pool[i * n:(i + 1) * n]
+            q.max_rows = max(1, self.max_rows // parts)
+            q.w = NetWeights.from_buffer_copy(self.w)  # the same weight pointers
+            q.w.max_grid = int(max_grid)
+            nbytes = ctypes.c_size_t()
+            check(self.lib.gmz_net_workspace_bytes(ctypes.byref(q.w), q.max_rows, ctypes.byref(nbytes)))
+            q.workspace = torch.empty(nbytes.value, dtype=torch.uint8, device=self.device)
+            q.tower_timer = q.repr_timer = None
+            q._children = []
+            out.append(q)
+        self._children = getattr(self, "_children", []) + out
+        return out
 
     def _ws(self, rows):
         if rows > self.max_rows:  # grow the scratch (k_heads / reward split-K partials)

@@ -146,7 +146,7 @@ def gpu_selfplay_worker(worker_id, worker_mode, data_queue, log_status_queue, ui
                         latest_model_step=None, log_queue=None, pause_event=None, *, device=0, num_games=1024,
                         model_update_queue=None, initial_model_requests_queue=None, state_dict=None, cfg=None,
                         seed=0, max_moves=None, emit_move_notices=True, db_path="outputs/training_state.db",
-                        reanalysis_games=64, precision="fp16", move_times=None):
+                        reanalysis_games=64, precision="fp16", move_times=None, streams=None):
     logger = logging.getLogger("GpuSelfPlay-%s" % worker_id)
     if log_queue is not None:
         try:
@@ -175,7 +175,7 @@ def gpu_selfplay_worker(worker_id, worker_mode, data_queue, log_status_queue, ui
         state_dict = W.synthetic_state_dict(c, seed=seed, with_projection=False)
     G = int(num_games)
     net = N.GomokuNetHip(state_dict, c, num_slots=G * (c.NUM_SIMULATIONS + 2), max_rows=G, precision=precision)
-    eng = E.BatchedSelfPlayEngine(c, num_games=G, net=net, seed=seed + 7919 * int(worker_id))
+    eng = E.make_engine(c, num_games=G, net=net, seed=seed + 7919 * int(worker_id), streams=streams)
     eng.reset_games()
     H, A = c.BOARD_SIZE, c.ACTION_SPACE_SIZE
     hist = GameHistory(G, A, eng.device, min_game_len=2 * c.N_IN_ROW - 1)

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define GMZ_ABI_VERSION 3
+#define GMZ_ABI_VERSION 4
 
 /* ------------------------------------------------------------------ misc */
 const char *gmz_last_error(void);
@@ -81,6 +81,8 @@ typedef struct gmz_engine_cfg {
   double c_scale;           /* config.C_SCALE */
   double minmax_delta;      /* config.VALUE_MINMAX_DELTA */
   double discount;          /* config.DISCOUNT */
+  int32_t game_offset;      /* index of game 0 in the device Gumbel noise stream (engines that split */
+                            /* one batch: the same noise per game as one engine with every game)  */
 } gmz_engine_cfg;
 
 /* Synchronous (allocates HBM pools).  Node slots per game = num_simulations + 2 (root, one new node per wave, scratch). */
@@ -202,6 +204,10 @@ typedef struct gmz_net_weights {
   int32_t dtype;                /* GMZ_NET_F16 (default) or GMZ_NET_BF16: the type of the 16-bit     */
                                 /* arrays above (conv / stem / reward_fc1 weights), of the hidden-   */
                                 /* state pool and of the towers' MFMA operands (f32 accumulation)    */
+  int32_t max_grid;             /* cap on the persistent tower grid in workgroups (one per CU); 0 =  */
+                                /* every CU.  Two engines on two streams cap it (3/4 of the CUs) so */
+                                /* one stream's tree and head kernels find CUs while the other's     */
+                                /* tower runs (engine.SplitSelfPlayEngine)                           */
 } gmz_net_weights;
 #define GMZ_NET_F16 0
 #define GMZ_NET_BF16 1

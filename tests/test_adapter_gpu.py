@@ -182,10 +182,12 @@ def test_recurrent_timeout_retries_the_wave(M):
     assert len(logs[1]) == len(logs[0]) + 1 and logs[1][4] == logs[1][3]  # the dropped request, re-sent
 
 
-def test_worker_records_equal_a_synchronous_loop(M):
+@pytest.mark.parametrize("streams", [1, 2])
+def test_worker_records_equal_a_synchronous_loop(M, streams):
     """The worker's device-side history harvested one move behind (worker.GameHistory) yields exactly
     the records of a plain synchronous loop over the same engine (same seed, same weights) that copies
-    every move's position / policy / value / action to the host before the next move."""
+    every move's position / policy / value / action to the host before the next move — also with the
+    worker's games split over two HIP streams (engine.SplitSelfPlayEngine)."""
     from datou_gomoku_muzero_amd import engine as E, network as N, records as R, weights as W
     from datou_gomoku_muzero_amd.worker import gpu_selfplay_worker
     mcts, GmzConfig = M
@@ -197,7 +199,8 @@ def test_worker_records_equal_a_synchronous_loop(M):
             return False
 
     dq = queue.Queue()
-    gpu_selfplay_worker(0, None, dq, None, None, Ev(), num_games=G, cfg=cfg, max_moves=moves, seed=seed)
+    gpu_selfplay_worker(0, None, dq, None, None, Ev(), num_games=G, cfg=cfg, max_moves=moves, seed=seed,
+                        streams=streams)
     got = []
     while not dq.empty():
         got.append(dq.get())

@@ -81,3 +81,25 @@ def test_gpus_must_match_world_size():
     p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "4"], env=env,
                        capture_output=True, text=True, timeout=120)
     assert p.returncode == 2 and "disagrees" in p.stderr
+
+
+def test_timer_stats_union_of_launch_intervals():
+    """busy time = union of the launch intervals of all streams' timers; mean = per launch."""
+    import bench
+
+    class Ev:
+        def __init__(self, t):
+            self.t = t
+
+        def elapsed_time(self, other):
+            return other.t - self.t
+
+    class T:
+        def __init__(self, iv):
+            self.pairs = [[Ev(a), Ev(b), 0] for a, b in iv]
+    base = Ev(0.0)
+    n, mean, busy = bench.timer_stats([T([(0, 2), (5, 6)]), T([(1, 3), (6.5, 7), (10, 10.5)])], base)
+    assert n == 5
+    assert abs(mean - (2 + 1 + 2 + 0.5 + 0.5) / 5) < 1e-12
+    assert abs(busy - (3 + 1 + 0.5 + 0.5)) < 1e-12
+    assert bench.timer_stats([], base) == (0, 0.0, 0.0)
