@@ -6,8 +6,8 @@ One *step* = one move of every game on this GPU: the full Gumbel-MuZero search (
 move itself (do_move + get_game_ended, workers.py:178-181), G games at once (config 2: G = 1024).
 Finished games restart immediately.  Data: synthetic — empty boards, random-init GomokuNetEZ
 (8 blocks x 128 channels, numpy-seeded), Gumbel noise from the device RNG.  The G games run as two
-half-size engines on two HIP streams (--streams 2, engine.SplitSelfPlayEngine: the same games as
-one engine, bit for bit; one half's tree/head kernels overlap the other half's tower).
+half-size engines on two HIP streams (15x15 MuZero default; engine.SplitSelfPlayEngine: the same games
+as one engine, bit for bit; one half's tree/head kernels overlap the other half's tower).
 
   python bench.py [--gpus N --steps K --warmup W]
 
@@ -96,9 +96,10 @@ def parse(argv=None):
     ap.add_argument("--blocks", type=int, default=8)
     ap.add_argument("--mode", default="MuZero")
     ap.add_argument("--net", default="hip", choices=["hip", "hash"])
-    ap.add_argument("--streams", type=int, default=2,
-                    help="HIP streams per GPU: the G games as this many half-size engines whose waves interleave "
-                         "(engine.SplitSelfPlayEngine; 1 = one BatchedSelfPlayEngine)")
+    ap.add_argument("--streams", type=int, default=None,
+                    help="HIP streams per GPU: the G games as this many engines whose waves interleave "
+                         "(engine.SplitSelfPlayEngine; 1 = one BatchedSelfPlayEngine; default: "
+                         "engine.default_streams, i.e. 2 for 15x15 MuZero, else 1)")
     ap.add_argument("--single-stream-moves", type=int, default=2,
                     help="with --streams > 1: moves of ONE engine on one stream after the timed region, for the two "
                          "kernels' single-stream launch times (0: skip)")
@@ -195,7 +196,7 @@ def result_line(args, world, dt, waves, G, backend=None):
                                % (args.size, args.size, args.mode, args.sims, G, args.blocks),
                    "games_per_gpu": G, "global_games": G * world, "board_size": args.size,
                    "num_simulations": args.sims, "mcts": args.mode, "waves_per_move": waves / max(1, args.steps),
-                   "ranks": world, "dist_backend": backend, "streams_per_gpu": getattr(args, "streams", 1),
+                   "ranks": world, "dist_backend": backend, "streams_per_gpu": getattr(args, "streams", None) or 1,
                    "parallelism": "dp%d (independent games per GPU, no collective)" % world},
     }
 
@@ -382,6 +383,8 @@ def main():
         net = N.GomokuNetHip(sd, cfg, num_slots=slots, max_rows=G, precision=args.precision)
     else:
         net = E.HashNetBackend(slots, cfg.ACTION_SPACE_SIZE)
+    if args.streams is None:
+        args.streams = E.default_streams(cfg, G)
     eng = E.make_engine(cfg, num_games=G, net=net, seed=args.seed + 7919 * rank, streams=args.streams)
     eng.reset_games()
     parts = eng.engines if args.streams > 1 else [eng]

@@ -376,17 +376,22 @@ class SplitSelfPlayEngine:
         return tuple(torch.cat([p[k] for p in parts]) for k in range(5))
 
 
-def default_streams(num_games):
-    """HIP streams for G games: two half-size engines from 256 games up (the measured gain of
-    SplitSelfPlayEngine needs each half's tower to fill a good share of the CUs), else one."""
-    return 2 if num_games >= 256 and num_games % 2 == 0 else 1
+def default_streams(cfg, num_games):
+    """HIP streams for G games, as measured (profiles/r02_dual_stream_sweep.txt, r02_configs_two_streams.txt):
+    two half-size engines for 15x15 MuZero from 256 games up (+5-7 % moves/s: the 0.8 ms tower leaves
+    room beside it for the other half's ~0.1 ms of tree and head kernels); one engine otherwise (19x19:
+    the 2.6 ms tower dwarfs the rest and loses more to the capped grid, -2 %; 9x9 AlphaZero: -4 %)."""
+    c = from_any(cfg)
+    if c.BOARD_SIZE == 15 and c.MCTS_IMPLEMENTATION == "MuZero" and num_games >= 256 and num_games % 2 == 0:
+        return 2
+    return 1
 
 
 def make_engine(cfg=None, num_games=1, net=None, device="cuda", seed=0, streams=None, **kw):
     """BatchedSelfPlayEngine, or SplitSelfPlayEngine over ``streams`` HIP streams when streams > 1
-    (None: default_streams(num_games))."""
+    (None: default_streams(cfg, num_games))."""
     if streams is None:
-        streams = default_streams(num_games)
+        streams = default_streams(cfg, num_games)
     if streams > 1:
         return SplitSelfPlayEngine(cfg, num_games, net, device, seed, parts=streams, **kw)
     return BatchedSelfPlayEngine(cfg, num_games, net, device, seed, **kw)
