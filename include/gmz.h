@@ -77,7 +77,7 @@ typedef struct gmz_engine_cfg {
   int32_t num_top_actions;  /* config.NUM_TOP_ACTIONS (<= 64) */
   int32_t mode;             /* 0 = AlphaZero (mcts.py:197), 1 = MuZero (mcts.py:288) */
   int32_t c_visit;          /* config.C_VISIT */
-  int32_t flags;             /* bit 0: no descent prefetch hint (node_last; A/B timing only, results identical) */
+  int32_t flags;             /* bit 0: no descent prefetch hint (node header .last; A/B timing only, results identical) */
   double c_scale;           /* config.C_SCALE */
   double minmax_delta;      /* config.VALUE_MINMAX_DELTA */
   double discount;          /* config.DISCOUNT */
