@@ -81,6 +81,20 @@ PEAK_MFMA_TFLOPS = 2500.0   # MI355X dense f16 / bf16 MFMA (MI355X_MICROARCH.md,
 PEAK_HBM_GBS = 8000.0
 
 
+def pmc_traffic(path, args, G, az):
+    """HBM bytes per launch from a committed PMC summary (tools/pmc_round2.sh -> tools/pmc_summary.py) when it
+    was measured on this configuration (15x15, 8 blocks, MuZero, G = 1024, same precision and streams)."""
+    if not os.path.exists(path) or (args.size, args.blocks, G) != (15, 8, 1024) or az:
+        return None
+    try:
+        pm = json.load(open(path))
+    except Exception:
+        return None
+    if pm.get("precision", "bf16") != args.precision or int(pm.get("streams", 1)) != int(args.streams or 1):
+        return None
+    return pm.get("hbm_bytes_per_launch")
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -123,6 +137,7 @@ def parse(argv=None):
     ap.add_argument("--loop-buffer", type=int, default=65536, help="replay shard capacity per rank")
     ap.add_argument("--loop-prefill", type=int, default=4096, help="synthetic slices in each shard before the loop")
     ap.add_argument("--pmc-file", default=os.path.join(REPO, "profiles", "pmc_tower_latest.json"))
+    ap.add_argument("--pmc-tree-file", default=os.path.join(REPO, "profiles", "pmc_tree_latest.json"))
     return ap.parse_args(argv)
 
 
@@ -443,14 +458,7 @@ def main():
         # delivered rate while the kernel runs: all launches' FLOP over the union of their intervals
         # (with one stream = the per-launch figure; with two, launches of the two streams overlap)
         achieved = flop * n_launch / (busy * 1e-3) / 1e12 if busy > 0 else 0.0
-        traffic = None
-        if os.path.exists(args.pmc_file) and (args.size, args.blocks) == (15, 8) and not az:  # the PMC pass's config
-            try:
-                pm = json.load(open(args.pmc_file))
-                if pm.get("precision", "bf16") == args.precision:
-                    traffic = pm.get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
+        traffic = pmc_traffic(args.pmc_file, args, G, az)
         kname = ("k_tower3<%d,REPR> (representation tower, stem + %d fused convs + head 1x1 convs)" % (args.size, 2 * args.blocks)
                  if az else "k_tower3<%d,DYN> (dynamics tower, %d fused convs + head 1x1 convs)" % (args.size, 1 + 2 * args.blocks))
         out["roofline"] = {"bound": "mfma", "kernel": kname + ", " + args.precision,
@@ -468,7 +476,8 @@ def main():
         gbs = bpl * n_tree / (busy_tree * 1e-3) / 1e9 if busy_tree > 0 else 0.0
         out["roofline_tree"] = {
             "bound": "hbm", "kernel": "k_expand_select<%d> (backup of wave i + selection of wave i+1)" % ((A + 63) // 64),
-            "achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS, "traffic": None,
+            "achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS,
+            "traffic": pmc_traffic(args.pmc_tree_file, args, G, az),
             "launches": n_tree, "mean_launch_ms": ms_tree, "bytes_per_launch": bpl,
             "mean_backup_levels": ctr["backup_levels"] / max(1, ctr["backups"]),
             "mean_select_levels": ctr["select_levels"] / max(1, ctr["selects"]),
