@@ -94,7 +94,7 @@ def main():
     from datou_gomoku_muzero_amd import engine as E, network as N, weights as W
     sd = W.synthetic_state_dict(cfg, seed=0, with_projection=False)
     net = N.GomokuNetHip(sd, cfg, num_slots=a.games * (a.sims + 2), max_rows=a.games)
-    eng = E.BatchedSelfPlayEngine(cfg, num_games=a.games, net=net, seed=0)
+    eng = E.make_engine(cfg, num_games=a.games, net=net, seed=0)  # the worker's own choice of streams
     eng.reset_games()
     for i in range(a.warmup + a.moves):
         if i == a.warmup:
@@ -110,7 +110,8 @@ def main():
                       "queues": "torch.multiprocessing (spawn) Queues, main.py sizes; consumer process unpickles",
                       "move_notices": not a.no_move_notices, "messages": dict(counts),
                       "consumer_done_s": t_cons, "engine_only_moves_per_s": engine_rate,
-                      "worker_over_engine": a.games * a.moves / steady / engine_rate}))
+                      "worker_over_engine": a.games * a.moves / steady / engine_rate,
+                      "streams": E.default_streams(cfg, a.games)}))
 
 
 if __name__ == "__main__":
