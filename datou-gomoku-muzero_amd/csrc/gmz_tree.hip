@@ -314,7 +314,7 @@ __device__ __forceinline__ NormQ norm_q_consts(const Dev &D, float mm_max, float
 // _get_transformed_completed_Qs and of the score denominator, exact); the float64 normalisation
 // (q - min) / den runs only for visited children, an unvisited one takes the per-descent constant nq0
 // (its q is 0.0): the same correctly rounded quotient either way.
-template <int NJ>
+template <int NJ, bool HINT>
 __device__ int select_nonroot(const Dev &D, const uint64_t (&lg)[NJ], int g, int u, int lane, const NormQ &nz,
                               int *child, const RowRegs<NJ> &cur, RowRegs<NJ> &nxt, int *nxt_u) {
   int n[NJ], ch[NJ];
@@ -339,7 +339,7 @@ __device__ int select_nonroot(const Dev &D, const uint64_t (&lg)[NJ], int g, int
   const int nvis = __builtin_amdgcn_readfirstlane(cur.hdr.z);
   *nxt_u = -1;
   const int al = __builtin_amdgcn_readfirstlane(cur.hdr.w);
-  if (!D.no_hint && al >= 0 && al < D.A) {
+  if (HINT && al >= 0 && al < D.A) {
     const int cp = bcast_slot<NJ>(ch, al);
     if (cp > 0 && cp < D.S) {
       row_fetch<NJ>(D, g, cp, lane, nxt);
@@ -406,7 +406,7 @@ __device__ int select_nonroot(const Dev &D, const uint64_t (&lg)[NJ], int g, int
   TP_ADD(2, tp2 - tp1);
   TP_ADD(3, tp3 - tp2);
 #endif
-  if (D.no_hint) return a;
+  if (!HINT) return a;
   // hint for the next visit: the argmax once this visit is counted (N_a + 1, sum N + 1), the same
   // policy otherwise — the deterministic selection spreads visits, so it often moves on from a.
   // A prediction only (the row it names is fetched early), so float32 scores suffice.
@@ -642,8 +642,9 @@ __global__ void __launch_bounds__(256) k_set_root(Dev D, const float *__restrict
   if (lane == 0) D.gs[g] = st;
 }
 
-// one wave: select the leaf of every active game and emit its network request
-template <int NJ>
+// one wave: select the leaf of every active game and emit its network request.  AZ: AlphaZero (the
+// path is replayed on the root board for the observation); MuZero keeps no board state here.
+template <int NJ, bool HINT, bool AZ>
 __device__ __forceinline__ void select_game(const Dev &D, int g, int lane, int32_t *__restrict__ in_slot,
                                             int32_t *__restrict__ act_out, int32_t *__restrict__ out_slot,
                                             float *__restrict__ obs) {
@@ -655,7 +656,7 @@ __device__ __forceinline__ void select_game(const Dev &D, int g, int lane, int32
       out_slot[g] = -1;
       act_out[g] = 0;
     }
-    if (D.mode == 0 && obs) {
+    if (AZ && obs) {
       float *o = obs + (size_t)g * 3 * A;
       for (int a = lane; a < 3 * A; a += WAVE) o[a] = 0.f;
     }
@@ -664,11 +665,11 @@ __device__ __forceinline__ void select_game(const Dev &D, int g, int lane, int32
   // AlphaZero replay state (mcts.py:236-248): lane-owned cells of the root board
   int8_t cell[NJ];
   const int8_t *b = D.boards + (size_t)g * A;
-  int cp = D.players[g];
+  int cp = AZ ? D.players[g] : 0;
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int a = lane + WAVE * j;
-    cell[j] = a < A ? b[a] : 0;
+    cell[j] = (AZ && a < A) ? b[a] : 0;
   }
   int u = 0, d = 0, a = 0, last = -1;
   int32_t *pu = D.path_u + (size_t)g * S, *pa = D.path_a + (size_t)g * S;
@@ -698,7 +699,7 @@ __device__ __forceinline__ void select_game(const Dev &D, int g, int lane, int32
       TP_ADD(7, 1);
       TP_ADD(11, u == nxt_u ? 1 : 0);
 #endif
-      a = select_nonroot<NJ>(D, lg, g, u, lane, nz, &c, cur, nxt, &nxt_u);
+      a = select_nonroot<NJ, HINT>(D, lg, g, u, lane, nz, &c, cur, nxt, &nxt_u);
     }
     if (lane == 0) {
       pu[d] = u;
@@ -722,13 +723,13 @@ __device__ __forceinline__ void select_game(const Dev &D, int g, int lane, int32
     st.n_nodes = leaf + 1;
     st.depth = d;
     st.leaf = leaf;
-    st.k = (D.mode == 1) ? st.n_sel : 1;
+    st.k = AZ ? 1 : st.n_sel;
     D.gs[g] = st;
     in_slot[g] = g * S + u;
     act_out[g] = a;
     out_slot[g] = g * S + leaf;
   }
-  if (D.mode == 0 && obs) {  // observation of the replayed board (mcts.py:251)
+  if (AZ && obs) {  // observation of the replayed board (mcts.py:251)
     float *o = obs + (size_t)g * 3 * A;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
@@ -866,12 +867,12 @@ __device__ __forceinline__ void expand_backup_game(const Dev &D, int g, int lane
   if (lane == 0) D.gs[g] = st;
 }
 
-template <int NJ>
+template <int NJ, bool HINT, bool AZ>
 __global__ void __launch_bounds__(256) k_select(Dev D, int32_t *__restrict__ in_slot, int32_t *__restrict__ act_out,
                                                 int32_t *__restrict__ out_slot, float *__restrict__ obs) {
   const int g = blockIdx.x * 4 + threadIdx.x / WAVE, lane = threadIdx.x & (WAVE - 1);
   if (g >= D.G) return;
-  select_game<NJ>(D, g, lane, in_slot, act_out, out_slot, obs);
+  select_game<NJ, HINT, AZ>(D, g, lane, in_slot, act_out, out_slot, obs);
   if (lane == 0) {  // selection counters (see k_expand_select): every selected game-wave is one network row
     const GameState s1 = D.gs[g];
     if (s1.active) {
@@ -894,8 +895,10 @@ __global__ void __launch_bounds__(256) k_expand_backup(Dev D, const float *__res
 // expand + backup of wave i, then select of wave i+1, in one launch: every game's tree is owned by
 // one wave, so the only dependency between the two phases is that wave's own stores (one kernel
 // boundary per simulation wave fewer)
-template <int NJ>
-__global__ void __launch_bounds__(256) k_expand_select(Dev D, const float *__restrict__ logits_in,
+// without the hint (large G: many waves per SIMD hide the row fetch) the kernel is held to 128 VGPRs:
+// 4 resident waves per SIMD instead of 3
+template <int NJ, bool HINT, bool AZ>
+__global__ void __launch_bounds__(256, (HINT || NJ > 4) ? 1 : 4) k_expand_select(Dev D, const float *__restrict__ logits_in,
                                                        const float *__restrict__ value_in,
                                                        const float *__restrict__ reward_in,
                                                        int32_t *__restrict__ in_slot, int32_t *__restrict__ act_out,
@@ -911,7 +914,7 @@ __global__ void __launch_bounds__(256) k_expand_select(Dev D, const float *__res
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_s_waitcnt(0);
   TP_STAMP(tk1);
-  select_game<NJ>(D, g, lane, in_slot, act_out, out_slot, obs);
+  select_game<NJ, HINT, AZ>(D, g, lane, in_slot, act_out, out_slot, obs);
 #ifdef GMZ_TREE_PROF
   __builtin_amdgcn_s_waitcnt(0);
   TP_STAMP(tk2);
@@ -1170,6 +1173,31 @@ static inline dim3 wave_grid(const gmz_engine *e) { return dim3((e->D.G + 3) / 4
     GMZ_LAUNCH_CHECK();                                                                                            \
   } while (0)
 
+// launch KERNEL<NJ, HINT, AZ> (the selection kernels: descent prefetch hint compiled in or out, the
+// AlphaZero board replay compiled in or out)
+#define GMZ_SEL_HA(KERNEL, NJV, h_, az_, e, s_, ...)                                                           \
+  do {                                                                                                         \
+    if (h_) {                                                                                                  \
+      if (az_) hipLaunchKernelGGL((KERNEL<NJV, true, true>), wave_grid(e), dim3(256), 0, s_, __VA_ARGS__);     \
+      else hipLaunchKernelGGL((KERNEL<NJV, true, false>), wave_grid(e), dim3(256), 0, s_, __VA_ARGS__);        \
+    } else {                                                                                                   \
+      if (az_) hipLaunchKernelGGL((KERNEL<NJV, false, true>), wave_grid(e), dim3(256), 0, s_, __VA_ARGS__);    \
+      else hipLaunchKernelGGL((KERNEL<NJV, false, false>), wave_grid(e), dim3(256), 0, s_, __VA_ARGS__);       \
+    }                                                                                                          \
+  } while (0)
+#define GMZ_LAUNCH_SEL(KERNEL, e, stream, ...)                                                                 \
+  do {                                                                                                         \
+    const int nj_ = ((e)->D.A + 63) / 64;                                                                      \
+    const bool h_ = !(e)->D.no_hint, az_ = (e)->D.mode == 0;                                                   \
+    hipStream_t s_ = (hipStream_t)(stream);                                                                    \
+    if (nj_ <= 1) GMZ_SEL_HA(KERNEL, 1, h_, az_, e, s_, __VA_ARGS__);                                          \
+    else if (nj_ <= 2) GMZ_SEL_HA(KERNEL, 2, h_, az_, e, s_, __VA_ARGS__);                                     \
+    else if (nj_ <= 4) GMZ_SEL_HA(KERNEL, 4, h_, az_, e, s_, __VA_ARGS__);                                     \
+    else if (nj_ <= 6) GMZ_SEL_HA(KERNEL, 6, h_, az_, e, s_, __VA_ARGS__);                                     \
+    else GMZ_SEL_HA(KERNEL, 8, h_, az_, e, s_, __VA_ARGS__);                                                   \
+    GMZ_LAUNCH_CHECK();                                                                                        \
+  } while (0)
+
 GMZ_EXPORT int gmz_engine_begin_move(gmz_engine *e, const double *gumbel, uint64_t seed, float *obs, void *stream) {
   if (!e || !obs) return fail("gmz_engine_begin_move: null argument");
   const uint32_t ctr = e->counter++;
@@ -1187,7 +1215,7 @@ GMZ_EXPORT int gmz_engine_select(gmz_engine *e, int32_t *in_slot, int32_t *actio
                                  void *stream) {
   if (!e || !in_slot || !action || !out_slot) return fail("gmz_engine_select: null argument");
   if (e->D.mode == 0 && !obs) return fail("gmz_engine_select: AlphaZero mode needs obs");
-  GMZ_LAUNCH_NJ(k_select, e, stream, e->D, in_slot, action, out_slot, obs);
+  GMZ_LAUNCH_SEL(k_select, e, stream, e->D, in_slot, action, out_slot, obs);
   return 0;
 }
 
@@ -1208,7 +1236,7 @@ GMZ_EXPORT int gmz_engine_expand_backup_select(gmz_engine *e, const float *logit
   if (e->D.mode == 1 && !reward) return fail("gmz_engine_expand_backup_select: MuZero mode needs reward");
   if (e->D.mode == 0 && !obs) return fail("gmz_engine_expand_backup_select: AlphaZero mode needs obs");
   const float *rw = e->D.mode == 1 ? reward : nullptr;
-  GMZ_LAUNCH_NJ(k_expand_select, e, stream, e->D, logits, value, rw, in_slot, action, out_slot, obs);
+  GMZ_LAUNCH_SEL(k_expand_select, e, stream, e->D, logits, value, rw, in_slot, action, out_slot, obs);
   return 0;
 }
 

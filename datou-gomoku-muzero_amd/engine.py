@@ -53,7 +53,7 @@ class HashNetBackend:
 class BatchedSelfPlayEngine:
     """G games per GPU.  ``cfg``: any object with the reference config attribute names."""
 
-    def __init__(self, cfg=None, num_games=1, net=None, device="cuda", seed=0, descent_hint=True, game_offset=0,
+    def __init__(self, cfg=None, num_games=1, net=None, device="cuda", seed=0, descent_hint=None, game_offset=0,
                  **overrides):
         self.cfg = from_any(cfg, **overrides)
         c = self.cfg
@@ -62,6 +62,8 @@ class BatchedSelfPlayEngine:
         self.lib = _lib.load()
         self.device = torch.device(device)
         self.G, self.A, self.size = int(num_games), c.ACTION_SPACE_SIZE, c.BOARD_SIZE
+        if descent_hint is None:  # the next-visit row prefetch pays at 1-2 waves per SIMD; from 4,096 games on,
+            descent_hint = self.G < 4096  # without it the kernel fits 4 waves per SIMD
         self.mode = 1 if c.MCTS_IMPLEMENTATION == "MuZero" else 0
         self.slots_per_game = c.NUM_SIMULATIONS + 2
         self.ecfg = _lib.EngineCfg(self.G, c.BOARD_SIZE, c.N_IN_ROW, c.NUM_SIMULATIONS, c.NUM_TOP_ACTIONS, self.mode,
@@ -264,7 +266,7 @@ class SplitSelfPlayEngine:
     tensors.  Calls fork from the caller's stream and join back to it."""
 
     def __init__(self, cfg=None, num_games=2, net=None, device="cuda", seed=0, parts=2, max_grid=None,
-                 descent_hint=True, **overrides):
+                 descent_hint=None, **overrides):
         self.cfg = from_any(cfg, **overrides)
         c = self.cfg
         G = int(num_games)
