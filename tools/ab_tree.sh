@@ -18,5 +18,6 @@ for kind in ("old", "new"):
     v = [json.load(open(f)) for f in sorted(glob.glob(sys.argv[1] + "/%s_*.json" % kind))]
     print(kind, "moves/s", " ".join("%.0f" % d["value"] for d in v), "| tower ms", " ".join("%.4f" % d["roofline"]["mean_launch_ms"] for d in v),
           "| tree us", " ".join("%.1f" % (d["roofline_tree"]["mean_launch_ms"] * 1e3) for d in v),
-          "| tree GB/s", " ".join("%.0f" % d["roofline_tree"]["achieved"] for d in v))
+          "| tree GB/s", " ".join("%.0f" % d["roofline_tree"]["achieved"] for d in v),
+          "| single-stream tree us", " ".join("%.1f" % (d.get("single_stream_kernels", {}).get("tree", {}).get("mean_launch_ms", 0) * 1e3) for d in v))
 PY
