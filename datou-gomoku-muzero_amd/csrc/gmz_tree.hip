@@ -407,26 +407,10 @@ __device__ int select_nonroot(const Dev &D, const uint64_t (&lg)[NJ], int g, int
   TP_ADD(3, tp3 - tp2);
 #endif
   if (!HINT) return a;
-  // hint for the next visit: the argmax once this visit is counted (N_a + 1, sum N + 1), the same
-  // policy otherwise — the deterministic selection spreads visits, so it often moves on from a.
-  // A prediction only (the row it names is fetched early), so float32 scores suffice.
-  float best2 = -INFINITY, sc2[NJ];
-  const float inv_tot2 = 1.0f / (float)(2 + tot);
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int aj = lane + WAVE * j;
-    sc2[j] = -INFINITY;
-    if (aj < D.A && ((lg[j] >> lane) & 1ull)) sc2[j] = (float)p[j] - (float)(n[j] + (aj == a)) * inv_tot2;
-    best2 = fmaxf(best2, sc2[j]);
-  }
-  best2 = dred_max_f(best2);
-  int a2 = a;
-#pragma unroll
-  for (int j = NJ - 1; j >= 0; --j) {
-    const uint64_t mk = __ballot(sc2[j] == best2 && best2 != -INFINITY);
-    if (mk) a2 = WAVE * j + __builtin_ctzll(mk);
-  }
-  if (lane == 0) D.hdr[(size_t)g * D.S + u].w = a2;
+  // hint for the next visit: the same child again.  The exact prediction (the argmax once this visit
+  // is counted: N_a + 1, sum N + 1) equals this visit's action 94.6 % of the time
+  // (profiles/r02_tree_phase_prof_hint_same.json); a prediction only, so the extra argmax is not worth its cost
+  if (lane == 0) D.hdr[(size_t)g * D.S + u].w = a;
   TP_STAMP(tp4);
 #ifdef GMZ_TREE_PROF
   TP_ADD(4, tp4 - tp3);
