@@ -282,6 +282,42 @@ __device__ __forceinline__ void row_fetch(const Dev &D, int g, int u, int lane, 
   r.hdr = D.hdr[(size_t)g * D.S + u];
 }
 
+// The descent prefetch lands in LDS, not registers: one wave's slot holds a node's edge row (NJ x 1 KB),
+// its logits (NJ x 256 B) and its header (16 B), moved by LDS-DMA (global_load_lds: no VGPRs), so the
+// hint costs the selection kernels no occupancy.
+template <int NJ>
+struct HintSlot {
+  static constexpr int EDGES = 0, LOGITS = NJ * 1024, HDR = NJ * 1280, BYTES = NJ * 1280 + 16;
+};
+template <int NJ>
+__device__ __forceinline__ void row_prefetch_lds(const Dev &D, int g, int u, int lane, uint8_t *slot) {
+  using L = HintSlot<NJ>;
+  const Edge *row = edge_row(D, g, u);
+  const float *lr = D.logits + ((size_t)g * D.S + u) * D.A;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int a = lane + WAVE * j, ac = a < D.A ? a : D.A - 1;
+    __builtin_amdgcn_global_load_lds((const void *)(row + ac),
+                                     (__attribute__((address_space(3))) void *)(slot + L::EDGES + j * 1024), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void *)(lr + ac),
+                                     (__attribute__((address_space(3))) void *)(slot + L::LOGITS + j * 256), 4, 0, 0);
+  }
+  if (lane < 4)
+    __builtin_amdgcn_global_load_lds((const void *)((const int *)(D.hdr + (size_t)g * D.S + u) + lane),
+                                     (__attribute__((address_space(3))) void *)(slot + L::HDR), 4, 0, 0);
+}
+template <int NJ>
+__device__ __forceinline__ void row_from_lds(const uint8_t *slot, int lane, RowRegs<NJ> &r) {
+  using L = HintSlot<NJ>;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA has landed
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    r.e[j] = *(const int4 *)(slot + L::EDGES + j * 1024 + lane * 16);
+    r.lv[j] = *(const float *)(slot + L::LOGITS + j * 256 + lane * 4);
+  }
+  r.hdr = *(const int4 *)(slot + L::HDR);
+}
+
 // Per-descent constants of the completed-Q normalisation (mm_max / mm_min do not change during a
 // selection): the denominator and the normalised Q of an unvisited child (q = 0.0, mcts.py:35-38).
 struct NormQ {
@@ -308,15 +344,15 @@ __device__ __forceinline__ NormQ norm_q_consts(const Dev &D, float mm_max, float
 // *child = its child id (from the row: no second dependent round trip per level).  The descent is one
 // dependent row fetch per level, so while this level's selection computes, the row of the child of the
 // hinted action (hdr.last: the predicted choice of this node's next visit, set at its last visit) is
-// fetched into `nxt` (*nxt_u = that child, -1 if none): the caller uses it when the prediction holds
-// and fetches afresh otherwise.  Results never depend on the hint.
+// fetched into the wave's LDS hint slot (*nxt_u = that child, -1 if none): the caller reads it from
+// LDS when the prediction holds and fetches afresh otherwise.  Results never depend on the hint.
 // The node header supplies sum N, max N and "every child visited" (the integer reductions of
 // _get_transformed_completed_Qs and of the score denominator, exact); the float64 normalisation
 // (q - min) / den runs only for visited children, an unvisited one takes the per-descent constant nq0
 // (its q is 0.0): the same correctly rounded quotient either way.
 template <int NJ, bool HINT>
 __device__ int select_nonroot(const Dev &D, const uint64_t (&lg)[NJ], int g, int u, int lane, const NormQ &nz,
-                              int *child, const RowRegs<NJ> &cur, RowRegs<NJ> &nxt, int *nxt_u) {
+                              int *child, const RowRegs<NJ> &cur, uint8_t *hint_slot, int *nxt_u) {
   int n[NJ], ch[NJ];
   float q[NJ];
   double p[NJ];
@@ -342,7 +378,7 @@ __device__ int select_nonroot(const Dev &D, const uint64_t (&lg)[NJ], int g, int
   if (HINT && al >= 0 && al < D.A) {
     const int cp = bcast_slot<NJ>(ch, al);
     if (cp > 0 && cp < D.S) {
-      row_fetch<NJ>(D, g, cp, lane, nxt);
+      row_prefetch_lds<NJ>(D, g, cp, lane, hint_slot);
       *nxt_u = cp;
     }
   }
@@ -631,7 +667,7 @@ __global__ void __launch_bounds__(256) k_set_root(Dev D, const float *__restrict
 template <int NJ, bool HINT, bool AZ>
 __device__ __forceinline__ void select_game(const Dev &D, int g, int lane, int32_t *__restrict__ in_slot,
                                             int32_t *__restrict__ act_out, int32_t *__restrict__ out_slot,
-                                            float *__restrict__ obs) {
+                                            float *__restrict__ obs, uint8_t *hint_slot) {
   const int A = D.A, S = D.S;
   GameState st = D.gs[g];
   if (!st.active) {
@@ -659,7 +695,7 @@ __device__ __forceinline__ void select_game(const Dev &D, int g, int lane, int32
   int32_t *pu = D.path_u + (size_t)g * S, *pa = D.path_a + (size_t)g * S;
   uint64_t lg[NJ];
   load_legal<NJ>(D, g, lg);
-  RowRegs<NJ> cur, nxt;
+  RowRegs<NJ> cur;
   int nxt_u = -1;
   const NormQ nz = norm_q_consts(D, st.mm_max, st.mm_min);
   for (;;) {
@@ -674,7 +710,7 @@ __device__ __forceinline__ void select_game(const Dev &D, int g, int lane, int32
 #endif
     } else {
       TP_STAMP(tf0);
-      if (u == nxt_u) cur = nxt;  // the hinted row is this node's
+      if (HINT && u == nxt_u) row_from_lds<NJ>(hint_slot, lane, cur);  // the hinted row is this node's
       else row_fetch<NJ>(D, g, u, lane, cur);
 #ifdef GMZ_TREE_PROF
       __builtin_amdgcn_s_waitcnt(0);
@@ -683,7 +719,7 @@ __device__ __forceinline__ void select_game(const Dev &D, int g, int lane, int32
       TP_ADD(7, 1);
       TP_ADD(11, u == nxt_u ? 1 : 0);
 #endif
-      a = select_nonroot<NJ, HINT>(D, lg, g, u, lane, nz, &c, cur, nxt, &nxt_u);
+      a = select_nonroot<NJ, HINT>(D, lg, g, u, lane, nz, &c, cur, hint_slot, &nxt_u);
     }
     if (lane == 0) {
       pu[d] = u;
@@ -856,7 +892,9 @@ __global__ void __launch_bounds__(256) k_select(Dev D, int32_t *__restrict__ in_
                                                 int32_t *__restrict__ out_slot, float *__restrict__ obs) {
   const int g = blockIdx.x * 4 + threadIdx.x / WAVE, lane = threadIdx.x & (WAVE - 1);
   if (g >= D.G) return;
-  select_game<NJ, HINT, AZ>(D, g, lane, in_slot, act_out, out_slot, obs);
+  __shared__ __attribute__((aligned(16))) uint8_t hint_lds[HINT ? 4 * HintSlot<NJ>::BYTES : 16];
+  select_game<NJ, HINT, AZ>(D, g, lane, in_slot, act_out, out_slot, obs,
+                            hint_lds + (HINT ? (threadIdx.x / WAVE) * HintSlot<NJ>::BYTES : 0));
   if (lane == 0) {  // selection counters (see k_expand_select): every selected game-wave is one network row
     const GameState s1 = D.gs[g];
     if (s1.active) {
@@ -898,7 +936,9 @@ __global__ void __launch_bounds__(256, (HINT || NJ > 4) ? 1 : 4) k_expand_select
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_s_waitcnt(0);
   TP_STAMP(tk1);
-  select_game<NJ, HINT, AZ>(D, g, lane, in_slot, act_out, out_slot, obs);
+  __shared__ __attribute__((aligned(16))) uint8_t hint_lds[HINT ? 4 * HintSlot<NJ>::BYTES : 16];
+  select_game<NJ, HINT, AZ>(D, g, lane, in_slot, act_out, out_slot, obs,
+                            hint_lds + (HINT ? (threadIdx.x / WAVE) * HintSlot<NJ>::BYTES : 0));
 #ifdef GMZ_TREE_PROF
   __builtin_amdgcn_s_waitcnt(0);
   TP_STAMP(tk2);
