@@ -294,9 +294,11 @@ __device__ __forceinline__ void row_prefetch_lds(const Dev &D, int g, int u, int
   using L = HintSlot<NJ>;
   const Edge *row = edge_row(D, g, u);
   const float *lr = D.logits + ((size_t)g * D.S + u) * D.A;
+  int ln = lane;
+  asm volatile("" : "+v"(ln));  // per-call lane offsets: not hoisted out of the descent (VGPR budget)
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
-    const int a = lane + WAVE * j, ac = a < D.A ? a : D.A - 1;
+    const int a = ln + WAVE * j, ac = a < D.A ? a : D.A - 1;
     __builtin_amdgcn_global_load_lds((const void *)(row + ac),
                                      (__attribute__((address_space(3))) void *)(slot + L::EDGES + j * 1024), 16, 0, 0);
     __builtin_amdgcn_global_load_lds((const void *)(lr + ac),
@@ -894,7 +896,7 @@ __global__ void __launch_bounds__(256) k_select(Dev D, int32_t *__restrict__ in_
   if (g >= D.G) return;
   __shared__ __attribute__((aligned(16))) uint8_t hint_lds[HINT ? 4 * HintSlot<NJ>::BYTES : 16];
   select_game<NJ, HINT, AZ>(D, g, lane, in_slot, act_out, out_slot, obs,
-                            hint_lds + (HINT ? (threadIdx.x / WAVE) * HintSlot<NJ>::BYTES : 0));
+                            hint_lds + (HINT ? __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE) * HintSlot<NJ>::BYTES : 0));
   if (lane == 0) {  // selection counters (see k_expand_select): every selected game-wave is one network row
     const GameState s1 = D.gs[g];
     if (s1.active) {
@@ -938,7 +940,7 @@ __global__ void __launch_bounds__(256, (HINT || NJ > 4) ? 1 : 4) k_expand_select
   TP_STAMP(tk1);
   __shared__ __attribute__((aligned(16))) uint8_t hint_lds[HINT ? 4 * HintSlot<NJ>::BYTES : 16];
   select_game<NJ, HINT, AZ>(D, g, lane, in_slot, act_out, out_slot, obs,
-                            hint_lds + (HINT ? (threadIdx.x / WAVE) * HintSlot<NJ>::BYTES : 0));
+                            hint_lds + (HINT ? __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE) * HintSlot<NJ>::BYTES : 0));
 #ifdef GMZ_TREE_PROF
   __builtin_amdgcn_s_waitcnt(0);
   TP_STAMP(tk2);
