@@ -712,8 +712,12 @@ __device__ __forceinline__ void select_game(const Dev &D, int g, int lane, int32
 #endif
     } else {
       TP_STAMP(tf0);
-      if (HINT && u == nxt_u) row_from_lds<NJ>(hint_slot, lane, cur);  // the hinted row is this node's
-      else row_fetch<NJ>(D, g, u, lane, cur);
+      if constexpr (HINT) {  // the row arrives through the wave's LDS slot: prefetched (the hint held) or now
+        if (u != nxt_u) row_prefetch_lds<NJ>(D, g, u, lane, hint_slot);
+        row_from_lds<NJ>(hint_slot, lane, cur);
+      } else {
+        row_fetch<NJ>(D, g, u, lane, cur);
+      }
 #ifdef GMZ_TREE_PROF
       __builtin_amdgcn_s_waitcnt(0);
       TP_STAMP(tf1);
@@ -919,10 +923,9 @@ __global__ void __launch_bounds__(256) k_expand_backup(Dev D, const float *__res
 // expand + backup of wave i, then select of wave i+1, in one launch: every game's tree is owned by
 // one wave, so the only dependency between the two phases is that wave's own stores (one kernel
 // boundary per simulation wave fewer)
-// without the hint (large G: many waves per SIMD hide the row fetch) the kernel is held to 128 VGPRs:
-// 4 resident waves per SIMD instead of 3
+// held to 128 VGPRs up to 15x15 boards (NJ <= 4): 4 resident waves per SIMD when G exceeds the SIMDs
 template <int NJ, bool HINT, bool AZ>
-__global__ void __launch_bounds__(256, (HINT || NJ > 4) ? 1 : 4) k_expand_select(Dev D, const float *__restrict__ logits_in,
+__global__ void __launch_bounds__(256, NJ > 4 ? 1 : 4) k_expand_select(Dev D, const float *__restrict__ logits_in,
                                                        const float *__restrict__ value_in,
                                                        const float *__restrict__ reward_in,
                                                        int32_t *__restrict__ in_slot, int32_t *__restrict__ act_out,
