@@ -15,6 +15,9 @@
 //   Edge edges[G][S][A]   {child, N, W, R} 16 B per (node, action): one dwordx4 per lane per
 //                         action, coalesced across the wave when a node's children are scanned
 //   float logits[G][S][A] node policy logits (network output)
+//   double expl[G][S][A2] exp(logit - max legal logit) per node, A2 = A rounded up to even: computed
+//                         once when the node is expanded; a non-root selection's softmax then needs
+//                         an exp only for its visited children (shift invariance, select_nonroot)
 //   int path_u/path_a[G][S], node_parent/node_action[G][S]
 //   int4 hdr[G][S]        per-node header {sum of child N, max child N, visited children, next-visit
 //                         hint}: maintained by the backup so that a selection step needs no integer
@@ -30,6 +33,7 @@
 #include "../../include/gmz.h"
 
 #include <math.h>
+#include <type_traits>
 #include <string.h>
 #include <vector>
 
@@ -54,6 +58,7 @@ struct GameState {
 struct Dev {
   Edge *edges;
   float *logits;
+  double *expl;  // [G][S][A2] exp(logit - max legal logit), written by the expansion
   int32_t *node_parent, *node_action, *path_u, *path_a, *sel;
   int4 *hdr;           // [G][S] NodeHdr {tot = sum N_child, maxn = max N_child, nvis = #children N > 0, last}
   int32_t *ctr;        // [G][4] k_expand_select work counters (gmz_engine_tree_counters)
@@ -63,13 +68,18 @@ struct Dev {
   double *gumbel;
   int8_t *boards, *players;
   int32_t *last_moves, *move_counts;
-  int G, A, S, size, n_sims, m_top, c_visit, mode;
+  int G, A, A2, S, size, n_sims, m_top, c_visit, mode;
   int game_offset;  // gmz_engine_cfg.game_offset: global index of game 0 (device Gumbel noise)
   int no_hint;  // gmz_engine_cfg.flags bit 0: descent prefetch hint off (timing A/B; results identical)
   double c_scale;
   float disc_f, delta_f;
 };
 
+// waves per SIMD the hint kernel is compiled for: 2 (<= 256 VGPRs) measured faster than 4 (128 VGPRs,
+// spills) at 1,024 games per engine (36.4 vs 46.9 us, profiles/r02_tree_expl_variants.txt)
+#ifndef GMZ_HINT_WPS
+#define GMZ_HINT_WPS 2
+#endif
 #ifdef GMZ_TREE_PROF
 // phase-cycle instrumentation (tools/tree_prof.py builds a separate library with -DGMZ_TREE_PROF)
 // per-wave accumulators in LDS (no global atomics inside the timed phases), flushed once per wave
@@ -261,61 +271,70 @@ __device__ __forceinline__ void load_legal(const Dev &D, int g, uint64_t (&lg)[N
   for (int j = 0; j < NJ; ++j) lg[j] = D.legal[(size_t)g * gmz::NJ + j];
 }
 
-// one non-root node's edge row, logits and selection hint in registers (index clamped, unconditional
-// loads: one memory round trip)
-template <int NJ>
+// one non-root node's edge row, its logits (EX = false) or cached exp(logit - max legal logit)
+// (EX = true), and its header in registers
+template <int NJ, bool EX>
 struct RowRegs {
   int4 e[NJ];
-  float lv[NJ];
+  typename std::conditional<EX, double, float>::type v[NJ];
   int4 hdr;  // the node's header {tot, maxn, nvis, last}
 };
+__device__ __forceinline__ const double *expl_row(const Dev &D, int g, int u) {
+  return D.expl + ((size_t)g * D.S + u) * D.A2;
+}
 template <int NJ>
-__device__ __forceinline__ void row_fetch(const Dev &D, int g, int u, int lane, RowRegs<NJ> &r) {
+__device__ __forceinline__ void row_fetch(const Dev &D, int g, int u, int lane, RowRegs<NJ, false> &r) {
+  // index clamped, unconditional loads: one memory round trip
   const Edge *row = edge_row(D, g, u);
   const float *lr = D.logits + ((size_t)g * D.S + u) * D.A;
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int a = lane + WAVE * j, ac = a < D.A ? a : D.A - 1;
     r.e[j] = *(const int4 *)(row + ac);
-    r.lv[j] = lr[ac];
+    r.v[j] = lr[ac];
   }
   r.hdr = D.hdr[(size_t)g * D.S + u];
 }
 
 // The descent prefetch lands in LDS, not registers: one wave's slot holds a node's edge row (NJ x 1 KB),
-// its logits (NJ x 256 B) and its header (16 B), moved by LDS-DMA (global_load_lds: no VGPRs), so the
-// hint costs the selection kernels no occupancy.
+// its exp row (actions in natural order, 16 B = two actions per lane and DMA: ceil(NJ/2) x 1 KB) and its
+// header (16 B), moved by LDS-DMA (global_load_lds: no VGPRs), so the hint costs the selection kernels
+// no occupancy.
 template <int NJ>
 struct HintSlot {
-  static constexpr int EDGES = 0, LOGITS = NJ * 1024, HDR = NJ * 1280, BYTES = NJ * 1280 + 16;
+  static constexpr int EDGES = 0, EXPL = NJ * 1024, HDR = EXPL + ((NJ + 1) / 2) * 1024, BYTES = HDR + 16;
 };
 template <int NJ>
 __device__ __forceinline__ void row_prefetch_lds(const Dev &D, int g, int u, int lane, uint8_t *slot) {
   using L = HintSlot<NJ>;
-  const Edge *row = edge_row(D, g, u);
-  const float *lr = D.logits + ((size_t)g * D.S + u) * D.A;
+  const char *row = (const char *)edge_row(D, g, u);
+  const char *xr = (const char *)expl_row(D, g, u);
   int ln = lane;
   asm volatile("" : "+v"(ln));  // per-call lane offsets: not hoisted out of the descent (VGPR budget)
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int a = ln + WAVE * j, ac = a < D.A ? a : D.A - 1;
-    __builtin_amdgcn_global_load_lds((const void *)(row + ac),
+    __builtin_amdgcn_global_load_lds((const void *)(row + (uint32_t)(ac * 16)),
                                      (__attribute__((address_space(3))) void *)(slot + L::EDGES + j * 1024), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds((const void *)(lr + ac),
-                                     (__attribute__((address_space(3))) void *)(slot + L::LOGITS + j * 256), 4, 0, 0);
+  }
+#pragma unroll
+  for (int i = 0; i < (NJ + 1) / 2; ++i) {
+    const int a = 2 * WAVE * i + 2 * ln, ac = a < D.A2 - 2 ? a : D.A2 - 2;
+    __builtin_amdgcn_global_load_lds((const void *)(xr + (uint32_t)(ac * 8)),
+                                     (__attribute__((address_space(3))) void *)(slot + L::EXPL + i * 1024), 16, 0, 0);
   }
   if (lane < 4)
     __builtin_amdgcn_global_load_lds((const void *)((const int *)(D.hdr + (size_t)g * D.S + u) + lane),
                                      (__attribute__((address_space(3))) void *)(slot + L::HDR), 4, 0, 0);
 }
 template <int NJ>
-__device__ __forceinline__ void row_from_lds(const uint8_t *slot, int lane, RowRegs<NJ> &r) {
+__device__ __forceinline__ void row_from_lds(const uint8_t *slot, int lane, RowRegs<NJ, true> &r) {
   using L = HintSlot<NJ>;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA has landed
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     r.e[j] = *(const int4 *)(slot + L::EDGES + j * 1024 + lane * 16);
-    r.lv[j] = *(const float *)(slot + L::LOGITS + j * 256 + lane * 4);
+    r.v[j] = *(const double *)(slot + L::EXPL + (lane + WAVE * j) * 8);
   }
   r.hdr = *(const int4 *)(slot + L::HDR);
 }
@@ -354,22 +373,24 @@ __device__ __forceinline__ NormQ norm_q_consts(const Dev &D, float mm_max, float
 // (its q is 0.0): the same correctly rounded quotient either way.
 template <int NJ, bool HINT>
 __device__ int select_nonroot(const Dev &D, const uint64_t (&lg)[NJ], int g, int u, int lane, const NormQ &nz,
-                              int *child, const RowRegs<NJ> &cur, uint8_t *hint_slot, int *nxt_u) {
+                              int *child, const RowRegs<NJ, HINT> &cur, uint8_t *hint_slot, int *nxt_u) {
   int n[NJ], ch[NJ];
-  float q[NJ];
   double p[NJ];
   TP_STAMP(tp0);
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) {  // get_qsa (mcts.py:35-38), as row_load
+  for (int j = 0; j < NJ; ++j) {
     const bool ok = lane + WAVE * j < D.A;
-    const int4 e = cur.e[j];
-    n[j] = ok ? e.y : 0;
-    ch[j] = ok ? e.x : -1;
+    n[j] = ok ? cur.e[j].y : 0;
+    ch[j] = ok ? cur.e[j].x : -1;
+  }
+  float q[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {  // get_qsa (mcts.py:35-38), as row_load
     q[j] = 0.f;
-    if (ok && n[j] > 0) {
-      const float v = __int_as_float(e.z) / (float)n[j];
+    if (n[j] > 0) {
+      const float v = __int_as_float(cur.e[j].z) / (float)n[j];
       const float dv = D.disc_f * v;
-      q[j] = __int_as_float(e.w) + dv;
+      q[j] = __int_as_float(cur.e[j].w) + dv;
     }
   }
   const int tot = __builtin_amdgcn_readfirstlane(cur.hdr.x);
@@ -385,8 +406,45 @@ __device__ int select_nonroot(const Dev &D, const uint64_t (&lg)[NJ], int g, int
     }
   }
   TP_STAMP(tp1);
-  if (nvis < D.A) {
-    // _get_transformed_completed_Qs, some child unvisited: float64 array (mcts.py:141-149)
+  if (HINT && nvis < D.A) {
+    // _get_transformed_completed_Qs, some child unvisited: float64 array (mcts.py:141-149), and
+    // _get_improved_policy's softmax of logits + transformed Q over the legal set (mcts.py:151-156).
+    // Latency-bound regime (the hint kernels: <= 2 waves per SIMD): softmax is shift invariant, so
+    // with E = exp(logit - max legal logit) cached at expansion and t0 = scale * nq0 the transformed
+    // Q of every unvisited child, p ~ E for an unvisited child and p ~ E * exp(t - t0) for a visited
+    // one: a level needs an exp only for its visited children (a few ulp from the reference's
+    // exp(logit + t - max): the 1e-12 policy tolerance of DESIGN §4).  With 4 waves per SIMD the
+    // cache's extra 4 B per child and level cost more than the exps it saves (the no-hint kernel
+    // below: DESIGN §5).
+    const double scale = (double)(D.c_visit + max_n) * D.c_scale;
+    const double t0 = scale * nz.nq0;
+    double x[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int a = lane + WAVE * j;
+      const bool ok = a < D.A && ((lg[j] >> lane) & 1ull);
+      x[j] = ok ? (double)cur.v[j] : 0.0;
+    }
+    if (nvis > 0 && nz.have_range) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        if (n[j] > 0) {  // visited (hence legal: it was selected under the legal mask)
+          double y = ((double)q[j] - (double)nz.mm_min) / (double)nz.den_f;
+          y = (y < 1.0) ? y : 1.0;
+          const double nq = (y > 0.0) ? y : 0.0;
+          x[j] *= exp(scale * nq - t0);
+        }
+      }
+    }
+    double sum = 0.0;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) sum += x[j];
+    sum = dred_sum_d(sum);
+    const double inv_s = 1.0 / sum;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) p[j] = x[j] * inv_s;
+  } else if (!HINT && nvis < D.A) {
+    // the same quantities from the logits: one exp per child (mcts.py:141-156)
     const double scale = (double)(D.c_visit + max_n) * D.c_scale;
     const double den = (double)nz.den_f;
     double x[NJ], m = -INFINITY;
@@ -401,7 +459,7 @@ __device__ int select_nonroot(const Dev &D, const uint64_t (&lg)[NJ], int g, int
       const double t = scale * nq;
       const int a = lane + WAVE * j;
       const bool ok = a < D.A && ((lg[j] >> lane) & 1ull);
-      x[j] = ok ? (double)cur.lv[j] + t : -INFINITY;  // _get_improved_policy (mcts.py:151-156)
+      x[j] = ok ? (double)cur.v[j] + t : -INFINITY;
       m = fmax(m, x[j]);
     }
     m = dred_max_d(m);
@@ -416,8 +474,12 @@ __device__ int select_nonroot(const Dev &D, const uint64_t (&lg)[NJ], int g, int
 #pragma unroll
     for (int j = 0; j < NJ; ++j) p[j] = x[j] * inv_s;
   } else {
+    // every child visited (rare below the root): the reference's array may be float32 -> the
+    // logits themselves, fetched here
     int mx_unused;
-    improved_policy<NJ>(D, lg, lane, cur.lv, n, q, nz.mm_max, nz.mm_min, p, mx_unused);
+    float lv[NJ];
+    logits_load<NJ>(D, D.logits + ((size_t)g * D.S + u) * D.A, lane, lv);
+    improved_policy<NJ>(D, lg, lane, lv, n, q, nz.mm_max, nz.mm_min, p, mx_unused);
   }
   TP_STAMP(tp2);
   double sc[NJ], best = -INFINITY;
@@ -697,7 +759,7 @@ __device__ __forceinline__ void select_game(const Dev &D, int g, int lane, int32
   int32_t *pu = D.path_u + (size_t)g * S, *pa = D.path_a + (size_t)g * S;
   uint64_t lg[NJ];
   load_legal<NJ>(D, g, lg);
-  RowRegs<NJ> cur;
+  RowRegs<NJ, HINT> cur;
   int nxt_u = -1;
   const NormQ nz = norm_q_consts(D, st.mm_max, st.mm_min);
   for (;;) {
@@ -769,7 +831,7 @@ __device__ __forceinline__ void select_game(const Dev &D, int g, int lane, int32
   }
 }
 
-template <int NJ>
+template <int NJ, bool EX>
 __device__ __forceinline__ void expand_backup_game(const Dev &D, int g, int lane, const float *__restrict__ logits_in,
                                                    const float *__restrict__ value_in,
                                                    const float *__restrict__ reward_in) {
@@ -784,10 +846,37 @@ __device__ __forceinline__ void expand_backup_game(const Dev &D, int g, int lane
   const int d = st.depth, leaf = st.leaf, k = st.k;
   // Node.expand (mcts.py:24-25): logits, reward; children row starts empty
   float *nl = D.logits + ((size_t)g * S + leaf) * A;
+  double *nx = D.expl + ((size_t)g * S + leaf) * D.A2;
   Edge *nrow = edge_row_w(D, g, leaf);
-  for (int a = lane; a < A; a += WAVE) {
-    nl[a] = logits_in[(size_t)g * A + a];
-    nrow[a] = Edge{-1, 0, 0.f, 0.f};
+  if (EX) {
+    // logits, and exp(logit - max legal logit) for the hint kernels' non-root softmax (select_nonroot)
+    uint64_t lg[NJ];
+    load_legal<NJ>(D, g, lg);
+    float lv[NJ], lm = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int a = lane + WAVE * j;
+      lv[j] = a < A ? logits_in[(size_t)g * A + a] : 0.f;
+      if (a < A && ((lg[j] >> lane) & 1ull)) lm = fmaxf(lm, lv[j]);
+    }
+    lm = dred_max_f(lm);
+    if (lm == -INFINITY) lm = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int a = lane + WAVE * j;
+      if (a < A) {
+        nl[a] = lv[j];
+        nrow[a] = Edge{-1, 0, 0.f, 0.f};
+      }
+    }
+#pragma unroll 1
+    for (int a = lane; a < A; a += WAVE)  // one exp live at a time (VGPR budget of the fused kernel)
+      nx[a] = exp((double)logits_in[(size_t)g * A + a] - (double)lm);
+  } else {
+    for (int a = lane; a < A; a += WAVE) {
+      nl[a] = logits_in[(size_t)g * A + a];
+      nrow[a] = Edge{-1, 0, 0.f, 0.f};
+    }
   }
   if (lane == 0) {
     D.node_parent[(size_t)g * S + leaf] = pu[d - 1];
@@ -917,7 +1006,9 @@ __global__ void __launch_bounds__(256) k_expand_backup(Dev D, const float *__res
                                                        const float *__restrict__ value_in,
                                                        const float *__restrict__ reward_in) {
   const int g = blockIdx.x * 4 + threadIdx.x / WAVE;
-  if (g < D.G) expand_backup_game<NJ>(D, g, threadIdx.x & (WAVE - 1), logits_in, value_in, reward_in);
+  if (g >= D.G) return;
+  if (D.no_hint) expand_backup_game<NJ, false>(D, g, threadIdx.x & (WAVE - 1), logits_in, value_in, reward_in);
+  else expand_backup_game<NJ, true>(D, g, threadIdx.x & (WAVE - 1), logits_in, value_in, reward_in);
 }
 
 // expand + backup of wave i, then select of wave i+1, in one launch: every game's tree is owned by
@@ -925,7 +1016,7 @@ __global__ void __launch_bounds__(256) k_expand_backup(Dev D, const float *__res
 // boundary per simulation wave fewer)
 // held to 128 VGPRs up to 15x15 boards (NJ <= 4): 4 resident waves per SIMD when G exceeds the SIMDs
 template <int NJ, bool HINT, bool AZ>
-__global__ void __launch_bounds__(256, NJ > 4 ? 1 : 4) k_expand_select(Dev D, const float *__restrict__ logits_in,
+__global__ void __launch_bounds__(256, NJ > 4 ? 1 : (HINT ? GMZ_HINT_WPS : 4)) k_expand_select(Dev D, const float *__restrict__ logits_in,
                                                        const float *__restrict__ value_in,
                                                        const float *__restrict__ reward_in,
                                                        int32_t *__restrict__ in_slot, int32_t *__restrict__ act_out,
@@ -937,7 +1028,7 @@ __global__ void __launch_bounds__(256, NJ > 4 ? 1 : 4) k_expand_select(Dev D, co
 #endif
   TP_STAMP(tk0);
   const int active0 = D.gs[g].active, depth0 = D.gs[g].depth;
-  expand_backup_game<NJ>(D, g, lane, logits_in, value_in, reward_in);
+  expand_backup_game<NJ, HINT>(D, g, lane, logits_in, value_in, reward_in);
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_s_waitcnt(0);
   TP_STAMP(tk1);
@@ -1102,6 +1193,7 @@ GMZ_EXPORT int gmz_engine_create(const gmz_engine_cfg *cfg, gmz_engine **out) {
   D.A = A;
   D.size = cfg->board_size;
   D.S = cfg->num_simulations + 2;
+  D.A2 = (A + 1) & ~1;
   D.n_sims = cfg->num_simulations;
   D.m_top = cfg->num_top_actions;
   D.c_visit = cfg->c_visit;
@@ -1115,6 +1207,7 @@ GMZ_EXPORT int gmz_engine_create(const gmz_engine_cfg *cfg, gmz_engine **out) {
   int rc = 0;
   rc |= dalloc(e, &D.edges, G * S * A);
   rc |= dalloc(e, &D.logits, G * S * A);
+  rc |= dalloc(e, &D.expl, G * S * (size_t)D.A2);
   rc |= dalloc(e, &D.node_parent, G * S);
   rc |= dalloc(e, &D.node_action, G * S);
   rc |= dalloc(e, &D.hdr, G * S);

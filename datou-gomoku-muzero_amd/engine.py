@@ -62,8 +62,9 @@ class BatchedSelfPlayEngine:
         self.lib = _lib.load()
         self.device = torch.device(device)
         self.G, self.A, self.size = int(num_games), c.ACTION_SPACE_SIZE, c.BOARD_SIZE
-        if descent_hint is None:  # the next-visit row prefetch (LDS-DMA) pays up to 4,096 games per engine;
-            descent_hint = self.G < 8192  # at 8,192, four waves per SIMD hide the fetch anyway
+        if descent_hint is None:  # the hint kernels (next-visit LDS prefetch, cached exp rows, 2 waves per
+            descent_hint = self.G < 4096  # SIMD) pay up to 2,048 games per engine; from 4,096 the 4-wave
+            # no-hint kernel hides the latency itself
         self.mode = 1 if c.MCTS_IMPLEMENTATION == "MuZero" else 0
         self.slots_per_game = c.NUM_SIMULATIONS + 2
         self.ecfg = _lib.EngineCfg(self.G, c.BOARD_SIZE, c.N_IN_ROW, c.NUM_SIMULATIONS, c.NUM_TOP_ACTIONS, self.mode,
