@@ -33,7 +33,9 @@ Prints ONE JSON line on rank 0 (schema: the driver contract) including
   loop_c4       : config C4 composed on every rank (datou-gomoku-muzero_amd/loop.py): self-play moves of
                   G games -> finished games' slices into the rank's PER shard -> DDP trainer steps ->
                   periodic weight push (RCCL broadcast) into the self-play network; moves/s and trainer
-                  steps/s of the whole job over the timed iterations;
+                  steps/s of the whole job over the timed iterations (time-sliced: moves, then steps);
+  loop_c4_concurrent : the same loop with each iteration's trainer steps on their own HIP stream,
+                  running beside that iteration's self-play moves;
   cpu_baseline  : the C oracle's search (oracle/gmz_oracle.c) with the float32 numpy network
                   (oracle/netref.py) on the same weights, rank 0 / N=1 only, bounded sample.
 """
@@ -128,6 +130,9 @@ def parse(argv=None):
     ap.add_argument("--trainer-buffer", type=int, default=4096, help="synthetic slices per rank's PER shard")
     ap.add_argument("--loop-iters", type=int, default=20, help="timed iterations of the C4 loop (0: no loop leg)")
     ap.add_argument("--loop-warmup", type=int, default=6)
+    ap.add_argument("--loop-modes", default="sliced",
+                    help="C4 loop legs: 'sliced' (moves then steps), 'concurrent' (steps on their own HIP stream "
+                         "beside the moves); comma-separated")
     ap.add_argument("--loop-games", type=int, default=1024, help="self-play games per GPU inside the C4 loop")
     ap.add_argument("--loop-moves-per-iter", type=int, default=1)
     ap.add_argument("--loop-train-per-iter", type=int, default=1)
@@ -526,22 +531,28 @@ def main():
         out["trainer"] = trainer_leg(args, world, rank, dist, backend)
     if args.loop_iters > 0 and args.net == "hip":
         from datou_gomoku_muzero_amd.loop import run_c4
-        torch.cuda.empty_cache()
-        d, dt_loop = run_c4(args, rank, world, dist, backend, log=log)
-        dt_loop = collective_max(dt_loop, dist, backend)
-        tot = {k: collective_sum(float(v), dist, backend) for k, v in d.items()}
-        out["loop_c4"] = {
-            "metric": "C4 loop: self-play moves/sec and trainer steps/sec with both running on every GPU",
-            "moves_per_s": tot["moves"] * args.loop_games / dt_loop, "trainer_steps_per_s": d["train_steps"] / dt_loop,
-            "unit": "moves/s, steps/s", "n_gpus": world, "iterations": args.loop_iters, "seconds": dt_loop,
-            "games_per_gpu": args.loop_games, "moves_per_iter": args.loop_moves_per_iter,
-            "train_steps_per_iter": args.loop_train_per_iter, "batch_per_gpu": args.trainer_batch,
-            "finished_games": int(tot["games"]), "slices_added": int(tot["slices"]),
-            "weight_pushes": d["weight_pushes"], "model_update_interval": args.loop_update_interval,
-            "data": "self-play from the trainer's initial weights; each PER shard pre-filled with %d synthetic "
-                    "slices so training starts at once" % args.loop_prefill,
-            "parallelism": "dp%d: self-play + replay shard per GPU; one gradient all-reduce + sharded-PER syncs "
-                           "per step; rank 0 weight broadcast per push" % world}
+        for mode in [m.strip() for m in args.loop_modes.split(",") if m.strip()]:
+            if mode not in ("sliced", "concurrent"):
+                raise SystemExit("bench.py: unknown --loop-modes entry %r" % mode)
+            args.loop_concurrent = mode == "concurrent"
+            torch.cuda.empty_cache()
+            d, dt_loop = run_c4(args, rank, world, dist, backend, log=log)
+            dt_loop = collective_max(dt_loop, dist, backend)
+            tot = {k: collective_sum(float(v), dist, backend) for k, v in d.items()}
+            out["loop_c4" if mode == "sliced" else "loop_c4_concurrent"] = {
+                "metric": "C4 loop: self-play moves/sec and trainer steps/sec with both running on every GPU",
+                "mode": mode + (": each iteration's trainer steps run on their own HIP stream beside its self-play "
+                                "moves" if mode == "concurrent" else ": each iteration = moves, then trainer steps"),
+                "moves_per_s": tot["moves"] * args.loop_games / dt_loop, "trainer_steps_per_s": d["train_steps"] / dt_loop,
+                "unit": "moves/s, steps/s", "n_gpus": world, "iterations": args.loop_iters, "seconds": dt_loop,
+                "games_per_gpu": args.loop_games, "moves_per_iter": args.loop_moves_per_iter,
+                "train_steps_per_iter": args.loop_train_per_iter, "batch_per_gpu": args.trainer_batch,
+                "finished_games": int(tot["games"]), "slices_added": int(tot["slices"]),
+                "weight_pushes": d["weight_pushes"], "model_update_interval": args.loop_update_interval,
+                "data": "self-play from the trainer's initial weights; each PER shard pre-filled with %d synthetic "
+                        "slices so training starts at once" % args.loop_prefill,
+                "parallelism": "dp%d: self-play + replay shard per GPU; one gradient all-reduce + sharded-PER syncs "
+                               "per step; rank 0 weight broadcast per push" % world}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.net == "hip":
         log("cpu baseline (bounded sample ~%.0f s)..." % args.cpu_baseline_sec)
         out["cpu_baseline"] = cpu_baseline(args, sd, cfg)

@@ -21,9 +21,13 @@ own share of the work, time-sliced on its GPU:
               inference network, as the inference server does on ModelWeightsUpdate.
 
 One *iteration* = ``moves_per_iter`` self-play moves of all G games, then ``train_steps_per_iter``
-trainer steps (all ranks together, once every shard holds a batch).  The self-play source and the
-inference network are pluggable (``SelfPlay`` on the GPU; tests drive the same loop on CPU with
-scripted games over gloo).
+trainer steps (all ranks together, once every shard holds a batch).  ``concurrent=True`` (GPU): the
+iteration's trainer steps and replay-shard updates are enqueued on a HIP stream of their own BEFORE
+its moves, so the trainer's many short kernels run beside the self-play towers instead of after them
+(the reference's trainer and self-play workers also run at the same time, main.py:91-109); the host
+waits for the previous iteration's training before enqueueing the next, so the backlog stays one
+iteration.  The self-play source and the inference network are pluggable (``SelfPlay`` on the GPU;
+tests drive the same loop on CPU with scripted games over gloo).
 """
 import time
 
@@ -104,7 +108,7 @@ class C4Loop:
     """The composed loop on one rank (see module docstring).  ``dist``: torch.distributed or None."""
 
     def __init__(self, selfplay, trainer, buffer, cfg, batch_size, dist=None, moves_per_iter=1,
-                 train_steps_per_iter=1, model_update_interval=1000, seed=0, device="cuda"):
+                 train_steps_per_iter=1, model_update_interval=1000, seed=0, device="cuda", concurrent=False):
         self.sp, self.tr, self.rb, self.cfg = selfplay, trainer, buffer, cfg
         self.B, self.dist = int(batch_size), dist
         self.moves_per_iter, self.train_steps_per_iter = int(moves_per_iter), int(train_steps_per_iter)
@@ -116,6 +120,11 @@ class C4Loop:
         self.games = self.slices = self.train_steps = self.weight_pushes = 0
         self.game_lengths = []
         self.last_logs = None
+        self.concurrent = bool(concurrent) and self.device.type == "cuda"
+        # concurrent mode: every replay-shard and trainer operation goes to this stream (one ordering
+        # for adds, samples, steps and priority updates); the self-play engines keep theirs
+        self.train_stream = torch.cuda.Stream(self.device) if self.concurrent else None
+        self._train_done = None
 
     # ---------------------------------------------------------------- pieces
     def _add_games(self, done):
@@ -141,6 +150,8 @@ class C4Loop:
 
     def push_weights(self):
         """ModelWeightsUpdate (workers.py:587-593): rank 0's trainer weights -> every rank's inference net."""
+        if self.train_stream is not None:
+            self.train_stream.synchronize()  # the step that made these weights has finished
         sd = self.tr.state_dict_cpu()
         if self.dist is not None and self.world > 1:
             dev = "cpu" if self.dist.get_backend() == "gloo" else self.device
@@ -159,15 +170,36 @@ class C4Loop:
 
     # ---------------------------------------------------------------- one iteration
     def iteration(self):
+        if self.concurrent:
+            return self._iteration_concurrent()
         for _ in range(self.moves_per_iter):
             self._add_games(self.sp.step())
         if self.train_steps_per_iter > 0 and self._all_ready():
             for _ in range(self.train_steps_per_iter):
                 self.train_step()
 
+    def _iteration_concurrent(self):
+        ts = self.train_stream
+        if self._train_done is not None:
+            self._train_done.synchronize()  # the previous iteration's training: backlog <= one iteration
+        if self.train_steps_per_iter > 0 and self._all_ready():
+            ts.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(ts):
+                for _ in range(self.train_steps_per_iter):
+                    self.train_step()
+        done = []
+        for _ in range(self.moves_per_iter):
+            done += self.sp.step()
+        with torch.cuda.stream(ts):  # after this iteration's steps on the same stream
+            self._add_games(done)
+        self._train_done = torch.cuda.Event()
+        self._train_done.record(ts)
+
     def run(self, iterations):
         for _ in range(iterations):
             self.iteration()
+        if self.train_stream is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self.train_stream)
         return self.stats()
 
     def stats(self):
@@ -194,7 +226,8 @@ def run_c4(args, rank, world, dist, backend, log=print):
                                         np.random.RandomState(args.seed + 31 * rank)))
     loop = C4Loop(sp, tr, rb, tcfg, args.trainer_batch, dist=dist if world > 1 else None,
                   moves_per_iter=args.loop_moves_per_iter, train_steps_per_iter=args.loop_train_per_iter,
-                  model_update_interval=args.loop_update_interval, seed=args.seed)
+                  model_update_interval=args.loop_update_interval, seed=args.seed,
+                  concurrent=getattr(args, "loop_concurrent", False))
     t_w = time.perf_counter()
     loop.run(args.loop_warmup)
     torch.cuda.synchronize()

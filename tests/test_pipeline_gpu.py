@@ -124,3 +124,31 @@ def test_c4_loop_on_the_gpu_pushes_trained_weights_into_self_play():
         for k, v in want.items():
             assert np.array_equal(sp.net._tensors[k].cpu().numpy(), v), k
     sp.close()
+
+
+def test_c4_loop_concurrent_stream_trains_and_pushes():
+    """loop.C4Loop(concurrent=True): the trainer steps and shard updates run on their own HIP stream
+    beside the self-play moves; the counts, the shard contents and the pushed weights are those of a
+    consistent loop (every finished game's slices in the shard, pushes = steps / interval, the last
+    push = the trainer's current weights)."""
+    from datou_gomoku_muzero_amd import loop as LP, network as N, trainer as T
+    from datou_gomoku_muzero_amd.config import GmzConfig
+    cfg = GmzConfig(BOARD_SIZE=6, NUM_SIMULATIONS=16, NUM_RES_BLOCKS=1)
+    tcfg = T.TrainConfig(BOARD_SIZE=6, NUM_RES_BLOCKS=1, PHYSICAL_BATCH_SIZE=16, TRAIN_BUFFER_SIZE=4096, ENABLE_PER=True)
+    tr = T.Trainer(tcfg, device="cuda")
+    sp = LP.SelfPlay(cfg, 32, tr.state_dict_cpu(), seed=3)
+    rb = T.ReplayBuffer(tcfg, device="cuda")
+    lp = LP.C4Loop(sp, tr, rb, tcfg, 16, moves_per_iter=2, train_steps_per_iter=1, model_update_interval=2,
+                   concurrent=True)
+    assert lp.concurrent and lp.train_stream is not None
+    st = lp.run(40)
+    torch.cuda.synchronize()
+    assert st["games"] > 0 and st["slices"] == len(rb) and st["train_steps"] > 0
+    assert st["weight_pushes"] == st["train_steps"] // 2 >= 1
+    assert torch.isfinite(lp.last_logs).all()
+    assert float(rb.prio[: len(rb)].min()) > 0  # every admitted slice carries a priority
+    if st["train_steps"] % 2 == 0:
+        want = N.pack_weights(tr.state_dict_cpu(), cfg, "fp16")
+        for k, v in want.items():
+            assert np.array_equal(sp.net._tensors[k].cpu().numpy(), v), k
+    sp.close()
