@@ -697,6 +697,18 @@ class _HalveGrad(torch.autograd.Function):
 
 
 AUTOCAST_CACHE = True  # autocast's weight casts once per step (and per graph replay), not per use: +1.3 %
+# the forward's two independent no-grad parts on side HIP streams (inside the captured step too): the
+# target network's float32 value (loss.py:54-55) and the five consistency representations of
+# obs[s+1] (loss.py:104), overlapping the unroll's dynamics chain; results are identical (same
+# kernels; every BatchNorm's running statistics are updated in the same order)
+CONCURRENT_FORWARD = True
+_SIDE_STREAMS = {}
+
+
+def _side_streams(device):
+    if device not in _SIDE_STREAMS:
+        _SIDE_STREAMS[device] = (torch.cuda.Stream(device), torch.cuda.Stream(device))
+    return _SIDE_STREAMS[device]
 
 
 def muzero_loss(model, target_model, batch, is_weights, cfg, k=None, flip=None, amp=False, amp_dtype=None,
@@ -727,14 +739,39 @@ def muzero_loss(model, target_model, batch, is_weights, cfg, k=None, flip=None, 
     c, W = cfg, cfg.LOSS_WEIGHTS
     vsup = (c.VALUE_SUPPORT_MIN, c.VALUE_SUPPORT_MAX, c.VALUE_SUPPORT_BINS)
     rsup = (c.REWARD_SUPPORT_MIN, c.REWARD_SUPPORT_MAX, c.REWARD_SUPPORT_BINS)
-    with torch.no_grad():
-        last_v = target_model.initial_value(obs[:, -1])[:, 0]
-        z = value_targets(rew, mval, last_v, c)
+    side = _side_streams(obs.device) if (CONCURRENT_FORWARD and obs.is_cuda) else None
+    if side is not None:  # the target network's value on side stream 0, from here to its first use
+        main = torch.cuda.current_stream(obs.device)
+        side[0].wait_stream(main)
+        with torch.cuda.stream(side[0]), torch.no_grad():
+            last_v = target_model.initial_value(obs[:, -1])[:, 0]
+            z = value_targets(rew, mval, last_v, c)
+    else:
+        with torch.no_grad():
+            last_v = target_model.initial_value(obs[:, -1])[:, 0]
+            z = value_targets(rew, mval, last_v, c)
     dev_type = obs.device.type
     zero = torch.zeros((), device=obs.device)
     with torch.autocast(dev_type, enabled=amp and dev_type == "cuda", dtype=amp_dtype or torch.float16,
                         cache_enabled=AUTOCAST_CACHE):
         h = model.representation(obs[:, 0])
+        tru_h = None
+        if side is not None:
+            # the consistency representations of obs[1..U] (no grad) on side stream 1, in step order
+            # after obs[0]'s (the representation BatchNorms' running statistics update in the
+            # reference's order); their projections stay on this stream, interleaved with the dynamics'
+            # projections as in the reference (the projection BatchNorm's running statistics)
+            masks = [act[:, s] != -1 for s in range(c.NUM_UNROLL_STEPS)]
+            side[1].wait_stream(main)
+            tru_h, tru_ev = [], []
+            with torch.cuda.stream(side[1]), torch.no_grad():
+                for s in range(c.NUM_UNROLL_STEPS):
+                    tru_h.append(model.representation(obs[:, s + 1], mask=masks[s]))
+                    ev = torch.cuda.Event()
+                    ev.record(side[1])
+                    tru_ev.append(ev)
+            main.wait_stream(side[0])
+            z.record_stream(main)
         pl, vl = model.prediction(h)
         lp = F.cross_entropy(pl.float(), pi[:, 0], reduction="none")
         lv = F.cross_entropy(vl.float(), scalar_to_support(z[:, 0], *vsup), reduction="none")
@@ -760,7 +797,12 @@ def muzero_loss(model, target_model, batch, is_weights, cfg, k=None, flip=None, 
                                                        reduction="none"), zero)
             dyn = model.project(hk, with_grad=True, mask=m)
             with torch.no_grad():
-                tru = model.project(model.representation(obs[:, s + 1], mask=m), with_grad=False, mask=m)
+                if tru_h is not None:
+                    main.wait_event(tru_ev[s])
+                    tru_h[s].record_stream(main)
+                    tru = model.project(tru_h[s], with_grad=False, mask=m)
+                else:
+                    tru = model.project(model.representation(obs[:, s + 1], mask=m), with_grad=False, mask=m)
             cons = cons + live * barlow_loss(dyn, tru, c.BARLOW_LAMBDA, m)
             h = _HalveGrad.apply(torch.where(m[:, None, None, None], hk, h))
     lp = lp / (steps + 1)
