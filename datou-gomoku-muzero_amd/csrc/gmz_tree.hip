@@ -1014,14 +1014,18 @@ __global__ void __launch_bounds__(256) k_expand_backup(Dev D, const float *__res
 // expand + backup of wave i, then select of wave i+1, in one launch: every game's tree is owned by
 // one wave, so the only dependency between the two phases is that wave's own stores (one kernel
 // boundary per simulation wave fewer)
-// held to 128 VGPRs up to 15x15 boards (NJ <= 4): 4 resident waves per SIMD when G exceeds the SIMDs
-template <int NJ, bool HINT, bool AZ>
-__global__ void __launch_bounds__(256, NJ > 4 ? 1 : (HINT ? GMZ_HINT_WPS : 4)) k_expand_select(Dev D, const float *__restrict__ logits_in,
+// held to 128 VGPRs up to 15x15 boards (NJ <= 4): 4 resident waves per SIMD when G exceeds the SIMDs.
+// WPB waves (games) per workgroup: 4 while every game has a resident wave (a workgroup spreads its
+// waves over the CU's 4 SIMDs); 1 when the games outnumber the resident waves, so that a wave whose
+// game finishes early frees its slot for the next game at once instead of its workgroup's slot
+// waiting for the slowest of 4 games (trees differ in depth)
+template <int NJ, bool HINT, bool AZ, int WPB = 4>
+__global__ void __launch_bounds__(64 * WPB, NJ > 4 ? 1 : (HINT ? GMZ_HINT_WPS : 4)) k_expand_select(Dev D, const float *__restrict__ logits_in,
                                                        const float *__restrict__ value_in,
                                                        const float *__restrict__ reward_in,
                                                        int32_t *__restrict__ in_slot, int32_t *__restrict__ act_out,
                                                        int32_t *__restrict__ out_slot, float *__restrict__ obs) {
-  const int g = blockIdx.x * 4 + threadIdx.x / WAVE, lane = threadIdx.x & (WAVE - 1);
+  const int g = blockIdx.x * WPB + threadIdx.x / WAVE, lane = threadIdx.x & (WAVE - 1);
   if (g >= D.G) return;
 #ifdef GMZ_TREE_PROF
   if (lane < 16) tp_lds[threadIdx.x / WAVE][lane] = 0;
@@ -1032,7 +1036,7 @@ __global__ void __launch_bounds__(256, NJ > 4 ? 1 : (HINT ? GMZ_HINT_WPS : 4)) k
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_s_waitcnt(0);
   TP_STAMP(tk1);
-  __shared__ __attribute__((aligned(16))) uint8_t hint_lds[HINT ? 4 * HintSlot<NJ>::BYTES : 16];
+  __shared__ __attribute__((aligned(16))) uint8_t hint_lds[HINT ? WPB * HintSlot<NJ>::BYTES : 16];
   select_game<NJ, HINT, AZ>(D, g, lane, in_slot, act_out, out_slot, obs,
                             hint_lds + (HINT ? __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE) * HintSlot<NJ>::BYTES : 0));
 #ifdef GMZ_TREE_PROF
@@ -1164,6 +1168,7 @@ struct gmz_engine {
   Dev D;
   int n_in_row;
   uint32_t counter;
+  int es_waves;  // resident waves of the engine's k_expand_select variant (0: not measured yet)
   void *bufs[32];
   int nbufs;
 };
@@ -1320,6 +1325,39 @@ static inline dim3 wave_grid(const gmz_engine *e) { return dim3((e->D.G + 3) / 4
     GMZ_LAUNCH_CHECK();                                                                                        \
   } while (0)
 
+// k_expand_select<NJ, H, AZ, WPB>: WPB = 1 when the games outnumber the variant's resident waves
+// (occupancy measured once per engine), else 4
+template <int NJ, bool H, bool AZ>
+static int launch_expand_select(gmz_engine *e, hipStream_t s, const float *logits, const float *value,
+                                const float *reward, int32_t *in_slot, int32_t *action, int32_t *out_slot, float *obs) {
+  if (!e->es_waves) {
+    int nb = 0, ncu = 0, dev = 0;
+    GMZ_HIP(hipGetDevice(&dev));
+    GMZ_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void *)k_expand_select<NJ, H, AZ, 4>, 256, 0));
+    GMZ_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    e->es_waves = (nb > 0 ? nb : 1) * ncu * 4;
+  }
+  const int G = e->D.G;
+  if (G > e->es_waves)
+    hipLaunchKernelGGL((k_expand_select<NJ, H, AZ, 1>), dim3(G), dim3(64), 0, s, e->D, logits, value, reward, in_slot,
+                       action, out_slot, obs);
+  else
+    hipLaunchKernelGGL((k_expand_select<NJ, H, AZ, 4>), dim3((G + 3) / 4), dim3(256), 0, s, e->D, logits, value, reward,
+                       in_slot, action, out_slot, obs);
+  GMZ_LAUNCH_CHECK();
+  return 0;
+}
+
+template <int NJ>
+static int launch_expand_select_nj(gmz_engine *e, hipStream_t s, const float *logits, const float *value,
+                                   const float *reward, int32_t *in_slot, int32_t *action, int32_t *out_slot, float *obs) {
+  const bool h = !e->D.no_hint, az = e->D.mode == 0;
+  if (h) return az ? launch_expand_select<NJ, true, true>(e, s, logits, value, reward, in_slot, action, out_slot, obs)
+                   : launch_expand_select<NJ, true, false>(e, s, logits, value, reward, in_slot, action, out_slot, obs);
+  return az ? launch_expand_select<NJ, false, true>(e, s, logits, value, reward, in_slot, action, out_slot, obs)
+            : launch_expand_select<NJ, false, false>(e, s, logits, value, reward, in_slot, action, out_slot, obs);
+}
+
 GMZ_EXPORT int gmz_engine_begin_move(gmz_engine *e, const double *gumbel, uint64_t seed, float *obs, void *stream) {
   if (!e || !obs) return fail("gmz_engine_begin_move: null argument");
   const uint32_t ctr = e->counter++;
@@ -1358,8 +1396,13 @@ GMZ_EXPORT int gmz_engine_expand_backup_select(gmz_engine *e, const float *logit
   if (e->D.mode == 1 && !reward) return fail("gmz_engine_expand_backup_select: MuZero mode needs reward");
   if (e->D.mode == 0 && !obs) return fail("gmz_engine_expand_backup_select: AlphaZero mode needs obs");
   const float *rw = e->D.mode == 1 ? reward : nullptr;
-  GMZ_LAUNCH_SEL(k_expand_select, e, stream, e->D, logits, value, rw, in_slot, action, out_slot, obs);
-  return 0;
+  hipStream_t s = (hipStream_t)stream;
+  const int nj = (e->D.A + 63) / 64;
+  if (nj <= 1) return launch_expand_select_nj<1>(e, s, logits, value, rw, in_slot, action, out_slot, obs);
+  if (nj <= 2) return launch_expand_select_nj<2>(e, s, logits, value, rw, in_slot, action, out_slot, obs);
+  if (nj <= 4) return launch_expand_select_nj<4>(e, s, logits, value, rw, in_slot, action, out_slot, obs);
+  if (nj <= 6) return launch_expand_select_nj<6>(e, s, logits, value, rw, in_slot, action, out_slot, obs);
+  return launch_expand_select_nj<8>(e, s, logits, value, rw, in_slot, action, out_slot, obs);
 }
 
 GMZ_EXPORT int gmz_engine_pending_waves(gmz_engine *e, int32_t *out) {
