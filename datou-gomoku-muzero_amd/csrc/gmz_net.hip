@@ -60,6 +60,8 @@ struct TowerArgs {
   int rows;
   uint16_t *xres;          // single-image boards (19x19): per-workgroup residual scratch (k_tower3)
   int max_grid;            // cap on the persistent grid (gmz_net_weights.max_grid; 0 = every CU)
+  int *tickets;            // k_tower3 board scheduling (one board per workgroup): [0] next row, [1]
+                           // workgroups done; zero between launches (the last workgroup resets them)
 };
 
 // MFMA operand element types of the towers and the reward GEMM (f32 accumulation either way).
@@ -191,8 +193,38 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
       rr[b] = (b > 0 && nx >= t.rows) ? rr[b - 1] : nx;
     }
   };
-  take_rows(blockIdx.x);
-  if (rr[0] >= t.rows) return;
+  // one board per workgroup (15x15, 19x19): boards are handed out in ticket order as workgroups
+  // become free (thread 0 takes the next active row; the launch's last workgroup resets the
+  // counters), so a workgroup that starts late — its CU still held by the other stream's tower —
+  // takes fewer boards instead of delaying the whole launch by its static share
+  __shared__ int s_row;
+  int *tk = t.tickets;
+  const bool dsched = NB == 1 && tk != nullptr;
+  auto fetch_row = [&]() {
+    int r = atomicAdd(&tk[0], 1);
+    while (r < t.rows && t.out_slot[r] < 0) r = atomicAdd(&tk[0], 1);
+    return r;
+  };
+  auto finish_launch = [&]() {
+    if (dsched && threadIdx.x == 0) {
+      __threadfence();
+      if (atomicAdd(&tk[1], 1) == (int)gridDim.x - 1) {
+        atomicExch(&tk[0], 0);
+        atomicExch(&tk[1], 0);
+      }
+    }
+  };
+  if (dsched) {
+    if (threadIdx.x == 0) s_row = fetch_row();
+    __syncthreads();
+    rr[0] = s_row;
+  } else {
+    take_rows(blockIdx.x);
+  }
+  if (rr[0] >= t.rows) {
+    finish_launch();
+    return;
+  }
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   // wave w -> (channel group nh, position group pg) = (w % NQ, w / NQ): the waves sharing a SIMD
   // (w, w+4, ...) get different position groups, so a short last group does not load one SIMD less
@@ -344,6 +376,8 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
       // the next layer's bias (for the last layer: the next board's layer 0) -> the other slot;
       // that slot was last read by the previous layer's epilogue, which the barrier has closed
       issue_bias(L + 1 < t.n_layers ? L + 1 : 0, (gl + 1) & 1);
+      // the next board's ticket, published by this (last) layer's barrier
+      if (dsched && L == t.n_layers - 1 && tid == 0) s_row = fetch_row();
       // this layer's bias is the C operand of every tile's first MFMA (no bias add in the epilogue)
       const float *bias = sbias + (gl & 1) * C;
       f32x4 bv[NTW];
@@ -476,7 +510,8 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
     int nrr[NB];
 #pragma unroll
     for (int b = 0; b < NB; ++b) nrr[b] = rr[b];
-    take_rows(rr[NB - 1] + gridDim.x);
+    if (dsched) rr[0] = s_row;
+    else take_rows(rr[NB - 1] + gridDim.x);
     if constexpr (DYN && !ONE && !(ABL & 32)) {
       if (rr[0] < t.rows)  // DYN has 1 + 2*blocks (odd) layers: the result is in img[1]
 #pragma unroll
@@ -516,6 +551,7 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
       if (rr[0] < t.rows) issue_input(rr[0], 0);  // single image: only now is it free
     }
   }
+  finish_launch();
   if ((ABL & 128) && lane == 0) {  // diagnostic build only: per-wave phase cycles -> pv_feat
     float *o = t.pv_feat + (blockIdx.x * NW + w) * 4;
     o[0] = (float)st_loop; o[1] = (float)st_epi; o[2] = (float)st_bar;
@@ -785,14 +821,19 @@ static constexpr int KSPLIT = 32;
 static size_t ws_head_bytes(int A, int rows) {
   return ((size_t)rows * pv_stride(A) + (size_t)KSPLIT * rows * 64 + (size_t)rows * 64) * sizeof(float);
 }
+static constexpr size_t WS_TICKETS = 256;
 static size_t ws_bytes(int A, int rows) {
   int H = 0;
   while (H * H < A) ++H;
-  return ws_head_bytes(A, rows) + (size_t)cu_count() * xres_bytes(H) + 256;
+  return WS_TICKETS + ws_head_bytes(A, rows) + (size_t)cu_count() * xres_bytes(H) + 256;
 }
+static float *ws_pv(void *workspace) { return (float *)((uint8_t *)workspace + WS_TICKETS); }
 static uint16_t *ws_xres(void *workspace, int A, int rows) {
-  return (uint16_t *)((uint8_t *)workspace + ws_head_bytes(A, rows));
+  return (uint16_t *)((uint8_t *)workspace + WS_TICKETS + ws_head_bytes(A, rows));
 }
+// the tower's two scheduling counters: the workspace's first 256 B, at the same place whatever the
+// row count (zero-filled when the workspace is allocated, include/gmz.h; every launch leaves them zero)
+static int *ws_tickets(void *workspace) { return (int *)workspace; }
 
 static int check_w(const gmz_net_weights *w) {
   if (!w) return fail("gmz_net: null weights");
@@ -815,7 +856,7 @@ GMZ_EXPORT int gmz_net_workspace_bytes(const gmz_net_weights *w, int rows, size_
 static int heads(const gmz_net_weights *w, const uint16_t *pool, const int32_t *out_slot, int rows, void *workspace,
                  float *logits, float *value, float *reward, hipStream_t s) {
   const int A = w->board_size * w->board_size, K = A * C;
-  float *pv = (float *)workspace;
+  float *pv = ws_pv(workspace);
   float *rpart = pv + (size_t)rows * pv_stride(A);
   float *vpre = rpart + (size_t)KSPLIT * rows * 64;
   const int nrt = (rows + 15) / 16, ncg = ((A + 15) / 16 + 3) / 4;
@@ -838,8 +879,8 @@ GMZ_EXPORT int gmz_net_initial_tower(const gmz_net_weights *w, const float *obs,
   if (rows <= 0 || !obs || !out_slot || !pool || !workspace) return fail("gmz_net_initial_tower: bad argument");
   const int H = w->board_size, A = H * H;
   TowerArgs a{w->repr_convs, w->repr_bias, 2 * w->blocks, w->repr_stem_w, w->repr_stem_b, nullptr, obs, pool,
-              nullptr, nullptr, out_slot, w->head_conv_w, w->head_conv_b, (float *)workspace, rows,
-              ws_xres(workspace, A, rows)};
+              nullptr, nullptr, out_slot, w->head_conv_w, w->head_conv_b, ws_pv(workspace), rows,
+              ws_xres(workspace, A, rows), 0, ws_tickets(workspace)};
   return tower(w, false, a, (hipStream_t)stream);
 }
 
@@ -863,8 +904,8 @@ GMZ_EXPORT int gmz_net_recurrent_tower(const gmz_net_weights *w, uint16_t *pool,
   if (rows <= 0 || !pool || !in_slot || !action || !out_slot || !workspace) return fail("gmz_net_recurrent_tower: bad argument");
   const int A = w->board_size * w->board_size;
   TowerArgs a{w->dyn_convs, w->dyn_bias, 1 + 2 * w->blocks, nullptr, nullptr, w->dyn_action, nullptr, pool,
-              in_slot, action, out_slot, w->head_conv_w, w->head_conv_b, (float *)workspace, rows,
-              ws_xres(workspace, A, rows)};
+              in_slot, action, out_slot, w->head_conv_w, w->head_conv_b, ws_pv(workspace), rows,
+              ws_xres(workspace, A, rows), 0, ws_tickets(workspace)};
   return tower(w, true, a, (hipStream_t)stream);
 }
 

@@ -252,7 +252,7 @@ class GomokuNetHip:
         self.w = w
         nbytes = ctypes.c_size_t()
         check(self.lib.gmz_net_workspace_bytes(ctypes.byref(w), self.max_rows, ctypes.byref(nbytes)))
-        self.workspace = torch.empty(nbytes.value, dtype=torch.uint8, device=self.device)
+        self.workspace = torch.zeros(nbytes.value, dtype=torch.uint8, device=self.device)
         for q in getattr(self, "_children", []):  # split() views follow the hot swap
             keep = q.w.max_grid
             q.w = NetWeights.from_buffer_copy(w)
@@ -273,7 +273,7 @@ class GomokuNetHip:
             q.w.max_grid = int(max_grid)
             nbytes = ctypes.c_size_t()
             check(self.lib.gmz_net_workspace_bytes(ctypes.byref(q.w), q.max_rows, ctypes.byref(nbytes)))
-            q.workspace = torch.empty(nbytes.value, dtype=torch.uint8, device=self.device)
+            q.workspace = torch.zeros(nbytes.value, dtype=torch.uint8, device=self.device)
             q.tower_timer = q.repr_timer = None
             q._children = []
             out.append(q)
@@ -285,7 +285,7 @@ class GomokuNetHip:
             self.max_rows = rows
             nbytes = ctypes.c_size_t()
             check(self.lib.gmz_net_workspace_bytes(ctypes.byref(self.w), rows, ctypes.byref(nbytes)))
-            self.workspace = torch.empty(nbytes.value, dtype=torch.uint8, device=self.device)
+            self.workspace = torch.zeros(nbytes.value, dtype=torch.uint8, device=self.device)
         return ptr(self.workspace)
 
     # ---- engine backend interface

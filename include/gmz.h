@@ -212,7 +212,9 @@ typedef struct gmz_net_weights {
 #define GMZ_NET_F16 0
 #define GMZ_NET_BF16 1
 
-/* Scratch needed by gmz_net_initial / gmz_net_recurrent for `rows` rows (caller allocates). */
+/* Scratch needed by gmz_net_initial / gmz_net_recurrent for `rows` rows (caller allocates, ZERO-FILLED
+ * once: its first 256 B hold the tower's board-scheduling counters, which every launch leaves zero;
+ * a workspace must not be shared by launches that may run concurrently). */
 int gmz_net_workspace_bytes(const gmz_net_weights *w, int rows, size_t *out);
 /* network.py:137-143 initial_inference: obs_dev f32[rows][3][A] -> logits f32[rows][A],
  * value f32[rows] (support_to_scalar), hidden state -> hid_pool_dev[out_slot[r]] (dtype [A][C]).
