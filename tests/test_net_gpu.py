@@ -149,6 +149,45 @@ def test_two_board_workgroups_are_batch_invariant(mods, size, prec):
         assert np.array_equal(net.hidden([3 * n + i]).cpu().numpy()[0], hb[i])
 
 
+
+@pytest.mark.parametrize("size", [15, 19])
+def test_ticket_scheduled_towers_are_batch_invariant(mods, size):
+    """One-board tower workgroups (15x15, 19x19) take rows in ticket order from counters in the net's
+    workspace that every launch must leave at zero: launches of different row counts on the same
+    workspace — more rows than CUs (workgroups take several boards, in any order), skipped rows
+    (slot -1), a capped grid — give every row bit-for-bit its output from a launch of its own."""
+    N, W, GmzConfig = mods
+    cfg = GmzConfig(BOARD_SIZE=size, NUM_RES_BLOCKS=1)
+    sd = W.synthetic_state_dict(cfg, seed=11 + size, with_projection=False)
+    n = 300 if size == 15 else 160
+    rs = np.random.RandomState(size + 3)
+    obs = _positions(size, n, rs)
+    acts = rs.randint(0, size * size, n)
+    net = N.GomokuNetHip(sd, cfg, num_slots=4 * n, max_rows=n)
+    slots = np.arange(n)
+    slots[rs.choice(n, n // 7, replace=False)] = -1
+    outs = []
+    for rows, cap in ((n, 0), (37, 0), (n, 64)):
+        net.w.max_grid = cap
+        sl = slots[:rows]
+        lg, v, _ = net.initial_inference(obs[:rows], slots=sl)
+        lg2, v2, r2 = net.recurrent_inference(np.where(sl < 0, 0, sl), acts[:rows], np.where(sl < 0, -1, sl + n))
+        torch.cuda.synchronize()
+        outs.append([t.cpu().numpy().copy() for t in (lg, v, lg2, v2, r2)])
+    net.w.max_grid = 0
+    for i in rs.choice(np.flatnonzero(slots[:37] >= 0), 6, replace=False):
+        o = 2 * n + i
+        a, b, _ = net.initial_inference(obs[i:i + 1], slots=[o])
+        c, d, e = net.recurrent_inference([o], acts[i:i + 1], [3 * n + i])
+        torch.cuda.synchronize()
+        for batch in outs:
+            for got, want in zip((a, b, c, d, e), batch):
+                assert np.array_equal(got.cpu().numpy()[0], want[i]), i
+    for got, want in zip(outs[0], outs[2]):  # the full batch on a capped grid: identical
+        live = slots >= 0
+        assert np.array_equal(got[live], want[live])
+
+
 def test_skipped_rows_untouched(mods):
     N, W, GmzConfig = mods
     cfg = GmzConfig(BOARD_SIZE=9, NUM_RES_BLOCKS=1)
