@@ -487,7 +487,11 @@ def main():
             "mean_backup_levels": ctr["backup_levels"] / max(1, ctr["backups"]),
             "mean_select_levels": ctr["select_levels"] / max(1, ctr["selects"]),
             "games_per_launch": ctr["backups"] / n_tree, "streams": args.streams, "busy_ms": busy_tree,
-            "achieved_per_launch": bpl / (ms_tree * 1e-3) / 1e9}
+            "achieved_per_launch": bpl / (ms_tree * 1e-3) / 1e9,
+            "note": ("two streams: each launch runs on the CUs the other stream's capped tower leaves free (about "
+                     "a quarter of them), so this is the kernel inside the step, not its own rate; "
+                     "single_stream_kernels.tree has the kernel alone on every CU" if args.streams > 1 else
+                     "one stream: the kernel alone on every CU")}
     if args.streams > 1 and args.single_stream_moves > 0:
         # the same G games as ONE engine on one stream (every CU per launch): the kernels' launch times
         # without the other stream beside them (not the headline: the two-stream step above is)
