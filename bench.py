@@ -36,8 +36,16 @@ Prints ONE JSON line on rank 0 (schema: the driver contract) including
                   steps/s of the whole job over the timed iterations (time-sliced: moves, then steps);
   loop_c4_concurrent : the same loop with each iteration's trainer steps on their own HIP stream,
                   running beside that iteration's self-play moves;
+  sublines      : BASELINE configs 5 and 1 on the GPU, a few steps each after the headline engine is freed:
+                  C5 = 19x19, 800 sims, 16 blocks (G games); C1 = 9x9 AlphaZero, 50 sims (G games), each with
+                  moves/s and the tower's and tree kernel's roofline fractions (one stream: every launch alone);
+  worker        : the drop-in worker (worker.gpu_selfplay_worker) over torch.multiprocessing queues with a
+                  consumer process unpickling every payload (the reference's process graph): moves/s over
+                  the steady-state moves including every per-move and per-game record, and its ratio to
+                  the headline engine rate;
   cpu_baseline  : the C oracle's search (oracle/gmz_oracle.c) with the float32 numpy network
-                  (oracle/netref.py) on the same weights, rank 0 / N=1 only, bounded sample.
+                  (oracle/netref.py) on the same weights, one single-threaded process per host core used
+                  (oracle/cpu_baseline.py), mid-game openings, rank 0 / N=1 only, bounded sample.
 """
 import argparse
 import json
@@ -123,22 +131,33 @@ def parse(argv=None):
                     help="MFMA operand type of the network towers (f32 accumulation either way)")
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--cpu-baseline-sec", type=float, default=20.0)
+    ap.add_argument("--cpu-baseline-procs", type=int, default=16,
+                    help="single-threaded oracle processes (capped by the cores this process may use)")
+    ap.add_argument("--sublines", default="c5,c1",
+                    help="BASELINE configs measured besides the headline: c5 (19x19/800/16 blocks), c1 (9x9 AlphaZero/50)")
+    ap.add_argument("--subline-games", type=int, default=1024)
+    ap.add_argument("--c5-steps", type=int, default=3)
+    ap.add_argument("--c1-steps", type=int, default=10)
+    ap.add_argument("--worker-moves", type=int, default=20, help="timed moves of the drop-in worker leg (0: skip)")
+    ap.add_argument("--worker-warmup", type=int, default=30,
+                    help="untimed worker moves first (games start empty: by then games finish every move)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--trainer-steps", type=int, default=20, help="timed trainer steps (0: no trainer leg)")
     ap.add_argument("--trainer-warmup", type=int, default=6)
     ap.add_argument("--trainer-batch", type=int, default=360)
     ap.add_argument("--trainer-buffer", type=int, default=4096, help="synthetic slices per rank's PER shard")
     ap.add_argument("--loop-iters", type=int, default=20, help="timed iterations of the C4 loop (0: no loop leg)")
-    ap.add_argument("--loop-warmup", type=int, default=6)
+    ap.add_argument("--loop-warmup", type=int, default=30,
+                    help="untimed iterations (games start from the empty board: after ~30 moves they finish every move)")
     ap.add_argument("--loop-modes", default="sliced",
                     help="C4 loop legs: 'sliced' (moves then steps), 'concurrent' (steps on their own HIP stream "
                          "beside the moves); comma-separated")
     ap.add_argument("--loop-games", type=int, default=1024, help="self-play games per GPU inside the C4 loop")
     ap.add_argument("--loop-moves-per-iter", type=int, default=1)
     ap.add_argument("--loop-train-per-iter", type=int, default=1)
-    ap.add_argument("--loop-update-interval", type=int, default=10,
-                    help="trainer steps between weight pushes (reference MODEL_UPDATE_INTERVAL = 1000; shortened "
-                         "so the timed window contains pushes)")
+    ap.add_argument("--loop-update-interval", type=int, default=1000,
+                    help="trainer steps between weight pushes (reference MODEL_UPDATE_INTERVAL = 1000); the cost of "
+                         "one push is measured separately (weight_push_ms)")
     ap.add_argument("--loop-buffer", type=int, default=65536, help="replay shard capacity per rank")
     ap.add_argument("--loop-prefill", type=int, default=4096, help="synthetic slices in each shard before the loop")
     ap.add_argument("--pmc-file", default=os.path.join(REPO, "profiles", "pmc_tower_latest.json"))
@@ -244,51 +263,44 @@ def timer_stats(timers, base):
     return n, mean, busy
 
 
-def cpu_baseline(args, sd, cfg):
-    """C oracle search + float32 numpy GomokuNetEZ on the host cores (reported baseline)."""
-    sys.path.insert(0, os.path.join(REPO, "oracle"))
-    import oracle
-    import netref
+def cpu_baseline(args):
+    """The C oracle's search + float32 numpy GomokuNetEZ on the host cores (reported baseline, kind
+    "port"): one single-threaded process per core used (oracle/cpu_baseline.py, started as child
+    processes), each playing its own game from a random opening of 0..~120 stones for about
+    ``--cpu-baseline-sec`` seconds; value = all processes' moves / the wall time of the slowest."""
     try:
-        from threadpoolctl import threadpool_info
-        cores = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+        avail = len(os.sched_getaffinity(0))
     except Exception:
-        cores = os.cpu_count() or 1
-    H = args.size
-    A = H * H
-
-    def init(obs):
-        p, v, h = netref.initial_inference(sd, obs)
-        return p, v[:, 0], list(h)
-
-    def rec(hs, acts):
-        p, v, h, r = netref.recurrent_inference(sd, np.stack(hs), acts)
-        return p, v[:, 0], r[:, 0], list(h)
-
-    net = oracle.CallbackNet(A, H, init, rec)
-    ocfg = oracle.make_cfg(H, args.sims, args.mode, hashnet=False)
-    rs = np.random.RandomState(args.seed)
-    board = np.zeros(A, np.int8)
-    player, last, moves, rows = 1, None, 0, 0
+        avail = os.cpu_count() or 1
+    P = max(1, min(args.cpu_baseline_procs, avail))
+    script = os.path.join(REPO, "oracle", "cpu_baseline.py")
+    env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
+    procs = []
     t0 = time.perf_counter()
-    while True:
-        net.reset()
-        pol, val, act, _, st = oracle.search(ocfg, board, player, last, int(np.count_nonzero(board)),
-                                             rs.gumbel(0, 1, A), net=net)
-        rows += st["n_initial"] + st["recurrent_rows"]
-        moves += 1
-        board[act] = player
-        last, player = act, -player
-        if oracle.game_ended(board, H, act, int(np.count_nonzero(board))) is not None:
-            board[:] = 0
-            player, last = 1, None
-        dt = time.perf_counter() - t0
-        if dt >= args.cpu_baseline_sec or moves >= 64:
-            break
-    return {"value": moves / dt, "unit": "moves/s", "cores": int(cores), "kind": "port",
-            "sample": "%d move(s) of one %dx%d game from the empty board, %d sims (%s), %d NN rows (the reference's "
-                      "duplicate-leaf batches kept), %.1f s; C oracle search + numpy fp32 GomokuNetEZ"
-                      % (moves, H, H, args.sims, args.mode, rows, dt)}
+    for i in range(P):
+        opening = (i * 8) % 128
+        cmd = [sys.executable, script, "--size", str(args.size), "--sims", str(args.sims), "--mode", args.mode,
+               "--blocks", str(args.blocks), "--seed", str(args.seed + 101 * i), "--weights-seed", str(args.seed),
+               "--opening", str(opening), "--seconds", str(args.cpu_baseline_sec)]
+        procs.append(subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env))
+    res = []
+    for p in procs:
+        out, err = p.communicate(timeout=args.cpu_baseline_sec * 6 + 120)
+        if p.returncode != 0:
+            raise RuntimeError("cpu_baseline worker failed: %s" % err[-2000:])
+        res.append(json.loads(out.strip().splitlines()[-1]))
+    wall = time.perf_counter() - t0
+    moves = sum(r["moves"] for r in res)
+    rows = sum(r["rows"] for r in res)
+    slowest = max(r["seconds"] for r in res)
+    stones = sorted(x for r in res for x in r["stones"])
+    return {"value": moves / slowest, "unit": "moves/s", "cores": P, "kind": "port",
+            "sample": "%d moves over %d single-threaded processes (one per core used; %d cores available to the "
+                      "process), each one %dx%d game from a random opening (%d..%d stones at the searched positions), "
+                      "%d sims (%s), %d NN rows (the reference's duplicate-leaf batches kept); slowest process %.1f s, "
+                      "wall %.1f s; C oracle search + numpy fp32 GomokuNetEZ (oracle/cpu_baseline.py)"
+                      % (moves, P, avail, args.size, args.size, stones[0], stones[-1], args.sims, args.mode, rows,
+                         slowest, wall)}
 
 
 def trainer_leg(args, world, rank, dist, backend):
@@ -361,38 +373,16 @@ def trainer_leg(args, world, rank, dist, backend):
                          "traffic": None}}
 
 
-def main():
-    args = parse()
-    env_world = os.environ.get("WORLD_SIZE")
-    if env_world is None and args.gpus > 1:
-        # no external launcher: one process per GPU, started here before any GPU call
-        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
-    world = int(env_world or "1")
-    if world != args.gpus:
-        log("bench.py: --gpus %d disagrees with WORLD_SIZE=%d" % (args.gpus, world))
-        sys.exit(2)
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    backend = None
-    if world > 1:
-        import torch.distributed as dist
-        # GMZ_DIST_BACKEND=gloo rehearses the N>1 path with several ranks sharing one GPU
-        backend = os.environ.get("GMZ_DIST_BACKEND", "nccl")
-        torch.cuda.set_device(local % torch.cuda.device_count())
-        dist.init_process_group(backend, init_method="env://")
-        if rank == 0:
-            log("torch.distributed: world_size=%d backend=%s (%s)" % (dist.get_world_size(), dist.get_backend(),
-                                                                      "RCCL" if backend == "nccl" else backend))
-    else:
-        torch.cuda.set_device(0)
+def selfplay_leg(args, rank, world, dist, backend, size, sims, mode, blocks, G, steps, warmup, streams=None,
+                 single_stream_moves=0, log_prefix=""):
+    """G games of (size, sims, mode, blocks) self-play on this rank's GPU: ``warmup`` untimed moves, then
+    ``steps`` timed moves (barrier + synchronize on both sides, max over ranks).  Returns a dict with
+    dt (s), waves, streams, roofline (dominant tower), roofline_tree and, with single_stream_moves > 0
+    and two streams, single_stream_kernels."""
     import datou_gomoku_muzero_amd.engine as E
     from datou_gomoku_muzero_amd import network as N, weights as W
     from datou_gomoku_muzero_amd.config import GmzConfig
-
-    cfg = GmzConfig(BOARD_SIZE=args.size, NUM_SIMULATIONS=args.sims, MCTS_IMPLEMENTATION=args.mode,
-                    NUM_RES_BLOCKS=args.blocks)
-    G = args.games
+    cfg = GmzConfig(BOARD_SIZE=size, NUM_SIMULATIONS=sims, MCTS_IMPLEMENTATION=mode, NUM_RES_BLOCKS=blocks)
     sd = W.synthetic_state_dict(cfg, seed=args.seed, with_projection=False)
     if dist is not None:  # the self-play tier's one exchange (SURVEY §8e): rank 0's weights -> all ranks (RCCL)
         from datou_gomoku_muzero_amd.weight_sync import broadcast_state_dict
@@ -403,24 +393,24 @@ def main():
         net = N.GomokuNetHip(sd, cfg, num_slots=slots, max_rows=G, precision=args.precision)
     else:
         net = E.HashNetBackend(slots, cfg.ACTION_SPACE_SIZE)
-    if args.streams is None:
-        args.streams = E.default_streams(cfg, G)
-    eng = E.make_engine(cfg, num_games=G, net=net, seed=args.seed + 7919 * rank, streams=args.streams)
+    if streams is None:
+        streams = E.default_streams(cfg, G)
+    eng = E.make_engine(cfg, num_games=G, net=net, seed=args.seed + 7919 * rank, streams=streams)
     eng.reset_games()
-    parts = eng.engines if args.streams > 1 else [eng]
-    pstreams = eng.streams if args.streams > 1 else [torch.cuda.current_stream()]
-    log("rank %d: engine G=%d %dx%d %s/%d, net=%s, %d stream(s)" % (rank, G, args.size, args.size, args.mode, args.sims,
-                                                                     args.net, args.streams))
+    parts = eng.engines if streams > 1 else [eng]
+    pstreams = eng.streams if streams > 1 else [torch.cuda.current_stream()]
+    log("%srank %d: engine G=%d %dx%d %s/%d, %d blocks, net=%s, %d stream(s)"
+        % (log_prefix, rank, G, size, size, mode, sims, blocks, args.net, streams))
 
     def step():
         eng.search()
         eng.play(reset_finished=True)
 
-    for i in range(args.warmup):
+    for i in range(warmup):
         step()
         torch.cuda.synchronize()
-        log("warmup %d/%d done" % (i + 1, args.warmup))
-    az = args.mode == "AlphaZero"  # AlphaZero searches run the representation tower per wave
+        log("%swarmup %d/%d done" % (log_prefix, i + 1, warmup))
+    az = mode == "AlphaZero"  # AlphaZero searches run the representation tower per wave
     timers, tree_timers = [], []
     for e, st in zip(parts, pstreams):  # HIP events on each part's launch stream
         if args.net == "hip":
@@ -440,61 +430,68 @@ def main():
     base.record()
     t0 = time.perf_counter()
     waves = 0
-    for i in range(args.steps):
+    for i in range(steps):
         step()
         waves += eng.waves_last
-        if (i + 1) % max(1, args.steps // 5) == 0:
-            log("step %d/%d" % (i + 1, args.steps))
+        if (i + 1) % max(1, steps // 5) == 0:
+            log("%sstep %d/%d" % (log_prefix, i + 1, steps))
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
-    dt = time.perf_counter() - t0
-    dt = collective_max(dt, dist, backend)
-    out = result_line(args, world, dt, waves, G, backend)
+    dt = collective_max(time.perf_counter() - t0, dist, backend)
+    res = {"dt": dt, "waves": waves, "streams": streams}
     ctr = eng.tree_counters()
+    traffic_note = "from the committed builder PMC pass %s (not measured in this run)"
+    fpr = (repr_flop_per_row if az else tower_flop_per_row)(size, blocks)
     if timers:
         n_launch, ms, busy = timer_stats(timers, base)
         # rows the searches requested (finished games' rows are skipped by the tower): every selected
         # game-wave is one row; AlphaZero's representation tower also runs each move's G root rows
-        rows = (ctr["selects"] + (G * args.steps if az else 0)) / max(1, n_launch)
-        fpr = (repr_flop_per_row if az else tower_flop_per_row)(args.size, args.blocks)
+        rows = (ctr["selects"] + (G * steps if az else 0)) / max(1, n_launch)
         flop = fpr * rows
         per_launch = flop / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
         # delivered rate while the kernel runs: all launches' FLOP over the union of their intervals
         # (with one stream = the per-launch figure; with two, launches of the two streams overlap)
         achieved = flop * n_launch / (busy * 1e-3) / 1e12 if busy > 0 else 0.0
-        traffic = pmc_traffic(args.pmc_file, args, G, az)
-        kname = ("k_tower3<%d,REPR> (representation tower, stem + %d fused convs + head 1x1 convs)" % (args.size, 2 * args.blocks)
-                 if az else "k_tower3<%d,DYN> (dynamics tower, %d fused convs + head 1x1 convs)" % (args.size, 1 + 2 * args.blocks))
-        out["roofline"] = {"bound": "mfma", "kernel": kname + ", " + args.precision,
+        is_c2 = (size, blocks, G, mode) == (15, 8, 1024, "MuZero")
+        traffic = pmc_traffic(args.pmc_file, args, G, az) if is_c2 else None
+        kname = ("k_tower3<%d,REPR> (representation tower, stem + %d fused convs + head 1x1 convs)" % (size, 2 * blocks)
+                 if az else "k_tower3<%d,DYN> (dynamics tower, %d fused convs + head 1x1 convs)" % (size, 1 + 2 * blocks))
+        res["roofline"] = {"bound": "mfma", "kernel": kname + ", " + args.precision,
                            "achieved": achieved, "peak": PEAK_MFMA_TFLOPS, "unit": "TFLOP/s",
                            "frac": achieved / PEAK_MFMA_TFLOPS, "traffic": traffic,
+                           "traffic_source": (traffic_note % os.path.relpath(args.pmc_file, REPO)) if traffic else None,
                            "launches": n_launch, "mean_launch_ms": ms, "rows_per_launch": rows,
-                           "flop_per_row": fpr, "streams": args.streams, "busy_ms": busy,
+                           "flop_per_row": fpr, "streams": streams, "busy_ms": busy,
                            "achieved_per_launch": per_launch,
                            "timing": "HIP events around every launch on its stream; achieved = algorithmic FLOP of all "
                                      "launches / busy_ms (union of the launch intervals of all streams)"}
     n_tree, ms_tree, busy_tree = timer_stats(tree_timers, base)
     if n_tree:
-        A = args.size * args.size
+        A = size * size
         bpl = tree_bytes(ctr, A) / n_tree
         gbs = bpl * n_tree / (busy_tree * 1e-3) / 1e9 if busy_tree > 0 else 0.0
-        out["roofline_tree"] = {
+        is_c2 = (size, blocks, G, mode) == (15, 8, 1024, "MuZero")
+        tr = pmc_traffic(args.pmc_tree_file, args, G, az) if is_c2 else None
+        res["roofline_tree"] = {
             "bound": "hbm", "kernel": "k_expand_select<%d> (backup of wave i + selection of wave i+1)" % ((A + 63) // 64),
             "achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS,
-            "traffic": pmc_traffic(args.pmc_tree_file, args, G, az),
+            "traffic": tr, "traffic_source": (traffic_note % os.path.relpath(args.pmc_tree_file, REPO)) if tr else None,
             "launches": n_tree, "mean_launch_ms": ms_tree, "bytes_per_launch": bpl,
             "mean_backup_levels": ctr["backup_levels"] / max(1, ctr["backups"]),
             "mean_select_levels": ctr["select_levels"] / max(1, ctr["selects"]),
-            "games_per_launch": ctr["backups"] / n_tree, "streams": args.streams, "busy_ms": busy_tree,
+            "games_per_launch": ctr["backups"] / n_tree, "streams": streams, "busy_ms": busy_tree,
             "achieved_per_launch": bpl / (ms_tree * 1e-3) / 1e9,
             "note": ("two streams: each launch runs on the CUs the other stream's capped tower leaves free (about "
                      "a quarter of them), so this is the kernel inside the step, not its own rate; "
-                     "single_stream_kernels.tree has the kernel alone on every CU" if args.streams > 1 else
+                     "single_stream_kernels.tree has the kernel alone on every CU" if streams > 1 else
                      "one stream: the kernel alone on every CU")}
-    if args.streams > 1 and args.single_stream_moves > 0:
+    if streams > 1 and single_stream_moves > 0:
         # the same G games as ONE engine on one stream (every CU per launch): the kernels' launch times
         # without the other stream beside them (not the headline: the two-stream step above is)
+        for e in parts:
+            e.net.tower_timer = e.net.repr_timer = None
+        eng.close()
         e1 = E.BatchedSelfPlayEngine(cfg, num_games=G, net=net, seed=args.seed + 7919 * rank + 1)
         e1.reset_games()
         e1.search()
@@ -510,27 +507,189 @@ def main():
         torch.cuda.synchronize()
         b1 = torch.cuda.Event(enable_timing=True)
         b1.record()
-        for _ in range(args.single_stream_moves):
+        for _ in range(single_stream_moves):
             e1.search()
             e1.play(reset_finished=True)
         torch.cuda.synchronize()
         c1 = e1.tree_counters()
-        ss = {"moves": args.single_stream_moves, "games": G}
+        ss = {"moves": single_stream_moves, "games": G}
         if t1 is not None:
             n1, m1, _ = timer_stats([t1], b1)
-            r1 = (c1["selects"] + (G * args.single_stream_moves if az else 0)) / max(1, n1)
+            r1 = (c1["selects"] + (G * single_stream_moves if az else 0)) / max(1, n1)
             a1 = fpr * r1 / (m1 * 1e-3) / 1e12
             ss["tower"] = {"mean_launch_ms": m1, "rows_per_launch": r1, "achieved": a1, "frac": a1 / PEAK_MFMA_TFLOPS}
         n2, m2, _ = timer_stats([tt1], b1)
         if n2:
-            g2 = tree_bytes(c1, args.size * args.size) / n2 / (m2 * 1e-3) / 1e9
+            g2 = tree_bytes(c1, size * size) / n2 / (m2 * 1e-3) / 1e9
             ss["tree"] = {"mean_launch_ms": m2, "achieved_gbs": g2, "frac": g2 / PEAK_HBM_GBS}
-        out["single_stream_kernels"] = ss
+        res["single_stream_kernels"] = ss
         net.tower_timer = net.repr_timer = None
         e1.close()
         del e1
+    eng.close()
+    del eng, net
+    torch.cuda.empty_cache()
+    return res
+
+
+SUBLINES = {  # BASELINE.json configs run on the GPU besides the headline (C2)
+    "c5": dict(size=19, sims=800, mode="MuZero", blocks=16,
+               name="C5: 19x19, 800 sims/move, GomokuNetEZ 16 blocks (BASELINE config 5)"),
+    "c1": dict(size=9, sims=50, mode="AlphaZero", blocks=8,
+               name="C1 on the GPU: 9x9 AlphaZero, 50 sims/move, 8 blocks (BASELINE config 1's search; the "
+                    "reference runs it with one CPU worker)"),
+}
+
+
+def subline(args, key, rank, world, dist, backend):
+    c = SUBLINES[key]
+    G = args.subline_games
+    steps, warmup = (args.c5_steps, 1) if key == "c5" else (args.c1_steps, 2)
+    r = selfplay_leg(args, rank, world, dist, backend, c["size"], c["sims"], c["mode"], c["blocks"], G, steps, warmup,
+                     log_prefix="[%s] " % key)
+    out = {"config": c["name"], "value": G * steps * world / r["dt"], "unit": "moves/s", "n_gpus": world,
+           "games_per_gpu": G, "steps": steps, "warmup": warmup, "ms_per_step": r["dt"] / steps * 1e3,
+           "waves_per_move": r["waves"] / max(1, steps), "streams": r["streams"], "dtype": args.precision}
+    for k in ("roofline", "roofline_tree"):
+        if k in r:
+            q = r[k]
+            out[k] = {x: q[x] for x in ("kernel", "achieved", "unit", "frac", "mean_launch_ms") if x in q}
+    return out
+
+
+def consumer_proc(qs, ctl, report):
+    """The reference's queue readers (DataLoader, DisplayManager, log reader; main.py:60-78): one thread
+    per queue, blocking gets that unpickle every payload, until a None sentinel; then the counts go to
+    ``report``.  Started by bench.py before anything touches the GPU; ``ctl`` starts a round (None: exit)."""
+    import threading
+    while True:
+        go = ctl.get()  # one round per worker leg; None ends the process
+        if go is None:
+            return
+        n, slices = {}, {}
+
+        def read(k, q):
+            c = sl = 0
+            while True:
+                item = q.get()
+                if item is None:
+                    break
+                c += 1
+                if k == "data":
+                    sl += len(item[1])
+            n[k], slices[k] = c, sl
+
+        th = [threading.Thread(target=read, args=(k, q)) for k, q in qs.items()]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        report.put(dict(n, slices=slices.get("data", 0)))
+
+
+class _Flag:
+    def __init__(self):
+        self.f = False
+
+    def is_set(self):
+        return self.f
+
+
+def start_consumer():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    qs = {"data": ctx.Queue(maxsize=50000), "ui": ctx.Queue(), "log": ctx.Queue(), "trainer": ctx.Queue()}
+    ctl, report = ctx.Queue(), ctx.Queue()
+    p = ctx.Process(target=consumer_proc, args=(qs, ctl, report), daemon=True)
+    p.start()
+    return p, qs, ctl, report
+
+
+def worker_leg(args, rank, world, dist, backend, consumer, engine_rate):
+    """worker.gpu_selfplay_worker (the drop-in for N universal_workers + the inference server,
+    workers.py:129-241 / 314-373) on this rank's GPU with real torch.multiprocessing queues and a
+    consumer process: moves/s over the steady-state moves, until every record of them is posted."""
+    from datou_gomoku_muzero_amd.worker import gpu_selfplay_worker
+    from datou_gomoku_muzero_amd.config import GmzConfig
+    proc, qs, ctl, report = consumer
+    cfg = GmzConfig(BOARD_SIZE=args.size, NUM_SIMULATIONS=args.sims, MCTS_IMPLEMENTATION=args.mode,
+                    NUM_RES_BLOCKS=args.blocks)
+    ctl.put(True)  # the consumer starts its readers
+    times = []
+    warm, moves = args.worker_warmup, args.worker_moves
+    if dist:
+        dist.barrier()
+    gpu_selfplay_worker(rank, None, qs["data"], qs["log"], qs["ui"], _Flag(), trainer_event_queue=qs["trainer"],
+                        num_games=args.games, cfg=cfg, max_moves=warm + moves, emit_move_notices=True,
+                        move_times=times, seed=args.seed + 7919 * rank, precision=args.precision,
+                        device=torch.cuda.current_device())
+    for q in qs.values():
+        q.put(None)
+    counts = report.get(timeout=300)
+    steady = collective_max(times[-1] - times[warm - 1], dist, backend)
+    tot = {k: collective_sum(float(v), dist, backend) for k, v in counts.items()}
+    value = args.games * moves * world / steady
+    return {"metric": "drop-in worker self-play moves/sec (worker.gpu_selfplay_worker, %dx%d, %d sims)"
+                      % (args.size, args.size, args.sims),
+            "value": value, "unit": "moves/s", "n_gpus": world, "games_per_gpu": args.games, "moves": moves,
+            "warmup_moves": warm, "steady_s": steady, "worker_over_engine": value / engine_rate if engine_rate else None,
+            "finished_games": int(tot.get("data", 0)), "slices": int(tot.get("slices", 0)),
+            "messages": {k: int(v) for k, v in tot.items() if k != "slices"},
+            "queues": "torch.multiprocessing (spawn) Queues of main.py's sizes; a consumer process unpickles every "
+                      "payload (GameRecord + TrainingSlices, SelfPlayMove / SelfPlayStatus / GameCompletedNotice)",
+            "timed": "from the host clock after warm-up move %d was queued to after the last move's records were "
+                     "posted (per-move history, winning-move scan, record building all inside)" % warm}
+
+
+def main():
+    args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # no external launcher: one process per GPU, started here before any GPU call
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+    world = int(env_world or "1")
+    if world != args.gpus:
+        log("bench.py: --gpus %d disagrees with WORLD_SIZE=%d" % (args.gpus, world))
+        sys.exit(2)
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # the worker leg's queue consumer: a child process started before anything touches the GPU
+    consumer = start_consumer() if (args.worker_moves > 0 and args.net == "hip") else None
+    dist = None
+    backend = None
+    if world > 1:
+        import torch.distributed as dist
+        # GMZ_DIST_BACKEND=gloo rehearses the N>1 path with several ranks sharing one GPU
+        backend = os.environ.get("GMZ_DIST_BACKEND", "nccl")
+        torch.cuda.set_device(local % torch.cuda.device_count())
+        dist.init_process_group(backend, init_method="env://")
+        if rank == 0:
+            log("torch.distributed: world_size=%d backend=%s (%s)" % (dist.get_world_size(), dist.get_backend(),
+                                                                      "RCCL" if backend == "nccl" else backend))
+    else:
+        torch.cuda.set_device(0)
+
+    G = args.games
+    r = selfplay_leg(args, rank, world, dist, backend, args.size, args.sims, args.mode, args.blocks, G, args.steps,
+                     args.warmup, streams=args.streams, single_stream_moves=args.single_stream_moves)
+    args.streams = r["streams"]
+    out = result_line(args, world, r["dt"], r["waves"], G, backend)
+    for k in ("roofline", "roofline_tree", "single_stream_kernels"):
+        if k in r:
+            out[k] = r[k]
+    if args.net == "hip":
+        subs = {}
+        for key in [k.strip() for k in args.sublines.split(",") if k.strip()]:
+            if key not in SUBLINES:
+                raise SystemExit("bench.py: unknown --sublines entry %r" % key)
+            subs[key] = subline(args, key, rank, world, dist, backend)
+        if subs:
+            out["sublines"] = subs
+    if consumer is not None:
+        out["worker"] = worker_leg(args, rank, world, dist, backend, consumer, out["value"])
+        consumer[2].put(None)  # the consumer process exits
+        torch.cuda.empty_cache()
     if args.trainer_steps > 0 and args.net == "hip":
-        del eng, net
         torch.cuda.empty_cache()
         out["trainer"] = trainer_leg(args, world, rank, dist, backend)
     if args.loop_iters > 0 and args.net == "hip":
@@ -542,7 +701,9 @@ def main():
             torch.cuda.empty_cache()
             d, dt_loop = run_c4(args, rank, world, dist, backend, log=log)
             dt_loop = collective_max(dt_loop, dist, backend)
+            push_ms = collective_max(d.pop("push_ms"), dist, backend)
             tot = {k: collective_sum(float(v), dist, backend) for k, v in d.items()}
+            step_ms = dt_loop / max(1, d["train_steps"]) * 1e3
             out["loop_c4" if mode == "sliced" else "loop_c4_concurrent"] = {
                 "metric": "C4 loop: self-play moves/sec and trainer steps/sec with both running on every GPU",
                 "mode": mode + (": each iteration's trainer steps run on their own HIP stream beside its self-play "
@@ -551,15 +712,20 @@ def main():
                 "unit": "moves/s, steps/s", "n_gpus": world, "iterations": args.loop_iters, "seconds": dt_loop,
                 "games_per_gpu": args.loop_games, "moves_per_iter": args.loop_moves_per_iter,
                 "train_steps_per_iter": args.loop_train_per_iter, "batch_per_gpu": args.trainer_batch,
+                "warmup_iterations": args.loop_warmup,
                 "finished_games": int(tot["games"]), "slices_added": int(tot["slices"]),
                 "weight_pushes": d["weight_pushes"], "model_update_interval": args.loop_update_interval,
-                "data": "self-play from the trainer's initial weights; each PER shard pre-filled with %d synthetic "
-                        "slices so training starts at once" % args.loop_prefill,
+                "weight_push_ms": push_ms,
+                "push_share_at_interval": {"interval": 1000, "ms_per_trainer_step": push_ms / 1000.0,
+                                           "share_of_iteration": push_ms / 1000.0 / step_ms if step_ms else None},
+                "data": "self-play games from the empty board with the trainer's weights (the timed window starts "
+                        "after %d warm-up iterations, so games finish inside it); each PER shard also pre-filled "
+                        "with %d synthetic slices so training starts at once" % (args.loop_warmup, args.loop_prefill),
                 "parallelism": "dp%d: self-play + replay shard per GPU; one gradient all-reduce + sharded-PER syncs "
                                "per step; rank 0 weight broadcast per push" % world}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.net == "hip":
         log("cpu baseline (bounded sample ~%.0f s)..." % args.cpu_baseline_sec)
-        out["cpu_baseline"] = cpu_baseline(args, sd, cfg)
+        out["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:

@@ -1338,7 +1338,9 @@ static int launch_expand_select(gmz_engine *e, hipStream_t s, const float *logit
     e->es_waves = (nb > 0 ? nb : 1) * ncu * 4;
   }
   const int G = e->D.G;
-  if (G > e->es_waves)
+  // gmz_engine_cfg.flags bits 1 / 2 force the 4-wave / 1-wave workgroups (parity tests of both variants)
+  const int fl = e->cfg.flags;
+  if ((fl & 4) || (!(fl & 2) && G > e->es_waves))
     hipLaunchKernelGGL((k_expand_select<NJ, H, AZ, 1>), dim3(G), dim3(64), 0, s, e->D, logits, value, reward, in_slot,
                        action, out_slot, obs);
   else

@@ -54,7 +54,7 @@ class BatchedSelfPlayEngine:
     """G games per GPU.  ``cfg``: any object with the reference config attribute names."""
 
     def __init__(self, cfg=None, num_games=1, net=None, device="cuda", seed=0, descent_hint=None, game_offset=0,
-                 **overrides):
+                 wpb=None, **overrides):
         self.cfg = from_any(cfg, **overrides)
         c = self.cfg
         if c.MCTS_IMPLEMENTATION not in ("AlphaZero", "MuZero"):
@@ -67,8 +67,13 @@ class BatchedSelfPlayEngine:
             # no-hint kernel hides the latency itself
         self.mode = 1 if c.MCTS_IMPLEMENTATION == "MuZero" else 0
         self.slots_per_game = c.NUM_SIMULATIONS + 2
+        if wpb not in (None, 1, 4):
+            raise ValueError("wpb: games per workgroup of the fused expand/select kernel must be None, 1 or 4")
+        self.descent_hint = bool(descent_hint)
+        # flags (include/gmz.h): bit 0 no hint; bits 1 / 2 force 4-wave / 1-wave workgroups (None: by occupancy)
+        flags = (0 if descent_hint else 1) | {None: 0, 4: 2, 1: 4}[wpb]
         self.ecfg = _lib.EngineCfg(self.G, c.BOARD_SIZE, c.N_IN_ROW, c.NUM_SIMULATIONS, c.NUM_TOP_ACTIONS, self.mode,
-                                   int(c.C_VISIT), 0 if descent_hint else 1, float(c.C_SCALE),
+                                   int(c.C_VISIT), flags, float(c.C_SCALE),
                                    float(c.VALUE_MINMAX_DELTA), float(c.DISCOUNT), int(game_offset))
         h = ctypes.c_void_p()
         check(self.lib.gmz_engine_create(ctypes.byref(self.ecfg), ctypes.byref(h)))
@@ -263,8 +268,9 @@ class SplitSelfPlayEngine:
     CUs the other half's tower leaves free, and each tower's ramp-up and tail overlap the other
     half's work (measured with tools/dual_stream_probe.py).  Every game's search is
     exactly the unsplit engine's: part i plays games [i*G/parts, (i+1)*G/parts) with ``game_offset``
-    so the device Gumbel noise per game is unchanged, and its outputs are row views of the full
-    tensors.  Calls fork from the caller's stream and join back to it."""
+    so the device Gumbel noise per game is unchanged, its outputs are row views of the full
+    tensors, and the descent-hint choice (hence the non-root softmax arithmetic) is
+    made from the total G, as for one engine.  Calls fork from the caller's stream and join back to it."""
 
     def __init__(self, cfg=None, num_games=2, net=None, device="cuda", seed=0, parts=2, max_grid=None,
                  descent_hint=None, **overrides):
@@ -279,6 +285,8 @@ class SplitSelfPlayEngine:
         self.mode = 1 if c.MCTS_IMPLEMENTATION == "MuZero" else 0
         self.slots_per_game = c.NUM_SIMULATIONS + 2
         g = self.g = G // parts
+        if descent_hint is None:  # chosen from the TOTAL game count, as one engine with every game would
+            descent_hint = G < 4096  # (the hint kernels' cached-exp softmax differs by a few ulp)
         if max_grid is None:
             max_grid = torch.cuda.get_device_properties(self.device).multi_processor_count * 3 // 4 if parts > 1 else 0
         if net is None:

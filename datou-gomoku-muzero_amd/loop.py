@@ -124,6 +124,8 @@ class C4Loop:
         # concurrent mode: every replay-shard and trainer operation goes to this stream (one ordering
         # for adds, samples, steps and priority updates); the self-play engines keep theirs
         self.train_stream = torch.cuda.Stream(self.device) if self.concurrent else None
+        # the self-play engines fork every move from this stream: weight swaps are enqueued on it
+        self.sp_stream = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
         self._train_done = None
 
     # ---------------------------------------------------------------- pieces
@@ -156,7 +158,14 @@ class C4Loop:
         if self.dist is not None and self.world > 1:
             dev = "cpu" if self.dist.get_backend() == "gloo" else self.device
             sd = broadcast_state_dict(sd, src=0, device=dev)
-        self.sp.load_weights(sd)
+        if self.sp_stream is not None:
+            # on the self-play stream, not the trainer's (concurrent mode calls this from inside the train
+            # stream's context): the copies of the new weights are then ordered before the next move's
+            # kernels, and after the previous move's, which join this stream
+            with torch.cuda.stream(self.sp_stream):
+                self.sp.load_weights(sd)
+        else:
+            self.sp.load_weights(sd)
         self.weight_pushes += 1
 
     def train_step(self):
@@ -243,7 +252,19 @@ def run_c4(args, rank, world, dist, backend, log=print):
         dist.barrier()
     dt = time.perf_counter() - t0
     s1 = loop.stats()
-    sp.close()
     d = {k: s1[k] - s0[k] for k in ("moves", "games", "slices", "train_steps", "weight_pushes")}
     d["buffer"] = s1["buffer"]
+    # one ModelWeightsUpdate (workers.py:587-593) on its own, after the timed window: rank 0's trainer
+    # weights -> broadcast -> every rank's inference network; the timed window runs the reference's
+    # interval (1000 steps), so this is what a push adds once per interval
+    n_push = 3
+    if dist is not None and world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_p = time.perf_counter()
+    for _ in range(n_push):
+        loop.push_weights()
+    torch.cuda.synchronize()
+    d["push_ms"] = (time.perf_counter() - t_p) / n_push * 1e3
+    sp.close()
     return d, dt

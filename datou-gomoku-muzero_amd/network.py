@@ -236,6 +236,7 @@ class GomokuNetHip:
         self.lib = _lib.load()
         self.max_rows = int(max_rows)
         self.pool = torch.empty(int(num_slots) * self.A * C, dtype=torch.int16, device=self.device)
+        self.workspace = None
         self.tower_timer = None  # optional KernelTimer around the dynamics tower launches (bench.py)
         self.repr_timer = None   # optional KernelTimer around the representation tower launches
         self.load_state_dict(state_dict)
@@ -250,9 +251,13 @@ class GomokuNetHip:
         for k, t in self._tensors.items():
             setattr(w, k, t.data_ptr())
         self.w = w
-        nbytes = ctypes.c_size_t()
-        check(self.lib.gmz_net_workspace_bytes(ctypes.byref(w), self.max_rows, ctypes.byref(nbytes)))
-        self.workspace = torch.zeros(nbytes.value, dtype=torch.uint8, device=self.device)
+        # the workspace (head scratch + the tower's scheduling counters, zero between launches) does not
+        # depend on the weights: a hot swap keeps it, so no zero-fill is ever queued on another stream
+        # behind launches that already use it
+        if getattr(self, "workspace", None) is None:
+            nbytes = ctypes.c_size_t()
+            check(self.lib.gmz_net_workspace_bytes(ctypes.byref(w), self.max_rows, ctypes.byref(nbytes)))
+            self.workspace = torch.zeros(nbytes.value, dtype=torch.uint8, device=self.device)
         for q in getattr(self, "_children", []):  # split() views follow the hot swap
             keep = q.w.max_grid
             q.w = NetWeights.from_buffer_copy(w)

@@ -77,7 +77,11 @@ typedef struct gmz_engine_cfg {
   int32_t num_top_actions;  /* config.NUM_TOP_ACTIONS (<= 64) */
   int32_t mode;             /* 0 = AlphaZero (mcts.py:197), 1 = MuZero (mcts.py:288) */
   int32_t c_visit;          /* config.C_VISIT */
-  int32_t flags;             /* bit 0: no descent prefetch hint (node header .last; A/B timing only, results identical) */
+  int32_t flags;            /* bit 0: no descent prefetch hint (node header .last; no-hint kernels form the non-root
+                               softmax from the logits, the hint kernels from cached exp rows: equal up to a few ulp
+                               of the improved policy); bit 1 / bit 2: force the 4-wave / 1-wave
+                               workgroups of the fused expand/select kernel (default: 1-wave workgroups once the
+                               games outnumber the variant's resident waves); results identical either way */
   double c_scale;           /* config.C_SCALE */
   double minmax_delta;      /* config.VALUE_MINMAX_DELTA */
   double discount;          /* config.DISCOUNT */

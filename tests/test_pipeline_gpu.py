@@ -90,7 +90,8 @@ def test_bench_spawns_its_own_ranks_gloo_rehearsal():
                         "--size", "9", "--sims", "50", "--blocks", "1", "--steps", "2", "--warmup", "1",
                         "--trainer-steps", "2", "--trainer-warmup", "4", "--trainer-batch", "16", "--trainer-buffer", "64",
                         "--loop-iters", "4", "--loop-warmup", "4", "--loop-games", "64", "--loop-update-interval", "2",
-                        "--loop-prefill", "64", "--loop-buffer", "4096"],
+                        "--loop-prefill", "64", "--loop-buffer", "4096", "--sublines", "c1", "--subline-games", "32",
+                        "--c1-steps", "2", "--worker-moves", "3", "--worker-warmup", "2"],
                        env=env, capture_output=True, text=True, timeout=280)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [l for l in p.stdout.splitlines() if l.startswith("{")]  # (gloo itself prints connection notes)
@@ -101,6 +102,11 @@ def test_bench_spawns_its_own_ranks_gloo_rehearsal():
     assert d["trainer"]["n_gpus"] == 2 and d["trainer"]["value"] > 0
     lc = d["loop_c4"]
     assert lc["n_gpus"] == 2 and lc["trainer_steps_per_s"] > 0 and lc["moves_per_s"] > 0 and lc["weight_pushes"] == 2
+    assert lc["weight_push_ms"] > 0
+    wk = d["worker"]
+    assert wk["n_gpus"] == 2 and wk["value"] > 0 and wk["messages"]["ui"] > 0
+    c1 = d["sublines"]["c1"]
+    assert c1["n_gpus"] == 2 and c1["value"] > 0 and 0 < c1["roofline"]["frac"] < 1
 
 
 def test_c4_loop_on_the_gpu_pushes_trained_weights_into_self_play():
@@ -151,4 +157,53 @@ def test_c4_loop_concurrent_stream_trains_and_pushes():
         want = N.pack_weights(tr.state_dict_cpu(), cfg, "fp16")
         for k, v in want.items():
             assert np.array_equal(sp.net._tensors[k].cpu().numpy(), v), k
+    sp.close()
+
+
+@pytest.mark.parametrize("concurrent", [False, True])
+def test_c4_loop_at_its_own_workload(concurrent):
+    """Config C4 at its own network and batch (BASELINE config 4): 15x15, GomokuNetEZ 128
+    filters x 8 blocks, B = 360, 5 unroll steps, PER; self-play of 128 games from the empty board at 32
+    simulations per move (the config's 400 cut so the test plays ~120 moves in seconds; the search code
+    is the same).  One engine stream, so the tower schedules boards by ticket (the workspace counters a
+    weight push must not disturb).  Checks, as main.py:91-109 / workers.py:379-439,587-593
+    run them: every finished game's slices reach the replay shard; the trainer samples those slices;
+    every push hot-swaps exactly the trainer's weights into the self-play network; and (concurrent:
+    trainer on its own HIP stream beside the moves) the same holds with the push on the trainer's stream."""
+    from datou_gomoku_muzero_amd import loop as LP, network as N, trainer as T, weights as W
+    from datou_gomoku_muzero_amd.config import GmzConfig
+    cfg = GmzConfig(BOARD_SIZE=15, NUM_SIMULATIONS=32, NUM_RES_BLOCKS=8)
+    tcfg = T.TrainConfig(BOARD_SIZE=15, NUM_RES_BLOCKS=8, PHYSICAL_BATCH_SIZE=360, TRAIN_BUFFER_SIZE=65536,
+                         ENABLE_PER=True)
+    tr = T.Trainer(tcfg, device="cuda")
+    sp = LP.SelfPlay(cfg, 128, tr.state_dict_cpu(), seed=3, streams=1)
+    rb = T.ReplayBuffer(tcfg, device="cuda")
+    prefill = 512
+    rb.add_arrays(*W.synthetic_slices(prefill, 15, tcfg.NUM_UNROLL_STEPS, np.random.RandomState(0)))
+    sampled = []
+    sample = rb.sample
+
+    def spy(B, rng=np.random, dist=None):
+        out = sample(B, rng, dist)
+        sampled.append(out[1].clone())
+        return out
+    rb.sample = spy
+    interval = 10
+    lp = LP.C4Loop(sp, tr, rb, tcfg, 360, moves_per_iter=2, train_steps_per_iter=1, model_update_interval=interval,
+                   concurrent=concurrent)
+    st = lp.run(60)
+    torch.cuda.synchronize()
+    assert st["games"] > 0, "no game finished in 120 moves"
+    assert st["slices"] == len(rb) - prefill, (st, len(rb))
+    assert st["train_steps"] == 60 and st["weight_pushes"] == 60 // interval
+    idx = torch.cat(sampled).cpu().numpy()
+    assert (idx >= prefill).sum() > 0, "the trainer never sampled a self-play slice"
+    assert np.isfinite(lp.last_logs.cpu().numpy()).all()
+    want = N.pack_weights(tr.state_dict_cpu(), cfg, "fp16")  # 60 steps: the last push is the current state
+    for k, v in want.items():
+        assert np.array_equal(sp.net._tensors[k].cpu().numpy(), v), k
+    # after the pushes the self-play network still searches: one more move plays every game
+    done = sp.step()
+    torch.cuda.synchronize()
+    assert isinstance(done, list)
     sp.close()

@@ -1,0 +1,62 @@
+#!/bin/bash
+# The one GPU-box runner (replaces the round-1/2 one-off gpu_*.sh / round*_profile.sh / pmc_round*.sh
+# scripts; their commands are the subcommands below).  Run on the box through gpurun, e.g.
+#   gpurun --timeout 1200 -- bash tools/gpu.sh tests r03a 'large or c4'
+#   gpurun --timeout 900  -- bash tools/gpu.sh bench r03a [bench.py args...]
+#   gpurun --timeout 900  -- bash tools/gpu.sh trace r03a        # rocprofv3 kernel stats of the default step
+#   gpurun --timeout 900  -- bash tools/gpu.sh pmc r03a          # PMC passes: tower + tree kernel
+# Every GPU step runs under its own timeout and the steps chain with &&: after a failure, nothing
+# further touches the GPU.  Output: gpurun_out/<tag>/.
+set -o pipefail
+CMD=$1
+TAG=${2:-x}
+shift 2
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+SP="--no-cpu-baseline --trainer-steps 0 --loop-iters 0 --sublines= --worker-moves 0"
+
+case $CMD in
+  tests)  # GPU test suite (optionally -k EXPR)
+    K=()
+    [ -n "$1" ] && K=(-k "$1")
+    timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${K[@]}" > $OUT/pytest.log 2>&1
+    rc=$?
+    echo "pytest rc=$rc $(tail -1 $OUT/pytest.log)"
+    grep -E "FAILED|^E  |differing searches" $OUT/pytest.log | head -30
+    exit $rc ;;
+  smoke)
+    timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
+    rc=$?; tail -2 $OUT/smoke.log; exit $rc ;;
+  bench)  # bench.py with the given arguments (default: the driver's default line)
+    timeout -k 10 800 python -u bench.py "$@" > $OUT/bench.json 2> $OUT/bench.err
+    rc=$?
+    tail -3 $OUT/bench.err
+    python3 tools/summarize_bench.py $OUT/bench.json
+    exit $rc ;;
+  trace)  # rocprofv3 kernel-trace stats of the default self-play step (+ the bench line under the tracer)
+    cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
+      python3 bench.py --steps 3 --warmup 1 $SP "$@" > $OUT/bench_under_trace.json 2> $OUT/trace.err || { echo "trace failed"; tail -5 $OUT/trace.err; exit 1; }
+    find $OUT/trace -name "*kernel_stats.csv" | head -1 | xargs -I{} cp {} $OUT/kernel_stats.csv
+    python3 - "$OUT" <<'PY'
+import csv, sys
+rows = list(csv.DictReader(open(sys.argv[1] + "/kernel_stats.csv")))
+for r in rows[:8]:
+    print("%-60s %6s calls avg %9.1f us %5.1f%%" % (r["Name"][:60], r["Calls"], float(r["AverageNs"]) / 1e3, float(r["Percentage"])))
+PY
+    ;;
+  pmc)  # one counter group per rocprofv3 run (MI355X_MICROARCH.md: separate passes) on the self-play step
+    cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+    for CTR in FETCH_SIZE WRITE_SIZE "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_MFMA" "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES"; do
+      NAME=$(echo $CTR | tr ' ' '_' | cut -c1-40)
+      timeout -s KILL 240 rocprofv3 --pmc $CTR --kernel-include-regex "k_tower3|k_expand_select" --output-format csv -d $OUT/$NAME -o pmc -- \
+        python3 bench.py --steps 1 --warmup 0 --single-stream-moves 0 $SP "$@" > $OUT/$NAME.json 2> $OUT/$NAME.err || { echo "pmc $CTR failed"; tail -3 $OUT/$NAME.err; exit 1; }
+      echo "pass $NAME done"
+    done
+    for K in "k_tower3<15, true" "k_expand_select"; do
+      echo "== $K"; python3 tools/pmc_summary.py $OUT "$K" fp16 2
+    done > $OUT/summary.txt
+    cat $OUT/summary.txt ;;
+  *)
+    echo "usage: tools/gpu.sh tests|smoke|bench|trace|pmc TAG [args]"; exit 2 ;;
+esac
