@@ -139,16 +139,19 @@ def parse(argv=None):
     ap.add_argument("--c5-steps", type=int, default=3)
     ap.add_argument("--c1-steps", type=int, default=10)
     ap.add_argument("--worker-moves", type=int, default=20, help="timed moves of the drop-in worker leg (0: skip)")
-    ap.add_argument("--worker-warmup", type=int, default=30,
-                    help="untimed worker moves first (games start empty: by then games finish every move)")
+    ap.add_argument("--worker-warmup", type=int, default=4, help="untimed worker moves first")
+    ap.add_argument("--worker-openings", type=int, default=80,
+                    help="staggered starts: each slot's first game from a random opening of 0..N stones "
+                         "(engine.random_openings), so games finish in the short timed window (0: empty boards)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--trainer-steps", type=int, default=20, help="timed trainer steps (0: no trainer leg)")
     ap.add_argument("--trainer-warmup", type=int, default=6)
     ap.add_argument("--trainer-batch", type=int, default=360)
     ap.add_argument("--trainer-buffer", type=int, default=4096, help="synthetic slices per rank's PER shard")
     ap.add_argument("--loop-iters", type=int, default=20, help="timed iterations of the C4 loop (0: no loop leg)")
-    ap.add_argument("--loop-warmup", type=int, default=30,
-                    help="untimed iterations (games start from the empty board: after ~30 moves they finish every move)")
+    ap.add_argument("--loop-warmup", type=int, default=6)
+    ap.add_argument("--loop-openings", type=int, default=80,
+                    help="staggered starts of the C4 loop's games (random openings of 0..N stones; 0: empty boards)")
     ap.add_argument("--loop-modes", default="sliced",
                     help="C4 loop legs: 'sliced' (moves then steps), 'concurrent' (steps on their own HIP stream "
                          "beside the moves); comma-separated")
@@ -619,10 +622,13 @@ def worker_leg(args, rank, world, dist, backend, consumer, engine_rate):
     warm, moves = args.worker_warmup, args.worker_moves
     if dist:
         dist.barrier()
+    import datou_gomoku_muzero_amd.engine as E
+    op = (E.random_openings(args.games, args.size, np.random.RandomState(args.seed + 29 * rank), args.worker_openings)
+          if args.worker_openings > 0 else None)
     gpu_selfplay_worker(rank, None, qs["data"], qs["log"], qs["ui"], _Flag(), trainer_event_queue=qs["trainer"],
                         num_games=args.games, cfg=cfg, max_moves=warm + moves, emit_move_notices=True,
                         move_times=times, seed=args.seed + 7919 * rank, precision=args.precision,
-                        device=torch.cuda.current_device())
+                        device=torch.cuda.current_device(), openings=op)
     for q in qs.values():
         q.put(None)
     counts = report.get(timeout=300)
@@ -633,10 +639,14 @@ def worker_leg(args, rank, world, dist, backend, consumer, engine_rate):
                       % (args.size, args.size, args.sims),
             "value": value, "unit": "moves/s", "n_gpus": world, "games_per_gpu": args.games, "moves": moves,
             "warmup_moves": warm, "steady_s": steady, "worker_over_engine": value / engine_rate if engine_rate else None,
+            "move_ms": [round((b - a) * 1e3, 2) for a, b in zip(times[warm - 1:-1], times[warm:])],
             "finished_games": int(tot.get("data", 0)), "slices": int(tot.get("slices", 0)),
             "messages": {k: int(v) for k, v in tot.items() if k != "slices"},
             "queues": "torch.multiprocessing (spawn) Queues of main.py's sizes; a consumer process unpickles every "
                       "payload (GameRecord + TrainingSlices, SelfPlayMove / SelfPlayStatus / GameCompletedNotice)",
+            "data": ("each slot's first game from a random opening of 0..%d stones (staggered starts; its record "
+                     "holds the moves searched from there), later games from the empty board" % args.worker_openings
+                     if args.worker_openings > 0 else "games from the empty board"),
             "timed": "from the host clock after warm-up move %d was queued to after the last move's records were "
                      "posted (per-move history, winning-move scan, record building all inside)" % warm}
 
@@ -718,9 +728,10 @@ def main():
                 "weight_push_ms": push_ms,
                 "push_share_at_interval": {"interval": 1000, "ms_per_trainer_step": push_ms / 1000.0,
                                            "share_of_iteration": push_ms / 1000.0 / step_ms if step_ms else None},
-                "data": "self-play games from the empty board with the trainer's weights (the timed window starts "
-                        "after %d warm-up iterations, so games finish inside it); each PER shard also pre-filled "
-                        "with %d synthetic slices so training starts at once" % (args.loop_warmup, args.loop_prefill),
+                "data": "self-play with the trainer's weights, each slot's first game from a random opening of "
+                        "0..%d stones (staggered starts, so games finish in the timed window; later games from the "
+                        "empty board); each PER shard also pre-filled with %d synthetic slices so training starts "
+                        "at once" % (args.loop_openings, args.loop_prefill),
                 "parallelism": "dp%d: self-play + replay shard per GPU; one gradient all-reduce + sharded-PER syncs "
                                "per step; rank 0 weight broadcast per push" % world}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.net == "hip":

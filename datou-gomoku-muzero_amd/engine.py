@@ -428,3 +428,46 @@ def winning_scan(boards, players, actions=None, n_in_row=5, counters=None, strea
     check(L.gmz_game_winning_scan(ptr(b), ptr(p), ptr(a), G, S, int(n_in_row), ptr(cls), ptr(mf), ptr(mt),
                                   _lib.stream_ptr(stream)))
     return cls
+
+
+def _has_five(board, n_in_row=5):
+    """Any run of n_in_row equal non-zero stones on an int8 [S,S] board (rows, columns, diagonals)."""
+    S = board.shape[0]
+    for b in (board, board.T):
+        for k in range(S - n_in_row + 1):
+            w = b[:, k:k + n_in_row]
+            if ((w == w[:, :1]).all(axis=1) & (w[:, 0] != 0)).any():
+                return True
+    for b in (board, board[:, ::-1]):
+        for off in range(-(S - n_in_row), S - n_in_row + 1):
+            d = np.diagonal(b, off)
+            for k in range(len(d) - n_in_row + 1):
+                w = d[k:k + n_in_row]
+                if w[0] != 0 and (w == w[0]).all():
+                    return True
+    return False
+
+
+def random_openings(G, size, rs, max_stones, n_in_row=5):
+    """Staggered game starts for measurements: game g gets an opening of uniform(0, max_stones) stones of
+    alternating colour (black first) on random cells, with no n_in_row line on the board, the player to
+    move after it and its last stone.  Returns (boards int8 [G,S,S], players int8 [G], last_moves int32 [G],
+    move_counts int32 [G]) for BatchedSelfPlayEngine.set_positions / GameHistory.set_start."""
+    A = size * size
+    boards = np.zeros((G, size, size), np.int8)
+    players = np.ones(G, np.int8)
+    last = np.full(G, -1, np.int32)
+    counts = rs.randint(0, max_stones + 1, G).astype(np.int32)
+    for g in range(G):
+        while True:
+            n = int(counts[g])
+            cells = rs.permutation(A)[:n]
+            b = np.zeros(A, np.int8)
+            b[cells[0::2]] = 1
+            b[cells[1::2]] = -1
+            if not _has_five(b.reshape(size, size), n_in_row):
+                break
+        boards[g] = b.reshape(size, size)
+        players[g] = 1 if n % 2 == 0 else -1
+        last[g] = cells[-1] if n else -1
+    return boards, players, last, counts

@@ -62,7 +62,7 @@ def slices_from_game(boards, players, lasts, pols, vals, acts, winner, H, discou
 class SelfPlay:
     """G games on this rank's GPU (the self-play half of the worker loop, worker.py)."""
 
-    def __init__(self, cfg, num_games, state_dict, seed=0, precision="fp16", streams=None):
+    def __init__(self, cfg, num_games, state_dict, seed=0, precision="fp16", streams=None, openings=None):
         from . import engine as E, network as N
         from .worker import GameHistory
         c = cfg
@@ -72,6 +72,9 @@ class SelfPlay:
         self.eng = E.make_engine(c, num_games=self.G, net=self.net, seed=seed, streams=streams)
         self.eng.reset_games()
         self.hist = GameHistory(self.G, c.ACTION_SPACE_SIZE, self.eng.device, min_game_len=2 * c.N_IN_ROW - 1)
+        if openings is not None:  # (boards, players, last_moves, move_counts): e.g. engine.random_openings
+            self.eng.set_positions(*openings)
+            self.hist.set_start(openings[3])
         dev = self.eng.device
         self.missed = (torch.zeros(self.G, dtype=torch.int32, device=dev), torch.zeros(self.G, dtype=torch.int32, device=dev))
         self.pending = None
@@ -227,7 +230,13 @@ def run_c4(args, rank, world, dist, backend, log=print):
                          MODEL_UPDATE_INTERVAL=args.loop_update_interval)
     tr = T.Trainer(tcfg, device="cuda")
     sd = tr.state_dict_cpu()  # the trainer's initial weights (rank 0's, broadcast by Trainer) feed self-play
-    sp = SelfPlay(cfg, args.loop_games, sd, seed=args.seed + 7919 * rank, precision=getattr(args, "precision", "fp16"))
+    openings = None
+    if getattr(args, "loop_openings", 0) > 0:  # staggered starts: games at every stage from the first move on
+        from .engine import random_openings
+        openings = random_openings(args.loop_games, args.size, np.random.RandomState(args.seed + 17 * rank),
+                                   args.loop_openings)
+    sp = SelfPlay(cfg, args.loop_games, sd, seed=args.seed + 7919 * rank, precision=getattr(args, "precision", "fp16"),
+                  openings=openings)
     rb = T.ReplayBuffer(tcfg, device="cuda")
     if args.loop_prefill:
         from .weights import synthetic_slices

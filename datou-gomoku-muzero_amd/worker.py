@@ -10,7 +10,9 @@ the same messages on the same queues:
 Weights: the inference server's handshake (``InitialModelRequest`` -> ``ModelWeightsUpdate``,
 workers.py:319-322) when ``initial_model_requests_queue``/``model_update_queue`` are given, and
 hot-swap between moves (workers.py:332-335); otherwise ``state_dict`` (or seeded synthetic weights).
-``worker_mode`` 1 (re-analysis, workers.py:243-305; off by default, config.py:85): the worker locks up to
+``openings`` (bench only): (boards, players, last_moves, move_counts) the first game of every slot
+starts from, e.g. engine.random_openings — so a short measurement sees games at every stage; their
+records hold the moves searched from there on.  ``worker_mode`` 1 (re-analysis, workers.py:243-305; off by default, config.py:85): the worker locks up to
 ``reanalysis_games`` stored games of the reference's SQLite database at a time (``db_path``), searches all
 their positions in batches of ``num_games`` on a second engine that shares the network, rewrites their
 slices and posts ``ReAnalysisStatus`` (reanalysis.py).  The current trainer step is the stored
@@ -75,12 +77,22 @@ class GameHistory:
         self.player = z(2, G, L, dt=torch.int8)
         self.last = z(2, G, L, dt=torch.int32)
         self.bank = z(G, dt=torch.int64)
+        # first recorded move index per (bank, game slot): 0 for games from the empty board; a game
+        # started from a given position (set_start) records from its move count on
+        self.start = np.zeros((2, G), dtype=np.int64)
         self.gidx = torch.arange(G, device=device)
         self.side = torch.cuda.Stream(device)
         self.k = 0
         pin = lambda dt: torch.zeros(G, dtype=dt).pin_memory()  # noqa: E731
         self.snaps = [dict(status=pin(torch.int8), mc=pin(torch.int32), bank=pin(torch.int64), mf=pin(torch.int32),
                            mt=pin(torch.int32), act=pin(torch.int32), ev=None) for _ in range(2)]
+
+    def set_start(self, move_counts):
+        """The current games start from positions with ``move_counts`` stones (before their first
+        move; every slot is still on bank 0): their records hold the searched moves from there on."""
+        assert self.k == 0, "set_start before the first move"
+        self.start[0] = np.asarray(move_counts, dtype=np.int64)
+        self.start[1] = 0
 
     def record(self, boards, players, last_moves, move_counts, policy, value, action):
         """Append this move's search inputs/outputs (all device tensors, before the move is played)."""
@@ -127,13 +139,16 @@ class GameHistory:
         with torch.cuda.stream(self.side):
             self.side.wait_event(sn["ev"])
             for g in fin:
+                bk = int(bank[g])
+                s0 = int(self.start[bk, g])
+                self.start[bk, g] = 0  # this bank's next game starts from the empty board
                 if act[g] < 0:
                     continue
-                n, bk = int(mc[g]) + 1, int(bank[g])
+                n = int(mc[g]) + 1 - s0
                 host = [torch.empty((n,) + tuple(t.shape[3:]), dtype=t.dtype, pin_memory=True)
                         for t in (self.board, self.player, self.last, self.pol, self.val, self.act)]
                 for h, t in zip(host, (self.board, self.player, self.last, self.pol, self.val, self.act)):
-                    h.copy_(t[bk, g, :n], non_blocking=True)
+                    h.copy_(t[bk, g, s0:s0 + n], non_blocking=True)
                 jobs.append((int(g), int(st[g]), n, int(sn["mf"][g]), int(sn["mt"][g]), host))
         self.side.synchronize()
         for g, winner, n, mf, mt, host in jobs:
@@ -146,7 +161,7 @@ def gpu_selfplay_worker(worker_id, worker_mode, data_queue, log_status_queue, ui
                         latest_model_step=None, log_queue=None, pause_event=None, *, device=0, num_games=1024,
                         model_update_queue=None, initial_model_requests_queue=None, state_dict=None, cfg=None,
                         seed=0, max_moves=None, emit_move_notices=True, db_path="outputs/training_state.db",
-                        reanalysis_games=64, precision="fp16", move_times=None, streams=None):
+                        reanalysis_games=64, precision="fp16", move_times=None, streams=None, openings=None):
     logger = logging.getLogger("GpuSelfPlay-%s" % worker_id)
     if log_queue is not None:
         try:
@@ -179,6 +194,9 @@ def gpu_selfplay_worker(worker_id, worker_mode, data_queue, log_status_queue, ui
     eng.reset_games()
     H, A = c.BOARD_SIZE, c.ACTION_SPACE_SIZE
     hist = GameHistory(G, A, eng.device, min_game_len=2 * c.N_IN_ROW - 1)
+    if openings is not None:  # bench: the first games start from given positions (E.random_openings)
+        eng.set_positions(*openings)
+        hist.set_start(openings[3])
     pool = ThreadPoolExecutor(max_workers=4)
     moves_done = 0
     # missed-win counters of workers.py:191-203, accumulated on the device move by move by the batched

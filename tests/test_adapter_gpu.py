@@ -182,12 +182,14 @@ def test_recurrent_timeout_retries_the_wave(M):
     assert len(logs[1]) == len(logs[0]) + 1 and logs[1][4] == logs[1][3]  # the dropped request, re-sent
 
 
-@pytest.mark.parametrize("streams", [1, 2])
-def test_worker_records_equal_a_synchronous_loop(M, streams):
+@pytest.mark.parametrize("streams,openings", [(1, False), (2, False), (2, True)])
+def test_worker_records_equal_a_synchronous_loop(M, streams, openings):
     """The worker's device-side history harvested one move behind (worker.GameHistory) yields exactly
     the records of a plain synchronous loop over the same engine (same seed, same weights) that copies
     every move's position / policy / value / action to the host before the next move — also with the
-    worker's games split over two HIP streams (engine.SplitSelfPlayEngine)."""
+    worker's games split over two HIP streams (engine.SplitSelfPlayEngine), and with the first game of
+    every slot started from a random opening (bench's staggered starts: its record holds the moves
+    searched from the opening on, the slot's later games start from the empty board)."""
     from datou_gomoku_muzero_amd import engine as E, network as N, records as R, weights as W
     from datou_gomoku_muzero_amd.worker import gpu_selfplay_worker
     mcts, GmzConfig = M
@@ -198,9 +200,10 @@ def test_worker_records_equal_a_synchronous_loop(M, streams):
         def is_set(self):
             return False
 
+    op = E.random_openings(G, 6, np.random.RandomState(11), 12) if openings else None
     dq = queue.Queue()
     gpu_selfplay_worker(0, None, dq, None, None, Ev(), num_games=G, cfg=cfg, max_moves=moves, seed=seed,
-                        streams=streams)
+                        streams=streams, openings=op)
     got = []
     while not dq.empty():
         got.append(dq.get())
@@ -209,6 +212,8 @@ def test_worker_records_equal_a_synchronous_loop(M, streams):
     net = N.GomokuNetHip(sd, cfg, num_slots=G * 18, max_rows=G)
     eng = E.BatchedSelfPlayEngine(cfg, num_games=G, net=net, seed=seed)
     eng.reset_games()
+    if op is not None:
+        eng.set_positions(*op)
     hist = [dict(obs=[], act=[], pol=[], val=[], brd=[]) for _ in range(G)]
     want = []
     for _ in range(moves):
