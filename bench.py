@@ -127,6 +127,11 @@ def parse(argv=None):
     ap.add_argument("--single-stream-moves", type=int, default=2,
                     help="with --streams > 1: moves of ONE engine on one stream after the timed region, for the two "
                          "kernels' single-stream launch times (0: skip)")
+    ap.add_argument("--layout", default=None, choices=["dense", "lists"],
+                    help="tree layout of the non-root nodes (engine.default_layout when omitted): dense child rows "
+                         "or compact lists of the visited children (identical results)")
+    ap.add_argument("--hint", default=None, choices=["on", "off"],
+                    help="descent prefetch hint / cached exp rows of the tree kernels (default: by game count)")
     ap.add_argument("--precision", default="fp16", choices=["fp16", "bf16"],
                     help="MFMA operand type of the network towers (f32 accumulation either way)")
     ap.add_argument("--seed", type=int, default=1234)
@@ -398,12 +403,14 @@ def selfplay_leg(args, rank, world, dist, backend, size, sims, mode, blocks, G, 
         net = E.HashNetBackend(slots, cfg.ACTION_SPACE_SIZE)
     if streams is None:
         streams = E.default_streams(cfg, G)
-    eng = E.make_engine(cfg, num_games=G, net=net, seed=args.seed + 7919 * rank, streams=streams)
+    tkw = dict(layout=args.layout, descent_hint=None if args.hint is None else args.hint == "on")
+    eng = E.make_engine(cfg, num_games=G, net=net, seed=args.seed + 7919 * rank, streams=streams, **tkw)
     eng.reset_games()
     parts = eng.engines if streams > 1 else [eng]
     pstreams = eng.streams if streams > 1 else [torch.cuda.current_stream()]
-    log("%srank %d: engine G=%d %dx%d %s/%d, %d blocks, net=%s, %d stream(s)"
-        % (log_prefix, rank, G, size, size, mode, sims, blocks, args.net, streams))
+    log("%srank %d: engine G=%d %dx%d %s/%d, %d blocks, net=%s, %d stream(s), %s tree, hint %s"
+        % (log_prefix, rank, G, size, size, mode, sims, blocks, args.net, streams, parts[0].layout,
+           parts[0].descent_hint))
 
     def step():
         eng.search()
@@ -484,6 +491,7 @@ def selfplay_leg(args, rank, world, dist, backend, size, sims, mode, blocks, G, 
             "mean_backup_levels": ctr["backup_levels"] / max(1, ctr["backups"]),
             "mean_select_levels": ctr["select_levels"] / max(1, ctr["selects"]),
             "games_per_launch": ctr["backups"] / n_tree, "streams": streams, "busy_ms": busy_tree,
+            "layout": parts[0].layout, "descent_hint": parts[0].descent_hint,
             "achieved_per_launch": bpl / (ms_tree * 1e-3) / 1e9,
             "note": ("two streams: each launch runs on the CUs the other stream's capped tower leaves free (about "
                      "a quarter of them), so this is the kernel inside the step, not its own rate; "
@@ -495,7 +503,7 @@ def selfplay_leg(args, rank, world, dist, backend, size, sims, mode, blocks, G, 
         for e in parts:
             e.net.tower_timer = e.net.repr_timer = None
         eng.close()
-        e1 = E.BatchedSelfPlayEngine(cfg, num_games=G, net=net, seed=args.seed + 7919 * rank + 1)
+        e1 = E.BatchedSelfPlayEngine(cfg, num_games=G, net=net, seed=args.seed + 7919 * rank + 1, **tkw)
         e1.reset_games()
         e1.search()
         e1.play(reset_finished=True)

@@ -11,7 +11,7 @@ import torch  # noqa: F401  (must precede the CDLL load: shared HIP runtime)
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GMZ_LIB") or os.path.join(PKG_DIR, "libgmz.so")  # GMZ_LIB: A/B builds (tools)
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 P = ctypes.c_void_p
 I = ctypes.c_int

@@ -14,6 +14,8 @@
 // k_heads: policy_fc, value MLP, reward fc2, support_to_scalar (network.py:9-13, 58-74, 84-88).
 #include <type_traits>
 #include "gmz_common.h"
+
+#include <atomic>
 #include "../../include/gmz.h"
 
 #include <hip/hip_bf16.h>
@@ -60,8 +62,9 @@ struct TowerArgs {
   int rows;
   uint16_t *xres;          // single-image boards (19x19): per-workgroup residual scratch (k_tower3)
   int max_grid;            // cap on the persistent grid (gmz_net_weights.max_grid; 0 = every CU)
-  int *tickets;            // k_tower3 board scheduling (one board per workgroup): [0] next row, [1]
-                           // workgroups done; zero between launches (the last workgroup resets them)
+  unsigned long long *tickets;  // k_tower3 board scheduling (one board per workgroup): {generation << 32 |
+                                // next row}, 8 B at the workspace head (see fetch_row)
+  uint32_t gen;                 // this launch's generation (unique per launch, never 0)
 };
 
 // MFMA operand element types of the towers and the reward GEMM (f32 accumulation either way).
@@ -194,26 +197,29 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
     }
   };
   // one board per workgroup (15x15, 19x19): boards are handed out in ticket order as workgroups
-  // become free (thread 0 takes the next active row; the launch's last workgroup resets the
-  // counters), so a workgroup that starts late — its CU still held by the other stream's tower —
-  // takes fewer boards instead of delaying the whole launch by its static share
+  // become free (thread 0 takes the next active row), so a workgroup that starts late — its CU still
+  // held by the other stream's tower — takes fewer boards instead of delaying the whole launch by its
+  // static share.  The ticket word carries the launch's generation in its high half: a workgroup that
+  // draws a word of another generation (the previous launch's, whatever state it was left in) starts
+  // this generation with a compare-and-swap (ticket 0) or, if another workgroup already did, draws
+  // again — so no launch has to reset the counter and none can inherit a stale one.
   __shared__ int s_row;
-  int *tk = t.tickets;
+  unsigned long long *tk = t.tickets;
   const bool dsched = NB == 1 && tk != nullptr;
-  auto fetch_row = [&]() {
-    int r = atomicAdd(&tk[0], 1);
-    while (r < t.rows && t.out_slot[r] < 0) r = atomicAdd(&tk[0], 1);
-    return r;
-  };
-  auto finish_launch = [&]() {
-    if (dsched && threadIdx.x == 0) {
-      __threadfence();
-      if (atomicAdd(&tk[1], 1) == (int)gridDim.x - 1) {
-        atomicExch(&tk[0], 0);
-        atomicExch(&tk[1], 0);
-      }
+  auto ticket = [&]() -> int {
+    for (;;) {
+      const unsigned long long old = atomicAdd(tk, 1ull);
+      if ((uint32_t)(old >> 32) == t.gen) return (int)(uint32_t)old;
+      const unsigned long long cur = old + 1ull;
+      if (atomicCAS(tk, cur, ((unsigned long long)t.gen << 32) | 1ull) == cur) return 0;
     }
   };
+  auto fetch_row = [&]() {
+    int r = ticket();
+    while (r < t.rows && t.out_slot[r] < 0) r = ticket();
+    return r;
+  };
+  auto finish_launch = [&]() {};
   if (dsched) {
     if (threadIdx.x == 0) s_row = fetch_row();
     __syncthreads();
@@ -782,6 +788,14 @@ static size_t xres_bytes(int H) {
   }
 }
 
+// tower launch generations (k_tower3's ticket word): unique per launch across every workspace, never 0
+static std::atomic<uint32_t> g_tower_gen{0};
+static uint32_t next_gen() {
+  uint32_t g;
+  do g = ++g_tower_gen; while (g == 0);
+  return g;
+}
+
 template <int H, bool DYN, typename E>
 static int launch_tower(const TowerArgs &a, hipStream_t s) {
   if (a.rows <= 0) return 0;
@@ -808,6 +822,7 @@ static int tower_e(int H, bool dyn, const TowerArgs &a, hipStream_t s) {
 static int tower(const gmz_net_weights *w, bool dyn, const TowerArgs &a0, hipStream_t s) {
   TowerArgs a = a0;
   a.max_grid = w->max_grid;
+  a.gen = next_gen();
   return w->dtype == GMZ_NET_BF16 ? tower_e<Bf16>(w->board_size, dyn, a, s) : tower_e<F16>(w->board_size, dyn, a, s);
 }
 
@@ -833,7 +848,7 @@ static uint16_t *ws_xres(void *workspace, int A, int rows) {
 }
 // the tower's two scheduling counters: the workspace's first 256 B, at the same place whatever the
 // row count (zero-filled when the workspace is allocated, include/gmz.h; every launch leaves them zero)
-static int *ws_tickets(void *workspace) { return (int *)workspace; }
+static unsigned long long *ws_tickets(void *workspace) { return (unsigned long long *)workspace; }
 
 static int check_w(const gmz_net_weights *w) {
   if (!w) return fail("gmz_net: null weights");

@@ -18,7 +18,10 @@
 //   double expl[G][S][A2] exp(logit - max legal logit) per node, A2 = A rounded up to even: computed
 //                         once when the node is expanded; a non-root selection's softmax then needs
 //                         an exp only for its visited children (shift invariance, select_nonroot)
-//   int path_u/path_a[G][S], node_parent/node_action[G][S]
+//   int path_u/path_a/path_e[G][S], node_parent/node_action[G][S]
+//   With compact child lists (gmz_engine_cfg.flags bit 3) a NON-ROOT node's edge row holds only its
+//   visited children, as entries {action << 16 | child, N, W, R} in first-visit order at the row's
+//   head (the root keeps the dense row); see ListSlot below.
 //   int4 hdr[G][S]        per-node header {sum of child N, max child N, visited children, next-visit
 //                         hint}: maintained by the backup so that a selection step needs no integer
 //                         wave reductions; the hint is the predicted choice of the node's next visit
@@ -60,6 +63,7 @@ struct Dev {
   float *logits;
   double *expl;  // [G][S][A2] exp(logit - max legal logit), written by the expansion
   int32_t *node_parent, *node_action, *path_u, *path_a, *sel;
+  int32_t *path_e;     // [G][S] child-list entry index of each non-root path level (compact child lists)
   int4 *hdr;           // [G][S] NodeHdr {tot = sum N_child, maxn = max N_child, nvis = #children N > 0, last}
   int32_t *ctr;        // [G][4] k_expand_select work counters (gmz_engine_tree_counters)
   GameState *gs;
@@ -71,6 +75,7 @@ struct Dev {
   int G, A, A2, S, size, n_sims, m_top, c_visit, mode;
   int game_offset;  // gmz_engine_cfg.game_offset: global index of game 0 (device Gumbel noise)
   int no_hint;  // gmz_engine_cfg.flags bit 0: descent prefetch hint off (timing A/B; results identical)
+  int lists;    // gmz_engine_cfg.flags bit 3: compact child lists for non-root nodes (see ListSlot)
   double c_scale;
   float disc_f, delta_f;
 };
@@ -519,7 +524,7 @@ __device__ int select_nonroot(const Dev &D, const uint64_t (&lg)[NJ], int g, int
 }
 
 // _select_action at the root (mcts.py:96-104): first least-visited entry of the selected list.
-__device__ int select_root(const Dev &D, int g, int lane, int n_sel, int *child) {
+__device__ int select_root(const Dev &D, int g, int lane, int n_sel, int *child, int *nchild) {
   int v = 0x7fffffff, i = 64 + lane, a = -1, c = -1;
   if (lane < n_sel) {
     a = D.sel[g * MAX_TOP + lane];
@@ -534,6 +539,228 @@ __device__ int select_root(const Dev &D, int g, int lane, int n_sel, int *child)
     if (ov < v || (ov == v && oi < i)) { v = ov; i = oi; a = oa; c = oc; }
   }
   *child = c;
+  *nchild = v;  // the chosen edge's N
+  return a;
+}
+
+// ------------------------------------------------------------------------------------------
+// Compact child lists (gmz_engine_cfg.flags bit 3).  A non-root node keeps the edges of
+// its VISITED children only: entries {action << 16 | child, N, W, R} in first-visit order at the head
+// of its edge row; the root keeps the dense row (root selection, halving and finish read it).  A
+// selection level then reads the node's header, its exp row (EX: the hint kernels) or logits and its
+// nvis entries, not the 16 B x A dense row; the entry lanes scatter their children's x (EX: E scaled
+// by exp(t - t0)) or normalised Q, and N, into a per-wave LDS view of the node in action order, and
+// from there on the arithmetic is the dense kernels' on the same values in the same order: results
+// bit-identical to the dense layout's (tests/test_tree_lists_gpu.py).
+// Per-wave LDS block: the DMA'd row (prefetched or fetched now) + the scatter view.
+template <int NJ, bool EX>
+struct ListSlot {
+  static constexpr int ROW = 0;                                         // E row (A2 f64) or logits (A f32)
+  static constexpr int ROWB = EX ? ((NJ + 1) / 2) * 1024 : NJ * 256;
+  static constexpr int ENT = ROWB;                                      // entries 0..63, 16 B each
+  static constexpr int HDR = ENT + 1024;                                // the node header
+  static constexpr int XS = HDR + 16;                                   // f64 per action: x (EX) or nq
+  static constexpr int NS = XS + NJ * 512;                              // int per action: N
+  static constexpr int CS = NS + NJ * 256;                              // int per action: entry << 16 | child
+  static constexpr int BYTES = CS + NJ * 256;
+};
+template <int NJ, bool EX>
+struct ListRegs {
+  typename std::conditional<EX, double, float>::type v[NJ];  // the row, lane's actions a = lane + 64 j
+  int4 ent;  // entry `lane` (valid for lane < min(nvis, entries DMA'd))
+  int4 hdr;
+};
+// entries worth DMA-ing for a child reached through an edge of visit count n: a node is expanded by
+// its first visit and gains at most one visited child per later visit, so nvis <= n - 1
+__device__ __forceinline__ int list_bound(const Dev &D, int n) {
+  const int cap = D.A < WAVE ? D.A : WAVE;
+  const int b = n - 1;
+  return b < 0 ? 0 : (b > cap ? cap : b);
+}
+template <int NJ, bool EX>
+__device__ __forceinline__ void list_fetch_lds(const Dev &D, int g, int u, int nent, int lane, uint8_t *blk) {
+  using L = ListSlot<NJ, EX>;
+  int ln = lane;
+  asm volatile("" : "+v"(ln));
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the block have returned
+  if constexpr (EX) {
+    const char *xr = (const char *)expl_row(D, g, u);
+#pragma unroll
+    for (int i = 0; i < (NJ + 1) / 2; ++i) {
+      const int a = 2 * WAVE * i + 2 * ln, ac = a < D.A2 - 2 ? a : D.A2 - 2;
+      __builtin_amdgcn_global_load_lds((const void *)(xr + (uint32_t)(ac * 8)),
+                                       (__attribute__((address_space(3))) void *)(blk + L::ROW + i * 1024), 16, 0, 0);
+    }
+  } else {
+    const float *lr = D.logits + ((size_t)g * D.S + u) * D.A;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int a = ln + WAVE * j, ac = a < D.A ? a : D.A - 1;
+      __builtin_amdgcn_global_load_lds((const void *)(lr + ac),
+                                       (__attribute__((address_space(3))) void *)(blk + L::ROW + j * 256), 4, 0, 0);
+    }
+  }
+  if (ln < nent)
+    __builtin_amdgcn_global_load_lds((const void *)((const char *)edge_row(D, g, u) + (uint32_t)(ln * 16)),
+                                     (__attribute__((address_space(3))) void *)(blk + L::ENT), 16, 0, 0);
+  if (lane < 4)
+    __builtin_amdgcn_global_load_lds((const void *)((const int *)(D.hdr + (size_t)g * D.S + u) + lane),
+                                     (__attribute__((address_space(3))) void *)(blk + L::HDR), 4, 0, 0);
+}
+template <int NJ, bool EX>
+__device__ __forceinline__ void list_from_lds(const uint8_t *blk, int lane, ListRegs<NJ, EX> &r) {
+  using L = ListSlot<NJ, EX>;
+  using T = typename std::conditional<EX, double, float>::type;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA has landed
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) r.v[j] = *(const T *)(blk + L::ROW + (lane + WAVE * j) * (int)sizeof(T));
+  r.ent = *(const int4 *)(blk + L::ENT + lane * 16);
+  r.hdr = *(const int4 *)(blk + L::HDR);
+}
+
+// _select_action at a non-root node (mcts.py:106-117) on a compact child list (`cur`, DMA'd through
+// the wave's block: `nent` entries in LDS, the rest read here).  Same decisions and arithmetic as
+// select_nonroot<NJ, EX> on the dense row.  Returns the action; *child / *nchild / *entry = the chosen
+// child's node id (-1: a new leaf), its edge N (0) and list entry (nvis: appended by the backup).
+// EX (the hint kernels): while this level computes, the row of the child chosen at this node's last
+// visit (hdr.w, a node id) is prefetched into the block (*nxt_u, *nxt_nent); hdr.w is then set to this
+// visit's child (leaf_next for a new leaf: the node the expansion will create).
+template <int NJ, bool EX>
+__device__ int select_nonroot_cl(const Dev &D, const uint64_t (&lg)[NJ], int g, int u, int lane, const NormQ &nz,
+                                 const ListRegs<NJ, EX> &cur, int nent, int leaf_next, uint8_t *blk, int *child,
+                                 int *nchild, int *entry, int *nxt_u, int *nxt_nent) {
+  using L = ListSlot<NJ, EX>;
+  const int tot = __builtin_amdgcn_readfirstlane(cur.hdr.x);
+  const int max_n = __builtin_amdgcn_readfirstlane(cur.hdr.y);
+  const int nvis = __builtin_amdgcn_readfirstlane(cur.hdr.z);
+  const int hint = __builtin_amdgcn_readfirstlane(cur.hdr.w);
+  *nxt_u = -1;
+  if (EX && hint > 0 && hint < D.S) {
+    const uint64_t hm = __ballot(lane < nvis && lane < nent && (cur.ent.x & 0xffff) == hint);
+    const int nb = hm ? list_bound(D, __builtin_amdgcn_readlane(cur.ent.y, __builtin_ctzll(hm))) : list_bound(D, WAVE + 1);
+    list_fetch_lds<NJ, EX>(D, g, hint, nb, lane, blk);
+    *nxt_u = hint;
+    *nxt_nent = nb;
+  }
+  double *X = (double *)(blk + L::XS);
+  float *QF = (float *)(blk + L::XS);
+  int *NN = (int *)(blk + L::NS), *CI = (int *)(blk + L::CS);
+  const bool allv = nvis >= D.A;  // every child visited: the float32 rule below (improved_policy)
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int a = lane + WAVE * j;
+    X[a] = EX ? (double)cur.v[j] : nz.nq0;
+    NN[a] = 0;
+  }
+  asm volatile("" ::: "memory");
+  const double scale = (double)(D.c_visit + max_n) * D.c_scale;
+  const double t0 = scale * nz.nq0;
+  const Edge *row = edge_row(D, g, u);
+  for (int i0 = 0; i0 < nvis; i0 += WAVE) {
+    const int i = i0 + lane;
+    int4 e = cur.ent;
+    if ((i0 > 0 || lane >= nent) && i < nvis) e = *(const int4 *)(row + i);
+    if (i < nvis) {
+      const int a = e.x >> 16, n = e.y;
+      const float v = __int_as_float(e.z) / (float)n;  // get_qsa (mcts.py:35-38), as select_nonroot
+      const float dv = D.disc_f * v;
+      const float q = __int_as_float(e.w) + dv;
+      if (allv) {
+        QF[a] = q;
+      } else {
+        double nq = nz.nq0;
+        if (nz.have_range) {
+          double y = ((double)q - (double)nz.mm_min) / (double)nz.den_f;
+          y = (y < 1.0) ? y : 1.0;
+          nq = (y > 0.0) ? y : 0.0;
+        }
+        if (EX) {
+          double x = X[a];
+          if (nz.have_range) x *= exp(scale * nq - t0);
+          X[a] = x;
+        } else {
+          X[a] = nq;
+        }
+      }
+      NN[a] = n;
+      CI[a] = (i << 16) | (e.x & 0xffff);
+    }
+  }
+  asm volatile("" ::: "memory");
+  int n[NJ];
+  double p[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) n[j] = NN[lane + WAVE * j];
+  if (!allv && EX) {  // select_nonroot's cached-exp softmax
+    double x[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int a = lane + WAVE * j;
+      const bool ok = a < D.A && ((lg[j] >> lane) & 1ull);
+      x[j] = ok ? X[a] : 0.0;
+    }
+    double sum = 0.0;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) sum += x[j];
+    sum = dred_sum_d(sum);
+    const double inv_s = 1.0 / sum;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) p[j] = x[j] * inv_s;
+  } else if (!allv) {  // select_nonroot's logits softmax
+    double x[NJ], m = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int a = lane + WAVE * j;
+      const bool ok = a < D.A && ((lg[j] >> lane) & 1ull);
+      x[j] = ok ? (double)cur.v[j] + scale * X[a] : -INFINITY;
+      m = fmax(m, x[j]);
+    }
+    m = dred_max_d(m);
+    double sum = 0.0;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      x[j] = (x[j] == -INFINITY) ? 0.0 : exp(x[j] - m);
+      sum += x[j];
+    }
+    sum = dred_sum_d(sum);
+    const double inv_s = 1.0 / sum;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) p[j] = x[j] * inv_s;
+  } else {
+    float q[NJ], lv[NJ];
+    int mx_unused;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) q[j] = QF[lane + WAVE * j];
+    logits_load<NJ>(D, D.logits + ((size_t)g * D.S + u) * D.A, lane, lv);
+    improved_policy<NJ>(D, lg, lane, lv, n, q, nz.mm_max, nz.mm_min, p, mx_unused);
+  }
+  double sc[NJ], best = -INFINITY;
+  const double inv_tot = 1.0 / (double)(1 + tot);
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int a = lane + WAVE * j;
+    sc[j] = -INFINITY;
+    if (a < D.A && ((lg[j] >> lane) & 1ull)) sc[j] = p[j] - (double)n[j] * inv_tot;
+    best = fmax(best, sc[j]);
+  }
+  best = dred_max_d(best);
+  int a = 0;  // np.argmax: first (lowest) action whose score equals the maximum
+#pragma unroll
+  for (int j = NJ - 1; j >= 0; --j) {
+    const uint64_t mk = __ballot(sc[j] == best && best != -INFINITY);
+    if (mk) a = WAVE * j + __builtin_ctzll(mk);
+  }
+  const int na = NN[a];
+  if (na > 0) {
+    const int ci = CI[a];
+    *child = ci & 0xffff;
+    *entry = ci >> 16;
+  } else {
+    *child = -1;
+    *entry = nvis;
+  }
+  *nchild = na;
+  if (EX && lane == 0) D.hdr[(size_t)g * D.S + u].w = na > 0 ? *child : leaf_next;
   return a;
 }
 
@@ -728,7 +955,7 @@ __global__ void __launch_bounds__(256) k_set_root(Dev D, const float *__restrict
 
 // one wave: select the leaf of every active game and emit its network request.  AZ: AlphaZero (the
 // path is replayed on the root board for the observation); MuZero keeps no board state here.
-template <int NJ, bool HINT, bool AZ>
+template <int NJ, bool HINT, bool AZ, bool CL>
 __device__ __forceinline__ void select_game(const Dev &D, int g, int lane, int32_t *__restrict__ in_slot,
                                             int32_t *__restrict__ act_out, int32_t *__restrict__ out_slot,
                                             float *__restrict__ obs, uint8_t *hint_slot) {
@@ -756,22 +983,30 @@ __device__ __forceinline__ void select_game(const Dev &D, int g, int lane, int32
     cell[j] = (AZ && a < A) ? b[a] : 0;
   }
   int u = 0, d = 0, a = 0, last = -1;
-  int32_t *pu = D.path_u + (size_t)g * S, *pa = D.path_a + (size_t)g * S;
+  int32_t *pu = D.path_u + (size_t)g * S, *pa = D.path_a + (size_t)g * S, *pe = D.path_e + (size_t)g * S;
   uint64_t lg[NJ];
   load_legal<NJ>(D, g, lg);
   RowRegs<NJ, HINT> cur;
-  int nxt_u = -1;
+  ListRegs<NJ, HINT> lcur;
+  int nxt_u = -1, nxt_nent = 0, nent_u = 0, ent = 0;
   const NormQ nz = norm_q_consts(D, st.mm_max, st.mm_min);
   for (;;) {
-    int c;
+    int c, cn = 0;
     if (u == 0) {
       TP_STAMP(tr0);
-      a = select_root(D, g, lane, st.n_sel, &c);
+      a = select_root(D, g, lane, st.n_sel, &c, &cn);
 #ifdef GMZ_TREE_PROF
       __builtin_amdgcn_s_waitcnt(0);
       TP_STAMP(tr1);
       TP_ADD(5, tr1 - tr0);
 #endif
+    } else if constexpr (CL) {  // the node's list arrives through the wave's LDS block: prefetched or now
+      int ne = nent_u;
+      if (u != nxt_u) list_fetch_lds<NJ, HINT>(D, g, u, nent_u, lane, hint_slot);
+      else ne = nxt_nent;
+      list_from_lds<NJ, HINT>(hint_slot, lane, lcur);
+      a = select_nonroot_cl<NJ, HINT>(D, lg, g, u, lane, nz, lcur, ne, st.n_nodes, hint_slot, &c, &cn, &ent, &nxt_u,
+                                      &nxt_nent);
     } else {
       TP_STAMP(tf0);
       if constexpr (HINT) {  // the row arrives through the wave's LDS slot: prefetched (the hint held) or now
@@ -792,8 +1027,10 @@ __device__ __forceinline__ void select_game(const Dev &D, int g, int lane, int32
     if (lane == 0) {
       pu[d] = u;
       pa[d] = a;
+      if (CL) pe[d] = ent;  // (root level: unused, the root row is dense)
     }
     d++;
+    if (CL) nent_u = list_bound(D, cn);
     // replay do_move(a) on the lane-owned copy (no legality check, as the reference)
     if ((a & 63) == lane) {
 #pragma unroll
@@ -831,16 +1068,16 @@ __device__ __forceinline__ void select_game(const Dev &D, int g, int lane, int32
   }
 }
 
-template <int NJ, bool EX>
+template <int NJ, bool EX, bool CL>
 __device__ __forceinline__ void expand_backup_game(const Dev &D, int g, int lane, const float *__restrict__ logits_in,
                                                    const float *__restrict__ value_in,
                                                    const float *__restrict__ reward_in) {
   const int A = D.A, S = D.S;
-  const int32_t *pu = D.path_u + (size_t)g * S, *pa = D.path_a + (size_t)g * S;
+  const int32_t *pu = D.path_u + (size_t)g * S, *pa = D.path_a + (size_t)g * S, *pe = D.path_e + (size_t)g * S;
   // the first 64 path entries by lane, loaded beside the GameState (not after it): a level's node and
   // action then come from a lane permute instead of a dependent memory round trip
   const int pl = lane < S ? lane : S - 1;
-  const int pu_l = pu[pl], pa_l = pa[pl];
+  const int pu_l = pu[pl], pa_l = pa[pl], pe_l = CL ? pe[pl] : 0;
   GameState st = D.gs[g];
   if (!st.active) return;
   const int d = st.depth, leaf = st.leaf, k = st.k;
@@ -866,7 +1103,7 @@ __device__ __forceinline__ void expand_backup_game(const Dev &D, int g, int lane
       const int a = lane + WAVE * j;
       if (a < A) {
         nl[a] = lv[j];
-        nrow[a] = Edge{-1, 0, 0.f, 0.f};
+        if (!CL) nrow[a] = Edge{-1, 0, 0.f, 0.f};  // (a compact list starts empty: nvis = 0)
       }
     }
 #pragma unroll 1
@@ -875,7 +1112,7 @@ __device__ __forceinline__ void expand_backup_game(const Dev &D, int g, int lane
   } else {
     for (int a = lane; a < A; a += WAVE) {
       nl[a] = logits_in[(size_t)g * A + a];
-      nrow[a] = Edge{-1, 0, 0.f, 0.f};
+      if (!CL) nrow[a] = Edge{-1, 0, 0.f, 0.f};
     }
   }
   if (lane == 0) {
@@ -896,13 +1133,20 @@ __device__ __forceinline__ void expand_backup_game(const Dev &D, int g, int lane
     int4 h = make_int4(0, 0, 0, 0);
     const int lvl = d - 1 - j;  // path index of this lane's edge
     const int pu_j = __shfl(pu_l, lvl & (WAVE - 1), 64), pa_j = __shfl(pa_l, lvl & (WAVE - 1), 64);
+    const int pe_j = CL ? __shfl(pe_l, lvl & (WAVE - 1), 64) : 0;
     if (j < d) {
       const int nu = lvl < WAVE ? pu_j : pu[lvl], na = lvl < WAVE ? pa_j : pa[lvl];
-      ep = edge_row_w(D, g, nu) + na;
       hp = D.hdr + (size_t)g * S + nu;
-      e = *ep;
       h = *hp;
-      if (j == 0) { e.child = leaf; e.r = r_leaf; }
+      if (CL && nu != 0) {  // a compact list entry; the leaf's edge is appended at entry nvis
+        ep = edge_row_w(D, g, nu) + (lvl < WAVE ? pe_j : pe[lvl]);
+        if (j == 0) e = Edge{(na << 16) | leaf, 0, 0.f, r_leaf};
+        else e = *ep;
+      } else {
+        ep = edge_row_w(D, g, nu) + na;
+        e = *ep;
+        if (j == 0) { e.child = leaf; e.r = r_leaf; }
+      }
     }
     const float rj = e.r;
     const int cnt = min(WAVE, d + 1 - base);
@@ -982,14 +1226,21 @@ __device__ __forceinline__ void expand_backup_game(const Dev &D, int g, int lane
   if (lane == 0) D.gs[g] = st;
 }
 
-template <int NJ, bool HINT, bool AZ>
+// per-wave LDS block of the selection kernels: the hint slot (dense + HINT), the list block (CL), none
+template <int NJ, bool HINT, bool CL>
+struct SelLds {
+  static constexpr int BYTES = CL ? ListSlot<NJ, HINT>::BYTES : (HINT ? HintSlot<NJ>::BYTES : 0);
+};
+
+template <int NJ, bool HINT, bool AZ, bool CL>
 __global__ void __launch_bounds__(256) k_select(Dev D, int32_t *__restrict__ in_slot, int32_t *__restrict__ act_out,
                                                 int32_t *__restrict__ out_slot, float *__restrict__ obs) {
   const int g = blockIdx.x * 4 + threadIdx.x / WAVE, lane = threadIdx.x & (WAVE - 1);
   if (g >= D.G) return;
-  __shared__ __attribute__((aligned(16))) uint8_t hint_lds[HINT ? 4 * HintSlot<NJ>::BYTES : 16];
-  select_game<NJ, HINT, AZ>(D, g, lane, in_slot, act_out, out_slot, obs,
-                            hint_lds + (HINT ? __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE) * HintSlot<NJ>::BYTES : 0));
+  constexpr int LB = SelLds<NJ, HINT, CL>::BYTES;
+  __shared__ __attribute__((aligned(16))) uint8_t hint_lds[LB ? 4 * LB : 16];
+  select_game<NJ, HINT, AZ, CL>(D, g, lane, in_slot, act_out, out_slot, obs,
+                                hint_lds + __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE) * LB);
   if (lane == 0) {  // selection counters (see k_expand_select): every selected game-wave is one network row
     const GameState s1 = D.gs[g];
     if (s1.active) {
@@ -1007,8 +1258,14 @@ __global__ void __launch_bounds__(256) k_expand_backup(Dev D, const float *__res
                                                        const float *__restrict__ reward_in) {
   const int g = blockIdx.x * 4 + threadIdx.x / WAVE;
   if (g >= D.G) return;
-  if (D.no_hint) expand_backup_game<NJ, false>(D, g, threadIdx.x & (WAVE - 1), logits_in, value_in, reward_in);
-  else expand_backup_game<NJ, true>(D, g, threadIdx.x & (WAVE - 1), logits_in, value_in, reward_in);
+  const int lane = threadIdx.x & (WAVE - 1);
+  if (D.lists) {
+    if (D.no_hint) expand_backup_game<NJ, false, true>(D, g, lane, logits_in, value_in, reward_in);
+    else expand_backup_game<NJ, true, true>(D, g, lane, logits_in, value_in, reward_in);
+  } else {
+    if (D.no_hint) expand_backup_game<NJ, false, false>(D, g, lane, logits_in, value_in, reward_in);
+    else expand_backup_game<NJ, true, false>(D, g, lane, logits_in, value_in, reward_in);
+  }
 }
 
 // expand + backup of wave i, then select of wave i+1, in one launch: every game's tree is owned by
@@ -1019,8 +1276,9 @@ __global__ void __launch_bounds__(256) k_expand_backup(Dev D, const float *__res
 // waves over the CU's 4 SIMDs); 1 when the games outnumber the resident waves, so that a wave whose
 // game finishes early frees its slot for the next game at once instead of its workgroup's slot
 // waiting for the slowest of 4 games (trees differ in depth)
-template <int NJ, bool HINT, bool AZ, int WPB = 4>
-__global__ void __launch_bounds__(64 * WPB, NJ > 4 ? 1 : (HINT ? GMZ_HINT_WPS : 4)) k_expand_select(Dev D, const float *__restrict__ logits_in,
+// The compact-list kernels (CL) hold 128 VGPRs (4 waves per SIMD) with the hint as well.
+template <int NJ, bool HINT, bool AZ, bool CL, int WPB = 4>
+__global__ void __launch_bounds__(64 * WPB, NJ > 4 ? 1 : ((HINT && !CL) ? GMZ_HINT_WPS : 4)) k_expand_select(Dev D, const float *__restrict__ logits_in,
                                                        const float *__restrict__ value_in,
                                                        const float *__restrict__ reward_in,
                                                        int32_t *__restrict__ in_slot, int32_t *__restrict__ act_out,
@@ -1032,13 +1290,14 @@ __global__ void __launch_bounds__(64 * WPB, NJ > 4 ? 1 : (HINT ? GMZ_HINT_WPS : 
 #endif
   TP_STAMP(tk0);
   const int active0 = D.gs[g].active, depth0 = D.gs[g].depth;
-  expand_backup_game<NJ, HINT>(D, g, lane, logits_in, value_in, reward_in);
+  expand_backup_game<NJ, HINT, CL>(D, g, lane, logits_in, value_in, reward_in);
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_s_waitcnt(0);
   TP_STAMP(tk1);
-  __shared__ __attribute__((aligned(16))) uint8_t hint_lds[HINT ? WPB * HintSlot<NJ>::BYTES : 16];
-  select_game<NJ, HINT, AZ>(D, g, lane, in_slot, act_out, out_slot, obs,
-                            hint_lds + (HINT ? __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE) * HintSlot<NJ>::BYTES : 0));
+  constexpr int LB = SelLds<NJ, HINT, CL>::BYTES;
+  __shared__ __attribute__((aligned(16))) uint8_t hint_lds[LB ? WPB * LB : 16];
+  select_game<NJ, HINT, AZ, CL>(D, g, lane, in_slot, act_out, out_slot, obs,
+                                hint_lds + __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE) * LB);
 #ifdef GMZ_TREE_PROF
   __builtin_amdgcn_s_waitcnt(0);
   TP_STAMP(tk2);
@@ -1189,6 +1448,8 @@ GMZ_EXPORT int gmz_engine_create(const gmz_engine_cfg *cfg, gmz_engine **out) {
   if (cfg->num_top_actions < 1 || cfg->num_top_actions > MAX_TOP) return fail("gmz_engine_create: num_top_actions must be in [1, 64]");
   if (cfg->num_simulations < 1) return fail("gmz_engine_create: num_simulations must be >= 1");
   if (cfg->mode != 0 && cfg->mode != 1) return fail("gmz_engine_create: mode must be 0 (AlphaZero) or 1 (MuZero)");
+  if ((cfg->flags & 8) && cfg->num_simulations + 2 > 65535)
+    return fail("gmz_engine_create: compact child lists need num_simulations + 2 <= 65535 (16-bit node ids)");
   gmz_engine *e = new gmz_engine();
   memset(e, 0, sizeof(*e));
   e->cfg = *cfg;
@@ -1204,6 +1465,7 @@ GMZ_EXPORT int gmz_engine_create(const gmz_engine_cfg *cfg, gmz_engine **out) {
   D.c_visit = cfg->c_visit;
   D.mode = cfg->mode;
   D.no_hint = cfg->flags & 1;
+  D.lists = (cfg->flags >> 3) & 1;
   D.game_offset = cfg->game_offset;
   D.c_scale = cfg->c_scale;
   D.disc_f = (float)cfg->discount;
@@ -1219,6 +1481,7 @@ GMZ_EXPORT int gmz_engine_create(const gmz_engine_cfg *cfg, gmz_engine **out) {
   rc |= dalloc(e, &D.ctr, G * 4);
   rc |= dalloc(e, &D.path_u, G * S);
   rc |= dalloc(e, &D.path_a, G * S);
+  rc |= dalloc(e, &D.path_e, G * S);
   rc |= dalloc(e, &D.sel, G * MAX_TOP);
   rc |= dalloc(e, &D.gs, G);
   rc |= dalloc(e, &D.legal, G * NJ);
@@ -1300,40 +1563,41 @@ static inline dim3 wave_grid(const gmz_engine *e) { return dim3((e->D.G + 3) / 4
     GMZ_LAUNCH_CHECK();                                                                                            \
   } while (0)
 
-// launch KERNEL<NJ, HINT, AZ> (the selection kernels: descent prefetch hint compiled in or out, the
-// AlphaZero board replay compiled in or out)
-#define GMZ_SEL_HA(KERNEL, NJV, h_, az_, e, s_, ...)                                                           \
-  do {                                                                                                         \
-    if (h_) {                                                                                                  \
-      if (az_) hipLaunchKernelGGL((KERNEL<NJV, true, true>), wave_grid(e), dim3(256), 0, s_, __VA_ARGS__);     \
-      else hipLaunchKernelGGL((KERNEL<NJV, true, false>), wave_grid(e), dim3(256), 0, s_, __VA_ARGS__);        \
-    } else {                                                                                                   \
-      if (az_) hipLaunchKernelGGL((KERNEL<NJV, false, true>), wave_grid(e), dim3(256), 0, s_, __VA_ARGS__);    \
-      else hipLaunchKernelGGL((KERNEL<NJV, false, false>), wave_grid(e), dim3(256), 0, s_, __VA_ARGS__);       \
-    }                                                                                                          \
-  } while (0)
-#define GMZ_LAUNCH_SEL(KERNEL, e, stream, ...)                                                                 \
-  do {                                                                                                         \
-    const int nj_ = ((e)->D.A + 63) / 64;                                                                      \
-    const bool h_ = !(e)->D.no_hint, az_ = (e)->D.mode == 0;                                                   \
-    hipStream_t s_ = (hipStream_t)(stream);                                                                    \
-    if (nj_ <= 1) GMZ_SEL_HA(KERNEL, 1, h_, az_, e, s_, __VA_ARGS__);                                          \
-    else if (nj_ <= 2) GMZ_SEL_HA(KERNEL, 2, h_, az_, e, s_, __VA_ARGS__);                                     \
-    else if (nj_ <= 4) GMZ_SEL_HA(KERNEL, 4, h_, az_, e, s_, __VA_ARGS__);                                     \
-    else if (nj_ <= 6) GMZ_SEL_HA(KERNEL, 6, h_, az_, e, s_, __VA_ARGS__);                                     \
-    else GMZ_SEL_HA(KERNEL, 8, h_, az_, e, s_, __VA_ARGS__);                                                   \
-    GMZ_LAUNCH_CHECK();                                                                                        \
-  } while (0)
+// k_select<NJ, HINT, AZ, CL> (descent prefetch hint, AlphaZero board replay and compact child lists
+// each compiled in or out)
+template <int NJ, bool H, bool AZ, bool CL>
+static int launch_select(gmz_engine *e, hipStream_t s, int32_t *in_slot, int32_t *action, int32_t *out_slot, float *obs) {
+  hipLaunchKernelGGL((k_select<NJ, H, AZ, CL>), wave_grid(e), dim3(256), 0, s, e->D, in_slot, action, out_slot, obs);
+  GMZ_LAUNCH_CHECK();
+  return 0;
+}
+template <int NJ>
+static int launch_select_nj(gmz_engine *e, hipStream_t s, int32_t *in_slot, int32_t *action, int32_t *out_slot,
+                            float *obs) {
+  const bool h = !e->D.no_hint, az = e->D.mode == 0, cl = e->D.lists != 0;
+#define GMZ_SEL_CASE(H_, AZ_, CL_) \
+  if (h == H_ && az == AZ_ && cl == CL_) return launch_select<NJ, H_, AZ_, CL_>(e, s, in_slot, action, out_slot, obs)
+  GMZ_SEL_CASE(true, true, true);
+  GMZ_SEL_CASE(true, true, false);
+  GMZ_SEL_CASE(true, false, true);
+  GMZ_SEL_CASE(true, false, false);
+  GMZ_SEL_CASE(false, true, true);
+  GMZ_SEL_CASE(false, true, false);
+  GMZ_SEL_CASE(false, false, true);
+  GMZ_SEL_CASE(false, false, false);
+#undef GMZ_SEL_CASE
+  return fail("launch_select: unreachable");
+}
 
-// k_expand_select<NJ, H, AZ, WPB>: WPB = 1 when the games outnumber the variant's resident waves
+// k_expand_select<NJ, H, AZ, CL, WPB>: WPB = 1 when the games outnumber the variant's resident waves
 // (occupancy measured once per engine), else 4
-template <int NJ, bool H, bool AZ>
+template <int NJ, bool H, bool AZ, bool CL>
 static int launch_expand_select(gmz_engine *e, hipStream_t s, const float *logits, const float *value,
                                 const float *reward, int32_t *in_slot, int32_t *action, int32_t *out_slot, float *obs) {
   if (!e->es_waves) {
     int nb = 0, ncu = 0, dev = 0;
     GMZ_HIP(hipGetDevice(&dev));
-    GMZ_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void *)k_expand_select<NJ, H, AZ, 4>, 256, 0));
+    GMZ_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void *)k_expand_select<NJ, H, AZ, CL, 4>, 256, 0));
     GMZ_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
     e->es_waves = (nb > 0 ? nb : 1) * ncu * 4;
   }
@@ -1341,11 +1605,11 @@ static int launch_expand_select(gmz_engine *e, hipStream_t s, const float *logit
   // gmz_engine_cfg.flags bits 1 / 2 force the 4-wave / 1-wave workgroups (parity tests of both variants)
   const int fl = e->cfg.flags;
   if ((fl & 4) || (!(fl & 2) && G > e->es_waves))
-    hipLaunchKernelGGL((k_expand_select<NJ, H, AZ, 1>), dim3(G), dim3(64), 0, s, e->D, logits, value, reward, in_slot,
-                       action, out_slot, obs);
-  else
-    hipLaunchKernelGGL((k_expand_select<NJ, H, AZ, 4>), dim3((G + 3) / 4), dim3(256), 0, s, e->D, logits, value, reward,
+    hipLaunchKernelGGL((k_expand_select<NJ, H, AZ, CL, 1>), dim3(G), dim3(64), 0, s, e->D, logits, value, reward,
                        in_slot, action, out_slot, obs);
+  else
+    hipLaunchKernelGGL((k_expand_select<NJ, H, AZ, CL, 4>), dim3((G + 3) / 4), dim3(256), 0, s, e->D, logits, value,
+                       reward, in_slot, action, out_slot, obs);
   GMZ_LAUNCH_CHECK();
   return 0;
 }
@@ -1353,11 +1617,20 @@ static int launch_expand_select(gmz_engine *e, hipStream_t s, const float *logit
 template <int NJ>
 static int launch_expand_select_nj(gmz_engine *e, hipStream_t s, const float *logits, const float *value,
                                    const float *reward, int32_t *in_slot, int32_t *action, int32_t *out_slot, float *obs) {
-  const bool h = !e->D.no_hint, az = e->D.mode == 0;
-  if (h) return az ? launch_expand_select<NJ, true, true>(e, s, logits, value, reward, in_slot, action, out_slot, obs)
-                   : launch_expand_select<NJ, true, false>(e, s, logits, value, reward, in_slot, action, out_slot, obs);
-  return az ? launch_expand_select<NJ, false, true>(e, s, logits, value, reward, in_slot, action, out_slot, obs)
-            : launch_expand_select<NJ, false, false>(e, s, logits, value, reward, in_slot, action, out_slot, obs);
+  const bool h = !e->D.no_hint, az = e->D.mode == 0, cl = e->D.lists != 0;
+#define GMZ_ES_CASE(H_, AZ_, CL_)        \
+  if (h == H_ && az == AZ_ && cl == CL_) \
+  return launch_expand_select<NJ, H_, AZ_, CL_>(e, s, logits, value, reward, in_slot, action, out_slot, obs)
+  GMZ_ES_CASE(true, true, true);
+  GMZ_ES_CASE(true, true, false);
+  GMZ_ES_CASE(true, false, true);
+  GMZ_ES_CASE(true, false, false);
+  GMZ_ES_CASE(false, true, true);
+  GMZ_ES_CASE(false, true, false);
+  GMZ_ES_CASE(false, false, true);
+  GMZ_ES_CASE(false, false, false);
+#undef GMZ_ES_CASE
+  return fail("launch_expand_select: unreachable");
 }
 
 GMZ_EXPORT int gmz_engine_begin_move(gmz_engine *e, const double *gumbel, uint64_t seed, float *obs, void *stream) {
@@ -1377,8 +1650,13 @@ GMZ_EXPORT int gmz_engine_select(gmz_engine *e, int32_t *in_slot, int32_t *actio
                                  void *stream) {
   if (!e || !in_slot || !action || !out_slot) return fail("gmz_engine_select: null argument");
   if (e->D.mode == 0 && !obs) return fail("gmz_engine_select: AlphaZero mode needs obs");
-  GMZ_LAUNCH_SEL(k_select, e, stream, e->D, in_slot, action, out_slot, obs);
-  return 0;
+  hipStream_t s = (hipStream_t)stream;
+  const int nj = (e->D.A + 63) / 64;
+  if (nj <= 1) return launch_select_nj<1>(e, s, in_slot, action, out_slot, obs);
+  if (nj <= 2) return launch_select_nj<2>(e, s, in_slot, action, out_slot, obs);
+  if (nj <= 4) return launch_select_nj<4>(e, s, in_slot, action, out_slot, obs);
+  if (nj <= 6) return launch_select_nj<6>(e, s, in_slot, action, out_slot, obs);
+  return launch_select_nj<8>(e, s, in_slot, action, out_slot, obs);
 }
 
 GMZ_EXPORT int gmz_engine_expand_backup(gmz_engine *e, const float *logits, const float *value, const float *reward,

@@ -54,7 +54,7 @@ class BatchedSelfPlayEngine:
     """G games per GPU.  ``cfg``: any object with the reference config attribute names."""
 
     def __init__(self, cfg=None, num_games=1, net=None, device="cuda", seed=0, descent_hint=None, game_offset=0,
-                 wpb=None, **overrides):
+                 wpb=None, layout=None, **overrides):
         self.cfg = from_any(cfg, **overrides)
         c = self.cfg
         if c.MCTS_IMPLEMENTATION not in ("AlphaZero", "MuZero"):
@@ -70,8 +70,14 @@ class BatchedSelfPlayEngine:
         if wpb not in (None, 1, 4):
             raise ValueError("wpb: games per workgroup of the fused expand/select kernel must be None, 1 or 4")
         self.descent_hint = bool(descent_hint)
-        # flags (include/gmz.h): bit 0 no hint; bits 1 / 2 force 4-wave / 1-wave workgroups (None: by occupancy)
-        flags = (0 if descent_hint else 1) | {None: 0, 4: 2, 1: 4}[wpb]
+        if layout is None:
+            layout = default_layout(self.G)
+        if layout not in ("dense", "lists"):
+            raise ValueError("layout: 'dense' (every node's full child row) or 'lists' (compact child lists)")
+        self.layout = layout
+        # flags (include/gmz.h): bit 0 no hint; bits 1 / 2 force 4-wave / 1-wave workgroups (None: by occupancy);
+        # bit 3 compact child lists for non-root nodes
+        flags = (0 if descent_hint else 1) | {None: 0, 4: 2, 1: 4}[wpb] | (8 if layout == "lists" else 0)
         self.ecfg = _lib.EngineCfg(self.G, c.BOARD_SIZE, c.N_IN_ROW, c.NUM_SIMULATIONS, c.NUM_TOP_ACTIONS, self.mode,
                                    int(c.C_VISIT), flags, float(c.C_SCALE),
                                    float(c.VALUE_MINMAX_DELTA), float(c.DISCOUNT), int(game_offset))
@@ -273,7 +279,7 @@ class SplitSelfPlayEngine:
     made from the total G, as for one engine.  Calls fork from the caller's stream and join back to it."""
 
     def __init__(self, cfg=None, num_games=2, net=None, device="cuda", seed=0, parts=2, max_grid=None,
-                 descent_hint=None, **overrides):
+                 descent_hint=None, layout=None, **overrides):
         self.cfg = from_any(cfg, **overrides)
         c = self.cfg
         G = int(num_games)
@@ -293,8 +299,10 @@ class SplitSelfPlayEngine:
             net = HashNetBackend(G * self.slots_per_game, self.A, device)
         self.net = net
         nets = net.split(parts, max_grid) if parts > 1 else [net]
-        self.engines = [BatchedSelfPlayEngine(c, g, nets[i], device, seed, descent_hint, game_offset=i * g)
-                        for i in range(parts)]
+        if layout is None:
+            layout = default_layout(G)
+        self.engines = [BatchedSelfPlayEngine(c, g, nets[i], device, seed, descent_hint, game_offset=i * g,
+                                              layout=layout) for i in range(parts)]
         self.streams = [torch.cuda.Stream(self.device) for _ in range(parts)]
         dev = self.device
         self.policy = torch.zeros(G, self.A, dtype=torch.float64, device=dev)
@@ -385,6 +393,12 @@ class SplitSelfPlayEngine:
     def root_stats(self):
         parts = [e.root_stats() for e in self.engines]
         return tuple(torch.cat([p[k] for p in parts]) for k in range(5))
+
+
+def default_layout(num_games):
+    """Tree layout of the non-root nodes: 'dense' (a 16-B edge per action) or 'lists' (compact lists of the
+    visited children, gmz_engine_cfg.flags bit 3).  Both give identical results (tests/test_tree_lists_gpu.py)."""
+    return "dense"
 
 
 def default_streams(cfg, num_games):

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define GMZ_ABI_VERSION 4
+#define GMZ_ABI_VERSION 5
 
 /* ------------------------------------------------------------------ misc */
 const char *gmz_last_error(void);
@@ -81,7 +81,9 @@ typedef struct gmz_engine_cfg {
                                softmax from the logits, the hint kernels from cached exp rows: equal up to a few ulp
                                of the improved policy); bit 1 / bit 2: force the 4-wave / 1-wave
                                workgroups of the fused expand/select kernel (default: 1-wave workgroups once the
-                               games outnumber the variant's resident waves); results identical either way */
+                               games outnumber the variant's resident waves); results identical either way;
+                               bit 3: compact child lists — a non-root node stores only its visited children's
+                               edges (needs num_simulations + 2 <= 65535); results identical to the dense rows */
   double c_scale;           /* config.C_SCALE */
   double minmax_delta;      /* config.VALUE_MINMAX_DELTA */
   double discount;          /* config.DISCOUNT */
@@ -217,8 +219,9 @@ typedef struct gmz_net_weights {
 #define GMZ_NET_BF16 1
 
 /* Scratch needed by gmz_net_initial / gmz_net_recurrent for `rows` rows (caller allocates, ZERO-FILLED
- * once: its first 256 B hold the tower's board-scheduling counters, which every launch leaves zero;
- * a workspace must not be shared by launches that may run concurrently). */
+ * once: its first 8 B hold the tower's board-scheduling ticket word, tagged with each launch's
+ * generation, so no launch depends on how the previous one ended; a workspace must not be shared by
+ * launches that may run concurrently). */
 int gmz_net_workspace_bytes(const gmz_net_weights *w, int rows, size_t *out);
 /* network.py:137-143 initial_inference: obs_dev f32[rows][3][A] -> logits f32[rows][A],
  * value f32[rows] (support_to_scalar), hidden state -> hid_pool_dev[out_slot[r]] (dtype [A][C]).

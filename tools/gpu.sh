@@ -19,8 +19,13 @@ case $CMD in
   tests)  # GPU test suite (optionally -k EXPR)
     K=()
     [ -n "$1" ] && K=(-k "$1")
+    # a heartbeat under gpurun_out/ while pytest runs: single tests (e.g. the fp32 agreement search) can run
+    # for minutes without a result line; pytest's own --timeout and the outer timeout bound any hang
+    ( while sleep 60; do date >> $OUT/heartbeat; done ) &
+    HB=$!
     timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${K[@]}" > $OUT/pytest.log 2>&1
     rc=$?
+    kill $HB
     echo "pytest rc=$rc $(tail -1 $OUT/pytest.log)"
     grep -E "FAILED|^E  |differing searches" $OUT/pytest.log | head -30
     exit $rc ;;
@@ -57,6 +62,16 @@ PY
       echo "== $K"; python3 tools/pmc_summary.py $OUT "$K" fp16 2
     done > $OUT/summary.txt
     cat $OUT/summary.txt ;;
+  layout)  # tree-kernel A/B: dense vs compact child lists, hint on/off, per game count (one stream)
+    for G in ${1:-1024 8192}; do
+      for L in dense lists; do
+        for H in on off; do
+          timeout -k 10 300 python -u bench.py --games $G --streams 1 --steps 3 --warmup 1 --layout $L --hint $H \
+            --single-stream-moves 0 $SP > $OUT/G${G}_${L}_${H}.json 2> $OUT/G${G}_${L}_${H}.err || { echo "G=$G $L $H failed"; tail -5 $OUT/G${G}_${L}_${H}.err; exit 1; }
+          python3 -c "import json,sys; d=json.load(open(sys.argv[1])); t=d['roofline_tree']; print('G=%5d %-5s hint=%-3s moves/s %8.0f  tree %7.1f us  %6.0f GB/s  frac %.3f  levels %.1f' % (d['config']['games_per_gpu'], t['layout'], sys.argv[2], d['value'], t['mean_launch_ms']*1e3, t['achieved'], t['frac'], t['mean_select_levels']))" $OUT/G${G}_${L}_${H}.json $H | tee -a $OUT/summary.txt
+        done
+      done
+    done ;;
   *)
     echo "usage: tools/gpu.sh tests|smoke|bench|trace|pmc TAG [args]"; exit 2 ;;
 esac

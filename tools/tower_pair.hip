@@ -41,7 +41,7 @@ __global__ void __launch_bounds__(512) k_tower_pair(TowerArgs t) {
   float *sbias = (float *)(smem + NB * IMG);
   float *saction = sbias + 2 * C;
   __shared__ int s_row[2];
-  int *tk = t.tickets;
+  int *tk = (int *)t.tickets;  // its own {next row, done} pair (k_tower3 uses a generation-tagged word)
 
   auto fetch_rows = [&]() {  // thread 0: the next two active rows (-1: none)
     int got[2] = {-1, -1}, n = 0;

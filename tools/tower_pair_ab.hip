@@ -19,9 +19,14 @@ int fail(const std::string &m) { fprintf(stderr, "%s\n", m.c_str()); return -1; 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
 
 template <bool DYN, int V>
-static void launch(const TowerArgs &a, int grid) {
+static void launch(const TowerArgs &a0, int grid) {
+  TowerArgs a = a0;
+  a.gen = next_gen();  // k_tower3's ticket generation (one per launch)
   if (V == 0) hipLaunchKernelGGL((k_tower3<15, DYN, 0, 3, 4, 2, 1, F16>), dim3(grid), dim3(512), 0, 0, a);
-  else hipLaunchKernelGGL((k_tower_pair<15, DYN, 0, 4, F16>), dim3(grid), dim3(512), 0, 0, a);
+  else {
+    (void)hipMemsetAsync(a.tickets, 0, 8, 0);  // k_tower_pair counts from 0 (a k_tower3 launch leaves its generation)
+    hipLaunchKernelGGL((k_tower_pair<15, DYN, 0, 4, F16>), dim3(grid), dim3(512), 0, 0, a);
+  }
 }
 
 template <bool DYN, int V>
@@ -54,7 +59,7 @@ int main(int argc, char **argv) {
   std::vector<int> in_slot(rows), out_slot(rows), action(rows);
   for (int r = 0; r < rows; ++r) { in_slot[r] = r; out_slot[r] = rows + r; action[r] = (r * 37) % A; }
   out_slot[rows / 3] = -1;  // one skipped row
-  uint16_t *dw, *dpool, *dstem, *dxres; float *dbias, *dact, *dhw, *dhb, *dpv, *dstemb, *dobs; int *din, *dout, *dac, *dtk;
+  uint16_t *dw, *dpool, *dstem, *dxres; float *dbias, *dact, *dhw, *dhb, *dpv, *dstemb, *dobs; int *din, *dout, *dac; unsigned long long *dtk;
   CK(hipMalloc(&dw, w.size() * 2)); CK(hipMalloc(&dpool, pool.size() * 2)); CK(hipMalloc(&dstem, stem.size() * 2));
   CK(hipMalloc(&dbias, bias.size() * 4)); CK(hipMalloc(&dact, act.size() * 4)); CK(hipMalloc(&dhw, hw.size() * 4));
   CK(hipMalloc(&dhb, 16)); CK(hipMalloc(&dpv, (size_t)rows * pv_stride(A) * 4)); CK(hipMalloc(&dstemb, 512));
