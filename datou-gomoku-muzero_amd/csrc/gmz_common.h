@@ -114,6 +114,7 @@ __device__ __forceinline__ float readlane_f(float v, int l) { return __int_as_fl
 
 __device__ __forceinline__ int op_max_i(int a, int b) { return a > b ? a : b; }
 __device__ __forceinline__ int op_sum_i(int a, int b) { return a + b; }
+__device__ __forceinline__ int op_min_i(int a, int b) { return a < b ? a : b; }
 __device__ __forceinline__ double op_max_d(double a, double b) { return fmax(a, b); }
 __device__ __forceinline__ double op_sum_d(double a, double b) { return a + b; }
 __device__ __forceinline__ float op_max_f(float a, float b) { return fmaxf(a, b); }
@@ -121,12 +122,39 @@ __device__ __forceinline__ float op_min_f(float a, float b) { return fminf(a, b)
 __device__ __forceinline__ float op_sum_f(float a, float b) { return a + b; }
 
 __device__ __forceinline__ int dred_max_i(int v) { GMZ_DPP_REDUCE(int, v, op_max_i, dpp_i, __builtin_amdgcn_readlane); return v; }
+__device__ __forceinline__ int dred_min_i(int v) { GMZ_DPP_REDUCE(int, v, op_min_i, dpp_i, __builtin_amdgcn_readlane); return v; }
 __device__ __forceinline__ int dred_sum_i(int v) { GMZ_DPP_REDUCE(int, v, op_sum_i, dpp_i, __builtin_amdgcn_readlane); return v; }
 __device__ __forceinline__ double dred_max_d(double v) { GMZ_DPP_REDUCE(double, v, op_max_d, dpp_d, readlane_d); return v; }
 __device__ __forceinline__ double dred_sum_d(double v) { GMZ_DPP_REDUCE(double, v, op_sum_d, dpp_d, readlane_d); return v; }
 __device__ __forceinline__ float dred_max_f(float v) { GMZ_DPP_REDUCE(float, v, op_max_f, dpp_f, readlane_f); return v; }
 __device__ __forceinline__ float dred_min_f(float v) { GMZ_DPP_REDUCE(float, v, op_min_f, dpp_f, readlane_f); return v; }
 __device__ __forceinline__ float dred_sum_f(float v) { GMZ_DPP_REDUCE(float, v, op_sum_f, dpp_f, readlane_f); return v; }
+
+// (max v, then the lowest a among equal v) over the wave in one DPP reduction (np.argmax's first index
+// when every lane holds its own best (v, a)); v must not be NaN.  Result wave-uniform.
+template <int CTRL>
+__device__ __forceinline__ void argmax_step(double &v, int &a) {
+  const double ov = dpp_d<CTRL>(v);
+  const int oa = dpp_i<CTRL>(a);
+  if (ov > v || (ov == v && oa < a)) { v = ov; a = oa; }
+}
+__device__ __forceinline__ void dred_argmax_first(double &v, int &a) {
+  argmax_step<DPP_QXOR1>(v, a);
+  argmax_step<DPP_QXOR2>(v, a);
+  argmax_step<DPP_HALF_MIRROR>(v, a);
+  argmax_step<DPP_MIRROR>(v, a);
+  // the four rows are uniform now: combine them on row order (lanes 0, 16, 32, 48)
+  double bv = readlane_d(v, 0);
+  int ba = __builtin_amdgcn_readlane(a, 0);
+#pragma unroll
+  for (int r = 16; r < 64; r += 16) {
+    const double ov = readlane_d(v, r);
+    const int oa = __builtin_amdgcn_readlane(a, r);
+    if (ov > bv || (ov == bv && oa < ba)) { bv = ov; ba = oa; }
+  }
+  v = bv;
+  a = ba;
+}
 
 __host__ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
   x ^= x >> 16; x *= 0x7FEB352Du; x ^= x >> 15; x *= 0x846CA68Bu; x ^= x >> 16;

@@ -62,9 +62,9 @@ struct TowerArgs {
   int rows;
   uint16_t *xres;          // single-image boards (19x19): per-workgroup residual scratch (k_tower3)
   int max_grid;            // cap on the persistent grid (gmz_net_weights.max_grid; 0 = every CU)
-  unsigned long long *tickets;  // k_tower3 board scheduling (one board per workgroup): {generation << 32 |
+  unsigned long long *tickets;  // k_tower3 board scheduling (one board per workgroup): {generation << 24 |
                                 // next row}, 8 B at the workspace head (see fetch_row)
-  uint32_t gen;                 // this launch's generation (unique per launch, never 0)
+  unsigned long long gen;       // this launch's generation (< 2^40, larger than every earlier launch's)
 };
 
 // MFMA operand element types of the towers and the reward GEMM (f32 accumulation either way).
@@ -199,19 +199,22 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
   // one board per workgroup (15x15, 19x19): boards are handed out in ticket order as workgroups
   // become free (thread 0 takes the next active row), so a workgroup that starts late — its CU still
   // held by the other stream's tower — takes fewer boards instead of delaying the whole launch by its
-  // static share.  The ticket word carries the launch's generation in its high half: a workgroup that
-  // draws a word of another generation (the previous launch's, whatever state it was left in) starts
-  // this generation with a compare-and-swap (ticket 0) or, if another workgroup already did, draws
-  // again — so no launch has to reset the counter and none can inherit a stale one.
+  // static share.  The ticket word is {generation: 40 bits, next row: 24 bits}; every launch has a new,
+  // larger generation (next_gen), so a workgroup that draws an older launch's word (whatever state that
+  // launch left it in) raises it to {this generation, 0} with atomicMax and draws again: no launch
+  // resets the counter, none inherits a stale one, and no compare-and-swap can be starved by the
+  // other workgroups' draws.
   __shared__ int s_row;
   unsigned long long *tk = t.tickets;
   const bool dsched = NB == 1 && tk != nullptr;
   auto ticket = [&]() -> int {
     for (;;) {
       const unsigned long long old = atomicAdd(tk, 1ull);
-      if ((uint32_t)(old >> 32) == t.gen) return (int)(uint32_t)old;
-      const unsigned long long cur = old + 1ull;
-      if (atomicCAS(tk, cur, ((unsigned long long)t.gen << 32) | 1ull) == cur) return 0;
+      if ((old >> 24) == t.gen) return (int)(old & 0xFFFFFFull);
+      // an older launch's word: start this generation at ticket 0 (generations only grow, so every
+      // workgroup that drew a stale word installs the same value and the first one wins; a draw made
+      // after that sees this generation)
+      atomicMax(tk, t.gen << 24);
     }
   };
   auto fetch_row = [&]() {
@@ -788,13 +791,10 @@ static size_t xres_bytes(int H) {
   }
 }
 
-// tower launch generations (k_tower3's ticket word): unique per launch across every workspace, never 0
-static std::atomic<uint32_t> g_tower_gen{0};
-static uint32_t next_gen() {
-  uint32_t g;
-  do g = ++g_tower_gen; while (g == 0);
-  return g;
-}
+// tower launch generations (k_tower3's ticket word): increasing across every launch of the process, from 1
+// (a zero-filled workspace holds generation 0); 2^40 launches at 10^4 per second last three years
+static std::atomic<unsigned long long> g_tower_gen{0};
+static unsigned long long next_gen() { return ++g_tower_gen; }
 
 template <int H, bool DYN, typename E>
 static int launch_tower(const TowerArgs &a, hipStream_t s) {
@@ -822,6 +822,7 @@ static int tower_e(int H, bool dyn, const TowerArgs &a, hipStream_t s) {
 static int tower(const gmz_net_weights *w, bool dyn, const TowerArgs &a0, hipStream_t s) {
   TowerArgs a = a0;
   a.max_grid = w->max_grid;
+  if (a.rows >= (1 << 24)) return fail("gmz_net: rows must be < 2^24 (24-bit tower tickets)");
   a.gen = next_gen();
   return w->dtype == GMZ_NET_BF16 ? tower_e<Bf16>(w->board_size, dyn, a, s) : tower_e<F16>(w->board_size, dyn, a, s);
 }

@@ -21,7 +21,7 @@
 //   int path_u/path_a/path_e[G][S], node_parent/node_action[G][S]
 //   With compact child lists (gmz_engine_cfg.flags bit 3) a NON-ROOT node's edge row holds only its
 //   visited children, as entries {action << 16 | child, N, W, R} in first-visit order at the row's
-//   head (the root keeps the dense row); see ListSlot below.
+//   head (the root keeps the dense row); see ListBuf below.
 //   int4 hdr[G][S]        per-node header {sum of child N, max child N, visited children, next-visit
 //                         hint}: maintained by the backup so that a selection step needs no integer
 //                         wave reductions; the hint is the predicted choice of the node's next visit
@@ -75,7 +75,7 @@ struct Dev {
   int G, A, A2, S, size, n_sims, m_top, c_visit, mode;
   int game_offset;  // gmz_engine_cfg.game_offset: global index of game 0 (device Gumbel noise)
   int no_hint;  // gmz_engine_cfg.flags bit 0: descent prefetch hint off (timing A/B; results identical)
-  int lists;    // gmz_engine_cfg.flags bit 3: compact child lists for non-root nodes (see ListSlot)
+  int lists;    // gmz_engine_cfg.flags bit 3: compact child lists for non-root nodes (see ListBuf)
   double c_scale;
   float disc_f, delta_f;
 };
@@ -84,6 +84,10 @@ struct Dev {
 // spills) at 1,024 games per engine (36.4 vs 46.9 us, profiles/r02_tree_expl_variants.txt)
 #ifndef GMZ_HINT_WPS
 #define GMZ_HINT_WPS 2
+#endif
+// waves per SIMD of the compact-list kernel without the prefetch
+#ifndef GMZ_CL_WPS
+#define GMZ_CL_WPS 5
 #endif
 #ifdef GMZ_TREE_PROF
 // phase-cycle instrumentation (tools/tree_prof.py builds a separate library with -DGMZ_TREE_PROF)
@@ -525,50 +529,41 @@ __device__ int select_nonroot(const Dev &D, const uint64_t (&lg)[NJ], int g, int
 
 // _select_action at the root (mcts.py:96-104): first least-visited entry of the selected list.
 __device__ int select_root(const Dev &D, int g, int lane, int n_sel, int *child, int *nchild) {
-  int v = 0x7fffffff, i = 64 + lane, a = -1, c = -1;
+  // (min N, then the first list position) as one integer key N << 7 | position (N < 2^24: gmz_engine_create)
+  int key = 0x7fffffff, a = -1, c = -1;
   if (lane < n_sel) {
     a = D.sel[g * MAX_TOP + lane];
     const Edge e = edge_row(D, g, 0)[a];
-    v = e.n;
+    key = (e.n << 7) | lane;
     c = e.child;
-    i = lane;
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    int ov = __shfl_xor(v, o, 64), oi = __shfl_xor(i, o, 64), oa = __shfl_xor(a, o, 64), oc = __shfl_xor(c, o, 64);
-    if (ov < v || (ov == v && oi < i)) { v = ov; i = oi; a = oa; c = oc; }
-  }
-  *child = c;
-  *nchild = v;  // the chosen edge's N
-  return a;
+  key = dred_min_i(key);
+  const int i = key & 127;
+  *child = __builtin_amdgcn_readlane(c, i);
+  *nchild = key >> 7;  // the chosen edge's N
+  return __builtin_amdgcn_readlane(a, i);
 }
 
 // ------------------------------------------------------------------------------------------
 // Compact child lists (gmz_engine_cfg.flags bit 3).  A non-root node keeps the edges of
 // its VISITED children only: entries {action << 16 | child, N, W, R} in first-visit order at the head
 // of its edge row; the root keeps the dense row (root selection, halving and finish read it).  A
-// selection level then reads the node's header, its exp row (EX: the hint kernels) or logits and its
-// nvis entries, not the 16 B x A dense row; the entry lanes scatter their children's x (EX: E scaled
-// by exp(t - t0)) or normalised Q, and N, into a per-wave LDS view of the node in action order, and
-// from there on the arithmetic is the dense kernels' on the same values in the same order: results
-// bit-identical to the dense layout's (tests/test_tree_lists_gpu.py).
-// Per-wave LDS block: the DMA'd row (prefetched or fetched now) + the scatter view.
-template <int NJ, bool EX>
-struct ListSlot {
-  static constexpr int ROW = 0;                                         // E row (A2 f64) or logits (A f32)
-  static constexpr int ROWB = EX ? ((NJ + 1) / 2) * 1024 : NJ * 256;
-  static constexpr int ENT = ROWB;                                      // entries 0..63, 16 B each
-  static constexpr int HDR = ENT + 1024;                                // the node header
-  static constexpr int XS = HDR + 16;                                   // f64 per action: x (EX) or nq
-  static constexpr int NS = XS + NJ * 512;                              // int per action: N
-  static constexpr int CS = NS + NJ * 256;                              // int per action: entry << 16 | child
-  static constexpr int BYTES = CS + NJ * 256;
-};
-template <int NJ, bool EX>
-struct ListRegs {
-  typename std::conditional<EX, double, float>::type v[NJ];  // the row, lane's actions a = lane + 64 j
-  int4 ent;  // entry `lane` (valid for lane < min(nvis, entries DMA'd))
-  int4 hdr;
+// selection level reads the node's header, its cached exp row E (written at expansion, as for the
+// dense hint kernels) and its nvis entries instead of the 16 B x A dense row, all DMA'd into a per-wave
+// LDS buffer.  The entry lanes overwrite their children's E in that buffer by -x, x = E * exp(t - t0)
+// (the sign bit marks a visited child; E >= +0), and the selection then runs on the buffer in place:
+// the softmax sum over the slots in the dense kernels' order, the unvisited children's scores at their
+// slot lanes, the visited children's at their entry lanes — the dense hint kernels' arithmetic on the
+// same values in the same order, so results are bit-identical to the dense layout with cached exp rows
+// (tests/test_tree_lists_gpu.py).  Nothing of a row is held in registers: 8 waves per SIMD without the
+// prefetch (one buffer per wave), and with it (PF) the hinted child's row is DMA'd into the wave's
+// second buffer while this level computes.
+template <int NJ>
+struct ListBuf {
+  static constexpr int ROW = 0;                      // E row, A2 f64 (natural action order)
+  static constexpr int ENT = ((NJ + 1) / 2) * 1024;  // entries 0..63, 16 B each
+  static constexpr int HDR = ENT + 1024;             // the node header
+  static constexpr int BYTES = HDR + 16;
 };
 // entries worth DMA-ing for a child reached through an edge of visit count n: a node is expanded by
 // its first visit and gains at most one visited child per later visit, so nvis <= n - 1
@@ -577,190 +572,245 @@ __device__ __forceinline__ int list_bound(const Dev &D, int n) {
   const int b = n - 1;
   return b < 0 ? 0 : (b > cap ? cap : b);
 }
-template <int NJ, bool EX>
-__device__ __forceinline__ void list_fetch_lds(const Dev &D, int g, int u, int nent, int lane, uint8_t *blk) {
-  using L = ListSlot<NJ, EX>;
+template <int NJ>
+__device__ __forceinline__ void list_fetch_lds(const Dev &D, int g, int u, int nent, int lane, uint8_t *buf) {
+  using L = ListBuf<NJ>;
   int ln = lane;
   asm volatile("" : "+v"(ln));
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the block have returned
-  if constexpr (EX) {
-    const char *xr = (const char *)expl_row(D, g, u);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the buffer have returned
+  const char *xr = (const char *)expl_row(D, g, u);
 #pragma unroll
-    for (int i = 0; i < (NJ + 1) / 2; ++i) {
-      const int a = 2 * WAVE * i + 2 * ln, ac = a < D.A2 - 2 ? a : D.A2 - 2;
-      __builtin_amdgcn_global_load_lds((const void *)(xr + (uint32_t)(ac * 8)),
-                                       (__attribute__((address_space(3))) void *)(blk + L::ROW + i * 1024), 16, 0, 0);
-    }
-  } else {
-    const float *lr = D.logits + ((size_t)g * D.S + u) * D.A;
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int a = ln + WAVE * j, ac = a < D.A ? a : D.A - 1;
-      __builtin_amdgcn_global_load_lds((const void *)(lr + ac),
-                                       (__attribute__((address_space(3))) void *)(blk + L::ROW + j * 256), 4, 0, 0);
-    }
+  for (int i = 0; i < (NJ + 1) / 2; ++i) {
+    const int a = 2 * WAVE * i + 2 * ln, ac = a < D.A2 - 2 ? a : D.A2 - 2;
+    __builtin_amdgcn_global_load_lds((const void *)(xr + (uint32_t)(ac * 8)),
+                                     (__attribute__((address_space(3))) void *)(buf + L::ROW + i * 1024), 16, 0, 0);
   }
   if (ln < nent)
     __builtin_amdgcn_global_load_lds((const void *)((const char *)edge_row(D, g, u) + (uint32_t)(ln * 16)),
-                                     (__attribute__((address_space(3))) void *)(blk + L::ENT), 16, 0, 0);
+                                     (__attribute__((address_space(3))) void *)(buf + L::ENT), 16, 0, 0);
   if (lane < 4)
     __builtin_amdgcn_global_load_lds((const void *)((const int *)(D.hdr + (size_t)g * D.S + u) + lane),
-                                     (__attribute__((address_space(3))) void *)(blk + L::HDR), 4, 0, 0);
+                                     (__attribute__((address_space(3))) void *)(buf + L::HDR), 4, 0, 0);
 }
-template <int NJ, bool EX>
-__device__ __forceinline__ void list_from_lds(const uint8_t *blk, int lane, ListRegs<NJ, EX> &r) {
-  using L = ListSlot<NJ, EX>;
-  using T = typename std::conditional<EX, double, float>::type;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA has landed
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) r.v[j] = *(const T *)(blk + L::ROW + (lane + WAVE * j) * (int)sizeof(T));
-  r.ent = *(const int4 *)(blk + L::ENT + lane * 16);
-  r.hdr = *(const int4 *)(blk + L::HDR);
+// entry i of node u: from the buffer (i < nent, DMA'd) or from HBM
+__device__ __forceinline__ int4 list_entry(const Dev &D, int g, int u, int i, int nent, const uint8_t *buf, int ent_off) {
+  if (i < nent && i < WAVE) return *(const int4 *)(buf + ent_off + i * 16);
+  return *(const int4 *)(edge_row(D, g, u) + i);
 }
 
-// _select_action at a non-root node (mcts.py:106-117) on a compact child list (`cur`, DMA'd through
-// the wave's block: `nent` entries in LDS, the rest read here).  Same decisions and arithmetic as
-// select_nonroot<NJ, EX> on the dense row.  Returns the action; *child / *nchild / *entry = the chosen
-// child's node id (-1: a new leaf), its edge N (0) and list entry (nvis: appended by the backup).
-// EX (the hint kernels): while this level computes, the row of the child chosen at this node's last
-// visit (hdr.w, a node id) is prefetched into the block (*nxt_u, *nxt_nent); hdr.w is then set to this
-// visit's child (leaf_next for a new leaf: the node the expansion will create).
-template <int NJ, bool EX>
-__device__ int select_nonroot_cl(const Dev &D, const uint64_t (&lg)[NJ], int g, int u, int lane, const NormQ &nz,
-                                 const ListRegs<NJ, EX> &cur, int nent, int leaf_next, uint8_t *blk, int *child,
+// _select_action at a non-root node (mcts.py:106-117) on its compact child list in LDS buffer `buf`
+// (`nent` entries DMA'd, the rest read from HBM).  Returns the action; *child / *nchild / *entry = the
+// chosen child's node id (-1: a new leaf), its edge N (0) and list entry (nvis: appended by the
+// backup).  PF: the row of the child chosen at this node's last visit (hdr.w, a node id) is DMA'd into
+// `nxt_buf` while this level computes (*nxt_u, *nxt_nent), and hdr.w is set to this visit's child
+// (leaf_next for a new leaf: the node the expansion will create).
+// lm: the lane's legal slots (bit j: action lane + 64 j is in the root legal set), from legal_slots
+template <int NJ>
+__device__ __forceinline__ int legal_slots(const Dev &D, const uint64_t (&lg)[NJ], int lane) {
+  int m = 0;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+    if (lane + WAVE * j < D.A && ((lg[j] >> lane) & 1ull)) m |= 1 << j;
+  return m;
+}
+template <int NJ, bool PF>
+__device__ int select_nonroot_cl(const Dev &D, const uint64_t (&lg)[NJ], int lm, int g, int u, int lane,
+                                 const NormQ &nz, int nent, int leaf_next, uint8_t *buf, uint8_t *nxt_buf, int *child,
                                  int *nchild, int *entry, int *nxt_u, int *nxt_nent) {
-  using L = ListSlot<NJ, EX>;
-  const int tot = __builtin_amdgcn_readfirstlane(cur.hdr.x);
-  const int max_n = __builtin_amdgcn_readfirstlane(cur.hdr.y);
-  const int nvis = __builtin_amdgcn_readfirstlane(cur.hdr.z);
-  const int hint = __builtin_amdgcn_readfirstlane(cur.hdr.w);
+  using L = ListBuf<NJ>;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA has landed
+  const int4 hdr = *(const int4 *)(buf + L::HDR);
+  const int tot = __builtin_amdgcn_readfirstlane(hdr.x);
+  const int max_n = __builtin_amdgcn_readfirstlane(hdr.y);
+  const int nvis = __builtin_amdgcn_readfirstlane(hdr.z);
+  const int hint = __builtin_amdgcn_readfirstlane(hdr.w);
+  // entry `lane` (valid below nvis): DMA'd below nent, else read now (a bound that missed; rare)
+  int4 e0 = *(const int4 *)(buf + L::ENT + lane * 16);
+  if (lane >= nent && lane < nvis) e0 = *(const int4 *)(edge_row(D, g, u) + lane);
   *nxt_u = -1;
-  if (EX && hint > 0 && hint < D.S) {
-    const uint64_t hm = __ballot(lane < nvis && lane < nent && (cur.ent.x & 0xffff) == hint);
-    const int nb = hm ? list_bound(D, __builtin_amdgcn_readlane(cur.ent.y, __builtin_ctzll(hm))) : list_bound(D, WAVE + 1);
-    list_fetch_lds<NJ, EX>(D, g, hint, nb, lane, blk);
+  if (PF && hint > 0 && hint < D.S) {
+    const uint64_t hm = __ballot(lane < nvis && lane < nent && (e0.x & 0xffff) == hint);
+    const int nb = hm ? list_bound(D, __builtin_amdgcn_readlane(e0.y, __builtin_ctzll(hm))) : list_bound(D, WAVE + 1);
+    list_fetch_lds<NJ>(D, g, hint, nb, lane, nxt_buf);
     *nxt_u = hint;
     *nxt_nent = nb;
   }
-  double *X = (double *)(blk + L::XS);
-  float *QF = (float *)(blk + L::XS);
-  int *NN = (int *)(blk + L::NS), *CI = (int *)(blk + L::CS);
-  const bool allv = nvis >= D.A;  // every child visited: the float32 rule below (improved_policy)
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int a = lane + WAVE * j;
-    X[a] = EX ? (double)cur.v[j] : nz.nq0;
-    NN[a] = 0;
-  }
-  asm volatile("" ::: "memory");
+  double *R = (double *)(buf + L::ROW);
   const double scale = (double)(D.c_visit + max_n) * D.c_scale;
   const double t0 = scale * nz.nq0;
-  const Edge *row = edge_row(D, g, u);
+  int a = 0;
+#ifdef GMZ_EXP_NOALLV
+  if (false) {
+#else
+  if (nvis >= D.A) {
+#endif
+    // every child visited (rare below the root): the reference's array may be float32 -> improved_policy's
+    // rule (transformed_q's float32/float64 choice, then the softmax) on N and q gathered into the
+    // buffer's row, computed slot by slot in passes that recompute the same values (no row in registers)
+    int2 *NQ = (int2 *)R;
+    for (int i0 = 0; i0 < nvis; i0 += WAVE) {
+      const int i = i0 + lane;
+      if (i < nvis) {
+        const int4 e = list_entry(D, g, u, i, nent, buf, L::ENT);
+        const float v = __int_as_float(e.z) / (float)e.y;
+        const float dv = D.disc_f * v;
+        NQ[e.x >> 16] = make_int2(e.y, __float_as_int(__int_as_float(e.w) + dv));
+      }
+    }
+    asm volatile("" ::: "memory");
+    const float *lrow = D.logits + ((size_t)g * D.S + u) * D.A;
+    // transformed_q, every child visited: normalised q in float32; a clamp (or no range) promotes to float64
+    auto nf_of = [&](int aa, int &clamped) -> float {
+      float x = 0.f;
+      if (nz.have_range && aa < D.A) {
+        x = (__int_as_float(NQ[aa].y) - nz.mm_min) / nz.den_f;
+        if (!(x < 1.0f)) { x = 1.0f; clamped = 1; }
+        if (!(x > 0.0f)) { x = 0.0f; clamped = 1; }
+      }
+      return x;
+    };
+    int promote = nz.have_range ? 0 : 1;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) (void)nf_of(lane + WAVE * j, promote);
+    promote = __ballot(promote != 0) != 0ull;
+    asm volatile("" ::: "memory");  // (each pass reloads its slot values: no row held in registers)
+    // x_j of the softmax (legal), -inf otherwise; float64 or float32 as the reference's array
+    auto x64 = [&](int j) -> double {
+      const int aa = lane + WAVE * j;
+      int dummy = 0;
+      const double t = scale * (double)nf_of(aa, dummy);
+      return (aa < D.A && ((lg[j] >> lane) & 1ull)) ? (double)lrow[aa < D.A ? aa : D.A - 1] + t : -INFINITY;
+    };
+    const float sf = (float)scale;
+    auto x32 = [&](int j) -> float {
+      const int aa = lane + WAVE * j;
+      int dummy = 0;
+      const float t = sf * nf_of(aa, dummy);
+      return (aa < D.A && ((lg[j] >> lane) & 1ull)) ? lrow[aa < D.A ? aa : D.A - 1] + t : -INFINITY;
+    };
+    double m64 = -INFINITY, s64 = 0.0;
+    float m32 = -INFINITY, s32 = 0.f;
+    if (promote) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) m64 = fmax(m64, x64(j));
+      m64 = dred_max_d(m64);
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const double x = x64(j);
+        s64 += (x == -INFINITY) ? 0.0 : exp(x - m64);
+      }
+      s64 = dred_sum_d(s64);
+    } else {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) m32 = fmaxf(m32, x32(j));
+      m32 = dred_max_f(m32);
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const float x = x32(j);
+        s32 += (x == -INFINITY) ? 0.f : expf(x - m32);
+      }
+      s32 = dred_sum_f(s32);
+    }
+    const double inv_s = 1.0 / s64;
+    const double inv_tot = 1.0 / (double)(1 + tot);
+    auto score = [&](int j) -> double {  // p - N / (1 + sum N) over the legal set
+      const int aa = lane + WAVE * j;
+      if (!(aa < D.A && ((lg[j] >> lane) & 1ull))) return -INFINITY;
+      double p;
+      if (promote) {
+        const double x = x64(j);
+        p = ((x == -INFINITY) ? 0.0 : exp(x - m64)) * inv_s;
+      } else {
+        const float x = x32(j);
+        p = (double)(((x == -INFINITY) ? 0.f : expf(x - m32)) / s32);
+      }
+      return p - (double)NQ[aa].x * inv_tot;
+    };
+    asm volatile("" ::: "memory");
+    double best = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) best = fmax(best, score(j));
+    best = dred_max_d(best);
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int j = NJ - 1; j >= 0; --j) {
+      const uint64_t mk = __ballot(score(j) == best && best != -INFINITY);
+      if (mk) a = WAVE * j + __builtin_ctzll(mk);
+    }
+  } else {
+    // visited children: R[a] = -(E * exp(scale * nq - t0)) (select_nonroot's cached-exp softmax term);
+    // entries past the first 64 (rare) are read from HBM in each pass
+    auto scatter = [&](const int4 &e) {
+      const int aa = e.x >> 16;
+      double x = R[aa];
+      if (nz.have_range) {
+        const float v = __int_as_float(e.z) / (float)e.y;  // get_qsa (mcts.py:35-38)
+        const float dv = D.disc_f * v;
+        const float q = __int_as_float(e.w) + dv;
+        double y = ((double)q - (double)nz.mm_min) / (double)nz.den_f;
+        y = (y < 1.0) ? y : 1.0;
+        const double nq = (y > 0.0) ? y : 0.0;
+        x *= exp(scale * nq - t0);
+      }
+      R[aa] = -x;
+    };
+    if (lane < nvis) scatter(e0);
+    for (int i0 = WAVE; i0 < nvis; i0 += WAVE)
+      if (i0 + lane < nvis) scatter(*(const int4 *)(edge_row(D, g, u) + i0 + lane));
+    asm volatile("" ::: "memory");
+    // the node's slots in registers (negative: visited); the softmax sum over the legal slots in
+    // select_nonroot's order (per lane j = 0..NJ-1, then the wave)
+    double xs[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) xs[j] = R[lane + WAVE * j];
+    double sum = 0.0;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) sum += ((lm >> j) & 1) ? fabs(xs[j]) : 0.0;
+    sum = dred_sum_d(sum);
+    const double inv_s = 1.0 / sum;
+    const double inv_tot = 1.0 / (double)(1 + tot);
+    // scores p - N / (1 + sum N): unvisited children (N = 0: p - 0 * inv_tot == p) at their slot lanes,
+    // visited ones at their entry lanes; np.argmax = (max score, then the lowest action) in one reduction
+    auto vscore = [&](const int4 &e) { return fabs(R[e.x >> 16]) * inv_s - (double)e.y * inv_tot; };
+    double bv = -INFINITY;
+    int ba = 1 << 30;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {  // ascending actions: strict > keeps the lowest of equal scores
+      const double sc = xs[j] * inv_s;
+      if (((lm >> j) & 1) && !signbit(xs[j]) && sc > bv) { bv = sc; ba = lane + WAVE * j; }
+    }
+    auto offer = [&](const int4 &e) {
+      const double sc = vscore(e);
+      const int aa = e.x >> 16;
+      if (sc > bv || (sc == bv && aa < ba)) { bv = sc; ba = aa; }
+    };
+    if (lane < nvis) offer(e0);
+    for (int i0 = WAVE; i0 < nvis; i0 += WAVE)
+      if (i0 + lane < nvis) offer(*(const int4 *)(edge_row(D, g, u) + i0 + lane));
+    dred_argmax_first(bv, ba);
+    a = (bv == -INFINITY || ba >= D.A) ? 0 : ba;
+  }
+  // the chosen child: its entry (visited) or a new leaf
+  int c = -1, en = nvis, na = 0;
   for (int i0 = 0; i0 < nvis; i0 += WAVE) {
     const int i = i0 + lane;
-    int4 e = cur.ent;
-    if ((i0 > 0 || lane >= nent) && i < nvis) e = *(const int4 *)(row + i);
-    if (i < nvis) {
-      const int a = e.x >> 16, n = e.y;
-      const float v = __int_as_float(e.z) / (float)n;  // get_qsa (mcts.py:35-38), as select_nonroot
-      const float dv = D.disc_f * v;
-      const float q = __int_as_float(e.w) + dv;
-      if (allv) {
-        QF[a] = q;
-      } else {
-        double nq = nz.nq0;
-        if (nz.have_range) {
-          double y = ((double)q - (double)nz.mm_min) / (double)nz.den_f;
-          y = (y < 1.0) ? y : 1.0;
-          nq = (y > 0.0) ? y : 0.0;
-        }
-        if (EX) {
-          double x = X[a];
-          if (nz.have_range) x *= exp(scale * nq - t0);
-          X[a] = x;
-        } else {
-          X[a] = nq;
-        }
-      }
-      NN[a] = n;
-      CI[a] = (i << 16) | (e.x & 0xffff);
+    int4 e = e0;
+    if (i0 > 0 && i < nvis) e = *(const int4 *)(edge_row(D, g, u) + i);
+    const uint64_t m = __ballot(i < nvis && (e.x >> 16) == a);
+    if (m) {
+      const int l = __builtin_ctzll(m);
+      c = __builtin_amdgcn_readlane(e.x, l) & 0xffff;
+      na = __builtin_amdgcn_readlane(e.y, l);
+      en = i0 + l;
+      break;
     }
   }
-  asm volatile("" ::: "memory");
-  int n[NJ];
-  double p[NJ];
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) n[j] = NN[lane + WAVE * j];
-  if (!allv && EX) {  // select_nonroot's cached-exp softmax
-    double x[NJ];
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int a = lane + WAVE * j;
-      const bool ok = a < D.A && ((lg[j] >> lane) & 1ull);
-      x[j] = ok ? X[a] : 0.0;
-    }
-    double sum = 0.0;
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) sum += x[j];
-    sum = dred_sum_d(sum);
-    const double inv_s = 1.0 / sum;
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) p[j] = x[j] * inv_s;
-  } else if (!allv) {  // select_nonroot's logits softmax
-    double x[NJ], m = -INFINITY;
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int a = lane + WAVE * j;
-      const bool ok = a < D.A && ((lg[j] >> lane) & 1ull);
-      x[j] = ok ? (double)cur.v[j] + scale * X[a] : -INFINITY;
-      m = fmax(m, x[j]);
-    }
-    m = dred_max_d(m);
-    double sum = 0.0;
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      x[j] = (x[j] == -INFINITY) ? 0.0 : exp(x[j] - m);
-      sum += x[j];
-    }
-    sum = dred_sum_d(sum);
-    const double inv_s = 1.0 / sum;
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) p[j] = x[j] * inv_s;
-  } else {
-    float q[NJ], lv[NJ];
-    int mx_unused;
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) q[j] = QF[lane + WAVE * j];
-    logits_load<NJ>(D, D.logits + ((size_t)g * D.S + u) * D.A, lane, lv);
-    improved_policy<NJ>(D, lg, lane, lv, n, q, nz.mm_max, nz.mm_min, p, mx_unused);
-  }
-  double sc[NJ], best = -INFINITY;
-  const double inv_tot = 1.0 / (double)(1 + tot);
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int a = lane + WAVE * j;
-    sc[j] = -INFINITY;
-    if (a < D.A && ((lg[j] >> lane) & 1ull)) sc[j] = p[j] - (double)n[j] * inv_tot;
-    best = fmax(best, sc[j]);
-  }
-  best = dred_max_d(best);
-  int a = 0;  // np.argmax: first (lowest) action whose score equals the maximum
-#pragma unroll
-  for (int j = NJ - 1; j >= 0; --j) {
-    const uint64_t mk = __ballot(sc[j] == best && best != -INFINITY);
-    if (mk) a = WAVE * j + __builtin_ctzll(mk);
-  }
-  const int na = NN[a];
-  if (na > 0) {
-    const int ci = CI[a];
-    *child = ci & 0xffff;
-    *entry = ci >> 16;
-  } else {
-    *child = -1;
-    *entry = nvis;
-  }
+  *child = c;
+  *entry = en;
   *nchild = na;
-  if (EX && lane == 0) D.hdr[(size_t)g * D.S + u].w = na > 0 ? *child : leaf_next;
+  if (PF && lane == 0) D.hdr[(size_t)g * D.S + u].w = na > 0 ? c : leaf_next;
   return a;
 }
 
@@ -987,8 +1037,8 @@ __device__ __forceinline__ void select_game(const Dev &D, int g, int lane, int32
   uint64_t lg[NJ];
   load_legal<NJ>(D, g, lg);
   RowRegs<NJ, HINT> cur;
-  ListRegs<NJ, HINT> lcur;
-  int nxt_u = -1, nxt_nent = 0, nent_u = 0, ent = 0;
+  int nxt_u = -1, nxt_nent = 0, nent_u = 0, ent = 0, cb = 0;
+  const int lm = CL ? legal_slots<NJ>(D, lg, lane) : 0;
   const NormQ nz = norm_q_consts(D, st.mm_max, st.mm_min);
   for (;;) {
     int c, cn = 0;
@@ -1000,13 +1050,16 @@ __device__ __forceinline__ void select_game(const Dev &D, int g, int lane, int32
       TP_STAMP(tr1);
       TP_ADD(5, tr1 - tr0);
 #endif
-    } else if constexpr (CL) {  // the node's list arrives through the wave's LDS block: prefetched or now
+    } else if constexpr (CL) {
+      // the node's list arrives in buffer cb of the wave's LDS block: prefetched there by the previous
+      // level (HINT: the hint held) or DMA'd now; the next level's prefetch goes to the other buffer
+      uint8_t *buf = hint_slot + cb * ListBuf<NJ>::BYTES;
       int ne = nent_u;
-      if (u != nxt_u) list_fetch_lds<NJ, HINT>(D, g, u, nent_u, lane, hint_slot);
+      if (u != nxt_u) list_fetch_lds<NJ>(D, g, u, nent_u, lane, buf);
       else ne = nxt_nent;
-      list_from_lds<NJ, HINT>(hint_slot, lane, lcur);
-      a = select_nonroot_cl<NJ, HINT>(D, lg, g, u, lane, nz, lcur, ne, st.n_nodes, hint_slot, &c, &cn, &ent, &nxt_u,
-                                      &nxt_nent);
+      a = select_nonroot_cl<NJ, HINT>(D, lg, lm, g, u, lane, nz, ne, st.n_nodes, buf,
+                                      hint_slot + (cb ^ 1) * ListBuf<NJ>::BYTES, &c, &cn, &ent, &nxt_u, &nxt_nent);
+      if (HINT) cb ^= 1;
     } else {
       TP_STAMP(tf0);
       if constexpr (HINT) {  // the row arrives through the wave's LDS slot: prefetched (the hint held) or now
@@ -1108,7 +1161,11 @@ __device__ __forceinline__ void expand_backup_game(const Dev &D, int g, int lane
     }
 #pragma unroll 1
     for (int a = lane; a < A; a += WAVE)  // one exp live at a time (VGPR budget of the fused kernel)
+#ifdef GMZ_EXP_NOEXP2
+      nx[a] = ((double)logits_in[(size_t)g * A + a] - (double)lm);
+#else
       nx[a] = exp((double)logits_in[(size_t)g * A + a] - (double)lm);
+#endif
   } else {
     for (int a = lane; a < A; a += WAVE) {
       nl[a] = logits_in[(size_t)g * A + a];
@@ -1151,8 +1208,8 @@ __device__ __forceinline__ void expand_backup_game(const Dev &D, int g, int lane
     const float rj = e.r;
     const int cnt = min(WAVE, d + 1 - base);
     float myv = 0.f;
-    for (int i = 0; i < cnt; ++i) {
-      const float ri = __shfl(rj, i, 64);
+    for (int i = 0; i < cnt; ++i) {  // (i is wave-uniform: a scalar read of lane i, no LDS permute)
+      const float ri = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(rj), i));
       if (lane == i) myv = v;
       if (base + i < d) {
         const float dv = D.disc_f * v;
@@ -1190,32 +1247,69 @@ __device__ __forceinline__ void expand_backup_game(const Dev &D, int g, int lane
   mn = dred_min_f(mn);
   // root lane (level d) owns the updated root stats; broadcast them
   const int root_lane = d & (WAVE - 1);
-  st.root_w = __shfl(st.root_w, root_lane, 64);
-  st.root_n = __shfl(st.root_n, root_lane, 64);
+  st.root_w = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(st.root_w), root_lane));
+  st.root_n = __builtin_amdgcn_readlane(st.root_n, root_lane);
   if (mx > st.mm_max) st.mm_max = mx;
   if (mn < st.mm_min) st.mm_min = mn;
   st.sim += k;
+#ifdef GMZ_EXP_NOHALV
+  if (false) {
+#else
   if (ready_next_phase(D, st)) {  // _sequential_halving (mcts.py:182-185)
-    int n[NJ];
-    float q[NJ];
-    double t64[NJ];
-    float t32[NJ];
-    int max_n;
-    row_load<NJ>(D, edge_row(D, g, 0), lane, n, q);
-    const int is32 = transformed_q<NJ>(D, lane, n, q, st.mm_max, st.mm_min, t64, t32, max_n);
+#endif
+    // _get_transformed_completed_Qs of the root (mcts.py:141-149, transformed_q) for the selected actions
+    // only: the reductions over the children (max N, any unvisited, float32 clamps) in one pass, then each
+    // lane's selected action's value (the same arithmetic as transformed_q, no row held in registers)
+    const Edge *root = edge_row(D, g, 0);
+    const bool have_range = st.mm_max > st.mm_min;
+    const float den_f = (st.mm_max - st.mm_min) + D.delta_f;
+    auto root_q = [&](const Edge &e) -> float {  // get_qsa (mcts.py:35-38), as row_load
+      if (e.n <= 0) return 0.f;
+      const float vv = e.w / (float)e.n;
+      const float dv = D.disc_f * vv;
+      return e.r + dv;
+    };
+    int mxn = 0, unv = 0, clamped = 0;
+    for (int a = lane; a < A; a += WAVE) {
+      const Edge e = root[a];
+      mxn = max(mxn, e.n);
+      unv |= e.n == 0;
+      if (have_range) {
+        const float x = (root_q(e) - st.mm_min) / den_f;
+        clamped |= !(x < 1.0f) || !(x > 0.0f);
+      }
+    }
+    mxn = dred_max_i(mxn);
+    const bool allv = __ballot(unv != 0) == 0ull;
+    const bool promote = !have_range || __ballot(clamped != 0) != 0ull;
+    const double scale = (double)(D.c_visit + mxn) * D.c_scale;
     const int ks = st.n_sel;
     const int ai = lane < ks ? D.sel[g * MAX_TOP + lane] : 0;
     double ti = 0.0;
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const double tv = is32 ? (double)t32[j] : t64[j];
-      const double got = __shfl(tv, ai & 63, 64);
-      if ((ai >> 6) == j) ti = got;
+    {
+      const float q = root_q(root[ai]);
+      if (!allv) {
+        double nq = 0.0;
+        if (have_range) {
+          double x = ((double)q - (double)st.mm_min) / (double)den_f;
+          x = (x < 1.0) ? x : 1.0;
+          nq = (x > 0.0) ? x : 0.0;
+        }
+        ti = scale * nq;
+      } else {
+        float nf = 0.f;
+        if (have_range) {
+          nf = (q - st.mm_min) / den_f;
+          if (!(nf < 1.0f)) nf = 1.0f;
+          if (!(nf > 0.0f)) nf = 0.0f;
+        }
+        ti = promote ? scale * (double)nf : (double)((float)scale * nf);
+      }
     }
     const double si = lane < ks ? (D.gumbel[(size_t)g * A + ai] + (double)D.logits[(size_t)g * S * A + ai]) + ti : 0.0;
     int rank = 0;
     for (int jj = 0; jj < ks; ++jj) {
-      const double sj = __shfl(si, jj, 64);
+      const double sj = readlane_d(si, jj);
       if (sj > si || (sj == si && jj < lane)) rank++;
     }
     const int keep = min(ks, st.m_cur);
@@ -1229,13 +1323,13 @@ __device__ __forceinline__ void expand_backup_game(const Dev &D, int g, int lane
 // per-wave LDS block of the selection kernels: the hint slot (dense + HINT), the list block (CL), none
 template <int NJ, bool HINT, bool CL>
 struct SelLds {
-  static constexpr int BYTES = CL ? ListSlot<NJ, HINT>::BYTES : (HINT ? HintSlot<NJ>::BYTES : 0);
+  static constexpr int BYTES = CL ? (HINT ? 2 : 1) * ListBuf<NJ>::BYTES : (HINT ? HintSlot<NJ>::BYTES : 0);
 };
 
 template <int NJ, bool HINT, bool AZ, bool CL>
 __global__ void __launch_bounds__(256) k_select(Dev D, int32_t *__restrict__ in_slot, int32_t *__restrict__ act_out,
                                                 int32_t *__restrict__ out_slot, float *__restrict__ obs) {
-  const int g = blockIdx.x * 4 + threadIdx.x / WAVE, lane = threadIdx.x & (WAVE - 1);
+  const int g = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + threadIdx.x / WAVE), lane = threadIdx.x & (WAVE - 1);
   if (g >= D.G) return;
   constexpr int LB = SelLds<NJ, HINT, CL>::BYTES;
   __shared__ __attribute__((aligned(16))) uint8_t hint_lds[LB ? 4 * LB : 16];
@@ -1260,8 +1354,7 @@ __global__ void __launch_bounds__(256) k_expand_backup(Dev D, const float *__res
   if (g >= D.G) return;
   const int lane = threadIdx.x & (WAVE - 1);
   if (D.lists) {
-    if (D.no_hint) expand_backup_game<NJ, false, true>(D, g, lane, logits_in, value_in, reward_in);
-    else expand_backup_game<NJ, true, true>(D, g, lane, logits_in, value_in, reward_in);
+    expand_backup_game<NJ, true, true>(D, g, lane, logits_in, value_in, reward_in);  // lists: exp rows always
   } else {
     if (D.no_hint) expand_backup_game<NJ, false, false>(D, g, lane, logits_in, value_in, reward_in);
     else expand_backup_game<NJ, true, false>(D, g, lane, logits_in, value_in, reward_in);
@@ -1276,21 +1369,23 @@ __global__ void __launch_bounds__(256) k_expand_backup(Dev D, const float *__res
 // waves over the CU's 4 SIMDs); 1 when the games outnumber the resident waves, so that a wave whose
 // game finishes early frees its slot for the next game at once instead of its workgroup's slot
 // waiting for the slowest of 4 games (trees differ in depth)
-// The compact-list kernels (CL) hold 128 VGPRs (4 waves per SIMD) with the hint as well.
+// The compact-list kernels (CL) keep no row in registers: 8 waves per SIMD (64 VGPRs, one 3 KB LDS
+// buffer per wave) without the prefetch, 5 with it (two buffers).
 template <int NJ, bool HINT, bool AZ, bool CL, int WPB = 4>
-__global__ void __launch_bounds__(64 * WPB, NJ > 4 ? 1 : ((HINT && !CL) ? GMZ_HINT_WPS : 4)) k_expand_select(Dev D, const float *__restrict__ logits_in,
+__global__ void __launch_bounds__(64 * WPB, NJ > 4 ? 1 : (CL ? (HINT ? 5 : GMZ_CL_WPS) : (HINT ? GMZ_HINT_WPS : 4))) k_expand_select(Dev D, const float *__restrict__ logits_in,
                                                        const float *__restrict__ value_in,
                                                        const float *__restrict__ reward_in,
                                                        int32_t *__restrict__ in_slot, int32_t *__restrict__ act_out,
                                                        int32_t *__restrict__ out_slot, float *__restrict__ obs) {
-  const int g = blockIdx.x * WPB + threadIdx.x / WAVE, lane = threadIdx.x & (WAVE - 1);
+  // the wave's game, wave-uniform (SGPR): every per-game scalar load stays scalar
+  const int g = __builtin_amdgcn_readfirstlane(blockIdx.x * WPB + threadIdx.x / WAVE), lane = threadIdx.x & (WAVE - 1);
   if (g >= D.G) return;
 #ifdef GMZ_TREE_PROF
   if (lane < 16) tp_lds[threadIdx.x / WAVE][lane] = 0;
 #endif
   TP_STAMP(tk0);
   const int active0 = D.gs[g].active, depth0 = D.gs[g].depth;
-  expand_backup_game<NJ, HINT, CL>(D, g, lane, logits_in, value_in, reward_in);
+  expand_backup_game<NJ, HINT || CL, CL>(D, g, lane, logits_in, value_in, reward_in);
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_s_waitcnt(0);
   TP_STAMP(tk1);
@@ -1448,6 +1543,7 @@ GMZ_EXPORT int gmz_engine_create(const gmz_engine_cfg *cfg, gmz_engine **out) {
   if (cfg->num_top_actions < 1 || cfg->num_top_actions > MAX_TOP) return fail("gmz_engine_create: num_top_actions must be in [1, 64]");
   if (cfg->num_simulations < 1) return fail("gmz_engine_create: num_simulations must be >= 1");
   if (cfg->mode != 0 && cfg->mode != 1) return fail("gmz_engine_create: mode must be 0 (AlphaZero) or 1 (MuZero)");
+  if (cfg->num_simulations >= (1 << 24)) return fail("gmz_engine_create: num_simulations must be < 2^24");
   if ((cfg->flags & 8) && cfg->num_simulations + 2 > 65535)
     return fail("gmz_engine_create: compact child lists need num_simulations + 2 <= 65535 (16-bit node ids)");
   gmz_engine *e = new gmz_engine();

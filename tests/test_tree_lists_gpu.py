@@ -1,14 +1,15 @@
 """Compact child lists (gmz_engine_cfg.flags bit 3, engine ``layout="lists"``) vs the dense layout.
 
 A non-root node's edge row holds only its visited children ({action << 16 | child, N, W, R} entries in
-first-visit order); a selection level scatters them into a per-wave LDS view in action order and then
-runs the dense kernels' arithmetic on the same values in the same order (gmz_tree.hip
-select_nonroot_cl).  So every search must equal the dense layout's BIT FOR BIT — policy, value, action,
-root visit counts, root N/W, MinMaxStats — with the hint kernels (cached exp rows) and with the no-hint
-kernels (the reference's exp(logit + t - max) arithmetic), fused and split entry points, 1- and 4-wave
-workgroups, every board size the kernels take (NJ = 1, 2, 4, 6, 8), including the all-children-visited
-float32 path (6x6 / 400) and lists longer than one wave (> 64 visited children).  The lists path is also
-checked directly against the reference's own MCTS fixtures (tests/golden/mcts_*.npz) and the C oracle.
+first-visit order); a selection level works on its cached exp row and entries in a per-wave LDS buffer,
+with the dense hint kernels' arithmetic on the same values in the same order (gmz_tree.hip
+select_nonroot_cl; the lists always use the cached exp rows, the hint setting only switches the descent
+prefetch).  So every search must equal the dense layout's with cached exp rows BIT FOR BIT — policy,
+value, action, root visit counts, root N/W, MinMaxStats — with and without the prefetch, fused and split
+entry points, 1- and 4-wave workgroups, every board size the kernels take (NJ = 1, 2, 4, 6, 8), including
+the all-children-visited float32 path (6x6 / 400) and lists longer than one wave (> 64 visited
+children).  The lists path is also checked directly against the reference's own MCTS fixtures
+(tests/golden/mcts_*.npz) and the C oracle.
 Reference: mcts.py:88-138 (select / backup), HashNet for tree parity independent of network floats.
 """
 import glob
@@ -92,9 +93,9 @@ def test_lists_equal_dense(E, size, sims, mode, G, max_stones, moves, hint):
     rs = np.random.RandomState(size * 100 + sims + G)
     pos = _positions(size, G, rs, max_stones)
     gumbels = [rs.gumbel(0, 1, (G, size * size)) for _ in range(moves)]
-    dense = _play(E, size, sims, mode, G, pos, gumbels, descent_hint=hint, layout="dense")
+    dense = _play(E, size, sims, mode, G, pos, gumbels, descent_hint=True, layout="dense")
     lists = _play(E, size, sims, mode, G, pos, gumbels, descent_hint=hint, layout="lists")
-    _assert_same(dense, lists, "lists vs dense (hint=%s)" % hint)
+    _assert_same(dense, lists, "lists (prefetch=%s) vs dense" % hint)
 
 
 @pytest.mark.parametrize("size,sims,mode,G", [(15, 400, "MuZero", 40), (9, 50, "AlphaZero", 24), (6, 400, "MuZero", 16)])
@@ -107,7 +108,7 @@ def test_lists_split_entry_points_equal_fused(E, size, sims, mode, G, hint):
     gumbels = [rs.gumbel(0, 1, (G, size * size))]
     fused = _play(E, size, sims, mode, G, pos, gumbels, fuse=True, descent_hint=hint, layout="lists")
     split = _play(E, size, sims, mode, G, pos, gumbels, fuse=False, descent_hint=hint, layout="lists")
-    dense = _play(E, size, sims, mode, G, pos, gumbels, fuse=False, descent_hint=hint, layout="dense")
+    dense = _play(E, size, sims, mode, G, pos, gumbels, fuse=False, descent_hint=True, layout="dense")
     _assert_same(fused, split, "fused vs split (lists)")
     _assert_same(split, dense, "lists vs dense (split entry points)")
 
@@ -143,7 +144,7 @@ def test_lists_large_g_equal_dense_and_oracle(E, G, hint, wpb):
     gumbels = [rs.gumbel(0, 1, (G, size * size))]
     kw = dict(descent_hint=hint) if wpb is None else dict(descent_hint=hint, wpb=wpb)
     lists = _play(E, size, sims, "MuZero", G, pos, gumbels, layout="lists", **kw)
-    dense = _play(E, size, sims, "MuZero", G, pos, gumbels, layout="dense", descent_hint=hint)
+    dense = _play(E, size, sims, "MuZero", G, pos, gumbels, layout="dense", descent_hint=True)
     _assert_same(lists, dense, "lists vs dense at G=%d" % G)
     pol, val, act, visits, rn, rw, mx, mn = lists[0]
     boards, players, lastm = pos

@@ -72,6 +72,17 @@ PY
         done
       done
     done ;;
+  layout_libs)  # k_expand_select of the list layout per occupancy build (GMZ_LIB) at each G, one stream
+    for G in ${1:-4096 8192}; do
+      for LIB in libgmz.so _alt/libgmz_cl5.so _alt/libgmz_cl6.so _alt/libgmz_cl7.so; do
+        for H in off on; do
+          N=G${G}_$(basename $LIB .so)_$H
+          GMZ_LIB=$PWD/datou-gomoku-muzero_amd/$LIB timeout -k 10 300 python -u bench.py --games $G --streams 1 --steps 3 --warmup 1 \
+            --layout lists --hint $H --single-stream-moves 0 $SP > $OUT/$N.json 2> $OUT/$N.err || { echo "$N failed"; tail -5 $OUT/$N.err; exit 1; }
+          python3 -c "import json,sys; d=json.load(open(sys.argv[1])); t=d['roofline_tree']; print('%-32s moves/s %8.0f  tree %7.1f us  %6.0f GB/s  frac %.3f' % (sys.argv[2], d['value'], t['mean_launch_ms']*1e3, t['achieved'], t['frac']))" $OUT/$N.json $N | tee -a $OUT/summary.txt
+        done
+      done
+    done ;;
   *)
     echo "usage: tools/gpu.sh tests|smoke|bench|trace|pmc TAG [args]"; exit 2 ;;
 esac
