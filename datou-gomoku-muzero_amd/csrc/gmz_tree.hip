@@ -85,7 +85,8 @@ struct Dev {
 #ifndef GMZ_HINT_WPS
 #define GMZ_HINT_WPS 2
 #endif
-// waves per SIMD of the compact-list kernel without the prefetch
+// waves per SIMD the compact-list kernels are compiled for: 5 (<= 96 VGPRs) is the most without spills
+// (6: 12 spills, 8: 27; the peaks are the f64 exp calls beside the descent's live state)
 #ifndef GMZ_CL_WPS
 #define GMZ_CL_WPS 5
 #endif
@@ -1369,10 +1370,10 @@ __global__ void __launch_bounds__(256) k_expand_backup(Dev D, const float *__res
 // waves over the CU's 4 SIMDs); 1 when the games outnumber the resident waves, so that a wave whose
 // game finishes early frees its slot for the next game at once instead of its workgroup's slot
 // waiting for the slowest of 4 games (trees differ in depth)
-// The compact-list kernels (CL) keep no row in registers: 8 waves per SIMD (64 VGPRs, one 3 KB LDS
-// buffer per wave) without the prefetch, 5 with it (two buffers).
+// The compact-list kernels (CL) keep one row's slots in registers only while scoring it: GMZ_CL_WPS (5)
+// waves per SIMD, one 3 KB LDS buffer per wave without the prefetch, two with it.
 template <int NJ, bool HINT, bool AZ, bool CL, int WPB = 4>
-__global__ void __launch_bounds__(64 * WPB, NJ > 4 ? 1 : (CL ? (HINT ? 5 : GMZ_CL_WPS) : (HINT ? GMZ_HINT_WPS : 4))) k_expand_select(Dev D, const float *__restrict__ logits_in,
+__global__ void __launch_bounds__(64 * WPB, NJ > 4 ? 1 : (CL ? GMZ_CL_WPS : (HINT ? GMZ_HINT_WPS : 4))) k_expand_select(Dev D, const float *__restrict__ logits_in,
                                                        const float *__restrict__ value_in,
                                                        const float *__restrict__ reward_in,
                                                        int32_t *__restrict__ in_slot, int32_t *__restrict__ act_out,

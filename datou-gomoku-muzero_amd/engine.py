@@ -62,9 +62,10 @@ class BatchedSelfPlayEngine:
         self.lib = _lib.load()
         self.device = torch.device(device)
         self.G, self.A, self.size = int(num_games), c.ACTION_SPACE_SIZE, c.BOARD_SIZE
-        if descent_hint is None:  # the hint kernels (next-visit LDS prefetch, cached exp rows, 2 waves per
-            descent_hint = self.G < 4096  # SIMD) pay up to 2,048 games per engine; from 4,096 the 4-wave
-            # no-hint kernel hides the latency itself
+        if descent_hint is None:  # the next-visit prefetch and cached exp rows: faster at every G measured,
+            descent_hint = True   # with the dense rows below 4,096 games per engine and the lists from there
+            # (profiles/r03_tree_layout_ab.txt); the no-hint dense kernels keep the reference's
+            # exp(logit + t - max) arithmetic (A/B and tests)
         self.mode = 1 if c.MCTS_IMPLEMENTATION == "MuZero" else 0
         self.slots_per_game = c.NUM_SIMULATIONS + 2
         if wpb not in (None, 1, 4):
@@ -291,8 +292,8 @@ class SplitSelfPlayEngine:
         self.mode = 1 if c.MCTS_IMPLEMENTATION == "MuZero" else 0
         self.slots_per_game = c.NUM_SIMULATIONS + 2
         g = self.g = G // parts
-        if descent_hint is None:  # chosen from the TOTAL game count, as one engine with every game would
-            descent_hint = G < 4096  # (the hint kernels' cached-exp softmax differs by a few ulp)
+        if descent_hint is None:  # the cached-exp softmax for every part, as one engine with every game
+            descent_hint = True   # (the layout may differ per part: results are identical)
         if max_grid is None:
             max_grid = torch.cuda.get_device_properties(self.device).multi_processor_count * 3 // 4 if parts > 1 else 0
         if net is None:
@@ -300,7 +301,7 @@ class SplitSelfPlayEngine:
         self.net = net
         nets = net.split(parts, max_grid) if parts > 1 else [net]
         if layout is None:
-            layout = default_layout(G)
+            layout = default_layout(g)
         self.engines = [BatchedSelfPlayEngine(c, g, nets[i], device, seed, descent_hint, game_offset=i * g,
                                               layout=layout) for i in range(parts)]
         self.streams = [torch.cuda.Stream(self.device) for _ in range(parts)]
@@ -396,9 +397,12 @@ class SplitSelfPlayEngine:
 
 
 def default_layout(num_games):
-    """Tree layout of the non-root nodes: 'dense' (a 16-B edge per action) or 'lists' (compact lists of the
-    visited children, gmz_engine_cfg.flags bit 3).  Both give identical results (tests/test_tree_lists_gpu.py)."""
-    return "dense"
+    """Tree layout of the non-root nodes of one engine: 'dense' (a 16-B edge per action) or 'lists'
+    (compact lists of the visited children, gmz_engine_cfg.flags bit 3), as measured on k_expand_select
+    (profiles/r03_tree_layout_ab.txt): the dense rows in the latency-bound regime (one wave per SIMD
+    or less, below 4,096 games), the lists from 4,096 (fewer bytes and instructions per tree level).
+    Results are identical either way (tests/test_tree_lists_gpu.py)."""
+    return "lists" if num_games >= 4096 else "dense"
 
 
 def default_streams(cfg, num_games):

@@ -109,16 +109,18 @@ def test_split_positions_and_masks(mods):
     _same(_moves(one, 2), _moves(two, 2))
 
 
-def test_split_picks_the_kernel_of_the_total_game_count(mods):
-    """At 4,096 games one engine runs the no-hint kernel (engine.py: G >= 4096); two halves of 2,048
-    must too (the choice is made from the total G), so the split engine plays the one engine's games
-    bit for bit (15x15 / 64 sims MuZero, HashNet, device Gumbel noise)."""
+def test_split_with_another_layout_plays_the_same_games(mods):
+    """At 4,096 games one engine runs the compact child lists (engine.default_layout: G >= 4096) and two
+    halves of 2,048 the dense rows, both with the cached-exp softmax (descent_hint, the default at every
+    G), so the split engine plays the one engine's games bit for bit (15x15 / 64 sims MuZero, HashNet,
+    device Gumbel noise)."""
     E, N, W, GmzConfig = mods
     cfg = GmzConfig(BOARD_SIZE=15, NUM_SIMULATIONS=64, MCTS_IMPLEMENTATION="MuZero")
     G = 4096
     one = E.BatchedSelfPlayEngine(cfg, num_games=G, seed=9)
     two = E.SplitSelfPlayEngine(cfg, num_games=G, seed=9, parts=2)
-    assert not one.descent_hint and not any(e.descent_hint for e in two.engines)
+    assert one.layout == "lists" and all(e.layout == "dense" for e in two.engines)
+    assert one.descent_hint and all(e.descent_hint for e in two.engines)
     one.reset_games()
     two.reset_games()
     _same(_moves(one, 3), _moves(two, 3))

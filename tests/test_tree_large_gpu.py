@@ -1,10 +1,11 @@
 """Large-G parity of the fused expand/backup + select kernel (gmz_tree.hip ``k_expand_select``).
 
-The engine picks the kernel variant by game count (engine.py, gmz_tree.hip launch_expand_select):
-  * the hint kernels (descent prefetch, cached exp rows) below 4,096 games per engine, the no-hint
-    kernel from 4,096;
+The kernel variant depends on the game count (engine.py, gmz_tree.hip launch_expand_select):
+  * the engine's default: cached exp rows + descent prefetch, dense rows below 4,096 games per engine and
+    compact child lists from 4,096 (tests/test_tree_lists_gpu.py); the no-hint dense kernel (the
+    reference's exp(logit + t - max) softmax) on request;
   * 4-wave workgroups while every game has a resident wave, 1-wave workgroups once the games
-    outnumber them (> 2,048 games with the 2-wave-per-SIMD hint kernel, > 4,096 with the no-hint one).
+    outnumber them.
 The smaller-G tests (test_engine_gpu.py) never reach the 1-wave variants, so this file runs both at
 sizes where the engine selects them on its own, 15x15 / 400 sims MuZero (config C2's search,
 mcts.py:288-362) with HashNet (tree parity independent of network floating point):
@@ -89,19 +90,20 @@ def _check_oracle(out, pos, games):
     return bad
 
 
-@pytest.mark.parametrize("G,hint", [(4160, False),   # the no-hint kernel's default regime past 4,096 games
-                                    (2112, True)])   # the hint kernel past its 2,048 resident waves
+@pytest.mark.parametrize("G,hint", [(4160, False),   # the no-hint dense kernel past 4,096 resident waves
+                                    (4160, True),    # the hint dense kernel there
+                                    (2112, True)])   # the hint dense kernel past 2,048
 def test_one_wave_workgroups_match_four_wave_and_oracle(E, G, hint):
     rs = np.random.RandomState(G)
     pos = _positions(G, rs)
-    one = _search(E, G, pos, descent_hint=hint, wpb=1)
-    four = _search(E, G, pos, descent_hint=hint, wpb=4)
+    one = _search(E, G, pos, descent_hint=hint, wpb=1, layout="dense")
+    four = _search(E, G, pos, descent_hint=hint, wpb=4, layout="dense")
     diff = _differing_games(one, four)
     assert len(diff) == 0, "games differing between 1-wave and 4-wave workgroups: %s" % diff[:20]
     assert np.array_equal(one["pol"], four["pol"])
-    # the engine's own choice at this G is the 1-wave variant (and the hint setting under test)
-    dflt = _search(E, G, pos)
-    assert len(_differing_games(dflt, one)) == 0 and np.array_equal(dflt["pol"], one["pol"])
+    if hint:  # the engine's own choice at this G (lists from 4,096, cached-exp softmax): the same games
+        dflt = _search(E, G, pos)
+        assert len(_differing_games(dflt, one)) == 0 and np.array_equal(dflt["pol"], one["pol"])
     sample = rs.choice(G, 64, replace=False)
     bad = _check_oracle(one, pos, sample)
     assert not bad, "games diverging from the oracle: %s" % bad
@@ -114,8 +116,8 @@ def test_hint_and_no_hint_kernels_agree_at_4096_games(E):
     G = 4096
     rs = np.random.RandomState(4096)
     pos = _positions(G, rs)
-    h = _search(E, G, pos, descent_hint=True)
-    n = _search(E, G, pos, descent_hint=False)
+    h = _search(E, G, pos, descent_hint=True, layout="dense")
+    n = _search(E, G, pos, descent_hint=False, layout="dense")
     diff = _differing_games(h, n)
     print("hint vs no-hint at %d games: %d differing searches" % (G, len(diff)))
     assert len(diff) == 0, "near-tie flips between the two softmax forms in games %s" % diff[:20]
