@@ -304,7 +304,7 @@ class SplitSelfPlayEngine:
             layout = default_layout(g)
         self.engines = [BatchedSelfPlayEngine(c, g, nets[i], device, seed, descent_hint, game_offset=i * g,
                                               layout=layout) for i in range(parts)]
-        self.streams = [torch.cuda.Stream(self.device) for _ in range(parts)]
+        self.streams = engine_streams(self.device, parts)
         dev = self.device
         self.policy = torch.zeros(G, self.A, dtype=torch.float64, device=dev)
         self.root_value = torch.zeros(G, dtype=torch.float32, device=dev)
@@ -394,6 +394,21 @@ class SplitSelfPlayEngine:
     def root_stats(self):
         parts = [e.root_stats() for e in self.engines]
         return tuple(torch.cat([p[k] for p in parts]) for k in range(5))
+
+
+_ENGINE_STREAMS = {}
+
+
+def engine_streams(device, parts):
+    """The HIP streams of the split engines: created once per device and process and shared by every
+    SplitSelfPlayEngine (one at a time).  HIP maps each new stream onto the device's hardware queues
+    round-robin (GPU_MAX_HW_QUEUES, 4 on MI355X), so streams created later — a second engine's, after a
+    trainer's side streams — can land on the queue of the default stream or of each other and serialise
+    the two halves: measured 123 vs 90 ms per move for the same worker (profiles/r03_worker_streams.txt)."""
+    key = (str(torch.device(device)), parts)
+    if key not in _ENGINE_STREAMS:
+        _ENGINE_STREAMS[key] = [torch.cuda.Stream(device) for _ in range(parts)]
+    return _ENGINE_STREAMS[key]
 
 
 def default_layout(num_games):
