@@ -28,8 +28,6 @@ Launch from main.py's ``process_definitions`` in place of the workers + server, 
                            initial_model_requests_queue=initial_model_requests_queue))
 """
 import logging
-import os
-import sys
 import time
 from concurrent.futures import ThreadPoolExecutor
 from queue import Empty
@@ -53,10 +51,6 @@ def board_states_to_obs(boards, players, last_moves, H):
     has = last_moves >= 0
     obs[np.nonzero(has)[0], 2, last_moves[has] // H, last_moves[has] % H] = 1
     return obs
-
-
-# s, while gpu_selfplay_worker runs (sys.setswitchinterval; restored after); env override for A/B runs
-GIL_SWITCH_INTERVAL = float(os.environ.get("GMZ_WORKER_SWITCH_INTERVAL", "2e-4"))
 
 
 class GameHistory:
@@ -204,11 +198,6 @@ def gpu_selfplay_worker(worker_id, worker_mode, data_queue, log_status_queue, ui
         eng.set_positions(*openings)
         hist.set_start(openings[3])
     pool = ThreadPoolExecutor(max_workers=4)
-    # the launch loop (this thread) drops the GIL in every ctypes / HIP call and must get it back at once:
-    # with the default 5 ms switch interval the record builders and the queue feeder threads (one
-    # SelfPlayMove per game and move) hold it that long while the GPU idles between waves
-    switch_interval = sys.getswitchinterval()
-    sys.setswitchinterval(min(switch_interval, GIL_SWITCH_INTERVAL))
     moves_done = 0
     # missed-win counters of workers.py:191-203, accumulated on the device move by move by the batched
     # find_winning_moves scan (gmz_game_winning_scan) instead of a Python scan per finished game
@@ -304,7 +293,6 @@ def gpu_selfplay_worker(worker_id, worker_mode, data_queue, log_status_queue, ui
             break
     drain(pending)
     pool.shutdown(wait=True)
-    sys.setswitchinterval(switch_interval)
     if move_times is not None:
         torch.cuda.synchronize()
         move_times.append(time.perf_counter())  # every move played and every record posted
