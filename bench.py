@@ -378,7 +378,25 @@ def trainer_leg(args, world, rank, dist, backend):
             "roofline": {"bound": "mfma", "kernel": "gmz_conv3x3 (128->128 3x3 conv, f16 NHWC, B=%d)" % B,
                          "achieved": ach, "peak": PEAK_MFMA_TFLOPS, "unit": "TFLOP/s", "frac": ach / PEAK_MFMA_TFLOPS,
                          "mean_launch_ms": ms, "timed": "standalone at the step's shape, %d launches" % n,
-                         "traffic": None}}
+                         "traffic": None},
+            "roofline_in_step": trainer_trace_summary(args)}
+
+
+def trainer_trace_summary(args):
+    """The dominant convolution inside the graph-replayed trainer step and the step's launch count, from the
+    committed rocprofv3 trace summary (tools/trainer_profile.sh -> tools/trainer_trace_summary.py; a HIP
+    graph's kernels cannot be timed from inside the process): builder-measured, not this run."""
+    path = os.path.join(REPO, "profiles", "r03_trainer_trace.json")
+    if not os.path.exists(path) or (args.size, args.blocks, args.trainer_batch) != (15, 8, 360):
+        return None
+    try:
+        d = json.load(open(path))
+    except Exception:
+        return None
+    out = dict(d.get("dominant", {}))
+    out.update(bound="mfma", launches_per_step=d.get("launches_per_step"), weight_gradient=d.get("weight_gradient"),
+               source="builder-measured: %s (%s)" % (os.path.relpath(path, REPO), d.get("source", "")))
+    return out
 
 
 def selfplay_leg(args, rank, world, dist, backend, size, sims, mode, blocks, G, steps, warmup, streams=None,

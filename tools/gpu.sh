@@ -72,6 +72,11 @@ PY
         done
       done
     done ;;
+  tree_curve)  # the default engine per game count: headline (two streams) + the tree kernel alone (one engine)
+    for G in ${1:-1024 2048 4096 8192}; do
+      timeout -k 10 400 python -u bench.py --games $G --steps 3 --warmup 1 $SP > $OUT/G$G.json 2> $OUT/G$G.err || { echo "G=$G failed"; tail -5 $OUT/G$G.err; exit 1; }
+      python3 -c "import json,sys; d=json.load(open(sys.argv[1])); t=d['roofline_tree']; s=d['single_stream_kernels']; print('G=%5d moves/s %8.0f | tree alone (%s, hint %s) %7.1f us %6.0f GB/s frac %.3f | in the step %6.1f us frac %.3f | tower alone frac %.3f' % (d['config']['games_per_gpu'], d['value'], t['layout'], t['descent_hint'], s['tree']['mean_launch_ms']*1e3, s['tree']['achieved_gbs'], s['tree']['frac'], t['mean_launch_ms']*1e3, t['frac'], s['tower']['frac']))" $OUT/G$G.json | tee -a $OUT/summary.txt
+    done ;;
   layout_libs)  # k_expand_select of the list layout per occupancy build (GMZ_LIB) at each G, one stream
     for G in ${1:-4096 8192}; do
       for LIB in libgmz.so _alt/libgmz_cl5.so _alt/libgmz_cl6.so _alt/libgmz_cl7.so; do
