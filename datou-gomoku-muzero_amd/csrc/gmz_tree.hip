@@ -58,6 +58,32 @@ struct GameState {
   int32_t pad1[2];
 };
 
+// a wave's GameState in SGPRs: the struct is loaded with vector loads (the kernels also store it, so the
+// compiler may not use the scalar cache) and would otherwise stay in 16 VGPRs across the descent
+__device__ __forceinline__ GameState uniform_state(const GameState &v) {
+  GameState s;
+  s.n_nodes = __builtin_amdgcn_readfirstlane(v.n_nodes);
+  s.sim = __builtin_amdgcn_readfirstlane(v.sim);
+  s.phase = __builtin_amdgcn_readfirstlane(v.phase);
+  s.m_cur = __builtin_amdgcn_readfirstlane(v.m_cur);
+  s.next_phase = __builtin_amdgcn_readfirstlane(v.next_phase);
+  s.root_n = __builtin_amdgcn_readfirstlane(v.root_n);
+  s.n_sel = __builtin_amdgcn_readfirstlane(v.n_sel);
+  s.active = __builtin_amdgcn_readfirstlane(v.active);
+  s.depth = __builtin_amdgcn_readfirstlane(v.depth);
+  s.k = __builtin_amdgcn_readfirstlane(v.k);
+  s.leaf = __builtin_amdgcn_readfirstlane(v.leaf);
+  s.n_legal = __builtin_amdgcn_readfirstlane(v.n_legal);
+  s.root_w = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.root_w)));
+  s.mm_max = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.mm_max)));
+  s.mm_min = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.mm_min)));
+  s.pad0 = 0.f;
+  s.used = __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v.used)),
+                            __builtin_amdgcn_readfirstlane(__double2loint(v.used)));
+  s.pad1[0] = s.pad1[1] = 0;
+  return s;
+}
+
 struct Dev {
   Edge *edges;
   float *logits;
@@ -85,10 +111,11 @@ struct Dev {
 #ifndef GMZ_HINT_WPS
 #define GMZ_HINT_WPS 2
 #endif
-// waves per SIMD the compact-list kernels are compiled for: 5 (<= 96 VGPRs) is the most without spills
-// (6: 12 spills, 8: 27; the peaks are the f64 exp calls beside the descent's live state)
+// waves per SIMD the compact-list kernels are compiled for (the prefetch variant at most 6: two LDS
+// buffers per wave): 6 = 80 VGPRs, 2 spilled values; measured at 8,192 games 107.8 us vs 109.9 at 5 (no
+// spills) and 107.3 at 8 (14 spills) (profiles/r03_tree_layout_ab.txt)
 #ifndef GMZ_CL_WPS
-#define GMZ_CL_WPS 5
+#define GMZ_CL_WPS 6
 #endif
 #ifdef GMZ_TREE_PROF
 // phase-cycle instrumentation (tools/tree_prof.py builds a separate library with -DGMZ_TREE_PROF)
@@ -275,10 +302,15 @@ __device__ __forceinline__ int bcast_slot(const int (&v)[NJ], int a) {
   return out;
 }
 
+// the root legal set (wave-uniform: kept in SGPRs, not in 2 * NJ VGPRs across the descent)
 template <int NJ>
 __device__ __forceinline__ void load_legal(const Dev &D, int g, uint64_t (&lg)[NJ]) {
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) lg[j] = D.legal[(size_t)g * gmz::NJ + j];
+  for (int j = 0; j < NJ; ++j) {
+    const uint64_t v = D.legal[(size_t)g * gmz::NJ + j];
+    lg[j] = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
+            (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+  }
 }
 
 // one non-root node's edge row, its logits (EX = false) or cached exp(logit - max legal logit)
@@ -368,6 +400,8 @@ __device__ __forceinline__ NormQ norm_q_consts(const Dev &D, float mm_max, float
     x = (x < 1.0) ? x : 1.0;
     z.nq0 = (x > 0.0) ? x : 0.0;
   }
+  z.nq0 = readlane_d(z.nq0, 0);  // wave-uniform (mm_max / mm_min are): SGPRs across the descent
+  z.den_f = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(z.den_f)));
   return z;
 }
 
@@ -1011,7 +1045,7 @@ __device__ __forceinline__ void select_game(const Dev &D, int g, int lane, int32
                                             int32_t *__restrict__ act_out, int32_t *__restrict__ out_slot,
                                             float *__restrict__ obs, uint8_t *hint_slot) {
   const int A = D.A, S = D.S;
-  GameState st = D.gs[g];
+  GameState st = uniform_state(D.gs[g]);
   if (!st.active) {
     if (lane == 0) {
       in_slot[g] = -1;
@@ -1132,7 +1166,7 @@ __device__ __forceinline__ void expand_backup_game(const Dev &D, int g, int lane
   // action then come from a lane permute instead of a dependent memory round trip
   const int pl = lane < S ? lane : S - 1;
   const int pu_l = pu[pl], pa_l = pa[pl], pe_l = CL ? pe[pl] : 0;
-  GameState st = D.gs[g];
+  GameState st = uniform_state(D.gs[g]);
   if (!st.active) return;
   const int d = st.depth, leaf = st.leaf, k = st.k;
   // Node.expand (mcts.py:24-25): logits, reward; children row starts empty
@@ -1373,7 +1407,7 @@ __global__ void __launch_bounds__(256) k_expand_backup(Dev D, const float *__res
 // The compact-list kernels (CL) keep one row's slots in registers only while scoring it: GMZ_CL_WPS (5)
 // waves per SIMD, one 3 KB LDS buffer per wave without the prefetch, two with it.
 template <int NJ, bool HINT, bool AZ, bool CL, int WPB = 4>
-__global__ void __launch_bounds__(64 * WPB, NJ > 4 ? 1 : (CL ? GMZ_CL_WPS : (HINT ? GMZ_HINT_WPS : 4))) k_expand_select(Dev D, const float *__restrict__ logits_in,
+__global__ void __launch_bounds__(64 * WPB, NJ > 4 ? 1 : (CL ? (HINT && GMZ_CL_WPS > 6 ? 6 : GMZ_CL_WPS) : (HINT ? GMZ_HINT_WPS : 4))) k_expand_select(Dev D, const float *__restrict__ logits_in,
                                                        const float *__restrict__ value_in,
                                                        const float *__restrict__ reward_in,
                                                        int32_t *__restrict__ in_slot, int32_t *__restrict__ act_out,
@@ -1385,7 +1419,7 @@ __global__ void __launch_bounds__(64 * WPB, NJ > 4 ? 1 : (CL ? GMZ_CL_WPS : (HIN
   if (lane < 16) tp_lds[threadIdx.x / WAVE][lane] = 0;
 #endif
   TP_STAMP(tk0);
-  const int active0 = D.gs[g].active, depth0 = D.gs[g].depth;
+  const int active0 = __builtin_amdgcn_readfirstlane(D.gs[g].active), depth0 = __builtin_amdgcn_readfirstlane(D.gs[g].depth);
   expand_backup_game<NJ, HINT || CL, CL>(D, g, lane, logits_in, value_in, reward_in);
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_s_waitcnt(0);

@@ -62,19 +62,21 @@ class BatchedSelfPlayEngine:
         self.lib = _lib.load()
         self.device = torch.device(device)
         self.G, self.A, self.size = int(num_games), c.ACTION_SPACE_SIZE, c.BOARD_SIZE
-        if descent_hint is None:  # the next-visit prefetch and cached exp rows: faster at every G measured,
-            descent_hint = True   # with the dense rows below 4,096 games per engine and the lists from there
-            # (profiles/r03_tree_layout_ab.txt); the no-hint dense kernels keep the reference's
-            # exp(logit + t - max) arithmetic (A/B and tests)
+        if layout is None:
+            layout = default_layout(self.G)
+        if layout not in ("dense", "lists"):
+            raise ValueError("layout: 'dense' (every node's full child row) or 'lists' (compact child lists)")
+        if descent_hint is None:
+            # dense rows: the hint kernels (cached exp rows + next-visit prefetch) at every G measured; the
+            # no-hint dense kernels keep the reference's exp(logit + t - max) form (A/B and tests).
+            # Compact lists always use the cached exp rows; there the hint only switches the prefetch,
+            # which measured slower (8,192 games: 110 vs 125 us; profiles/r03_tree_layout_ab.txt)
+            descent_hint = layout == "dense"
         self.mode = 1 if c.MCTS_IMPLEMENTATION == "MuZero" else 0
         self.slots_per_game = c.NUM_SIMULATIONS + 2
         if wpb not in (None, 1, 4):
             raise ValueError("wpb: games per workgroup of the fused expand/select kernel must be None, 1 or 4")
         self.descent_hint = bool(descent_hint)
-        if layout is None:
-            layout = default_layout(self.G)
-        if layout not in ("dense", "lists"):
-            raise ValueError("layout: 'dense' (every node's full child row) or 'lists' (compact child lists)")
         self.layout = layout
         # flags (include/gmz.h): bit 0 no hint; bits 1 / 2 force 4-wave / 1-wave workgroups (None: by occupancy);
         # bit 3 compact child lists for non-root nodes
@@ -292,8 +294,8 @@ class SplitSelfPlayEngine:
         self.mode = 1 if c.MCTS_IMPLEMENTATION == "MuZero" else 0
         self.slots_per_game = c.NUM_SIMULATIONS + 2
         g = self.g = G // parts
-        if descent_hint is None:  # the cached-exp softmax for every part, as one engine with every game
-            descent_hint = True   # (the layout may differ per part: results are identical)
+        # descent_hint / layout None: each part's defaults — the cached-exp softmax in every part, as one
+        # engine with every game (the layout may differ per part: results are identical)
         if max_grid is None:
             max_grid = torch.cuda.get_device_properties(self.device).multi_processor_count * 3 // 4 if parts > 1 else 0
         if net is None:

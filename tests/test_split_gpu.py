@@ -110,9 +110,9 @@ def test_split_positions_and_masks(mods):
 
 
 def test_split_with_another_layout_plays_the_same_games(mods):
-    """At 4,096 games one engine runs the compact child lists (engine.default_layout: G >= 4096) and two
-    halves of 2,048 the dense rows, both with the cached-exp softmax (descent_hint, the default at every
-    G), so the split engine plays the one engine's games bit for bit (15x15 / 64 sims MuZero, HashNet,
+    """At 4,096 games one engine runs the compact child lists (engine.default_layout: G >= 4096; without
+    the prefetch) and two halves of 2,048 the dense rows with the hint kernels: the cached-exp softmax in
+    both, so the split engine plays the one engine's games bit for bit (15x15 / 64 sims MuZero, HashNet,
     device Gumbel noise)."""
     E, N, W, GmzConfig = mods
     cfg = GmzConfig(BOARD_SIZE=15, NUM_SIMULATIONS=64, MCTS_IMPLEMENTATION="MuZero")
@@ -120,7 +120,7 @@ def test_split_with_another_layout_plays_the_same_games(mods):
     one = E.BatchedSelfPlayEngine(cfg, num_games=G, seed=9)
     two = E.SplitSelfPlayEngine(cfg, num_games=G, seed=9, parts=2)
     assert one.layout == "lists" and all(e.layout == "dense" for e in two.engines)
-    assert one.descent_hint and all(e.descent_hint for e in two.engines)
+    assert not one.descent_hint and all(e.descent_hint for e in two.engines)
     one.reset_games()
     two.reset_games()
     _same(_moves(one, 3), _moves(two, 3))

@@ -79,7 +79,7 @@ PY
     done ;;
   layout_libs)  # k_expand_select of the list layout per occupancy build (GMZ_LIB) at each G, one stream
     for G in ${1:-4096 8192}; do
-      for LIB in libgmz.so _alt/libgmz_cl5.so _alt/libgmz_cl6.so _alt/libgmz_cl7.so; do
+      for LIB in libgmz.so ${LIBS:-_alt/libgmz_cl6.so _alt/libgmz_cl8.so}; do
         for H in off on; do
           N=G${G}_$(basename $LIB .so)_$H
           GMZ_LIB=$PWD/datou-gomoku-muzero_amd/$LIB timeout -k 10 300 python -u bench.py --games $G --streams 1 --steps 3 --warmup 1 \
