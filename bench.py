@@ -39,6 +39,8 @@ Prints ONE JSON line on rank 0 (schema: the driver contract) including
   sublines      : BASELINE configs 5 and 1 on the GPU, a few steps each after the headline engine is freed:
                   C5 = 19x19, 800 sims, 16 blocks (G games); C1 = 9x9 AlphaZero, 50 sims (G games), each with
                   moves/s and the tower's and tree kernel's roofline fractions (one stream: every launch alone);
+                  g8192 = config 2's search on 8,192 trees as one engine (the tree kernel alone at SURVEY §8(d)'s
+                  measurement point; skipped, and said so, on a GPU without ~230 GiB free);
   worker        : the drop-in worker (worker.gpu_selfplay_worker) over torch.multiprocessing queues with a
                   consumer process unpickling every payload (the reference's process graph): moves/s over
                   the steady-state moves including every per-move and per-game record, and its ratio to
@@ -138,8 +140,10 @@ def parse(argv=None):
     ap.add_argument("--cpu-baseline-sec", type=float, default=20.0)
     ap.add_argument("--cpu-baseline-procs", type=int, default=16,
                     help="single-threaded oracle processes (capped by the cores this process may use)")
-    ap.add_argument("--sublines", default="c5,c1",
-                    help="BASELINE configs measured besides the headline: c5 (19x19/800/16 blocks), c1 (9x9 AlphaZero/50)")
+    ap.add_argument("--sublines", default="c5,c1,g8192",
+                    help="measured besides the headline: c5 (BASELINE config 5: 19x19/800/16 blocks), c1 (config 1: 9x9 "
+                         "AlphaZero/50), g8192 (config 2's search on 8,192 trees, one engine: the tree kernel's "
+                         "SURVEY 8(d) measurement point)")
     ap.add_argument("--subline-games", type=int, default=1024)
     ap.add_argument("--c5-steps", type=int, default=3)
     ap.add_argument("--c1-steps", type=int, default=10)
@@ -567,22 +571,34 @@ SUBLINES = {  # BASELINE.json configs run on the GPU besides the headline (C2)
     "c1": dict(size=9, sims=50, mode="AlphaZero", blocks=8,
                name="C1 on the GPU: 9x9 AlphaZero, 50 sims/move, 8 blocks (BASELINE config 1's search; the "
                     "reference runs it with one CPU worker)"),
+    # SURVEY §8(d)'s tree-kernel measurement point (>= 8,192 trees): config C2's search with 8,192 games as ONE
+    # engine on one stream (compact child lists, engine.default_layout), so roofline_tree is the kernel alone
+    "g8192": dict(size=15, sims=400, mode="MuZero", blocks=8, games=8192, streams=1, steps=2, warmup=1,
+                  min_free_gb=230,
+                  name="C2's search at 8,192 trees on one GPU (one engine, one stream): the tree kernel at SURVEY "
+                       "8(d)'s >= 8,192-tree measurement point"),
 }
 
 
 def subline(args, key, rank, world, dist, backend):
     c = SUBLINES[key]
-    G = args.subline_games
-    steps, warmup = (args.c5_steps, 1) if key == "c5" else (args.c1_steps, 2)
+    G = c.get("games", args.subline_games)
+    steps, warmup = {"c5": (args.c5_steps, 1), "c1": (args.c1_steps, 2)}.get(key, (c.get("steps", 2), c.get("warmup", 1)))
+    if "min_free_gb" in c:  # a bounded leg: skipped (and said so) when this GPU lacks the memory
+        torch.cuda.empty_cache()
+        free = torch.cuda.mem_get_info()[0] / 2 ** 30
+        if collective_max(-free, dist, backend) > -c["min_free_gb"]:
+            return {"config": c["name"], "skipped": "needs %d GiB free per GPU, %.0f GiB free" % (c["min_free_gb"], free)}
     r = selfplay_leg(args, rank, world, dist, backend, c["size"], c["sims"], c["mode"], c["blocks"], G, steps, warmup,
-                     log_prefix="[%s] " % key)
+                     streams=c.get("streams"), log_prefix="[%s] " % key)
     out = {"config": c["name"], "value": G * steps * world / r["dt"], "unit": "moves/s", "n_gpus": world,
            "games_per_gpu": G, "steps": steps, "warmup": warmup, "ms_per_step": r["dt"] / steps * 1e3,
            "waves_per_move": r["waves"] / max(1, steps), "streams": r["streams"], "dtype": args.precision}
     for k in ("roofline", "roofline_tree"):
         if k in r:
             q = r[k]
-            out[k] = {x: q[x] for x in ("kernel", "achieved", "unit", "frac", "mean_launch_ms") if x in q}
+            out[k] = {x: q[x] for x in ("kernel", "achieved", "unit", "frac", "mean_launch_ms", "bytes_per_launch",
+                                        "layout", "games_per_launch", "mean_select_levels") if x in q}
     return out
 
 

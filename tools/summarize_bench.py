@@ -18,8 +18,12 @@ def main(path):
         print("single stream: tower %.3f ms frac %.3f | tree %.1f us frac %.3f" % (
             ss["tower"]["mean_launch_ms"], ss["tower"]["frac"], ss["tree"]["mean_launch_ms"] * 1e3, ss["tree"]["frac"]))
     for k, v in d.get("sublines", {}).items():
-        print("%s: %.1f moves/s  tower frac %.3f  tree frac %.3f" % (
-            k, v["value"], v.get("roofline", {}).get("frac", 0), v.get("roofline_tree", {}).get("frac", 0)))
+        if "skipped" in v:
+            print("%s: skipped (%s)" % (k, v["skipped"]))
+            continue
+        print("%s: %.1f moves/s  tower frac %.3f  tree frac %.3f (%.1f us)" % (
+            k, v["value"], v.get("roofline", {}).get("frac", 0), v.get("roofline_tree", {}).get("frac", 0),
+            v.get("roofline_tree", {}).get("mean_launch_ms", 0) * 1e3))
     w = d.get("worker")
     if w:
         print("worker: %.1f moves/s (%.3f of engine), %d games, %d slices" % (
