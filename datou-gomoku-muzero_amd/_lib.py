@@ -48,6 +48,7 @@ _SIGS = {
     "gmz_engine_finish_move": ([P, P, P, P, P], I),
     "gmz_engine_play": ([P, P, P, I, P], I),
     "gmz_engine_root_stats": ([P, P, P, P, P, P, P], I),
+    "gmz_engine_max_visited_children": ([P, P], I),
     "gmz_engine_wave_k": ([P, P, P], I),
     "gmz_engine_wave_depth": ([P, P, P], I),
     "gmz_engine_tree_counters": ([P, P, I, P], I),

@@ -1548,6 +1548,18 @@ __global__ void k_root_stats(Dev D, int32_t *visits, int32_t *root_n, float *roo
   }
 }
 
+// max over the non-root nodes (1 .. n_nodes - 1 of each game) of the header's visited-children count
+__global__ void k_max_nvis(Dev D, int32_t *out) {
+  const int g = blockIdx.y;
+  if (g >= D.G) return;
+  const int n = D.gs[g].n_nodes;
+  int m = 0;
+  for (int u = 1 + blockIdx.x * blockDim.x + threadIdx.x; u < n && u < D.S; u += gridDim.x * blockDim.x)
+    m = max(m, D.hdr[(size_t)g * D.S + u].z);
+  m = wave_max_i(m);
+  if ((threadIdx.x & (WAVE - 1)) == 0) atomicMax(out, m);
+}
+
 }  // namespace gmz
 
 using namespace gmz;
@@ -1906,6 +1918,22 @@ GMZ_EXPORT int gmz_tree_prof_read(unsigned long long *out16, int reset) {
   return 0;
 }
 #endif
+
+GMZ_EXPORT int gmz_engine_max_visited_children(gmz_engine *e, int32_t *out) {
+  if (!e || !out) return fail("null argument");
+  int32_t *d = nullptr;
+  GMZ_HIP(hipMalloc(&d, sizeof(int32_t)));
+  int rc = 0;
+  if (hipMemset(d, 0, sizeof(int32_t)) != hipSuccess) rc = fail("gmz_engine_max_visited_children: memset failed");
+  if (!rc) {
+    hipLaunchKernelGGL(k_max_nvis, dim3(1, e->D.G), dim3(256), 0, 0, e->D, d);
+    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(out, d, sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess)
+      rc = fail("gmz_engine_max_visited_children: kernel failed");
+  }
+  (void)hipFree(d);
+  return rc;
+}
 
 GMZ_EXPORT int gmz_engine_root_stats(gmz_engine *e, int32_t *visits, int32_t *root_n, float *root_w, float *mm_max,
                                      float *mm_min, void *stream) {

@@ -255,6 +255,12 @@ class BatchedSelfPlayEngine:
         t = c.to(torch.int64).sum(0).tolist()
         return dict(backups=t[0], backup_levels=t[1], selects=t[2], select_levels=t[3])
 
+    def max_visited_children(self):
+        """Largest visited-children count of any non-root node in the current trees (diagnostics, synchronous)."""
+        out = ctypes.c_int32()
+        check(self.lib.gmz_engine_max_visited_children(self.handle, ctypes.byref(out)))
+        return out.value
+
     def root_stats(self):
         G, A, dev = self.G, self.A, self.device
         visits = torch.zeros(G, A, dtype=torch.int32, device=dev)

@@ -167,6 +167,9 @@ int gmz_engine_tree_counters(gmz_engine *e, int32_t *ctr_dev, int reset, void *s
  * int32[G][A], root (N, W) and MinMaxStats (max, min) per game. */
 int gmz_engine_root_stats(gmz_engine *e, int32_t *visits_dev, int32_t *root_n_dev, float *root_w_dev,
                           float *mm_max_dev, float *mm_min_dev, void *stream);
+/* Diagnostics: the largest number of visited children of any NON-ROOT node in the current trees
+ * (node header count; with compact child lists the longest list), *out on the host.  Synchronous. */
+int gmz_engine_max_visited_children(gmz_engine *e, int32_t *out);
 
 /* ------------------------------------------------------------------ HashNet test network */
 /* Deterministic integer-hash network (definition: oracle/hashnet.py) used for tree parity.

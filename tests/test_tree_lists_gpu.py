@@ -51,6 +51,9 @@ def _positions(size, G, rs, max_stones):
     return boards, players, lastm
 
 
+MAX_NVIS = {}  # (size, sims, mode, G, layout) -> longest child list seen after any move
+
+
 def _play(E, size, sims, mode, G, pos, gumbels, fuse=True, **kw):
     """len(gumbels) moves (search + play) from the positions; per move the search outputs + root stats."""
     eng = E.BatchedSelfPlayEngine(None, num_games=G, BOARD_SIZE=size, NUM_SIMULATIONS=sims, MCTS_IMPLEMENTATION=mode,
@@ -58,11 +61,13 @@ def _play(E, size, sims, mode, G, pos, gumbels, fuse=True, **kw):
     eng.fuse_waves = fuse
     eng.set_positions(*pos)
     outs = []
+    key = (size, sims, mode, G, eng.layout)
     for gm in gumbels:
         pol, val, act = eng.search(gumbel=gm)
         visits, rn, rw, mx, mn = eng.root_stats()
         torch.cuda.synchronize()
         outs.append([x.cpu().numpy().copy() for x in (pol, val, act, visits, rn, rw, mx, mn)])
+        MAX_NVIS[key] = max(MAX_NVIS.get(key, 0), eng.max_visited_children())
         eng.play(reset_finished=True)
     eng.close()
     del eng
@@ -96,6 +101,12 @@ def test_lists_equal_dense(E, size, sims, mode, G, max_stones, moves, hint):
     dense = _play(E, size, sims, mode, G, pos, gumbels, descent_hint=True, layout="dense")
     lists = _play(E, size, sims, mode, G, pos, gumbels, descent_hint=hint, layout="lists")
     _assert_same(dense, lists, "lists (prefetch=%s) vs dense" % hint)
+    nv = MAX_NVIS[(size, sims, mode, G, "lists")]
+    assert nv == MAX_NVIS[(size, sims, mode, G, "dense")]  # the same trees
+    if (size, sims) == (9, 800):  # the case that exercises lists longer than one wave
+        assert nv > 64, nv
+    if size == 6 and sims == 400:  # and the one whose nodes visit every child (the float32 rule)
+        assert nv == 36, nv
 
 
 @pytest.mark.parametrize("size,sims,mode,G", [(15, 400, "MuZero", 40), (9, 50, "AlphaZero", 24), (6, 400, "MuZero", 16)])
