@@ -111,6 +111,11 @@ struct Dev {
 #ifndef GMZ_HINT_WPS
 #define GMZ_HINT_WPS 2
 #endif
+// largest exponent scale * (1 - nq0) the cached-exp softmax takes (f64 overflows past exp(709.8); A terms
+// summed): beyond it a level uses the logits form
+#ifndef GMZ_EX_MAX_EXP
+#define GMZ_EX_MAX_EXP 600.0
+#endif
 // waves per SIMD the compact-list kernels are compiled for (the prefetch variant at most 6: two LDS
 // buffers per wave): 6 = 80 VGPRs, 2 spilled values; measured at 8,192 games 107.8 us vs 109.9 at 5 (no
 // spills) and 107.3 at 8 (14 spills) (profiles/r03_tree_layout_ab.txt)
@@ -450,7 +455,11 @@ __device__ int select_nonroot(const Dev &D, const uint64_t (&lg)[NJ], int g, int
     }
   }
   TP_STAMP(tp1);
-  if (HINT && nvis < D.A) {
+  // the cached-exp form p ~ E * exp(t - t0) needs exp(scale * (nq - nq0)) <= exp(scale * (1 - nq0)) to stay
+  // far from f64 overflow; past GMZ_EX_MAX_EXP (visit counts in the thousands: scale = c_visit + max N) the
+  // level takes the logits form below, the reference's exp(logit + t - max) (tools/deep_tree_probe.py)
+  const bool ex_ok = !nz.have_range || (double)(D.c_visit + max_n) * D.c_scale * (1.0 - nz.nq0) <= GMZ_EX_MAX_EXP;
+  if (HINT && nvis < D.A && ex_ok) {
     // _get_transformed_completed_Qs, some child unvisited: float64 array (mcts.py:141-149), and
     // _get_improved_policy's softmax of logits + transformed Q over the legal set (mcts.py:151-156).
     // Latency-bound regime (the hint kernels: <= 2 waves per SIMD): softmax is shift invariant, so
@@ -487,10 +496,16 @@ __device__ int select_nonroot(const Dev &D, const uint64_t (&lg)[NJ], int g, int
     const double inv_s = 1.0 / sum;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) p[j] = x[j] * inv_s;
-  } else if (!HINT && nvis < D.A) {
-    // the same quantities from the logits: one exp per child (mcts.py:141-156)
+  } else if (nvis < D.A) {
+    // the same quantities from the logits: one exp per child (mcts.py:141-156); the hint kernels' rows
+    // carry E, so they read the node's logits here
     const double scale = (double)(D.c_visit + max_n) * D.c_scale;
     const double den = (double)nz.den_f;
+    float lv[NJ];
+    if constexpr (HINT) logits_load<NJ>(D, D.logits + ((size_t)g * D.S + u) * D.A, lane, lv);
+    else
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) lv[j] = (float)cur.v[j];
     double x[NJ], m = -INFINITY;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
@@ -503,7 +518,7 @@ __device__ int select_nonroot(const Dev &D, const uint64_t (&lg)[NJ], int g, int
       const double t = scale * nq;
       const int a = lane + WAVE * j;
       const bool ok = a < D.A && ((lg[j] >> lane) & 1ull);
-      x[j] = ok ? (double)cur.v[j] + t : -INFINITY;
+      x[j] = ok ? (double)lv[j] + t : -INFINITY;
       m = fmax(m, x[j]);
     }
     m = dred_max_d(m);
@@ -776,25 +791,51 @@ __device__ int select_nonroot_cl(const Dev &D, const uint64_t (&lg)[NJ], int lm,
     }
   } else {
     // visited children: R[a] = -(E * exp(scale * nq - t0)) (select_nonroot's cached-exp softmax term);
-    // entries past the first 64 (rare) are read from HBM in each pass
+    // entries past the first 64 (rare) are read from HBM in each pass.  Past GMZ_EX_MAX_EXP (select_nonroot's
+    // ex_ok) the entries store -nq instead, and the slots then hold the logits form exp(logit + t - max)
+    const bool ex_ok = !nz.have_range || scale * (1.0 - nz.nq0) <= GMZ_EX_MAX_EXP;
     auto scatter = [&](const int4 &e) {
       const int aa = e.x >> 16;
       double x = R[aa];
+      double nq = nz.nq0;
       if (nz.have_range) {
         const float v = __int_as_float(e.z) / (float)e.y;  // get_qsa (mcts.py:35-38)
         const float dv = D.disc_f * v;
         const float q = __int_as_float(e.w) + dv;
         double y = ((double)q - (double)nz.mm_min) / (double)nz.den_f;
         y = (y < 1.0) ? y : 1.0;
-        const double nq = (y > 0.0) ? y : 0.0;
-        x *= exp(scale * nq - t0);
+        nq = (y > 0.0) ? y : 0.0;
+        if (ex_ok) x *= exp(scale * nq - t0);
       }
-      R[aa] = -x;
+      R[aa] = ex_ok ? -x : -nq;
     };
     if (lane < nvis) scatter(e0);
     for (int i0 = WAVE; i0 < nvis; i0 += WAVE)
       if (i0 + lane < nvis) scatter(*(const int4 *)(edge_row(D, g, u) + i0 + lane));
     asm volatile("" ::: "memory");
+    if (!ex_ok) {  // select_nonroot's logits form, written back into the slots (sign: visited)
+      const float *lrow = D.logits + ((size_t)g * D.S + u) * D.A;
+      double m = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int aa = lane + WAVE * j;
+        const double r = R[aa];
+        const double t = scale * (signbit(r) ? -r : nz.nq0);
+        const double x = ((lm >> j) & 1) ? (double)lrow[aa < D.A ? aa : D.A - 1] + t : -INFINITY;
+        m = fmax(m, x);
+      }
+      m = dred_max_d(m);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int aa = lane + WAVE * j;
+        const double r = R[aa];
+        const double t = scale * (signbit(r) ? -r : nz.nq0);
+        const double x = ((lm >> j) & 1) ? (double)lrow[aa < D.A ? aa : D.A - 1] + t : -INFINITY;
+        const double xe = (x == -INFINITY) ? 0.0 : exp(x - m);
+        R[aa] = signbit(r) ? -xe : xe;
+      }
+      asm volatile("" ::: "memory");
+    }
     // the node's slots in registers (negative: visited); the softmax sum over the legal slots in
     // select_nonroot's order (per lane j = 0..NJ-1, then the wave)
     double xs[NJ];
