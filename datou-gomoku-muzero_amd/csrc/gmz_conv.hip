@@ -7,7 +7,7 @@
 // kernels plus the zeroing pass it runs before each of them (trainer.py, training step of
 // loss.py:30-158).
 //
-// Work item = (board, half of the output channels): 2N items for N boards, so the 256 CUs see ~3
+// Work item = (board, half of the output channels; the halves on one XCD): 2N items for N boards, so the 256 CUs see ~3
 // rounds at N = 360 instead of 1.4.  Two 256-thread workgroups per CU (one padded image each,
 // 78 KB at 15x15).  Per item: the board's NHWC activations are DMA'd (global_load_lds) into the
 // padded LDS image of k_tower3 (gmz_net.hip: cell (yy, xx) at yy*RS + xx*PS, conflict-free
@@ -113,7 +113,11 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
   const int nq = w & 1, pg = w >> 1;
   const int g4 = lane >> 4;
   const int cg = (g4 & 1) * 8 + (g4 >> 1);
-  const int half = blockIdx.x & 1;
+  // XCD-aware items: workgroups are dealt to the 8 XCDs round-robin by index, so workgroup i runs on
+  // XCD i % 8; the two halves of a board are workgroups i and i ^ 8 (same XCD, dispatched together),
+  // and the second one's board DMA is served by that XCD's L2 instead of HBM
+  const int half = (blockIdx.x >> 3) & 1;
+  const int b0 = (blockIdx.x >> 4) * 8 + (blockIdx.x & 7);  // first board; also the statistics slot
   const int ntile0 = half * 4 + nq * NTW;  // this wave's first n-tile (of 8)
 
   for (int i = tid; i < I::BYTES / 16; i += NTHR) *(uint4 *)(img + i * 16) = make_uint4(0, 0, 0, 0);
@@ -146,7 +150,7 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
     for (int e = 0; e < 4; ++e) s1[nt][e] = s2[nt][e] = 0.f;
   int nvalid = 0;
 
-  for (int b = blockIdx.x >> 1; b < N; b += gridDim.x >> 1) {
+  for (int b = b0; b < N; b += gridDim.x >> 1) {
     // ---- board b -> image interior: 1 KB pieces of each board row's run of cells
     const uint8_t *src = (const uint8_t *)(x + (size_t)b * A * CC);
     for (int j = w; j < H * I::RUN_DMA; j += NW) {
@@ -255,7 +259,7 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
       a += (double)red[(g * 64 + tid) * 2];
       q += (double)red[(g * 64 + tid) * 2 + 1];
     }
-    double *out = stats + ((size_t)(blockIdx.x >> 1) * CC + half * 64 + tid) * 3;
+    double *out = stats + ((size_t)b0 * CC + half * 64 + tid) * 3;
     out[0] = a;
     out[1] = q;
     out[2] = (double)nvalid * A;
@@ -425,8 +429,8 @@ static int cu_count_conv() {
 
 constexpr int CONV_PG = 2;  // position groups per workgroup: 2 -> 4 waves, 8|7 tiles per wave
 
-int conv3_grid(int N) {
-  const long items = 2L * N, cap = 2L * 2 * cu_count_conv();
+int conv3_grid(int N) {  // a multiple of 16 (whole XCD pairs; workgroups past the boards do nothing)
+  const long items = (2L * N + 15) / 16 * 16, cap = 2L * 2 * cu_count_conv() / 16 * 16;
   return (int)(items < cap ? items : cap);
 }
 
