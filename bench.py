@@ -397,8 +397,8 @@ def trainer_trace_summary(args):
         d = json.load(open(path))
     except Exception:
         return None
-    out = dict(d.get("dominant", {}))
-    out.update(bound="mfma", launches_per_step=d.get("launches_per_step"), weight_gradient=d.get("weight_gradient"),
+    out = dict(d.get("dominant", {}))  # launches_per_step / ms_per_step here: the dominant kernel's, per step
+    out.update(bound="mfma", step_launches=d.get("launches_per_step"), weight_gradient=d.get("weight_gradient"),
                source="builder-measured: %s (%s)" % (os.path.relpath(path, REPO), d.get("source", "")))
     return out
 
