@@ -93,16 +93,17 @@ PEAK_MFMA_TFLOPS = 2500.0   # MI355X dense f16 / bf16 MFMA (MI355X_MICROARCH.md,
 PEAK_HBM_GBS = 8000.0
 
 
-def pmc_traffic(path, args, G, az):
-    """HBM bytes per launch from a committed PMC summary (tools/pmc_round2.sh -> tools/pmc_summary.py) when it
-    was measured on this configuration (15x15, 8 blocks, MuZero, G = 1024, same precision and streams)."""
+def pmc_traffic(path, args, G, az, streams):
+    """HBM bytes per launch from a committed PMC summary (tools/gpu.sh pmc -> tools/pmc_summary.py) when it
+    was measured on this configuration (15x15, 8 blocks, MuZero, G = 1024, same precision and the same
+    number of streams as this run resolved to)."""
     if not os.path.exists(path) or (args.size, args.blocks, G) != (15, 8, 1024) or az:
         return None
     try:
         pm = json.load(open(path))
     except Exception:
         return None
-    if pm.get("precision", "bf16") != args.precision or int(pm.get("streams", 1)) != int(args.streams or 1):
+    if pm.get("precision", "bf16") != args.precision or int(pm.get("streams", 1)) != int(streams or 1):
         return None
     return pm.get("hbm_bytes_per_launch")
 
@@ -486,7 +487,7 @@ def selfplay_leg(args, rank, world, dist, backend, size, sims, mode, blocks, G, 
         # (with one stream = the per-launch figure; with two, launches of the two streams overlap)
         achieved = flop * n_launch / (busy * 1e-3) / 1e12 if busy > 0 else 0.0
         is_c2 = (size, blocks, G, mode) == (15, 8, 1024, "MuZero")
-        traffic = pmc_traffic(args.pmc_file, args, G, az) if is_c2 else None
+        traffic = pmc_traffic(args.pmc_file, args, G, az, streams) if is_c2 else None
         kname = ("k_tower3<%d,REPR> (representation tower, stem + %d fused convs + head 1x1 convs)" % (size, 2 * blocks)
                  if az else "k_tower3<%d,DYN> (dynamics tower, %d fused convs + head 1x1 convs)" % (size, 1 + 2 * blocks))
         res["roofline"] = {"bound": "mfma", "kernel": kname + ", " + args.precision,
@@ -504,7 +505,7 @@ def selfplay_leg(args, rank, world, dist, backend, size, sims, mode, blocks, G, 
         bpl = tree_bytes(ctr, A) / n_tree
         gbs = bpl * n_tree / (busy_tree * 1e-3) / 1e9 if busy_tree > 0 else 0.0
         is_c2 = (size, blocks, G, mode) == (15, 8, 1024, "MuZero")
-        tr = pmc_traffic(args.pmc_tree_file, args, G, az) if is_c2 else None
+        tr = pmc_traffic(args.pmc_tree_file, args, G, az, streams) if is_c2 else None
         res["roofline_tree"] = {
             "bound": "hbm", "kernel": "k_expand_select<%d> (backup of wave i + selection of wave i+1)" % ((A + 63) // 64),
             "achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS,

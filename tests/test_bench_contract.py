@@ -103,3 +103,20 @@ def test_timer_stats_union_of_launch_intervals():
     assert abs(mean - (2 + 1 + 2 + 0.5 + 0.5) / 5) < 1e-12
     assert abs(busy - (3 + 1 + 0.5 + 0.5)) < 1e-12
     assert bench.timer_stats([], base) == (0, 0.0, 0.0)
+
+
+def test_pmc_traffic_matches_the_resolved_stream_count():
+    """roofline.traffic comes from the committed PMC pass only when that pass measured this
+    configuration: C2 with the number of streams the run resolved to (the default two for C2, which
+    the command line leaves unset)."""
+    import json
+    import bench
+    pm = json.load(open(os.path.join(REPO, "profiles", "pmc_tower_latest.json")))
+
+    class A:
+        size, blocks, precision, streams = 15, 8, pm["precision"], None
+    path = os.path.join(REPO, "profiles", "pmc_tower_latest.json")
+    assert bench.pmc_traffic(path, A, 1024, False, int(pm["streams"])) == pm["hbm_bytes_per_launch"]
+    assert bench.pmc_traffic(path, A, 1024, False, int(pm["streams"]) + 1) is None
+    assert bench.pmc_traffic(path, A, 2048, False, int(pm["streams"])) is None
+    assert bench.pmc_traffic(path, A, 1024, True, int(pm["streams"])) is None
