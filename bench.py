@@ -588,8 +588,12 @@ def subline(args, key, rank, world, dist, backend):
     if "min_free_gb" in c:  # a bounded leg: skipped (and said so) when this GPU lacks the memory
         torch.cuda.empty_cache()
         free = torch.cuda.mem_get_info()[0] / 2 ** 30
-        if collective_max(-free, dist, backend) > -c["min_free_gb"]:
-            return {"config": c["name"], "skipped": "needs %d GiB free per GPU, %.0f GiB free" % (c["min_free_gb"], free)}
+        # ranks sharing a GPU (the gloo rehearsal of N > 1 on one card) each need the leg's memory
+        share = ranks_per_gpu(dist)
+        need = c["min_free_gb"] * share
+        if collective_max(-free, dist, backend) > -need:
+            return {"config": c["name"], "skipped": "needs %d GiB free per GPU (%d rank(s) per GPU), %.0f GiB free"
+                    % (need, share, free)}
     r = selfplay_leg(args, rank, world, dist, backend, c["size"], c["sims"], c["mode"], c["blocks"], G, steps, warmup,
                      streams=c.get("streams"), log_prefix="[%s] " % key)
     out = {"config": c["name"], "value": G * steps * world / r["dt"], "unit": "moves/s", "n_gpus": world,
@@ -601,6 +605,19 @@ def subline(args, key, rank, world, dist, backend):
             out[k] = {x: q[x] for x in ("kernel", "achieved", "unit", "frac", "mean_launch_ms", "bytes_per_launch",
                                         "layout", "games_per_launch", "mean_select_levels") if x in q}
     return out
+
+
+def ranks_per_gpu(dist):
+    """How many ranks use this rank's GPU (1 on a node with one rank per GPU): ranks are matched by
+    host name and the device's PCI location, gathered over the process group."""
+    if dist is None:
+        return 1
+    import socket
+    p = torch.cuda.get_device_properties(torch.cuda.current_device())
+    me = (socket.gethostname(), p.pci_domain_id, p.pci_bus_id, p.pci_device_id)
+    everyone = [None] * dist.get_world_size()
+    dist.all_gather_object(everyone, me)
+    return sum(1 for x in everyone if x == me)
 
 
 def consumer_proc(qs, ctl, report):

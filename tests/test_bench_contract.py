@@ -120,3 +120,27 @@ def test_pmc_traffic_matches_the_resolved_stream_count():
     assert bench.pmc_traffic(path, A, 1024, False, int(pm["streams"]) + 1) is None
     assert bench.pmc_traffic(path, A, 2048, False, int(pm["streams"])) is None
     assert bench.pmc_traffic(path, A, 1024, True, int(pm["streams"])) is None
+
+
+def _rank_share(rank, world, port, out):
+    import torch.distributed as dist
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import torch
+
+    class P:  # both ranks report the same device (the one-card rehearsal)
+        pci_domain_id, pci_bus_id, pci_device_id = 0, 3, 0
+    torch.cuda.get_device_properties = lambda i: P
+    torch.cuda.current_device = lambda: 0
+    out[rank] = bench.ranks_per_gpu(dist)
+    dist.destroy_process_group()
+
+
+def test_ranks_per_gpu_counts_ranks_sharing_a_device():
+    import bench
+    assert bench.ranks_per_gpu(None) == 1
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_rank_share, args=(2, _free_port(), out), nprocs=2, join=True)
+    assert out[0] == out[1] == 2
