@@ -689,11 +689,7 @@ __device__ int select_nonroot_cl(const Dev &D, const uint64_t (&lg)[NJ], int lm,
   const double scale = (double)(D.c_visit + max_n) * D.c_scale;
   const double t0 = scale * nz.nq0;
   int a = 0;
-#ifdef GMZ_EXP_NOALLV
-  if (false) {
-#else
   if (nvis >= D.A) {
-#endif
     // every child visited (rare below the root): the reference's array may be float32 -> improved_policy's
     // rule (transformed_q's float32/float64 choice, then the softmax) on N and q gathered into the
     // buffer's row, computed slot by slot in passes that recompute the same values (no row in registers)
@@ -1237,11 +1233,7 @@ __device__ __forceinline__ void expand_backup_game(const Dev &D, int g, int lane
     }
 #pragma unroll 1
     for (int a = lane; a < A; a += WAVE)  // one exp live at a time (VGPR budget of the fused kernel)
-#ifdef GMZ_EXP_NOEXP2
-      nx[a] = ((double)logits_in[(size_t)g * A + a] - (double)lm);
-#else
       nx[a] = exp((double)logits_in[(size_t)g * A + a] - (double)lm);
-#endif
   } else {
     for (int a = lane; a < A; a += WAVE) {
       nl[a] = logits_in[(size_t)g * A + a];
@@ -1328,11 +1320,7 @@ __device__ __forceinline__ void expand_backup_game(const Dev &D, int g, int lane
   if (mx > st.mm_max) st.mm_max = mx;
   if (mn < st.mm_min) st.mm_min = mn;
   st.sim += k;
-#ifdef GMZ_EXP_NOHALV
-  if (false) {
-#else
   if (ready_next_phase(D, st)) {  // _sequential_halving (mcts.py:182-185)
-#endif
     // _get_transformed_completed_Qs of the root (mcts.py:141-149, transformed_q) for the selected actions
     // only: the reductions over the children (max N, any unvisited, float32 clamps) in one pass, then each
     // lane's selected action's value (the same arithmetic as transformed_q, no row held in registers)
