@@ -532,7 +532,30 @@ class _Dynamics(_Trunk):
             emb = emb.contiguous(memory_format=torch.channels_last)   # cat keeps channels-last
         nxt = super().forward(torch.cat((h, emb), dim=1), mask)
         fc0, act, fc2 = self.reward_fc
-        return nxt, fc2(act(_linear(fc0, nxt.reshape(n, -1))))
+        return nxt, fc2(act(_linear_flat(fc0, nxt)))
+
+
+FLAT_NHWC = True  # channels-last flatten for the K = 28,800 Linears (False: NCHW copy per use; A/B)
+
+
+def _bigk_weight(w, dt, perm):
+    """w (f32 [O, K]) in the autocast dtype, cached per optimiser step (version counter, as
+    _packed_conv_weight; inside a captured step the first use converts).  perm = (C, HW): the columns
+    reordered from the reference's NCHW flatten (k = c*HW + p) to the channels-last one (k = p*C + c),
+    so a channels-last hidden state flattens as a view instead of a transposing copy per use."""
+    key = ("bigk", dt, perm)
+    cache = w.__dict__.setdefault("_gmz_pack", {})
+    hit = cache.get(key)
+    if hit is not None and hit[0] == w._version:
+        return hit[1]
+    if perm is None:
+        out = w.detach().to(dt)
+    else:
+        C, HW = perm
+        out = torch.empty(w.shape, dtype=dt, device=w.device)
+        out.view(w.shape[0], HW, C).copy_(w.detach().view(w.shape[0], C, HW).transpose(1, 2))
+    cache[key] = (w._version, out)
+    return out
 
 
 class _BigKLinear(torch.autograd.Function):
@@ -540,28 +563,44 @@ class _BigKLinear(torch.autograd.Function):
     fp16/bf16 autocast.  hipBLASLt runs x @ W^T at B = 360 on 24 workgroups (83 us for 28800->512);
     here K is split in 16 chunks, one batched GEMM with float32 outputs summed in float32 (33 us),
     rounded once to the autocast dtype like the single GEMM's output.  Backward: dx = dy W, and
-    dW = (x^T dy)^T (26 us vs 39 us for dy^T x at K = B = 360)."""
+    dW = (x^T dy)^T (26 us vs 39 us for dy^T x at K = B = 360).
+    perm = (C, HW): x is a channels-last hidden state flattened as (p, c) and W's columns are used in
+    that order (_bigk_weight); dW goes back to the parameter's (c, p) order in the one strided pass
+    that adds it into the f32 .grad."""
     SPLIT = 16
 
     @staticmethod
-    def forward(ctx, x, w, b, dt):
-        xs, ws = x.to(dt), w.to(dt)
+    def forward(ctx, x, w, b, dt, perm=None):
+        xs, ws = x.to(dt), _bigk_weight(w, dt, perm)
         n, K = xs.shape
         S = _BigKLinear.SPLIT
         y = torch.bmm(xs.view(n, S, K // S).transpose(0, 1), ws.view(-1, S, K // S).permute(1, 2, 0),
                       out_dtype=torch.float32).sum(0)
-        ctx.save_for_backward(xs, ws)
-        ctx.wdtype = w.dtype
+        ctx.save_for_backward(xs, ws, w)
+        ctx.perm = perm
         return (y + b).to(dt) if b is not None else y.to(dt)
 
     @staticmethod
     def backward(ctx, gy):
-        xs, ws = ctx.saved_tensors
+        xs, ws, w = ctx.saved_tensors
         gy = gy.to(xs.dtype)
         gx = gy @ ws if ctx.needs_input_grad[0] else None
-        gw = (xs.t() @ gy).t().to(ctx.wdtype) if ctx.needs_input_grad[1] else None
+        gw = None
+        if ctx.needs_input_grad[1]:
+            gwt = xs.t() @ gy  # [K, O] in x's column order
+            O = w.shape[0]
+            if ctx.perm is None:
+                src, dst_shape = gwt.t(), w.shape
+            else:
+                C, HW = ctx.perm
+                src, dst_shape = gwt.view(HW, C, O).permute(2, 1, 0), (O, C, HW)
+            if w.grad is not None and w.grad.dtype == torch.float32 and w.grad.is_contiguous():
+                w.grad.view(dst_shape).add_(src)  # no gradient tensor, no AccumulateGrad add
+            else:
+                gw = torch.empty(w.shape, dtype=w.dtype, device=w.device)
+                gw.view(dst_shape).copy_(src)
         gb = gy.sum(0, dtype=torch.float32) if ctx.needs_input_grad[2] else None
-        return gx, gw, gb, None
+        return gx, gw, gb, None, None
 
 
 def _linear(lin, x):
@@ -572,13 +611,28 @@ def _linear(lin, x):
     return lin(x)
 
 
+def _linear_flat(lin, h):
+    """lin(h flattened per row in the reference's NCHW order, network.py:95,105).  A channels-last
+    hidden state under GPU autocast is flattened as a view in (p, c) order and meets W's columns
+    reordered the same way (_BigKLinear perm): no transposing copy of h per use."""
+    n = h.shape[0]
+    if (FLAT_NHWC and h.is_cuda and torch.is_autocast_enabled("cuda") and h.dim() == 4 and not h.is_contiguous()
+            and h.is_contiguous(memory_format=torch.channels_last)):
+        C, HW = h.shape[1], h.shape[2] * h.shape[3]
+        K = C * HW
+        if K >= 4096 and K % _BigKLinear.SPLIT == 0 and lin.weight.shape[1] == K:
+            return _BigKLinear.apply(h.permute(0, 2, 3, 1).reshape(n, K), lin.weight, lin.bias,
+                                     torch.get_autocast_dtype("cuda"), (C, HW))
+    return _linear(lin, h.reshape(n, -1))
+
+
 class _Projection(nn.Module):
     def __init__(self, din, hidden=512, out=512):
         super().__init__()
         self.fc1, self.bn1, self.fc2 = nn.Linear(din, hidden), nn.BatchNorm1d(hidden, eps=1e-4), nn.Linear(hidden, out)
 
     def forward(self, h, mask=None):
-        return self.fc2(_bn_act(self.bn1, _linear(self.fc1, h.reshape(h.shape[0], -1)), mask))
+        return self.fc2(_bn_act(self.bn1, _linear_flat(self.fc1, h), mask))
 
 
 class TrainNet(nn.Module):

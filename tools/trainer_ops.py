@@ -60,3 +60,24 @@ for (name, shp), n in ops.most_common(a.top):
 print("\nGPU kernels by launching aten op (top-level):")
 print(prof.key_averages(group_by_input_shape=True).table(sort_by="cuda_time_total", row_limit=a.top, max_name_column_width=40,
                                                           max_shapes_column_width=70))
+
+# which ops launch the small elementwise kernels (copies, casts, adds): innermost aten op with its input
+# shapes and its outermost ancestor (an autograd node name in the backward, a module op forward)
+pat = ("copy", "CUDAFunctor_add", "direct_copy", "float16", "FillFunctor")
+who = Counter()
+wtime = Counter()
+for e in prof.events():
+    if e.device_type.name != "CPU":
+        continue
+    for k in getattr(e, "kernels", []) or []:
+        if not any(p in k.name for p in pat):
+            continue
+        top = e
+        while top.cpu_parent is not None:
+            top = top.cpu_parent
+        key = (k.name[:60], e.name, str(e.input_shapes)[:70], top.name[:60])
+        who[key] += 1
+        wtime[key] += k.duration
+print("\nsmall elementwise kernels by launching op (innermost op, shapes, outermost ancestor):")
+for key, n in sorted(who.items(), key=lambda kv: -wtime[kv[0]])[:a.top]:
+    print(f"{n:4d} {wtime[key]:8.0f} us  {key[0]:<60} | {key[1]} {key[2]} | {key[3]}")
