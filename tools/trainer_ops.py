@@ -81,3 +81,4 @@ for e in prof.events():
 print("\nsmall elementwise kernels by launching op (innermost op, shapes, outermost ancestor):")
 for key, n in sorted(who.items(), key=lambda kv: -wtime[kv[0]])[:a.top]:
     print(f"{n:4d} {wtime[key]:8.0f} us  {key[0]:<60} | {key[1]} {key[2]} | {key[3]}")
+
