@@ -317,6 +317,11 @@ int gmz_conv3x3_wgrad(int dtype, int H, const void *x_dev, const void *dy_dev, i
                       int64_t s1, int64_t s2, int64_t s3, int accumulate, void *workspace_dev, void *stream);
 int gmz_conv3x3_forward_stats(int dtype, int H, const void *x_dev, const void *packed_dev, void *y_dev, int N,
                               const uint8_t *mask_dev, double *stats_dev, void *stream);
+/* dst_dev[o][c][p] += src_dev[(p*C + c)*O + o] (f32 accumulate; src dtype 0 = f32, 1 = f16, 2 = bf16):
+ * the weight gradient x^T dy of a K = C*P Linear whose input was a channels-last [N][P][C] hidden state
+ * flattened in (p, c) order, added into the f32 .grad of W [O][C*P] (the reference's NCHW flatten,
+ * network.py:95,105; loss.py:70-107 backward).  One add per element: the result is order-independent. */
+int gmz_grad_add_t(int dtype, const void *src_dev, int P, int C, int O, float *dst_dev, void *stream);
 
 #ifdef __cplusplus
 }
