@@ -63,7 +63,7 @@ print(prof.key_averages(group_by_input_shape=True).table(sort_by="cuda_time_tota
 
 # which ops launch the small elementwise kernels (copies, casts, adds): innermost aten op with its input
 # shapes and its outermost ancestor (an autograd node name in the backward, a module op forward)
-pat = ("copy", "CUDAFunctor_add", "direct_copy", "float16", "FillFunctor")
+pat = ("copy", "CUDAFunctor_add", "direct_copy", "float16", "FillFunctor", "type_sp", "reduce_kernel")
 who = Counter()
 wtime = Counter()
 for e in prof.events():
