@@ -61,6 +61,7 @@ _SIGS = {
     "gmz_bn_eval": ([I, I, P, P, I, I, I, P, P, P, P, ctypes.c_float, I, P, P, P], I),
     "gmz_conv3x3_pack": ([I, P, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, I, P, P], I),
     "gmz_conv3x3_forward": ([I, I, P, P, P, I, P], I),
+    "gmz_conv3x3_forward_add": ([I, I, P, P, P, P, I, P], I),
     "gmz_conv3x3_stats_slots": ([I, ctypes.POINTER(ctypes.c_int)], I),
     "gmz_conv3x3_wgrad_workspace_bytes": ([I, ctypes.POINTER(ctypes.c_size_t)], I),
     "gmz_conv3x3_wgrad": ([I, I, P, P, I, P, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, I, P, P], I),

@@ -98,7 +98,7 @@ __global__ void __launch_bounds__(256) k_pack_conv(const float *__restrict__ w, 
 template <int H, typename T, int PG>
 __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restrict__ x, const uint16_t *__restrict__ wpk,
                                                   uint16_t *__restrict__ y, int N, const uint8_t *__restrict__ mask,
-                                                  double *__restrict__ stats) {
+                                                  double *__restrict__ stats, const uint16_t *__restrict__ addend) {
   using I = CImg<H>;
   using M = Mfma<T>;
   typedef typename M::V V;
@@ -202,6 +202,7 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
 
     // ---- epilogue: 4 consecutive output channels of one position per lane -> 8-byte store
     uint16_t *dst = y + (size_t)b * A * CC;
+    const uint16_t *add = addend ? addend + (size_t)b * A * CC : nullptr;  // + addend, rounded once
     const bool counted = stats && (!mask || mask[b]);
     nvalid += counted;
 #pragma unroll
@@ -213,8 +214,14 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
       for (int nt = 0; nt < NTW; ++nt) {
         const int n0 = (ntile0 + nt) * 16 + g4 * 4;
         u16x4_t o;
+        if (add) {
+          const u16x4_t ad = *(const u16x4_t *)(add + (size_t)p * CC + n0);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = M::bits(acc[nt][i][e]);
+          for (int e = 0; e < 4; ++e) o[e] = M::bits(acc[nt][i][e] + M::value(ad[e]));
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = M::bits(acc[nt][i][e]);
+        }
         *(u16x4_t *)(dst + (size_t)p * CC + n0) = o;
         if (counted) {
 #pragma unroll
@@ -435,19 +442,20 @@ int conv3_grid(int N) {  // a multiple of 16 (whole XCD pairs; workgroups past t
 }
 
 template <int H, typename T>
-int launch_conv3(const void *x, const void *wpk, void *y, int N, const uint8_t *mask, double *stats, hipStream_t st) {
+int launch_conv3(const void *x, const void *wpk, void *y, int N, const uint8_t *mask, double *stats, const void *addend,
+                 hipStream_t st) {
   hipLaunchKernelGGL((k_conv3<H, T, CONV_PG>), dim3(conv3_grid(N)), dim3(128 * CONV_PG), 0, st, (const uint16_t *)x,
-                     (const uint16_t *)wpk, (uint16_t *)y, N, mask, stats);
+                     (const uint16_t *)wpk, (uint16_t *)y, N, mask, stats, (const uint16_t *)addend);
   GMZ_LAUNCH_CHECK();
   return 0;
 }
 
 template <typename T>
-int conv3_dispatch(int H, const void *x, const void *wpk, void *y, int N, const uint8_t *mask, double *stats,
+int conv3_dispatch(int H, const void *x, const void *wpk, void *y, int N, const uint8_t *mask, double *stats, const void *addend,
                    hipStream_t st) {
   switch (H) {
-    case 9: return launch_conv3<9, T>(x, wpk, y, N, mask, stats, st);
-    case 15: return launch_conv3<15, T>(x, wpk, y, N, mask, stats, st);
+    case 9: return launch_conv3<9, T>(x, wpk, y, N, mask, stats, addend, st);
+    case 15: return launch_conv3<15, T>(x, wpk, y, N, mask, stats, addend, st);
   }
   return fail("gmz_conv3x3: board size must be 9 or 15");
 }
@@ -502,13 +510,25 @@ GMZ_EXPORT int gmz_conv3x3_forward_stats(int dtype, int H, const void *x, const 
   if (N <= 0) return fail("gmz_conv3x3_forward: N must be positive");
   if (((uintptr_t)x | (uintptr_t)packed | (uintptr_t)y) & 15) return fail("gmz_conv3x3_forward: operands must be 16-B aligned");
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == 1) return conv3_dispatch<__half>(H, x, packed, y, N, mask, stats, st);
-  if (dtype == 2) return conv3_dispatch<__hip_bfloat16>(H, x, packed, y, N, mask, stats, st);
+  if (dtype == 1) return conv3_dispatch<__half>(H, x, packed, y, N, mask, stats, nullptr, st);
+  if (dtype == 2) return conv3_dispatch<__hip_bfloat16>(H, x, packed, y, N, mask, stats, nullptr, st);
   return fail("gmz_conv3x3_forward: dtype must be 1 (f16) or 2 (bf16)");
 }
 
 GMZ_EXPORT int gmz_conv3x3_forward(int dtype, int H, const void *x, const void *packed, void *y, int N, void *stream) {
   return gmz_conv3x3_forward_stats(dtype, H, x, packed, y, N, nullptr, nullptr, stream);
+}
+
+GMZ_EXPORT int gmz_conv3x3_forward_add(int dtype, int H, const void *x, const void *packed, const void *addend, void *y,
+                                       int N, void *stream) {
+  if (!x || !packed || !y || !addend) return fail("gmz_conv3x3_forward_add: null operand");
+  if (N <= 0) return fail("gmz_conv3x3_forward_add: N must be positive");
+  if (((uintptr_t)x | (uintptr_t)packed | (uintptr_t)y | (uintptr_t)addend) & 15)
+    return fail("gmz_conv3x3_forward_add: operands must be 16-B aligned");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == 1) return conv3_dispatch<__half>(H, x, packed, y, N, nullptr, nullptr, addend, st);
+  if (dtype == 2) return conv3_dispatch<__hip_bfloat16>(H, x, packed, y, N, nullptr, nullptr, addend, st);
+  return fail("gmz_conv3x3_forward_add: dtype must be 1 (f16) or 2 (bf16)");
 }
 
 GMZ_EXPORT int gmz_conv3x3_wgrad_workspace_bytes(int N, size_t *out) {

@@ -161,7 +161,7 @@ class _FusedMaskedBN(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, gamma, beta, res, mask, running_mean, running_var, num_batches, eps, momentum, relu,
-                stats=None):
+                stats=None, link=None):
         from . import _lib
         L = _lib.load()
         layout = _bn_layout(x)
@@ -188,6 +188,7 @@ class _FusedMaskedBN(torch.autograd.Function):
         ctx.save_for_backward(x, y, mask, gamma, save)
         ctx.relu, ctx.has_res, ctx.layout = relu, res is not None, layout
         ctx.beta = beta
+        ctx.link = link
         return y
 
     @staticmethod
@@ -216,9 +217,13 @@ class _FusedMaskedBN(torch.autograd.Function):
                                          _lib.ptr(mask), B, C, S, _lib.ptr(gamma), _lib.ptr(save), int(ctx.relu),
                                          _lib.ptr(dx), _lib.ptr(dres), _lib.ptr(dgamma), _lib.ptr(dbeta),
                                          _lib.ptr(ws), _lib.stream_ptr(), int(acc)))
+        if ctx.link is not None and dres is not None:
+            # the residual's gradient goes to the block's first conv, whose input-gradient epilogue adds it
+            # (_ResLink): autograd then has one gradient for the block input, no accumulation pass
+            ctx.link.dres, dres = dres, None
         if acc:
-            return dx, None, None, dres, None, None, None, None, None, None, None, None
-        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None, None
+            return dx, None, None, dres, None, None, None, None, None, None, None, None, None
+        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None
 
 
 _WS_BYTES = {}
@@ -235,16 +240,18 @@ def _bn_workspace(layout, B, C, S, device):
     return torch.empty((_WS_BYTES[key] + 7) // 8, dtype=torch.float64, device=device)
 
 
-def _bn_act(mod, x, mask=None, res=None, relu=True):
+def _bn_act(mod, x, mask=None, res=None, relu=True, link=None):
     """relu?(BatchNorm(x) (+ res)) with row-masked training statistics (see ``_bn``).  Training-mode
-    BatchNorm on the GPU runs the fused HIP kernels; eval mode and the CPU use PyTorch ops."""
+    BatchNorm on the GPU runs the fused HIP kernels; eval mode and the CPU use PyTorch ops.  ``link``:
+    the block's _ResLink, used when ``res`` is the very tensor its first HIP conv consumed."""
     if FUSED_BN and mod.training and x.is_cuda and x.dtype in _BN_DTYPES:
         if res is not None:
             res = res.to(x.dtype)
         m = None if mask is None else mask.contiguous().view(torch.uint8)
+        use = link if (link is not None and res is not None and link.xin is res) else None
         return _FusedMaskedBN.apply(x, mod.weight, mod.bias, res, m, mod.running_mean, mod.running_var,
                                     mod.num_batches_tracked, mod.eps, mod.momentum, relu,
-                                    getattr(x, "_gmz_bnstats", None))
+                                    getattr(x, "_gmz_bnstats", None), use)
     if (FUSED_BN and not mod.training and x.is_cuda and x.dtype in _BN_DTYPES and _bn_layout(x) is not None
             and not (torch.is_grad_enabled() and (x.requires_grad or mod.weight.requires_grad))):
         return _bn_eval(mod, x, res, relu)
@@ -361,13 +368,34 @@ def _packed_conv_weight(w, dtype, transpose):
 _STATS_SLOTS = {}
 
 
-def _conv3x3_hip(x, packed, mask=None, stats=None):
+def _conv3x3_hip(x, packed, mask=None, stats=None, addend=None):
     from . import _lib
     y = torch.empty_like(x, memory_format=torch.channels_last)
+    if addend is not None:  # y = round(conv + addend) (the residual gradient folded into the input gradient)
+        addend = addend.to(x.dtype).contiguous(memory_format=torch.channels_last)
+        _lib.check(_lib.load().gmz_conv3x3_forward_add(_CONV_DTYPES[x.dtype], x.shape[2], _lib.ptr(x), _lib.ptr(packed),
+                                                       _lib.ptr(addend), _lib.ptr(y), x.shape[0], _lib.stream_ptr()))
+        return y
     _lib.check(_lib.load().gmz_conv3x3_forward_stats(_CONV_DTYPES[x.dtype], x.shape[2], _lib.ptr(x), _lib.ptr(packed),
                                                      _lib.ptr(y), x.shape[0], _lib.ptr(mask), _lib.ptr(stats),
                                                      _lib.stream_ptr()))
     return y
+
+
+# the residual blocks' identity-path gradient folded into conv1's input-gradient epilogue (_ResLink):
+# one gradient for the block input instead of two plus an autograd accumulation pass per block
+FUSED_RES_GRAD = True
+
+
+class _ResLink:
+    """Hand-off between one residual block's bn2 (which produces the identity path's gradient) and its
+    conv1 (whose input-gradient kernel adds it): xin = the tensor conv1 consumed (the block input),
+    dres = the gradient bn2's backward left for conv1's backward (always the later of the two)."""
+    __slots__ = ("xin", "dres")
+
+    def __init__(self):
+        self.xin = None
+        self.dres = None
 
 
 # the 128->128 convs' weight gradient on gmz_conv3x3_wgrad instead of MIOpen: exact (f32 accumulation,
@@ -414,15 +442,19 @@ class _Conv3x3NHWC(torch.autograd.Function):
     converts it (what autocast's cast would do)."""
 
     @staticmethod
-    def forward(ctx, x, w, mask=None, stats=None):
+    def forward(ctx, x, w, mask=None, stats=None, link=None):
         ctx.save_for_backward(x, w)
+        ctx.link = link
         return _conv3x3_hip(x, _packed_conv_weight(w, x.dtype, 0), mask, stats)
 
     @staticmethod
     def backward(ctx, gy):
         x, w = ctx.saved_tensors
         gy = gy.to(x.dtype).contiguous(memory_format=torch.channels_last)
-        gx = _conv3x3_hip(gy, _packed_conv_weight(w, x.dtype, 1)) if ctx.needs_input_grad[0] else None
+        add = None
+        if ctx.link is not None:
+            add, ctx.link.dres = ctx.link.dres, None
+        gx = _conv3x3_hip(gy, _packed_conv_weight(w, x.dtype, 1), addend=add) if ctx.needs_input_grad[0] else None
         gw = None
         if ctx.needs_input_grad[1]:
             if HIP_WGRAD:
@@ -440,14 +472,14 @@ class _Conv3x3NHWC(torch.autograd.Function):
                     gw = None
                 else:
                     gw = gw.to(w.dtype)
-        return gx, gw, None, None
+        return gx, gw, None, None, None
 
 
 def _conv3(cin, cout):
     return nn.Conv2d(cin, cout, 3, padding=1, bias=False)
 
 
-def _conv3_apply(conv, x, bn=None, mask=None):
+def _conv3_apply(conv, x, bn=None, mask=None, link=None):
     """conv(x), on the HIP kernels when they cover the case (see ``_Conv3x3NHWC``).  ``bn``: the
     training-mode BatchNorm that consumes the output — the kernel's epilogue then also reduces its
     (row-masked) statistics, attached to the output for ``_bn_act`` (no separate reduction pass)."""
@@ -459,7 +491,10 @@ def _conv3_apply(conv, x, bn=None, mask=None):
             if bn is not None and bn.training and FUSED_BN:
                 st = _conv_stats_buffer(x.shape[0], x.device)
             m = None if mask is None else mask.contiguous().view(torch.uint8)
-            y = _Conv3x3NHWC.apply(x.to(dt), conv.weight, m, None if st is None else st[0])
+            xin = x.to(dt)
+            y = _Conv3x3NHWC.apply(xin, conv.weight, m, None if st is None else st[0], link)
+            if link is not None:
+                link.xin = xin
             if st is not None:
                 y._gmz_bnstats = st
             return y
@@ -475,8 +510,9 @@ class _Block(nn.Module):
         self.conv2, self.bn2 = _conv3(c, c), nn.BatchNorm2d(c, eps=1e-4)
 
     def forward(self, x, mask=None):
-        y = _bn_act(self.bn1, _conv3_apply(self.conv1, x, self.bn1, mask), mask)
-        return _bn_act(self.bn2, _conv3_apply(self.conv2, y, self.bn2, mask), mask, res=x)
+        link = _ResLink() if (FUSED_RES_GRAD and torch.is_grad_enabled() and x.requires_grad) else None
+        y = _bn_act(self.bn1, _conv3_apply(self.conv1, x, self.bn1, mask, link=link), mask)
+        return _bn_act(self.bn2, _conv3_apply(self.conv2, y, self.bn2, mask), mask, res=x, link=link)
 
 
 class _Trunk(nn.Module):

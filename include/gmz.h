@@ -303,6 +303,12 @@ int gmz_bn_eval(int dtype, int layout, const void *x_dev, const void *res_dev, i
 int gmz_conv3x3_pack(int dtype, const float *w_dev, int64_t s0, int64_t s1, int64_t s2, int64_t s3, int transpose,
                      void *packed_dev, void *stream);
 int gmz_conv3x3_forward(int dtype, int H, const void *x_dev, const void *packed_dev, void *y_dev, int N, void *stream);
+/* The same convolution plus an addend of the output's shape and dtype, rounded once:
+ * y = round(conv(x, W) + addend).  The residual blocks' input gradient with the identity path's
+ * gradient folded in (network.py:40-47 backward: d(block input) = conv1'(d conv1 out) + d(residual)),
+ * in place of a separate gradient-accumulation pass.  addend_dev 16-B aligned. */
+int gmz_conv3x3_forward_add(int dtype, int H, const void *x_dev, const void *packed_dev, const void *addend_dev,
+                            void *y_dev, int N, void *stream);
 /* The same convolution, also writing the BatchNorm statistics of the (rounded) output over the boards
  * whose mask_dev byte is nonzero (NULL: all): stats_dev f64 [slots][128][3] = (sum, sum of squares,
  * counted positions) per slot, slots from gmz_conv3x3_stats_slots(N) — the partials layout
