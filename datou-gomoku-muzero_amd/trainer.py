@@ -90,15 +90,17 @@ def support_to_scalar(logits, vmin, vmax, bins):
 
 
 def scalar_to_support(x, vmin, vmax, bins):
-    """network.py:15-25: two-hot projection of a clamped scalar onto the support grid."""
-    x = x.clamp(vmin, vmax)
+    """network.py:15-25: two-hot projection of a clamped scalar onto the support grid; x of any shape
+    -> [*x.shape, bins] (elementwise, so a whole [B, steps] block at once gives each column's values)."""
+    shape = x.shape
+    x = x.reshape(-1).clamp(vmin, vmax)
     pos = (x - vmin) * ((bins - 1) / (vmax - vmin))
     lo, hi = torch.floor(pos).long(), torch.ceil(pos).long()
     w_hi = pos - lo.float()
     out = torch.zeros(x.shape[0], bins, device=x.device)
     out.scatter_add_(1, lo[:, None], (1 - w_hi)[:, None])
     out.scatter_add_(1, hi[:, None], w_hi[:, None])
-    return out
+    return out.view(*shape, bins)
 
 
 # ------------------------------------------------------------------------------ network
@@ -867,7 +869,11 @@ def muzero_loss(model, target_model, batch, is_weights, cfg, k=None, flip=None, 
             z.record_stream(main)
         pl, vl = model.prediction(h)
         lp = F.cross_entropy(pl.float(), pi[:, 0], reduction="none")
-        lv = F.cross_entropy(vl.float(), scalar_to_support(z[:, 0], *vsup), reduction="none")
+        # the support targets of every step in two calls (the per-step calls were ~10 tiny kernels each)
+        # (step-major, so each step's [B, bins] block is contiguous)
+        zsup = scalar_to_support(z.t().contiguous(), *vsup)       # [U+1, B, bins]
+        rsupt = scalar_to_support(rew.t().contiguous(), *rsup)    # [U, B, bins]
+        lv = F.cross_entropy(vl.float(), zsup[0], reduction="none")
         # loss.py:78 passes softmax(logits) to support_to_scalar, which applies softmax again:
         # the PER priority is computed from that doubly-softmaxed value (kept as the reference does)
         v0 = support_to_scalar(F.softmax(vl.float(), dim=1), *vsup)
@@ -884,9 +890,9 @@ def muzero_loss(model, target_model, batch, is_weights, cfg, k=None, flip=None, 
             hk, rl = model.dynamics(h, torch.where(m, act_aug[:, s], torch.zeros_like(act_aug[:, s])), mask=m)
             plk, vlk = model.prediction(hk, mask=m)
             lp = lp + torch.where(m, F.cross_entropy(plk.float(), pi[:, s + 1], reduction="none"), zero)
-            lv = lv + torch.where(m, F.cross_entropy(vlk.float(), scalar_to_support(z[:, s + 1], *vsup),
+            lv = lv + torch.where(m, F.cross_entropy(vlk.float(), zsup[s + 1],
                                                      reduction="none"), zero)
-            lr_ = lr_ + torch.where(m, F.cross_entropy(rl.float(), scalar_to_support(rew[:, s], *rsup),
+            lr_ = lr_ + torch.where(m, F.cross_entropy(rl.float(), rsupt[s],
                                                        reduction="none"), zero)
             dyn = model.project(hk, with_grad=True, mask=m)
             with torch.no_grad():
