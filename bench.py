@@ -141,7 +141,7 @@ def parse(argv=None):
     ap.add_argument("--cpu-baseline-sec", type=float, default=20.0)
     ap.add_argument("--cpu-baseline-procs", type=int, default=16,
                     help="single-threaded oracle processes (capped by the cores this process may use)")
-    ap.add_argument("--sublines", default="c5,c1,g8192",
+    ap.add_argument("--sublines", default="empty_board,c5,c1,g8192",
                     help="measured besides the headline: c5 (BASELINE config 5: 19x19/800/16 blocks), c1 (config 1: 9x9 "
                          "AlphaZero/50), g8192 (config 2's search on 8,192 trees, one engine: the tree kernel's "
                          "SURVEY 8(d) measurement point)")
@@ -173,6 +173,19 @@ def parse(argv=None):
                          "one push is measured separately (weight_push_ms)")
     ap.add_argument("--loop-buffer", type=int, default=65536, help="replay shard capacity per rank")
     ap.add_argument("--loop-prefill", type=int, default=4096, help="synthetic slices in each shard before the loop")
+    ap.add_argument("--stagger", type=int, default=80,
+                    help="headline starts (SURVEY 8(d)): k in {0,4,8} opening stones plus uniform(0, N) staggered "
+                         "stones per game from RandomState(seed + game id), so games finish and restart inside the "
+                         "timed moves; -1: empty boards (rounds 1-3's headline)")
+    ap.add_argument("--isolate", default="auto", choices=["auto", "on", "off"],
+                    help="run each phase (headline, extras, trainer, loop) as fresh rank processes under a wall-time "
+                         "cap (auto: when N > 1)")
+    ap.add_argument("--dist-timeout", type=float, default=150.0,
+                    help="seconds: bound on every collective of a rank process (init_process_group timeout)")
+    ap.add_argument("--phase-timeout-selfplay", type=float, default=240.0)
+    ap.add_argument("--phase-timeout-extras", type=float, default=200.0)
+    ap.add_argument("--phase-timeout-trainer", type=float, default=150.0)
+    ap.add_argument("--phase-timeout-loop", type=float, default=180.0)
     ap.add_argument("--pmc-file", default=os.path.join(REPO, "profiles", "pmc_tower_latest.json"))
     ap.add_argument("--pmc-tree-file", default=os.path.join(REPO, "profiles", "pmc_tree_latest.json"))
     return ap.parse_args(argv)
@@ -234,6 +247,17 @@ def collective_sum(x, dist, backend="nccl"):
     return float(t.item())
 
 
+def collective_gather(x, dist, backend="nccl"):
+    """Every rank's float, in rank order (a one-hot all-reduce SUM)."""
+    if dist is None:
+        return [x]
+    dev = "cuda" if backend == "nccl" else "cpu"
+    t = torch.zeros(dist.get_world_size(), device=dev, dtype=torch.float64)
+    t[dist.get_rank()] = x
+    dist.all_reduce(t)
+    return [float(v) for v in t.tolist()]
+
+
 def result_line(args, world, dt, waves, G, backend=None):
     """The JSON object rank 0 prints (without roofline / cpu_baseline / trainer)."""
     total_moves = G * args.steps * world
@@ -244,13 +268,30 @@ def result_line(args, world, dt, waves, G, backend=None):
         "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": getattr(args, "precision", "fp16"), "data": "synthetic",
         "config": {"workload": "%dx%d Gumbel %s, %d sims/move, %d concurrent games per GPU, GomokuNetEZ %d blocks x "
-                               "128 ch (numpy-seeded random init), empty-board starts, device Gumbel RNG"
-                               % (args.size, args.size, args.mode, args.sims, G, args.blocks),
+                               "128 ch (numpy-seeded random init), %s, device Gumbel RNG"
+                               % (args.size, args.size, args.mode, args.sims, G, args.blocks, starts_text(args)),
                    "games_per_gpu": G, "global_games": G * world, "board_size": args.size,
                    "num_simulations": args.sims, "mcts": args.mode, "waves_per_move": waves / max(1, args.steps),
                    "ranks": world, "dist_backend": backend, "streams_per_gpu": getattr(args, "streams", None) or 1,
                    "parallelism": "dp%d (independent games per GPU, no collective)" % world},
     }
+
+
+def starts_text(args):
+    if getattr(args, "stagger", -1) < 0:
+        return "empty-board starts"
+    return ("steady-state starts: game g from RandomState(seed + g) with k in {0,4,8} opening stones plus "
+            "uniform(0, %d) staggered stones (engine.seeded_openings; finished games restart from the empty "
+            "board inside the timed moves)" % args.stagger)
+
+
+def headline_openings(args, rank, G, size, n_in_row=5):
+    """The headline's start positions: global game ids rank*G .. rank*G + G - 1."""
+    if getattr(args, "stagger", 0) < 0:
+        return None
+    import datou_gomoku_muzero_amd.engine as E
+    return E.seeded_openings(range(rank * G, (rank + 1) * G), size, args.seed, stagger=args.stagger,
+                             n_in_row=n_in_row)
 
 
 def timer_stats(timers, base):
@@ -405,10 +446,12 @@ def trainer_trace_summary(args):
 
 
 def selfplay_leg(args, rank, world, dist, backend, size, sims, mode, blocks, G, steps, warmup, streams=None,
-                 single_stream_moves=0, log_prefix=""):
+                 single_stream_moves=0, log_prefix="", openings=None):
     """G games of (size, sims, mode, blocks) self-play on this rank's GPU: ``warmup`` untimed moves, then
-    ``steps`` timed moves (barrier + synchronize on both sides, max over ranks).  Returns a dict with
-    dt (s), waves, streams, roofline (dominant tower), roofline_tree and, with single_stream_moves > 0
+    ``steps`` timed moves (barrier + synchronize on both sides, max over ranks).  ``openings``: the games'
+    start positions (engine.seeded_openings; None = empty boards).  Returns a dict with dt (s, max over
+    ranks), rank_dt (every rank's own time), finished_games (games that ended in the timed moves, all
+    ranks), waves, streams, roofline (dominant tower), roofline_tree and, with single_stream_moves > 0
     and two streams, single_stream_kernels."""
     import datou_gomoku_muzero_amd.engine as E
     from datou_gomoku_muzero_amd import network as N, weights as W
@@ -429,15 +472,22 @@ def selfplay_leg(args, rank, world, dist, backend, size, sims, mode, blocks, G, 
     tkw = dict(layout=args.layout, descent_hint=None if args.hint is None else args.hint == "on")
     eng = E.make_engine(cfg, num_games=G, net=net, seed=args.seed + 7919 * rank, streams=streams, **tkw)
     eng.reset_games()
+    if openings is not None:
+        eng.set_positions(*openings)
     parts = eng.engines if streams > 1 else [eng]
     pstreams = eng.streams if streams > 1 else [torch.cuda.current_stream()]
     log("%srank %d: engine G=%d %dx%d %s/%d, %d blocks, net=%s, %d stream(s), %s tree, hint %s"
         % (log_prefix, rank, G, size, size, mode, sims, blocks, args.net, streams, parts[0].layout,
            parts[0].descent_hint))
 
+    finished = torch.zeros((), dtype=torch.int64, device="cuda")
+    count = [False]
+
     def step():
         eng.search()
-        eng.play(reset_finished=True)
+        st = eng.play(reset_finished=True)
+        if count[0]:  # +1 / -1 winner or 0 draw: the game ended on this move (and restarts from the empty board)
+            finished.add_(((st == 1) | (st == -1) | (st == 0)).sum())
 
     for i in range(warmup):
         step()
@@ -463,6 +513,7 @@ def selfplay_leg(args, rank, world, dist, backend, size, sims, mode, blocks, G, 
     base.record()
     t0 = time.perf_counter()
     waves = 0
+    count[0] = True
     for i in range(steps):
         step()
         waves += eng.waves_last
@@ -471,8 +522,10 @@ def selfplay_leg(args, rank, world, dist, backend, size, sims, mode, blocks, G, 
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
-    dt = collective_max(time.perf_counter() - t0, dist, backend)
-    res = {"dt": dt, "waves": waves, "streams": streams}
+    own = time.perf_counter() - t0
+    dt = collective_max(own, dist, backend)
+    res = {"dt": dt, "waves": waves, "streams": streams, "rank_dt": collective_gather(own, dist, backend),
+           "finished_games": int(collective_sum(float(finished.item()), dist, backend))}
     ctr = eng.tree_counters()
     traffic_note = "from the committed builder PMC pass %s (not measured in this run)"
     fpr = (repr_flop_per_row if az else tower_flop_per_row)(size, blocks)
@@ -567,6 +620,10 @@ def selfplay_leg(args, rank, world, dist, backend, size, sims, mode, blocks, G, 
 
 
 SUBLINES = {  # BASELINE.json configs run on the GPU besides the headline (C2)
+    # the headline's configuration from empty boards (the round 1-3 headline, kept for continuity): the first
+    # warmup + steps moves of every game, so no game ends and the tree shapes are those of openings
+    "empty_board": dict(size=15, sims=400, mode="MuZero", blocks=8, headline_games=True, headline_steps=True,
+                        name="C2 from empty boards (no game ends in the window; rounds 1-3's headline workload)"),
     "c5": dict(size=19, sims=800, mode="MuZero", blocks=16,
                name="C5: 19x19, 800 sims/move, GomokuNetEZ 16 blocks (BASELINE config 5)"),
     "c1": dict(size=9, sims=50, mode="AlphaZero", blocks=8,
@@ -583,8 +640,10 @@ SUBLINES = {  # BASELINE.json configs run on the GPU besides the headline (C2)
 
 def subline(args, key, rank, world, dist, backend):
     c = SUBLINES[key]
-    G = c.get("games", args.subline_games)
+    G = args.games if c.get("headline_games") else c.get("games", args.subline_games)
     steps, warmup = {"c5": (args.c5_steps, 1), "c1": (args.c1_steps, 2)}.get(key, (c.get("steps", 2), c.get("warmup", 1)))
+    if c.get("headline_steps"):
+        steps, warmup = args.steps, args.warmup
     if "min_free_gb" in c:  # a bounded leg: skipped (and said so) when this GPU lacks the memory
         torch.cuda.empty_cache()
         free = torch.cuda.mem_get_info()[0] / 2 ** 30
@@ -598,7 +657,8 @@ def subline(args, key, rank, world, dist, backend):
                      streams=c.get("streams"), log_prefix="[%s] " % key)
     out = {"config": c["name"], "value": G * steps * world / r["dt"], "unit": "moves/s", "n_gpus": world,
            "games_per_gpu": G, "steps": steps, "warmup": warmup, "ms_per_step": r["dt"] / steps * 1e3,
-           "waves_per_move": r["waves"] / max(1, steps), "streams": r["streams"], "dtype": args.precision}
+           "waves_per_move": r["waves"] / max(1, steps), "streams": r["streams"], "dtype": args.precision,
+           "finished_games": r["finished_games"]}
     for k in ("roofline", "roofline_tree"):
         if k in r:
             q = r[k]
@@ -683,7 +743,8 @@ def worker_leg(args, rank, world, dist, backend, consumer, engine_rate):
     if dist:
         dist.barrier()
     import datou_gomoku_muzero_amd.engine as E
-    op = (E.random_openings(args.games, args.size, np.random.RandomState(args.seed + 29 * rank), args.worker_openings)
+    op = (E.random_openings(args.games, args.size, np.random.RandomState(args.seed + 29 * rank), args.worker_openings,
+                            n_in_row=cfg.N_IN_ROW)
           if args.worker_openings > 0 else None)
     gpu_selfplay_worker(rank, None, qs["data"], qs["log"], qs["ui"], _Flag(), trainer_event_queue=qs["trainer"],
                         num_games=args.games, cfg=cfg, max_moves=warm + moves, emit_move_notices=True,
@@ -711,6 +772,258 @@ def worker_leg(args, rank, world, dist, backend, consumer, engine_rate):
                      "posted (per-move history, winning-move scan, record building all inside)" % warm}
 
 
+PHASE_ENV = "GMZ_BENCH_PHASE"
+PHASE_MARK = "GMZ_PHASE_RESULT "
+
+
+def phase_keys(name, args):
+    """The keys of the line a phase fills (a phase that fails puts {"error": ...} in each)."""
+    modes = [m.strip() for m in args.loop_modes.split(",") if m.strip()]
+    return {"selfplay": [],
+            "extras": (["sublines"] if [k for k in args.sublines.split(",") if k.strip()] else [])
+            + (["worker"] if args.worker_moves > 0 else []),
+            "trainer": ["trainer"],
+            "loop": ["loop_c4" if m == "sliced" else "loop_c4_concurrent" for m in modes]}[name]
+
+
+def phase_plan(args):
+    """The phases this run needs, in order, with their wall-time caps (s).  ``selfplay`` = the headline
+    (+ its single-stream kernel times); ``extras`` = the sublines and the drop-in worker leg (self-play only:
+    no collective but barriers and timing reductions); ``trainer`` and ``loop`` carry the heavy RCCL traffic
+    (gradient all-reduce, PER syncs, weight broadcast)."""
+    plan = [("selfplay", args.phase_timeout_selfplay)]
+    if args.net == "hip":
+        if [k for k in args.sublines.split(",") if k.strip()] or args.worker_moves > 0:
+            plan.append(("extras", args.phase_timeout_extras))
+        if args.trainer_steps > 0:
+            plan.append(("trainer", args.phase_timeout_trainer))
+        if args.loop_iters > 0 and [m for m in args.loop_modes.split(",") if m.strip()]:
+            plan.append(("loop", args.phase_timeout_loop))
+    return plan
+
+
+def inject_failure(phase, rank):
+    """GMZ_BENCH_INJECT_FAIL=<phase>:<rank> makes that rank's leg of that phase raise after the process
+    group is up, so its peers are left waiting in a collective (the failure an untested RCCL path would
+    cause) - the rehearsal that the headline survives it."""
+    spec = os.environ.get("GMZ_BENCH_INJECT_FAIL", "")
+    if spec and spec == "%s:%d" % (phase, rank):
+        raise RuntimeError("injected failure (GMZ_BENCH_INJECT_FAIL=%s)" % spec)
+
+
+def run_phase(phase, args, rank, world, dist, backend, consumer=None, out=None):
+    """The legs of one phase on this rank; returns the line's fragment (rank 0's is the one printed).
+    In-process mode passes ``out`` (the line so far) so the worker leg can quote the headline rate."""
+    frag = {}
+    if phase == "selfplay":
+        G = args.games
+        r = selfplay_leg(args, rank, world, dist, backend, args.size, args.sims, args.mode, args.blocks, G,
+                         args.steps, args.warmup, streams=args.streams, single_stream_moves=args.single_stream_moves,
+                         openings=headline_openings(args, rank, G, args.size))
+        args.streams = r["streams"]
+        frag = result_line(args, world, r["dt"], r["waves"], G, backend)
+        frag["finished_games"] = r["finished_games"]
+        frag["rank_values"] = [G * args.steps / t if t > 0 else None for t in r["rank_dt"]]
+        for k in ("roofline", "roofline_tree", "single_stream_kernels"):
+            if k in r:
+                frag[k] = r[k]
+        return frag
+    inject_failure(phase, rank)
+    if phase == "extras":
+        subs = {}
+        for key in [k.strip() for k in args.sublines.split(",") if k.strip()]:
+            if key not in SUBLINES:
+                raise SystemExit("bench.py: unknown --sublines entry %r" % key)
+            subs[key] = subline(args, key, rank, world, dist, backend)
+        if subs:
+            frag["sublines"] = subs
+        if consumer is not None:
+            rate = (out or {}).get("value") or args.headline_value
+            frag["worker"] = worker_leg(args, rank, world, dist, backend, consumer, rate)
+            consumer[2].put(None)  # the consumer process exits
+            torch.cuda.empty_cache()
+    elif phase == "trainer":
+        torch.cuda.empty_cache()
+        frag["trainer"] = trainer_leg(args, world, rank, dist, backend)
+    elif phase == "loop":
+        frag.update(loop_legs(args, rank, world, dist, backend))
+    return frag
+
+
+def loop_legs(args, rank, world, dist, backend):
+    from datou_gomoku_muzero_amd.loop import run_c4
+    out = {}
+    for mode in [m.strip() for m in args.loop_modes.split(",") if m.strip()]:
+        if mode not in ("sliced", "concurrent"):
+            raise SystemExit("bench.py: unknown --loop-modes entry %r" % mode)
+        args.loop_concurrent = mode == "concurrent"
+        torch.cuda.empty_cache()
+        d, dt_loop = run_c4(args, rank, world, dist, backend, log=log)
+        dt_loop = collective_max(dt_loop, dist, backend)
+        push_ms = collective_max(d.pop("push_ms"), dist, backend)
+        tot = {k: collective_sum(float(v), dist, backend) for k, v in d.items()}
+        step_ms = dt_loop / max(1, d["train_steps"]) * 1e3
+        out["loop_c4" if mode == "sliced" else "loop_c4_concurrent"] = {
+            "metric": "C4 loop: self-play moves/sec and trainer steps/sec with both running on every GPU",
+            "mode": mode + (": each iteration's trainer steps run on their own HIP stream beside its self-play "
+                            "moves" if mode == "concurrent" else ": each iteration = moves, then trainer steps"),
+            "moves_per_s": tot["moves"] * args.loop_games / dt_loop, "trainer_steps_per_s": d["train_steps"] / dt_loop,
+            "unit": "moves/s, steps/s", "n_gpus": world, "iterations": args.loop_iters, "seconds": dt_loop,
+            "games_per_gpu": args.loop_games, "moves_per_iter": args.loop_moves_per_iter,
+            "train_steps_per_iter": args.loop_train_per_iter, "batch_per_gpu": args.trainer_batch,
+            "warmup_iterations": args.loop_warmup,
+            "finished_games": int(tot["games"]), "slices_added": int(tot["slices"]),
+            "weight_pushes": d["weight_pushes"], "model_update_interval": args.loop_update_interval,
+            "weight_push_ms": push_ms,
+            "push_share_at_interval": {"interval": 1000, "ms_per_trainer_step": push_ms / 1000.0,
+                                       "share_of_iteration": push_ms / 1000.0 / step_ms if step_ms else None},
+            "data": "self-play with the trainer's weights, each slot's first game from a random opening of "
+                    "0..%d stones (staggered starts, so games finish in the timed window; later games from the "
+                    "empty board); each PER shard also pre-filled with %d synthetic slices so training starts "
+                    "at once" % (args.loop_openings, args.loop_prefill),
+            "parallelism": "dp%d: self-play + replay shard per GPU; one gradient all-reduce + sharded-PER syncs "
+                           "per step; rank 0 weight broadcast per push" % world}
+    return out
+
+
+def init_dist(args, rank, local, world):
+    """This process's GPU and (world > 1) its process group, every collective bounded by --dist-timeout."""
+    import datetime
+    dist = backend = None
+    if world > 1:
+        import torch.distributed as dist
+        # GMZ_DIST_BACKEND=gloo rehearses the N>1 path with several ranks sharing one GPU
+        backend = os.environ.get("GMZ_DIST_BACKEND", "nccl")
+        torch.cuda.set_device(local % torch.cuda.device_count())
+        dist.init_process_group(backend, init_method="env://",
+                                timeout=datetime.timedelta(seconds=args.dist_timeout))
+        if rank == 0:
+            log("torch.distributed: world_size=%d backend=%s (%s)" % (dist.get_world_size(), dist.get_backend(),
+                                                                      "RCCL" if backend == "nccl" else backend))
+    else:
+        torch.cuda.set_device(0)
+    return dist, backend
+
+
+def phase_child(args, phase, rank, local, world):
+    """A phase's rank process (started by ``orchestrate``): its legs, then rank 0 prints the fragment."""
+    consumer = start_consumer() if (phase == "extras" and args.worker_moves > 0 and args.net == "hip") else None
+    dist, backend = init_dist(args, rank, local, world)
+    frag = run_phase(phase, args, rank, world, dist, backend, consumer)
+    if rank == 0:
+        print(PHASE_MARK + json.dumps(frag), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+def _parse_fragment(text):
+    for line in reversed((text or "").splitlines()):
+        if line.startswith(PHASE_MARK):
+            return json.loads(line[len(PHASE_MARK):])
+    return None
+
+
+def orchestrate(args, argv, rank, world, script=None):
+    """N > 1: this rank process never touches the GPU.  Every phase runs as a FRESH set of rank processes
+    (one per rank, a process group of their own on a new port) under a wall-time cap, so a failure or hang
+    in one phase - the trainer's first multi-rank RCCL all-reduce, say - cannot take the headline with it.
+    The rank processes talk over a CPU (gloo) group: the phase ports, and each phase's exit status (a rank
+    whose phase process failed raises a flag in the group's store, and its peers stop theirs at once instead
+    of waiting for their collectives to time out).  Rank 0 assembles the ONE line: the selfplay phase's
+    fragment, then each later phase's, or {"error": ...} in the keys of a phase that failed or timed out."""
+    import datetime
+    import torch.distributed as dist
+    caps = phase_plan(args)
+    dist.init_process_group("gloo", init_method="env://",
+                            timeout=datetime.timedelta(seconds=max(c for _, c in caps) + 300))
+    store = None
+    try:
+        from torch.distributed import distributed_c10d as c10d
+        store = c10d._get_default_store()
+    except Exception:
+        store = None
+    box = [[_free_port() for _ in caps] if rank == 0 else None]
+    dist.broadcast_object_list(box, src=0)
+    ports = box[0]
+    out, phases = None, {}
+    for (name, cap), port in zip(caps, ports):
+        env = dict(os.environ, MASTER_PORT=str(port), **{PHASE_ENV: name})
+        env.pop("TORCHELASTIC_USE_AGENT_STORE", None)  # the phase group hosts its own store
+        if out is not None and out.get("value"):
+            env["GMZ_BENCH_HEADLINE_VALUE"] = repr(out["value"])
+        t0 = time.time()
+        # its own session: a kill takes the phase's helper processes (the worker leg's queue consumer) with it
+        p = subprocess.Popen([sys.executable, "-u", script or os.path.abspath(__file__)] + list(argv), env=env,
+                             stdout=subprocess.PIPE, text=True, start_new_session=True)
+        flag = "gmz_phase_failed/%s" % name
+        status, text = None, ""
+        import threading
+        buf = []
+        reader = threading.Thread(target=lambda: buf.append(p.stdout.read()), daemon=True)
+        reader.start()
+        while True:
+            code = p.poll()
+            if code is not None:
+                status = "ok" if code == 0 else "exit %d" % code
+                break
+            if time.time() - t0 > cap:
+                status = "timeout after %d s" % cap
+                break
+            if store is not None:
+                try:
+                    if store.check([flag]):
+                        status = "stopped: another rank's %s phase failed" % name
+                        break
+                except Exception:
+                    pass
+            time.sleep(0.25)
+        if p.poll() is None:
+            import signal
+            try:
+                os.killpg(p.pid, signal.SIGKILL)  # the process group this phase started (its own session)
+            except ProcessLookupError:
+                pass
+            p.wait()
+        reader.join(timeout=30)
+        text = buf[0] if buf else ""
+        if status != "ok" and store is not None and not status.startswith("stopped"):
+            try:
+                store.set(flag, "1")
+            except Exception:
+                pass
+        every = [None] * world
+        dist.all_gather_object(every, {"status": status, "seconds": round(time.time() - t0, 1)})
+        if rank == 0:
+            frag = _parse_fragment(text)
+            failed = [i for i, e in enumerate(every) if e["status"] != "ok"]
+            phases[name] = {"ranks": every, "cap_s": cap}
+            log("phase %s: %s" % (name, ", ".join("rank %d %s (%.1f s)" % (i, e["status"], e["seconds"])
+                                                  for i, e in enumerate(every))))
+            if name == "selfplay":
+                if frag is None or failed:
+                    out = {"metric": "self-play moves/sec (15x15, 400 sims)", "value": None, "unit": "moves/s",
+                           "n_gpus": world, "higher_is_better": True,
+                           "error": "headline phase failed: %s" % "; ".join(
+                               "rank %d %s" % (i, every[i]["status"]) for i in failed) if failed else
+                           "headline phase printed no result"}
+                else:
+                    out = frag
+            else:
+                if frag is not None and not failed:
+                    out.update(frag)
+                else:
+                    err = {"error": "phase %s failed: %s" % (name, "; ".join(
+                        "rank %d %s" % (i, every[i]["status"]) for i in failed) or "no result"), "n_gpus": world}
+                    for k in phase_keys(name, args):  # rank 0's numbers, if any, kept but flagged
+                        out[k] = dict((frag or {}).get(k) or {}, **err)
+    if rank == 0:
+        out["phases"] = {"isolated": True, "detail": phases,
+                         "note": "each phase ran as fresh rank processes with a wall-time cap (bench.orchestrate)"}
+        print(json.dumps(out), flush=True)
+    dist.destroy_process_group()
+    return 0 if (rank != 0 or out.get("value")) else 1
+
+
 def main():
     args = parse()
     env_world = os.environ.get("WORLD_SIZE")
@@ -723,77 +1036,31 @@ def main():
         sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # the worker leg's queue consumer: a child process started before anything touches the GPU
+    args.headline_value = float(os.environ.get("GMZ_BENCH_HEADLINE_VALUE", "0")) or None
+    phase = os.environ.get(PHASE_ENV)
+    if phase:  # a phase's rank process
+        phase_child(args, phase, rank, local, world)
+        return
+    isolate = args.isolate == "on" or (args.isolate == "auto" and world > 1)
+    if isolate:
+        rc = orchestrate(args, sys.argv[1:], rank, world)
+        sys.exit(rc)
+    # one process (the N = 1 default): every phase in this process, in order; a later phase's failure is
+    # recorded in its keys and does not lose the headline
     consumer = start_consumer() if (args.worker_moves > 0 and args.net == "hip") else None
-    dist = None
-    backend = None
-    if world > 1:
-        import torch.distributed as dist
-        # GMZ_DIST_BACKEND=gloo rehearses the N>1 path with several ranks sharing one GPU
-        backend = os.environ.get("GMZ_DIST_BACKEND", "nccl")
-        torch.cuda.set_device(local % torch.cuda.device_count())
-        dist.init_process_group(backend, init_method="env://")
-        if rank == 0:
-            log("torch.distributed: world_size=%d backend=%s (%s)" % (dist.get_world_size(), dist.get_backend(),
-                                                                      "RCCL" if backend == "nccl" else backend))
-    else:
-        torch.cuda.set_device(0)
-
-    G = args.games
-    r = selfplay_leg(args, rank, world, dist, backend, args.size, args.sims, args.mode, args.blocks, G, args.steps,
-                     args.warmup, streams=args.streams, single_stream_moves=args.single_stream_moves)
-    args.streams = r["streams"]
-    out = result_line(args, world, r["dt"], r["waves"], G, backend)
-    for k in ("roofline", "roofline_tree", "single_stream_kernels"):
-        if k in r:
-            out[k] = r[k]
-    if args.net == "hip":
-        subs = {}
-        for key in [k.strip() for k in args.sublines.split(",") if k.strip()]:
-            if key not in SUBLINES:
-                raise SystemExit("bench.py: unknown --sublines entry %r" % key)
-            subs[key] = subline(args, key, rank, world, dist, backend)
-        if subs:
-            out["sublines"] = subs
-    if consumer is not None:
-        out["worker"] = worker_leg(args, rank, world, dist, backend, consumer, out["value"])
-        consumer[2].put(None)  # the consumer process exits
-        torch.cuda.empty_cache()
-    if args.trainer_steps > 0 and args.net == "hip":
-        torch.cuda.empty_cache()
-        out["trainer"] = trainer_leg(args, world, rank, dist, backend)
-    if args.loop_iters > 0 and args.net == "hip":
-        from datou_gomoku_muzero_amd.loop import run_c4
-        for mode in [m.strip() for m in args.loop_modes.split(",") if m.strip()]:
-            if mode not in ("sliced", "concurrent"):
-                raise SystemExit("bench.py: unknown --loop-modes entry %r" % mode)
-            args.loop_concurrent = mode == "concurrent"
-            torch.cuda.empty_cache()
-            d, dt_loop = run_c4(args, rank, world, dist, backend, log=log)
-            dt_loop = collective_max(dt_loop, dist, backend)
-            push_ms = collective_max(d.pop("push_ms"), dist, backend)
-            tot = {k: collective_sum(float(v), dist, backend) for k, v in d.items()}
-            step_ms = dt_loop / max(1, d["train_steps"]) * 1e3
-            out["loop_c4" if mode == "sliced" else "loop_c4_concurrent"] = {
-                "metric": "C4 loop: self-play moves/sec and trainer steps/sec with both running on every GPU",
-                "mode": mode + (": each iteration's trainer steps run on their own HIP stream beside its self-play "
-                                "moves" if mode == "concurrent" else ": each iteration = moves, then trainer steps"),
-                "moves_per_s": tot["moves"] * args.loop_games / dt_loop, "trainer_steps_per_s": d["train_steps"] / dt_loop,
-                "unit": "moves/s, steps/s", "n_gpus": world, "iterations": args.loop_iters, "seconds": dt_loop,
-                "games_per_gpu": args.loop_games, "moves_per_iter": args.loop_moves_per_iter,
-                "train_steps_per_iter": args.loop_train_per_iter, "batch_per_gpu": args.trainer_batch,
-                "warmup_iterations": args.loop_warmup,
-                "finished_games": int(tot["games"]), "slices_added": int(tot["slices"]),
-                "weight_pushes": d["weight_pushes"], "model_update_interval": args.loop_update_interval,
-                "weight_push_ms": push_ms,
-                "push_share_at_interval": {"interval": 1000, "ms_per_trainer_step": push_ms / 1000.0,
-                                           "share_of_iteration": push_ms / 1000.0 / step_ms if step_ms else None},
-                "data": "self-play with the trainer's weights, each slot's first game from a random opening of "
-                        "0..%d stones (staggered starts, so games finish in the timed window; later games from the "
-                        "empty board); each PER shard also pre-filled with %d synthetic slices so training starts "
-                        "at once" % (args.loop_openings, args.loop_prefill),
-                "parallelism": "dp%d: self-play + replay shard per GPU; one gradient all-reduce + sharded-PER syncs "
-                               "per step; rank 0 weight broadcast per push" % world}
+    dist, backend = init_dist(args, rank, local, world)
+    out = None
+    for name, _ in phase_plan(args):
+        if name == "selfplay":
+            out = run_phase(name, args, rank, world, dist, backend)
+            continue
+        try:
+            out.update(run_phase(name, args, rank, world, dist, backend, consumer, out))
+        except Exception as ex:  # noqa: BLE001 - recorded in the line; the headline is already measured
+            import traceback
+            traceback.print_exc()
+            for k in phase_keys(name, args):
+                out.setdefault(k, {"error": "phase %s failed: %r" % (name, ex), "n_gpus": world})
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.net == "hip":
         log("cpu baseline (bounded sample ~%.0f s)..." % args.cpu_baseline_sec)
         out["cpu_baseline"] = cpu_baseline(args)

@@ -284,8 +284,9 @@ class SplitSelfPlayEngine:
     half's work (measured with tools/dual_stream_probe.py).  Every game's search is
     exactly the unsplit engine's: part i plays games [i*G/parts, (i+1)*G/parts) with ``game_offset``
     so the device Gumbel noise per game is unchanged, its outputs are row views of the full
-    tensors, and the descent-hint choice (hence the non-root softmax arithmetic) is
-    made from the total G, as for one engine.  Calls fork from the caller's stream and join back to it."""
+    tensors.  Layout and descent hint default per part (from G/parts games: ``default_layout(g)``);
+    every default uses the cached-exp softmax, so the results equal one engine's with
+    all G games whatever layout each side picks.  Calls fork from the caller's stream and join back."""
 
     def __init__(self, cfg=None, num_games=2, net=None, device="cuda", seed=0, parts=2, max_grid=None,
                  descent_hint=None, layout=None, **overrides):
@@ -487,6 +488,42 @@ def _has_five(board, n_in_row=5):
                 if w[0] != 0 and (w == w[0]).all():
                     return True
     return False
+
+
+def _place_stones(rs, A, size, n, n_in_row):
+    """n stones of alternating colour (black first) on random cells of an empty board with no n_in_row
+    line, drawn from ``rs`` (redrawn until the board holds no line).  Returns (board int8[A], cells)."""
+    while True:
+        cells = rs.permutation(A)[:n]
+        b = np.zeros(A, np.int8)
+        b[cells[0::2]] = 1
+        b[cells[1::2]] = -1
+        if not _has_five(b.reshape(size, size), n_in_row):
+            return b, cells
+
+
+def seeded_openings(game_ids, size, seed, ks=(0, 4, 8), stagger=0, n_in_row=5):
+    """SURVEY §8(d)'s synthetic starts: game ``gid`` draws from ``RandomState(seed + gid)`` an opening of
+    k in ``ks`` stones (empty boards plus k in {0, 4, 8}) and, with ``stagger`` > 0, uniform(0, stagger)
+    further stones (at most 2A/5 in all), so that the G games are spread over their lifetimes and some finish (and restart
+    from the empty board) in any window of a few moves: the steady state a long self-play run is in.
+    Returns (boards int8 [G,S,S], players int8 [G], last_moves int32 [G], move_counts int32 [G])."""
+    A = size * size
+    G = len(game_ids)
+    boards = np.zeros((G, size, size), np.int8)
+    players = np.ones(G, np.int8)
+    last = np.full(G, -1, np.int32)
+    counts = np.zeros(G, np.int32)
+    for i, gid in enumerate(game_ids):
+        rs = np.random.RandomState((int(seed) + int(gid)) % (2 ** 32))
+        n = int(ks[rs.randint(len(ks))]) + (int(rs.randint(0, stagger + 1)) if stagger > 0 else 0)
+        n = min(n, 2 * A // 5)  # small boards: room left to play, and a line-free draw stays likely
+        b, cells = _place_stones(rs, A, size, n, n_in_row)
+        boards[i] = b.reshape(size, size)
+        players[i] = 1 if n % 2 == 0 else -1
+        last[i] = cells[-1] if n else -1
+        counts[i] = n
+    return boards, players, last, counts
 
 
 def random_openings(G, size, rs, max_stones, n_in_row=5):

@@ -164,7 +164,12 @@ class C4Loop:
         if self.sp_stream is not None:
             # on the self-play stream, not the trainer's (concurrent mode calls this from inside the train
             # stream's context): the copies of the new weights are then ordered before the next move's
-            # kernels, and after the previous move's, which join this stream
+            # kernels, and after the previous move's, which join this stream.  With RCCL the broadcast
+            # filled its device buffers on the CURRENT stream (the trainer's in concurrent mode), so the
+            # self-play stream waits for that stream before it reads them
+            cur = torch.cuda.current_stream(self.device)
+            if cur != self.sp_stream:
+                self.sp_stream.wait_stream(cur)
             with torch.cuda.stream(self.sp_stream):
                 self.sp.load_weights(sd)
         else:
@@ -234,7 +239,7 @@ def run_c4(args, rank, world, dist, backend, log=print):
     if getattr(args, "loop_openings", 0) > 0:  # staggered starts: games at every stage from the first move on
         from .engine import random_openings
         openings = random_openings(args.loop_games, args.size, np.random.RandomState(args.seed + 17 * rank),
-                                   args.loop_openings)
+                                   args.loop_openings, n_in_row=cfg.N_IN_ROW)
     sp = SelfPlay(cfg, args.loop_games, sd, seed=args.seed + 7919 * rank, precision=getattr(args, "precision", "fp16"),
                   openings=openings)
     rb = T.ReplayBuffer(tcfg, device="cuda")

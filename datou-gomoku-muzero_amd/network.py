@@ -18,6 +18,7 @@ hidden-state pool; MFMA accumulation is float32 either way and gfx950 runs both 
 ``GomokuNetHip`` owns the 16-bit hidden-state slot pool (HBM) and launches the kernels through the
 C ABI (include/gmz.h gmz_net_*).  It is the ``net`` backend of engine.BatchedSelfPlayEngine.
 """
+import contextlib
 import copy
 import ctypes
 
@@ -285,18 +286,24 @@ class GomokuNetHip:
         self._children = getattr(self, "_children", []) + out
         return out
 
-    def _ws(self, rows):
+    def _ws(self, rows, stream=None):
         if rows > self.max_rows:  # grow the scratch (k_heads / reward split-K partials)
             self.max_rows = rows
             nbytes = ctypes.c_size_t()
             check(self.lib.gmz_net_workspace_bytes(ctypes.byref(self.w), rows, ctypes.byref(nbytes)))
-            self.workspace = torch.zeros(nbytes.value, dtype=torch.uint8, device=self.device)
+            # zero-filled on the launch stream, so the fill is ordered before this launch's tower reads
+            # its ticket word (the caller's current stream may be another one)
+            raw = stream.value if isinstance(stream, ctypes.c_void_p) else stream
+            st = (torch.cuda.ExternalStream(raw, device=self.device) if raw else
+                  torch.cuda.default_stream(self.device) if stream is not None else None)
+            with torch.cuda.stream(st) if st is not None else contextlib.nullcontext():
+                self.workspace = torch.zeros(nbytes.value, dtype=torch.uint8, device=self.device)
         return ptr(self.workspace)
 
     # ---- engine backend interface
     def initial(self, obs, out_slot, logits, value, stream):
         rows = obs.shape[0]
-        ws = self._ws(rows)
+        ws = self._ws(rows, stream)
         t = self.repr_timer
         if t is not None:
             t.start()
@@ -309,7 +316,7 @@ class GomokuNetHip:
 
     def recurrent(self, in_slot, action, out_slot, logits, value, reward, stream):
         rows = in_slot.shape[0]
-        ws = self._ws(rows)
+        ws = self._ws(rows, stream)
         t = self.tower_timer
         if t is not None:
             t.start()

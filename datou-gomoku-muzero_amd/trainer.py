@@ -405,6 +405,10 @@ class _ResLink:
 # 26.4-26.5 -> 26.8-27.0 steps/s (same-box A/B, tools/bench_trainer.py --hip-wgrad).  The kernel's
 # per-board LDS DMA is not yet overlapped with its k-loop (~40 % MFMA busy)
 HIP_WGRAD = True
+# set by Trainer only while its own backward runs (its .grad tensors are views of the flat bucket that
+# nothing else reads): the HIP weight gradients then add straight into .grad and return None to
+# autograd.  Every other caller (torch.autograd.grad, hooks, other reducers) gets them through autograd.
+_DIRECT_GRAD = [False]
 _WGRAD_WS = {}
 
 
@@ -460,16 +464,19 @@ class _Conv3x3NHWC(torch.autograd.Function):
         gw = None
         if ctx.needs_input_grad[1]:
             if HIP_WGRAD:
-                # accumulated straight into the f32 .grad (the trainer's flat-bucket view; created when
-                # absent): no f16 gradient tensor, no cast, no AccumulateGrad add
-                if w.grad is None:
-                    w.grad = torch.zeros_like(w)
-                _conv3x3_wgrad_hip(x, gy, w.grad)
+                if _DIRECT_GRAD[0] and w.grad is not None and w.grad.dtype == torch.float32:
+                    # inside Trainer's backward: accumulated straight into the f32 .grad (the flat-bucket
+                    # view): no f16 gradient tensor, no cast, no AccumulateGrad add
+                    _conv3x3_wgrad_hip(x, gy, w.grad)
+                else:  # any other caller: the gradient goes back through autograd
+                    gw = torch.zeros_like(w, dtype=torch.float32)
+                    _conv3x3_wgrad_hip(x, gy, gw)
+                    gw = gw.to(w.dtype)
             else:
                 wd = torch.empty(w.shape, dtype=x.dtype, device=w.device, memory_format=torch.channels_last)  # shape only
                 gw = torch.ops.aten.convolution_backward(gy, x, wd, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
                                                          [False, True, False])[1]
-                if w.grad is not None and w.grad.dtype == torch.float32:
+                if _DIRECT_GRAD[0] and w.grad is not None and w.grad.dtype == torch.float32:
                     w.grad.add_(gw)  # one mixed-dtype add into the f32 .grad instead of a cast + AccumulateGrad
                     gw = None
                 else:
@@ -627,7 +634,8 @@ class _BigKLinear(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             gwt = xs.t() @ gy  # [K, O] in x's column order
             O = w.shape[0]
-            acc = w.grad is not None and w.grad.dtype == torch.float32 and w.grad.is_contiguous()
+            acc = (_DIRECT_GRAD[0] and w.grad is not None and w.grad.dtype == torch.float32
+                   and w.grad.is_contiguous())
             if ctx.perm is None:
                 gw = gwt.t().to(w.dtype)
             else:
@@ -1121,7 +1129,11 @@ class Trainer:
     def _forward_backward(self, batch, is_weights, acc=1, k=None, flip=None, augmented=False):
         loss, logs, td = muzero_loss(self.model, self.target, batch, is_weights, self.cfg, k=k, flip=flip,
                                      amp=self.amp, amp_dtype=self.amp_dtype, sync_logs=False, augmented=augmented)
-        self.scaler.scale(loss / acc).backward()
+        _DIRECT_GRAD[0] = True
+        try:
+            self.scaler.scale(loss / acc).backward()
+        finally:
+            _DIRECT_GRAD[0] = False
         return logs, td
 
     def _allreduce(self):

@@ -224,7 +224,10 @@ typedef struct gmz_net_weights {
 /* Scratch needed by gmz_net_initial / gmz_net_recurrent for `rows` rows (caller allocates, ZERO-FILLED
  * once: its first 8 B hold the tower's board-scheduling ticket word, tagged with each launch's
  * generation, so no launch depends on how the previous one ended; a workspace must not be shared by
- * launches that may run concurrently). */
+ * launches that may run concurrently).  The generation comes from a host counter and is baked into
+ * each launch's arguments, so the tower entry points (gmz_net_initial*, gmz_net_recurrent*) must NOT
+ * be captured into a HIP graph: every replay would reuse one generation and, from the second replay
+ * on, compute no boards. */
 int gmz_net_workspace_bytes(const gmz_net_weights *w, int rows, size_t *out);
 /* network.py:137-143 initial_inference: obs_dev f32[rows][3][A] -> logits f32[rows][A],
  * value f32[rows] (support_to_scalar), hidden state -> hid_pool_dev[out_slot[r]] (dtype [A][C]).

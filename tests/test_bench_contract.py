@@ -144,3 +144,81 @@ def test_ranks_per_gpu_counts_ranks_sharing_a_device():
     out = mgr.dict()
     mp.spawn(_rank_share, args=(2, _free_port(), out), nprocs=2, join=True)
     assert out[0] == out[1] == 2
+
+
+_PHASE_CHILD = r'''
+import json, os, sys, time
+phase, rank = os.environ["GMZ_BENCH_PHASE"], int(os.environ["RANK"])
+assert "TORCHELASTIC_USE_AGENT_STORE" not in os.environ
+frag = {"selfplay": {"metric": "m", "value": 10.0 + rank, "port": os.environ["MASTER_PORT"]},
+        "extras": {"sublines": {"c1": {"value": 1.0}}, "worker": {"value": 2.0}},
+        "trainer": {"trainer": {"value": 3.0}}, "loop": {"loop_c4": {"moves_per_s": 4.0}}}[phase]
+if phase == "trainer" and rank == 1:
+    sys.exit(3)                      # a rank whose phase fails
+if phase == "trainer" and rank == 0:
+    time.sleep(120)                  # its peer, stuck in a collective: stopped by the failure flag
+if phase == "loop" and rank == 1:
+    time.sleep(120)                  # a hang: stopped by the phase's wall-time cap
+if rank == 0:
+    print("GMZ_PHASE_RESULT " + json.dumps(frag), flush=True)
+'''
+
+_PHASE_PARENT = r'''
+import os, sys
+sys.path.insert(0, %r)
+import bench
+import torch.distributed as d
+_init = d.init_process_group
+
+
+def init(*a, **k):  # as under torch.distributed.run: the agent's store flag is in the rank's env
+    _init(*a, **k)
+    os.environ["TORCHELASTIC_USE_AGENT_STORE"] = "True"
+
+
+d.init_process_group = init
+argv = ["--gpus", "2", "--phase-timeout-loop", "6", "--sublines", "c1", "--worker-moves", "1"]
+if "RANK" not in os.environ:
+    sys.exit(bench.spawn_ranks(2, [], script=os.path.abspath(__file__)))
+args = bench.parse(argv)
+sys.exit(bench.orchestrate(args, argv, int(os.environ["RANK"]), 2, script=%r))
+'''
+
+
+def test_isolated_phases_keep_the_headline_when_a_later_phase_fails(tmp_path):
+    """bench.orchestrate (N > 1): every phase runs as fresh rank processes; a rank whose trainer phase
+    exits non-zero stops its peer (store flag) long before that peer's sleep ends, a hanging loop phase is
+    killed at its cap, and rank 0 still prints ONE line: the headline intact, {"error": ...} in the keys
+    of the failed phases, the extras merged."""
+    import json
+    import subprocess
+    import time
+    child = tmp_path / "child.py"
+    child.write_text(_PHASE_CHILD)
+    parent = tmp_path / "parent.py"
+    parent.write_text(_PHASE_PARENT % (REPO, str(child)))
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env.pop("RANK", None)
+    t0 = time.time()
+    p = subprocess.Popen([sys.executable, str(parent)], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                         text=True, start_new_session=True)
+    try:
+        out, err = p.communicate(timeout=200)
+    finally:
+        if p.poll() is None:
+            os.killpg(p.pid, 9)  # this test's own process group (the spawned ranks with it)
+            p.communicate()
+    p.stdout, p.stderr = out, err
+    took = time.time() - t0
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    d = json.loads(lines[0])
+    assert d["value"] == 10.0 and d["metric"] == "m"
+    assert d["sublines"] == {"c1": {"value": 1.0}} and d["worker"] == {"value": 2.0}
+    assert "error" in d["trainer"] and "rank 1 exit 3" in d["trainer"]["error"]
+    assert "error" in d["loop_c4"] and "timeout" in d["loop_c4"]["error"]
+    ranks = d["phases"]["detail"]["trainer"]["ranks"]
+    assert ranks[0]["status"].startswith("stopped") and ranks[0]["seconds"] < 60
+    assert took < 150

@@ -79,28 +79,36 @@ def test_selfplay_records_train_and_hot_swap(tmp_path):
 
 def test_bench_spawns_its_own_ranks_gloo_rehearsal():
     """`python bench.py --gpus 2` with no external launcher starts 2 rank processes (here sharing the
-    one GPU over gloo) and rank 0 prints ONE line with n_gpus 2 and the global game count."""
+    one GPU over gloo); each phase (headline, extras, trainer, loop) runs as fresh rank processes under a
+    wall-time cap, and rank 0 prints ONE line with n_gpus 2 and the global game count.  The trainer phase
+    of rank 1 is made to fail (GMZ_BENCH_INJECT_FAIL) while rank 0 waits in its collectives: the line
+    still carries the headline, the extras and the loop (whose DDP trainer steps over the same group
+    type), and {"error": ...} in "trainer" only."""
     import json
     import subprocess
     import sys
     from conftest import REPO
-    env = dict(os.environ, GMZ_DIST_BACKEND="gloo")
+    env = dict(os.environ, GMZ_DIST_BACKEND="gloo", GMZ_BENCH_INJECT_FAIL="trainer:1")
     env.pop("WORLD_SIZE", None)
     p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--games", "64",
                         "--size", "9", "--sims", "50", "--blocks", "1", "--steps", "2", "--warmup", "1",
                         "--trainer-steps", "2", "--trainer-warmup", "4", "--trainer-batch", "16", "--trainer-buffer", "64",
                         "--loop-iters", "4", "--loop-warmup", "4", "--loop-games", "64", "--loop-update-interval", "2",
                         "--loop-prefill", "64", "--loop-buffer", "4096", "--sublines", "c1", "--subline-games", "32",
-                        "--c1-steps", "2", "--worker-moves", "3", "--worker-warmup", "2"],
-                       env=env, capture_output=True, text=True, timeout=280)
+                        "--c1-steps", "2", "--worker-moves", "3", "--worker-warmup", "2", "--dist-timeout", "60",
+                        "--phase-timeout-trainer", "90"],
+                       env=env, capture_output=True, text=True, timeout=400)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [l for l in p.stdout.splitlines() if l.startswith("{")]  # (gloo itself prints connection notes)
     assert len(lines) == 1, p.stdout
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["config"]["global_games"] == 128 and d["config"]["ranks"] == 2
+    assert d["value"] > 0 and len(d["rank_values"]) == 2 and all(v > 0 for v in d["rank_values"])
     assert "world_size=2" in p.stderr
-    assert d["trainer"]["n_gpus"] == 2 and d["trainer"]["value"] > 0
+    assert "error" in d["trainer"] and "rank 1" in d["trainer"]["error"], d["trainer"]
+    assert d["phases"]["isolated"] and set(d["phases"]["detail"]) == {"selfplay", "extras", "trainer", "loop"}
     lc = d["loop_c4"]
+    assert "error" not in lc
     assert lc["n_gpus"] == 2 and lc["trainer_steps_per_s"] > 0 and lc["moves_per_s"] > 0 and lc["weight_pushes"] == 2
     assert lc["weight_push_ms"] > 0
     wk = d["worker"]
