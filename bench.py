@@ -462,7 +462,7 @@ def selfplay_leg(args, rank, world, dist, backend, size, sims, mode, blocks, G, 
         from datou_gomoku_muzero_amd.weight_sync import broadcast_state_dict
         dev = "cuda" if backend == "nccl" else "cpu"
         sd = {k: v.cpu().numpy() for k, v in broadcast_state_dict(sd, src=0, device=dev).items()}
-    slots = G * (cfg.NUM_SIMULATIONS + 2)
+    slots = E.hidden_slots(cfg, G)  # the steady-state pool (grows if late-game searches need more)
     if args.net == "hip":
         net = N.GomokuNetHip(sd, cfg, num_slots=slots, max_rows=G, precision=args.precision)
     else:

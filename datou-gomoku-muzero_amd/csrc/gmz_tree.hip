@@ -27,6 +27,9 @@
 //                         wave reductions; the hint is the predicted choice of the node's next visit
 //   per-game scalars GameState[G]
 // S = num_simulations + 2 node slots per game (root + <= 1 new node per wave + 1 scratch slot).
+// The network's hidden states are NOT addressed by this stride: node u of game g has hidden-state slot
+// hbase[g] + u (gmz_engine_set_hidden_bases), so the caller sizes each game's share of the pool by the
+// nodes its search can create (MuZero: one per wave, engine.py) instead of S.
 //
 // Numerics: float32 statistics with -ffp-contract=off and IEEE division reproduce the reference's
 // numpy-float32 arithmetic bit-for-bit; the completed-Q/softmax path is float64 exactly where the
@@ -92,6 +95,8 @@ struct Dev {
   int32_t *path_e;     // [G][S] child-list entry index of each non-root path level (compact child lists)
   int4 *hdr;           // [G][S] NodeHdr {tot = sum N_child, maxn = max N_child, nvis = #children N > 0, last}
   int32_t *ctr;        // [G][4] k_expand_select work counters (gmz_engine_tree_counters)
+  int32_t *hbase;      // [G] hidden-state slot of game g's node 0: node u's hidden state is pool slot hbase[g] + u
+                       //     (gmz_engine_set_hidden_bases; default g * S)
   GameState *gs;
   uint64_t *legal;  // [G][NJ]
   int16_t *set_rank;
@@ -1170,14 +1175,15 @@ __device__ __forceinline__ void select_game(const Dev &D, int g, int lane, int32
   }
   const int leaf = st.n_nodes;
   if (lane == 0) {
+    const int hb = D.hbase[g];  // the game's hidden-state slots (the network's pool), one per node
     st.n_nodes = leaf + 1;
     st.depth = d;
     st.leaf = leaf;
     st.k = AZ ? 1 : st.n_sel;
     D.gs[g] = st;
-    in_slot[g] = g * S + u;
+    in_slot[g] = hb + u;
     act_out[g] = a;
-    out_slot[g] = g * S + leaf;
+    out_slot[g] = hb + leaf;
   }
   if (AZ && obs) {  // observation of the replayed board (mcts.py:251)
     float *o = obs + (size_t)g * 3 * A;
@@ -1651,6 +1657,7 @@ GMZ_EXPORT int gmz_engine_create(const gmz_engine_cfg *cfg, gmz_engine **out) {
   rc |= dalloc(e, &D.node_action, G * S);
   rc |= dalloc(e, &D.hdr, G * S);
   rc |= dalloc(e, &D.ctr, G * 4);
+  rc |= dalloc(e, &D.hbase, G);
   rc |= dalloc(e, &D.path_u, G * S);
   rc |= dalloc(e, &D.path_a, G * S);
   rc |= dalloc(e, &D.path_e, G * S);
@@ -1670,6 +1677,14 @@ GMZ_EXPORT int gmz_engine_create(const gmz_engine_cfg *cfg, gmz_engine **out) {
   if (hipMemset(D.gs, 0, G * sizeof(GameState)) != hipSuccess || hipMemset(D.ctr, 0, G * 16) != hipSuccess) {
     gmz_engine_destroy(e);
     return fail("gmz_engine_create: hipMemset failed");
+  }
+  {  // default hidden-state slots: game g's nodes at g * S + u (a pool of G * S slots)
+    std::vector<int32_t> hb(G);
+    for (size_t g = 0; g < G; ++g) hb[g] = (int32_t)(g * S);
+    if (hipMemcpy(D.hbase, hb.data(), G * sizeof(int32_t), hipMemcpyHostToDevice) != hipSuccess) {
+      gmz_engine_destroy(e);
+      return fail("gmz_engine_create: hipMemcpy failed");
+    }
   }
   hipLaunchKernelGGL(k_reset_games, dim3(1, D.G), dim3(256), 0, 0, D, (const uint8_t *)nullptr);
   if (hipDeviceSynchronize() != hipSuccess) {
@@ -1925,6 +1940,13 @@ GMZ_EXPORT int gmz_engine_wave_depth(gmz_engine *e, int32_t *depth_dev, void *st
   if (!e || !depth_dev) return fail("gmz_engine_wave_depth: null argument");
   hipLaunchKernelGGL(k_wave_depth, dim3((e->D.G + 255) / 256), dim3(256), 0, (hipStream_t)stream, e->D, depth_dev);
   GMZ_LAUNCH_CHECK();
+  return 0;
+}
+
+GMZ_EXPORT int gmz_engine_set_hidden_bases(gmz_engine *e, const int32_t *hbase_dev, void *stream) {
+  if (!e || !hbase_dev) return fail("gmz_engine_set_hidden_bases: null argument");
+  GMZ_HIP(hipMemcpyAsync(e->D.hbase, hbase_dev, (size_t)e->D.G * sizeof(int32_t), hipMemcpyDeviceToDevice,
+                         (hipStream_t)stream));
   return 0;
 }
 

@@ -13,6 +13,7 @@ parity) and ``network.GomokuNetHip`` (GomokuNetEZ on MFMA kernels).
 Everything stays resident in HBM; the only host<->device traffic per move is the game status
 (G bytes) used to size the next move's wave loop, plus whatever the caller copies out.
 """
+import contextlib
 import ctypes
 
 import numpy as np
@@ -29,6 +30,12 @@ class HashNetBackend:
     def __init__(self, num_slots, action_space, device="cuda"):
         self.A = action_space
         self.pool = torch.zeros(num_slots, dtype=torch.int32, device=device)  # uint32 ids
+
+    def ensure_slots(self, n):
+        """At least ``n`` hidden-state slots (a larger pool, contents not kept: called between moves)."""
+        if n > self.pool.numel():
+            torch.cuda.synchronize(self.pool.device)
+            self.pool = torch.zeros(int(n * 1.25) + 1, dtype=torch.int32, device=self.pool.device)
 
     def split(self, parts, max_grid=0):
         """Backends over disjoint equal slices of the pool (SplitSelfPlayEngine)."""
@@ -90,7 +97,10 @@ class BatchedSelfPlayEngine:
         self.seed = int(seed)
         self.fuse_waves = True  # expand/backup + next select in one launch (False: the two entry points)
         G, A, dev = self.G, self.A, self.device
-        self.net = net if net is not None else HashNetBackend(G * self.slots_per_game, A, device)
+        # hidden-state slots per game by legal-move count (gmz_engine_set_hidden_bases): MuZero creates one
+        # node per wave (mcts.py:320-350), so a game needs waves(L) + 2 slots, not num_simulations + 2
+        self._slot_need = slot_need_table(self.ecfg, A, self.mode, self.lib)
+        self.net = net if net is not None else HashNetBackend(G * int(self._slot_need[A]), A, device)
         f32, i32 = torch.float32, torch.int32
         self.obs = torch.zeros(G, 3, c.BOARD_SIZE, c.BOARD_SIZE, dtype=f32, device=dev)
         self.logits = torch.zeros(G, A, dtype=f32, device=dev)
@@ -99,7 +109,13 @@ class BatchedSelfPlayEngine:
         self.in_slot = torch.zeros(G, dtype=i32, device=dev)
         self.out_slot = torch.zeros(G, dtype=i32, device=dev)
         self.act_req = torch.zeros(G, dtype=i32, device=dev)
+        # hidden-state slot of each game's root (= its node 0): hbase[g], rewritten when the bases move
         self.root_slot = torch.arange(G, dtype=i32, device=dev) * self.slots_per_game
+        self._hb_host = [torch.zeros(G, dtype=i32).pin_memory() for _ in range(2)]
+        self._hb_events = [None, None]
+        self._hb_flip = 0
+        self._hb_last = None  # the bases last handed to the engine (host copy)
+        self.hidden_slots_used = 0
         self.policy = torch.zeros(G, A, dtype=torch.float64, device=dev)
         self.root_value = torch.zeros(G, dtype=f32, device=dev)
         self.action = torch.zeros(G, dtype=i32, device=dev)
@@ -175,6 +191,40 @@ class BatchedSelfPlayEngine:
                 self._n_legal[played & ended] = np.maximum(self._n_legal[played & ended] - 1, 0)
             self._status_event = None
 
+    def _place_hidden(self, s, stream=None):
+        """Give every game the hidden-state slots its coming search can use: waves(L) + 2 for MuZero at
+        its legal count L (num_simulations + 2 for AlphaZero), packed game after game into the network's
+        pool.  L is known exactly after set_positions / reset_games; after a play() whose status has not
+        been read yet it is the last search's L - 1, or A for a game that ended and restarted: the larger
+        need of the two is taken.  The bases change only when a game's need does (late-game positions with
+        fewer than NUM_TOP_ACTIONS legal moves); then they are copied to the device on the search's stream."""
+        nl = self._n_legal
+        need = self._slot_need[np.clip(nl, 0, self.A)]
+        if self._status_event is not None:  # a move was played since nl was read
+            need = np.maximum(self._slot_need[np.clip(nl - 1, 0, self.A)], self._slot_need[self.A])
+        base = np.zeros(self.G, np.int64)
+        np.cumsum(need[:-1], out=base[1:])
+        total = int(base[-1] + need[-1])
+        if self._hb_last is not None and np.array_equal(base, self._hb_last):
+            return
+        if total >= 2 ** 31:
+            raise ValueError("hidden-state pool: %d slots exceed the int32 slot index" % total)
+        if hasattr(self.net, "ensure_slots"):
+            self.net.ensure_slots(total)
+        i = self._hb_flip
+        self._hb_flip ^= 1
+        if self._hb_events[i] is not None:
+            self._hb_events[i].synchronize()  # (a copy two placements ago: long done)
+        self._hb_host[i].numpy()[:] = base
+        with torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext():
+            self.root_slot.copy_(self._hb_host[i], non_blocking=True)  # on the search's stream
+            ev = torch.cuda.Event()
+            ev.record()
+        self._hb_events[i] = ev
+        check(self.lib.gmz_engine_set_hidden_bases(self.handle, ptr(self.root_slot), s))
+        self._hb_last = base
+        self.hidden_slots_used = total
+
     def waves_needed(self):
         out = ctypes.c_int32()
         nl = np.ascontiguousarray(self._n_legal, dtype=np.int32)
@@ -198,6 +248,7 @@ class BatchedSelfPlayEngine:
         g = None
         if gumbel is not None:
             g = torch.as_tensor(gumbel, dtype=torch.float64).to(self.device).contiguous()
+        self._place_hidden(s, stream)
         check(L.gmz_engine_begin_move(self.handle, ptr(g), self.seed, ptr(self.obs), s))
         self.net.initial(self.obs, self.root_slot, self.logits, self.value, s)
         check(L.gmz_engine_set_root(self.handle, ptr(self.logits), ptr(self.value), s))
@@ -306,7 +357,7 @@ class SplitSelfPlayEngine:
         if max_grid is None:
             max_grid = torch.cuda.get_device_properties(self.device).multi_processor_count * 3 // 4 if parts > 1 else 0
         if net is None:
-            net = HashNetBackend(G * self.slots_per_game, self.A, device)
+            net = HashNetBackend(hidden_slots(c, G), self.A, device)
         self.net = net
         nets = net.split(parts, max_grid) if parts > 1 else [net]
         if layout is None:
@@ -403,6 +454,40 @@ class SplitSelfPlayEngine:
     def root_stats(self):
         parts = [e.root_stats() for e in self.engines]
         return tuple(torch.cat([p[k] for p in parts]) for k in range(5))
+
+
+def slot_need_table(ecfg, A, mode, lib=None):
+    """Hidden-state slots one game's search can use, by legal-move count L = 0..A: MuZero creates the
+    root and one node per wave (mcts.py:320-350), i.e. gmz_engine_waves_for_legal(L) + 1, plus one
+    spare; AlphaZero one node per simulation (mcts.py:233-268): num_simulations + 2."""
+    L = lib if lib is not None else _lib.load()
+    tab = np.full(A + 1, ecfg.num_simulations + 2, np.int64)
+    if mode == 1:
+        out = ctypes.c_int32()
+        for n in range(A + 1):
+            one = np.array([n], np.int32)
+            check(L.gmz_engine_waves_for_legal(ctypes.byref(ecfg), one.ctypes.data_as(ctypes.c_void_p), 1,
+                                               ctypes.byref(out)))
+            tab[n] = out.value + 2
+    return tab
+
+
+def hidden_slots(cfg, num_games):
+    """Initial size of the network's hidden-state pool for ``num_games`` games: every game at a legal
+    count >= NUM_TOP_ACTIONS (MuZero C2: 102 slots per game instead of NUM_SIMULATIONS + 2 = 402; the
+    pool grows if late-game positions need more, BatchedSelfPlayEngine._place_hidden)."""
+    c = from_any(cfg)
+    A = c.ACTION_SPACE_SIZE
+    mode = 1 if c.MCTS_IMPLEMENTATION == "MuZero" else 0
+    ecfg = _lib.EngineCfg(1, c.BOARD_SIZE, c.N_IN_ROW, c.NUM_SIMULATIONS, c.NUM_TOP_ACTIONS, mode, int(c.C_VISIT), 0,
+                          float(c.C_SCALE), float(c.VALUE_MINMAX_DELTA), float(c.DISCOUNT), 0)
+    if mode == 0:
+        return int(num_games) * (c.NUM_SIMULATIONS + 2)
+    out = ctypes.c_int32()
+    one = np.array([A], np.int32)
+    check(_lib.load().gmz_engine_waves_for_legal(ctypes.byref(ecfg), one.ctypes.data_as(ctypes.c_void_p), 1,
+                                                 ctypes.byref(out)))
+    return int(num_games) * (out.value + 2)
 
 
 _ENGINE_STREAMS = {}

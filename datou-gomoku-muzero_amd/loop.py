@@ -67,7 +67,7 @@ class SelfPlay:
         from .worker import GameHistory
         c = cfg
         self.cfg, self.G = c, int(num_games)
-        self.net = N.GomokuNetHip(state_dict, c, num_slots=self.G * (c.NUM_SIMULATIONS + 2), max_rows=self.G,
+        self.net = N.GomokuNetHip(state_dict, c, num_slots=E.hidden_slots(c, self.G), max_rows=self.G,
                                   precision=precision)
         self.eng = E.make_engine(c, num_games=self.G, net=self.net, seed=seed, streams=streams)
         self.eng.reset_games()

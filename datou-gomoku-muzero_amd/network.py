@@ -221,7 +221,9 @@ class GomokuNetHip:
     """GomokuNetEZ initial/recurrent inference on the device (engine ``net`` backend).
 
     ``num_slots`` hidden-state slots of 16-bit [A][128] (``precision``: "fp16" default, or "bf16")
-    live in ``self.pool`` (HBM); the engine addresses them as ``game * slots_per_game + node``.
+    live in ``self.pool`` (HBM); the engine addresses node u of game g as slot hbase[g] + u, the per-game
+    bases packed by the legal-move count of each search (engine.BatchedSelfPlayEngine._place_hidden;
+    ``engine.hidden_slots(cfg, G)`` is the steady-state size, the pool grows when a search needs more).
     """
 
     def __init__(self, state_dict, cfg=None, num_slots=1, max_rows=1, device="cuda", precision="fp16", **overrides):
@@ -264,6 +266,14 @@ class GomokuNetHip:
             q.w = NetWeights.from_buffer_copy(w)
             q.w.max_grid = keep
             q._tensors = self._tensors
+
+    def ensure_slots(self, n):
+        """At least ``n`` hidden-state slots in ``self.pool`` (engine._place_hidden, between moves: the
+        contents are not kept).  A split() view that outgrows its slice gets a pool of its own."""
+        per = self.A * C
+        if n * per > self.pool.numel():
+            torch.cuda.synchronize(self.device)  # no launch still reads or writes the old pool
+            self.pool = torch.empty(int(n * 1.25 + 1) * per, dtype=torch.int16, device=self.device)
 
     def split(self, parts, max_grid=0):
         """``parts`` backends over disjoint, equal slices of this hidden-state pool that share the

@@ -752,6 +752,24 @@ def barlow_loss(z1, z2, lam, mask=None):
     return on + lam * off
 
 
+def barlow_loss_steps(z1, z2, lam, mask):
+    """barlow_loss of U unroll steps at once: z1, z2 [U, B, D], mask bool [U, B] -> [U] (each step's
+    loss over its own live rows; one batched standardisation and one bmm instead of U of each)."""
+    z1, z2 = z1.float(), z2.float()
+    w = mask.to(torch.float32)[..., None]
+    n = w.sum(1, keepdim=True).clamp(min=1.0)  # [U, 1, 1]
+
+    def std(z):
+        zc = z - (z * w).sum(1, keepdim=True) / n
+        return zc * torch.rsqrt((zc * zc * w).sum(1, keepdim=True) / n + 1e-5) * w
+
+    c = torch.bmm(std(z1).transpose(1, 2), std(z2)) / n  # [U, D, D]
+    diag = torch.diagonal(c, dim1=1, dim2=2)
+    on = (diag - 1).pow(2).sum(1)
+    off = c.pow(2).sum((1, 2)) - diag.pow(2).sum(1)
+    return on + lam * off
+
+
 def augment(obs, pi, act, k, flip):
     """loss.py:36-51: rotate the board planes k quarter turns (and mirror), the policies and the
     action indices with them.  obs [B, U+1, 3, H, W]; pi [B, U+1, A]; act [B, U] (-1 kept)."""
@@ -805,6 +823,9 @@ AUTOCAST_CACHE = True  # autocast's weight casts once per step (and per graph re
 # obs[s+1] (loss.py:104), overlapping the unroll's dynamics chain; results are identical (same
 # kernels; every BatchNorm's running statistics are updated in the same order)
 CONCURRENT_FORWARD = True
+# the unroll steps' cross-entropies and Barlow losses batched over the steps after the unroll (one call
+# each over the stacked [U, B, .] head outputs) instead of per step (False: per step, for A/B)
+BATCHED_LOSS = True
 _SIDE_STREAMS = {}
 
 
@@ -889,7 +910,9 @@ def muzero_loss(model, target_model, batch, is_weights, cfg, k=None, flip=None, 
         lr_ = torch.zeros(obs.shape[0], device=obs.device)
         steps = zero
         cons = zero
-        for s in range(c.NUM_UNROLL_STEPS):
+        U = c.NUM_UNROLL_STEPS
+        per_step = []  # BATCHED_LOSS: each step's head outputs, their loss terms taken after the unroll
+        for s in range(U):
             m = act[:, s] != -1
             live = m.any().to(torch.float32)   # 0: the reference's `continue` (loss.py:90-91)
             steps = steps + live
@@ -897,11 +920,12 @@ def muzero_loss(model, target_model, batch, is_weights, cfg, k=None, flip=None, 
             # sub-batch h[m] computation, loss.py:89-107, with fixed shapes)
             hk, rl = model.dynamics(h, torch.where(m, act_aug[:, s], torch.zeros_like(act_aug[:, s])), mask=m)
             plk, vlk = model.prediction(hk, mask=m)
-            lp = lp + torch.where(m, F.cross_entropy(plk.float(), pi[:, s + 1], reduction="none"), zero)
-            lv = lv + torch.where(m, F.cross_entropy(vlk.float(), zsup[s + 1],
-                                                     reduction="none"), zero)
-            lr_ = lr_ + torch.where(m, F.cross_entropy(rl.float(), rsupt[s],
-                                                       reduction="none"), zero)
+            if not BATCHED_LOSS:
+                lp = lp + torch.where(m, F.cross_entropy(plk.float(), pi[:, s + 1], reduction="none"), zero)
+                lv = lv + torch.where(m, F.cross_entropy(vlk.float(), zsup[s + 1],
+                                                         reduction="none"), zero)
+                lr_ = lr_ + torch.where(m, F.cross_entropy(rl.float(), rsupt[s],
+                                                           reduction="none"), zero)
             dyn = model.project(hk, with_grad=True, mask=m)
             with torch.no_grad():
                 if tru_h is not None:
@@ -910,8 +934,26 @@ def muzero_loss(model, target_model, batch, is_weights, cfg, k=None, flip=None, 
                     tru = model.project(tru_h[s], with_grad=False, mask=m)
                 else:
                     tru = model.project(model.representation(obs[:, s + 1], mask=m), with_grad=False, mask=m)
-            cons = cons + live * barlow_loss(dyn, tru, c.BARLOW_LAMBDA, m)
+            if BATCHED_LOSS:
+                per_step.append((m, plk, vlk, rl, dyn, tru))
+            else:
+                cons = cons + live * barlow_loss(dyn, tru, c.BARLOW_LAMBDA, m)
             h = _HalveGrad.apply(torch.where(m[:, None, None, None], hk, h))
+        if BATCHED_LOSS and U > 0:
+            # the U steps' cross-entropies and consistency losses as one call each over the stacked
+            # [U, B, .] outputs (masked rows zeroed, summed over the steps): the same per-row values as
+            # the per-step calls, ~5x fewer kernels in the forward and the backward
+            ms, pls, vls, rls, dyns, trus = (torch.stack(x) for x in zip(*per_step))
+            B = ms.shape[1]
+
+            def ce(logits, target):
+                x = logits.float().reshape(U * B, -1)
+                return F.cross_entropy(x, target.reshape(U * B, -1), reduction="none").view(U, B)
+            lp = lp + torch.where(ms, ce(pls, pi[:, 1:].transpose(0, 1)), zero).sum(0)
+            lv = lv + torch.where(ms, ce(vls, zsup[1:]), zero).sum(0)
+            lr_ = lr_ + torch.where(ms, ce(rls, rsupt), zero).sum(0)
+            live_s = ms.any(1).to(torch.float32)
+            cons = (live_s * barlow_loss_steps(dyns, trus, c.BARLOW_LAMBDA, ms)).sum()
     lp = lp / (steps + 1)
     lv = lv / (steps + 1)
     lr_ = lr_ / steps.clamp(min=1.0)

@@ -189,7 +189,7 @@ def gpu_selfplay_worker(worker_id, worker_mode, data_queue, log_status_queue, ui
     if state_dict is None:
         state_dict = W.synthetic_state_dict(c, seed=seed, with_projection=False)
     G = int(num_games)
-    net = N.GomokuNetHip(state_dict, c, num_slots=G * (c.NUM_SIMULATIONS + 2), max_rows=G, precision=precision)
+    net = N.GomokuNetHip(state_dict, c, num_slots=E.hidden_slots(c, G), max_rows=G, precision=precision)
     eng = E.make_engine(c, num_games=G, net=net, seed=seed + 7919 * int(worker_id), streams=streams)
     eng.reset_games()
     H, A = c.BOARD_SIZE, c.ACTION_SPACE_SIZE

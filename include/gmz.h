@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define GMZ_ABI_VERSION 5
+#define GMZ_ABI_VERSION 6
 
 /* ------------------------------------------------------------------ misc */
 const char *gmz_last_error(void);
@@ -113,10 +113,17 @@ int gmz_engine_begin_move(gmz_engine *e, const double *gumbel_dev, uint64_t seed
 /* Step 2 (mcts.py:308-317): root.expand(logits), backup(root value), Gumbel top-k.
  * logits_dev f32[G][A], value_dev f32[G] = initial_inference outputs for obs of step 1. */
 int gmz_engine_set_root(gmz_engine *e, const float *logits_dev, const float *value_dev, void *stream);
+/* Hidden-state slots of the network's pool (the reference's Node.hidden_state, mcts.py:24-25): node u of
+ * game g uses slot hbase[g] + u.  hbase_dev int32[G] is copied (stream-ordered) into the engine and holds
+ * from the next select on; the default is g * (num_simulations + 2).  A MuZero search creates one node per
+ * wave (mcts.py:320-350), so the caller may give game g only gmz_engine_waves_for_legal(its legal count)
+ * + 2 slots (engine.py sizes the pool per move this way); the root's slot hbase[g] is the
+ * initial_inference output slot. */
+int gmz_engine_set_hidden_bases(gmz_engine *e, const int32_t *hbase_dev, void *stream);
 /* Step 3 (mcts.py:326-336 / 233-253): one wave.  For each game with an unfinished search:
  * descend to the leaf, allocate its node, and emit the network request
- *   MuZero:    in_slot_dev[g] = g*slots + parent node, action_dev[g] = leaf action,
- *              out_slot_dev[g] = g*slots + new node (slots = num_simulations + 2);
+ *   MuZero:    in_slot_dev[g] = hbase[g] + parent node, action_dev[g] = leaf action,
+ *              out_slot_dev[g] = hbase[g] + new node (gmz_engine_set_hidden_bases);
  *   AlphaZero: obs_dev[g] = observation of the root board replayed along the path,
  *              out_slot_dev[g] as above.
  * Games whose search has finished get in_slot = out_slot = -1 (network rows may be skipped). */

@@ -93,7 +93,7 @@ def main():
     # the bare engine on the same box and workload (bench.py's step: search + play), for the ratio
     from datou_gomoku_muzero_amd import engine as E, network as N, weights as W
     sd = W.synthetic_state_dict(cfg, seed=0, with_projection=False)
-    net = N.GomokuNetHip(sd, cfg, num_slots=a.games * (a.sims + 2), max_rows=a.games)
+    net = N.GomokuNetHip(sd, cfg, num_slots=E.hidden_slots(cfg, a.games), max_rows=a.games)
     eng = E.make_engine(cfg, num_games=a.games, net=net, seed=0)  # the worker's own choice of streams
     eng.reset_games()
     for i in range(a.warmup + a.moves):
