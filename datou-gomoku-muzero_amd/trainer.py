@@ -115,6 +115,12 @@ def _bn(mod, x, mask=None):
     untouched (the reference skips such a step)."""
     if mask is None or not mod.training:
         return mod(x)
+    if SUBBATCH_BN:  # diagnostics: the reference's own computation, native BatchNorm on the gathered live rows
+        idx = mask.nonzero().squeeze(1)
+        if idx.numel() == 0:
+            return x * 0
+        ys = mod(x.index_select(0, idx))
+        return torch.zeros(x.shape, dtype=ys.dtype, device=x.device).index_copy(0, idx, ys)
     x = x.float()
     dims = [0] + list(range(2, x.dim()))
     shape = [1, -1] + [1] * (x.dim() - 2)
@@ -137,6 +143,10 @@ def _bn(mod, x, mask=None):
     return y
 
 
+# diagnostics only (tools/trainer_ragged_diag.py, tests): _bn runs the reference's sub-batch BatchNorm — the
+# live rows gathered (h[m], loss.py:89-93) through the native module, in the activation dtype (float16
+# under autocast, as the reference's AMP on CUDA) — instead of the row-masked float32 statistics
+SUBBATCH_BN = False
 _BN_DTYPES = {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2}
 FUSED_BN = True  # device BatchNorm layers of a training-mode model run the HIP kernels (gmz_train.hip)
 
