@@ -135,6 +135,8 @@ def parse(argv=None):
                          "or compact lists of the visited children (identical results)")
     ap.add_argument("--hint", default=None, choices=["on", "off"],
                     help="descent prefetch hint / cached exp rows of the tree kernels (default: by game count)")
+    ap.add_argument("--pair", default=None, choices=["on", "off"],
+                    help="two waves per game in the fused tree kernel (engine.default_pair when omitted)")
     ap.add_argument("--precision", default="fp16", choices=["fp16", "bf16"],
                     help="MFMA operand type of the network towers (f32 accumulation either way)")
     ap.add_argument("--seed", type=int, default=1234)
@@ -469,7 +471,8 @@ def selfplay_leg(args, rank, world, dist, backend, size, sims, mode, blocks, G, 
         net = E.HashNetBackend(slots, cfg.ACTION_SPACE_SIZE)
     if streams is None:
         streams = E.default_streams(cfg, G)
-    tkw = dict(layout=args.layout, descent_hint=None if args.hint is None else args.hint == "on")
+    tkw = dict(layout=args.layout, descent_hint=None if args.hint is None else args.hint == "on",
+               pair=None if getattr(args, "pair", None) is None else args.pair == "on")
     eng = E.make_engine(cfg, num_games=G, net=net, seed=args.seed + 7919 * rank, streams=streams, **tkw)
     eng.reset_games()
     if openings is not None:
@@ -567,7 +570,7 @@ def selfplay_leg(args, rank, world, dist, backend, size, sims, mode, blocks, G, 
             "mean_backup_levels": ctr["backup_levels"] / max(1, ctr["backups"]),
             "mean_select_levels": ctr["select_levels"] / max(1, ctr["selects"]),
             "games_per_launch": ctr["backups"] / n_tree, "streams": streams, "busy_ms": busy_tree,
-            "layout": parts[0].layout, "descent_hint": parts[0].descent_hint,
+            "layout": parts[0].layout, "descent_hint": parts[0].descent_hint, "waves_per_game": 2 if parts[0].pair else 1,
             "achieved_per_launch": bpl / (ms_tree * 1e-3) / 1e9,
             "note": ("two streams: each launch runs on the CUs the other stream's capped tower leaves free (about "
                      "a quarter of them), so this is the kernel inside the step, not its own rate; "

@@ -1199,10 +1199,14 @@ __device__ __forceinline__ void select_game(const Dev &D, int g, int lane, int32
   }
 }
 
-template <int NJ, bool EX, bool CL>
+// WPG = 2 (k_expand_select_pair: two waves per game, wave wv): the expansion's row writes are split by
+// action word (wave wv writes words [wv * NJ/2, (wv + 1) * NJ/2)), both waves compute the leaf's max legal
+// logit over the whole row, and only wave 0 runs the backup and writes the per-game state.
+template <int NJ, bool EX, bool CL, int WPG = 1>
 __device__ __forceinline__ void expand_backup_game(const Dev &D, int g, int lane, const float *__restrict__ logits_in,
                                                    const float *__restrict__ value_in,
-                                                   const float *__restrict__ reward_in) {
+                                                   const float *__restrict__ reward_in, int wv = 0) {
+  static_assert(WPG == 1 || (WPG == 2 && NJ % 2 == 0 && EX && !CL), "two-wave expansion: dense rows with exp rows");
   const int A = D.A, S = D.S;
   const int32_t *pu = D.path_u + (size_t)g * S, *pa = D.path_a + (size_t)g * S, *pe = D.path_e + (size_t)g * S;
   // the first 64 path entries by lane, loaded beside the GameState (not after it): a level's node and
@@ -1229,23 +1233,31 @@ __device__ __forceinline__ void expand_backup_game(const Dev &D, int g, int lane
     }
     lm = dred_max_f(lm);
     if (lm == -INFINITY) lm = 0.f;
+    constexpr int J0 = WPG == 2 ? NJ / 2 : 0;  // this wave's first word (times wv)
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int a = lane + WAVE * j;
-      if (a < A) {
+      if (a < A && (WPG == 1 || j / (NJ / 2) == wv)) {
         nl[a] = lv[j];
         if (!CL) nrow[a] = Edge{-1, 0, 0.f, 0.f};  // (a compact list starts empty: nvis = 0)
       }
     }
+    if constexpr (WPG == 1) {
 #pragma unroll 1
-    for (int a = lane; a < A; a += WAVE)  // one exp live at a time (VGPR budget of the fused kernel)
-      nx[a] = exp((double)logits_in[(size_t)g * A + a] - (double)lm);
+      for (int a = lane; a < A; a += WAVE)  // one exp live at a time (VGPR budget of the fused kernel)
+        nx[a] = exp((double)logits_in[(size_t)g * A + a] - (double)lm);
+    } else {
+#pragma unroll 1
+      for (int a = lane + WAVE * J0 * wv; a < A && a < WAVE * J0 * (wv + 1); a += WAVE)
+        nx[a] = exp((double)logits_in[(size_t)g * A + a] - (double)lm);
+    }
   } else {
     for (int a = lane; a < A; a += WAVE) {
       nl[a] = logits_in[(size_t)g * A + a];
       if (!CL) nrow[a] = Edge{-1, 0, 0.f, 0.f};
     }
   }
+  if (WPG == 2 && wv != 0) return;  // the backup and the per-game state: wave 0
   if (lane == 0) {
     D.node_parent[(size_t)g * S + leaf] = pu[d - 1];
     D.node_action[(size_t)g * S + leaf] = pa[d - 1];
@@ -1477,6 +1489,245 @@ __global__ void __launch_bounds__(64 * WPB, NJ > 4 ? 1 : (CL ? (HINT && GMZ_CL_W
   // levels backed up, game-waves selected, levels walked by the selection (incl. the root level).
   // Lane 0 wrote the GameState in select_game, so its own read sees the new depth.
   if (lane == 0 && active0) {
+    const GameState s1 = D.gs[g];
+    int4 c = ((int4 *)D.ctr)[g];
+    c.x += 1;
+    c.y += depth0;
+    if (s1.active) { c.z += 1; c.w += s1.depth; }
+    ((int4 *)D.ctr)[g] = c;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Two waves per game (gmz_engine_cfg.flags bit 4; MuZero, dense rows with the descent hint, NJ = 4, i.e.
+// 129..256 actions: 15x15).  At 1,024 games per engine the one-wave kernel runs ONE wave per SIMD and
+// every level's dependent chain (row -> completed Q -> softmax -> scores -> argmax) is exposed; here a
+// 128-thread workgroup owns one game and wave h owns the action words 2h, 2h + 1 (actions 128h ..
+// 128h + 127): each wave fetches and scores half of a node's row, and per level two LDS exchanges (with
+// one barrier each) join the halves — the softmax denominator, then the (max score, first action,
+// child) of np.argmax, ties to the lower action = wave 0.  The root level (the least-visited selected
+// action) and the rare levels (every child visited, or the cached-exp form past GMZ_EX_MAX_EXP) run
+// redundantly in both waves on the whole row, as the one-wave kernel computes them.  The softmax sum is
+// the two waves' partial sums added (the one-wave kernel adds the four slots per lane first): a few ulp
+// in the improved policy, the same class of difference as the cached-exp form, checked
+// against the oracle by the same parity tests.
+struct PairLds {
+  static constexpr int EDGES = 0, EXPL = 2 * 1024, HDR = EXPL + 1024, HALF = HDR + 16;  // one wave's half row
+  static constexpr int XCH = 2 * HALF, BYTES = XCH + 64;
+};
+struct PairXch {
+  double sum[2];
+  double best[2];
+  int act[2], child[2];
+  int cp, pad[3];
+};
+
+// this wave's half of node u's row (edges of words 2h, 2h + 1, the exp values of actions 128h .. 128h + 127,
+// the header) into its half slot by LDS-DMA
+__device__ __forceinline__ void pair_row_dma(const Dev &D, int g, int u, int h, int lane, uint8_t *half) {
+  const char *row = (const char *)edge_row(D, g, u);
+  const char *xr = (const char *)expl_row(D, g, u);
+  int ln = lane;
+  asm volatile("" : "+v"(ln));
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj) {
+    const int a = ln + WAVE * (2 * h + jj), ac = a < D.A ? a : D.A - 1;
+    __builtin_amdgcn_global_load_lds((const void *)(row + (uint32_t)(ac * 16)),
+                                     (__attribute__((address_space(3))) void *)(half + PairLds::EDGES + jj * 1024), 16, 0, 0);
+  }
+  {
+    const int a = 2 * WAVE * h + 2 * ln, ac = a < D.A2 - 2 ? a : D.A2 - 2;
+    __builtin_amdgcn_global_load_lds((const void *)(xr + (uint32_t)(ac * 8)),
+                                     (__attribute__((address_space(3))) void *)(half + PairLds::EXPL), 16, 0, 0);
+  }
+  if (lane < 4)
+    __builtin_amdgcn_global_load_lds((const void *)((const int *)(D.hdr + (size_t)g * D.S + u) + lane),
+                                     (__attribute__((address_space(3))) void *)(half + PairLds::HDR), 4, 0, 0);
+}
+
+// _select_action at a non-root node (mcts.py:106-117), the halves of the row in the two waves
+__device__ int select_nonroot_pair(const Dev &D, const uint64_t (&lg)[4], int g, int u, int h, int lane,
+                                   const NormQ &nz, int *child, uint8_t *half, PairXch *xch, int *nxt_u) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA has landed
+  int4 e[2];
+  double ev[2];
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj) {
+    e[jj] = *(const int4 *)(half + PairLds::EDGES + jj * 1024 + lane * 16);
+    ev[jj] = *(const double *)(half + PairLds::EXPL + (lane + WAVE * jj) * 8);
+  }
+  const int4 hdr = *(const int4 *)(half + PairLds::HDR);
+  const int tot = __builtin_amdgcn_readfirstlane(hdr.x);
+  const int max_n = __builtin_amdgcn_readfirstlane(hdr.y);
+  const int nvis = __builtin_amdgcn_readfirstlane(hdr.z);
+  const int al = __builtin_amdgcn_readfirstlane(hdr.w);
+  *nxt_u = -1;
+  const bool ex_ok = !nz.have_range || (double)(D.c_visit + max_n) * D.c_scale * (1.0 - nz.nq0) <= GMZ_EX_MAX_EXP;
+  if (!(nvis < D.A && ex_ok)) {
+    // rare levels: both waves on the whole row, the one-wave kernel's arithmetic (logits form / float32 path)
+    RowRegs<4, false> cur;
+    row_fetch<4>(D, g, u, lane, cur);
+    int dummy;
+    return select_nonroot<4, false>(D, lg, g, u, lane, nz, child, cur, nullptr, &dummy);
+  }
+  int n[2], ch[2];
+  float q[2];
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj) {
+    const bool ok = lane + WAVE * (2 * h + jj) < D.A;
+    n[jj] = ok ? e[jj].y : 0;
+    ch[jj] = ok ? e[jj].x : -1;
+    q[jj] = 0.f;
+    if (n[jj] > 0) {  // get_qsa (mcts.py:35-38), as row_load
+      const float v = __int_as_float(e[jj].z) / (float)n[jj];
+      const float dv = D.disc_f * v;
+      q[jj] = __int_as_float(e[jj].w) + dv;
+    }
+  }
+  // the hinted action's child (prefetch target of the next level): published by the wave that owns it
+  const bool hint_ok = al >= 0 && al < D.A;
+  if (hint_ok && (al >> 7) == h) {
+    const int src = al & 63, js = (al >> 6) & 1;
+    const int cp = js ? __builtin_amdgcn_readlane(ch[1], src) : __builtin_amdgcn_readlane(ch[0], src);
+    if (lane == 0) xch->cp = cp;
+  }
+  // cached-exp softmax of the improved policy (select_nonroot, first branch)
+  const double scale = (double)(D.c_visit + max_n) * D.c_scale;
+  const double t0 = scale * nz.nq0;
+  double x[2];
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj) {
+    const int j = 2 * h + jj, a = lane + WAVE * j;
+    const bool ok = a < D.A && ((lg[j] >> lane) & 1ull);
+    x[jj] = ok ? ev[jj] : 0.0;
+  }
+  if (nvis > 0 && nz.have_range) {
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      if (n[jj] > 0) {
+        double y = ((double)q[jj] - (double)nz.mm_min) / (double)nz.den_f;
+        y = (y < 1.0) ? y : 1.0;
+        const double nq = (y > 0.0) ? y : 0.0;
+        x[jj] *= exp(scale * nq - t0);
+      }
+    }
+  }
+  double part = x[0] + x[1];
+  part = dred_sum_d(part);
+  if (lane == 0) xch->sum[h] = part;
+  __syncthreads();  // exchange 1: partial sums, the hinted child
+  const double sum = xch->sum[0] + xch->sum[1];
+  if (hint_ok) {
+    const int cp = xch->cp;
+    if (cp > 0 && cp < D.S) {  // this wave's half of the hinted child's row, while this level finishes
+      pair_row_dma(D, g, cp, h, lane, half);
+      *nxt_u = cp;
+    }
+  }
+  const double inv_s = 1.0 / sum;
+  const double inv_tot = 1.0 / (double)(1 + tot);
+  double sc[2], best = -INFINITY;
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj) {
+    const int j = 2 * h + jj, a = lane + WAVE * j;
+    sc[jj] = -INFINITY;
+    if (a < D.A && ((lg[j] >> lane) & 1ull)) sc[jj] = x[jj] * inv_s - (double)n[jj] * inv_tot;
+    best = fmax(best, sc[jj]);
+  }
+  best = dred_max_d(best);
+  int a = 0, cl = -1;  // first (lowest) action of this half with the half's best score
+#pragma unroll
+  for (int jj = 1; jj >= 0; --jj) {
+    const uint64_t mk = __ballot(sc[jj] == best && best != -INFINITY);
+    if (mk) {
+      const int src = __builtin_ctzll(mk);
+      a = WAVE * (2 * h + jj) + src;
+      cl = jj ? __builtin_amdgcn_readlane(ch[1], src) : __builtin_amdgcn_readlane(ch[0], src);
+    }
+  }
+  if (best == -INFINITY) cl = __builtin_amdgcn_readlane(ch[0], 0);  // (the one-wave kernel: action 0's child)
+  if (lane == 0) {
+    xch->best[h] = best;
+    xch->act[h] = best == -INFINITY ? 0 : a;
+    xch->child[h] = cl;
+  }
+  __syncthreads();  // exchange 2: np.argmax over the two halves (ties: the lower action, wave 0's)
+  const double b0 = xch->best[0], b1 = xch->best[1];
+  const int w = (b1 > b0) ? 1 : 0;
+  const int act = xch->act[w];
+  *child = xch->child[w];
+  // hint for the next visit: the same child again (select_nonroot)
+  if (h == 0 && lane == 0) D.hdr[(size_t)g * D.S + u].w = act;
+  return act;
+}
+
+// select_game for the two-wave workgroup (MuZero, dense rows with the hint); wave 0 writes every output
+__device__ void select_game_pair(const Dev &D, int g, int h, int lane, int32_t *__restrict__ in_slot,
+                                 int32_t *__restrict__ act_out, int32_t *__restrict__ out_slot, uint8_t *lds) {
+  const int S = D.S;
+  GameState st = uniform_state(D.gs[g]);
+  if (!st.active) {
+    if (h == 0 && lane == 0) {
+      in_slot[g] = -1;
+      out_slot[g] = -1;
+      act_out[g] = 0;
+    }
+    return;
+  }
+  uint8_t *half = lds + h * PairLds::HALF;
+  PairXch *xch = (PairXch *)(lds + PairLds::XCH);
+  int u = 0, d = 0, a = 0;
+  int32_t *pu = D.path_u + (size_t)g * S, *pa = D.path_a + (size_t)g * S;
+  uint64_t lg[4];
+  load_legal<4>(D, g, lg);
+  int nxt_u = -1;
+  const NormQ nz = norm_q_consts(D, st.mm_max, st.mm_min);
+  for (;;) {
+    int c, cn = 0;
+    if (u == 0) {
+      a = select_root(D, g, lane, st.n_sel, &c, &cn);
+    } else {
+      if (u != nxt_u) pair_row_dma(D, g, u, h, lane, half);
+      a = select_nonroot_pair(D, lg, g, u, h, lane, nz, &c, half, xch, &nxt_u);
+    }
+    if (h == 0 && lane == 0) {
+      pu[d] = u;
+      pa[d] = a;
+    }
+    d++;
+    if (c < 0) break;
+    u = c;
+    if (d >= S - 1) break;  // cannot happen (tree depth < nodes); keeps the loop bounded
+  }
+  const int leaf = st.n_nodes;
+  if (h == 0 && lane == 0) {
+    const int hb = D.hbase[g];
+    st.n_nodes = leaf + 1;
+    st.depth = d;
+    st.leaf = leaf;
+    st.k = st.n_sel;
+    D.gs[g] = st;
+    in_slot[g] = hb + u;
+    act_out[g] = a;
+    out_slot[g] = hb + leaf;
+  }
+}
+
+// expand + backup of wave i, then select of wave i+1, one 128-thread workgroup per game (see above)
+__global__ void __launch_bounds__(128, 4) k_expand_select_pair(Dev D, const float *__restrict__ logits_in,
+                                                              const float *__restrict__ value_in,
+                                                              const float *__restrict__ reward_in,
+                                                              int32_t *__restrict__ in_slot, int32_t *__restrict__ act_out,
+                                                              int32_t *__restrict__ out_slot) {
+  const int g = blockIdx.x;
+  if (g >= D.G) return;
+  const int h = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE), lane = threadIdx.x & (WAVE - 1);
+  __shared__ __attribute__((aligned(16))) uint8_t lds[PairLds::BYTES];
+  const int active0 = __builtin_amdgcn_readfirstlane(D.gs[g].active), depth0 = __builtin_amdgcn_readfirstlane(D.gs[g].depth);
+  expand_backup_game<4, true, false, 2>(D, g, lane, logits_in, value_in, reward_in, h);
+  __syncthreads();  // wave 0's backup (tree statistics, GameState) before either wave selects
+  select_game_pair(D, g, h, lane, in_slot, act_out, out_slot, lds);
+  if (h == 0 && lane == 0 && active0) {  // work counters, as k_expand_select
     const GameState s1 = D.gs[g];
     int4 c = ((int4 *)D.ctr)[g];
     c.x += 1;
@@ -1781,6 +2032,14 @@ static int launch_select_nj(gmz_engine *e, hipStream_t s, int32_t *in_slot, int3
 template <int NJ, bool H, bool AZ, bool CL>
 static int launch_expand_select(gmz_engine *e, hipStream_t s, const float *logits, const float *value,
                                 const float *reward, int32_t *in_slot, int32_t *action, int32_t *out_slot, float *obs) {
+  if constexpr (NJ == 4 && H && !AZ && !CL) {
+    if (e->cfg.flags & 16) {  // two waves per game (k_expand_select_pair)
+      hipLaunchKernelGGL(k_expand_select_pair, dim3(e->D.G), dim3(128), 0, s, e->D, logits, value, reward, in_slot,
+                         action, out_slot);
+      GMZ_LAUNCH_CHECK();
+      return 0;
+    }
+  }
   if (!e->es_waves) {
     int nb = 0, ncu = 0, dev = 0;
     GMZ_HIP(hipGetDevice(&dev));

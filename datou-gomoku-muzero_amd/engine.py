@@ -61,7 +61,7 @@ class BatchedSelfPlayEngine:
     """G games per GPU.  ``cfg``: any object with the reference config attribute names."""
 
     def __init__(self, cfg=None, num_games=1, net=None, device="cuda", seed=0, descent_hint=None, game_offset=0,
-                 wpb=None, layout=None, **overrides):
+                 wpb=None, layout=None, pair=None, **overrides):
         self.cfg = from_any(cfg, **overrides)
         c = self.cfg
         if c.MCTS_IMPLEMENTATION not in ("AlphaZero", "MuZero"):
@@ -85,9 +85,14 @@ class BatchedSelfPlayEngine:
             raise ValueError("wpb: games per workgroup of the fused expand/select kernel must be None, 1 or 4")
         self.descent_hint = bool(descent_hint)
         self.layout = layout
+        # two waves per game in the fused expand/select kernel (MuZero, dense rows with the hint, 129..256
+        # actions; k_expand_select_pair): None = default_pair(G)
+        pair_ok = self.mode == 1 and layout == "dense" and self.descent_hint and 128 < self.A <= 256
+        self.pair = bool(pair_ok and (default_pair(self.G) if pair is None else pair))
         # flags (include/gmz.h): bit 0 no hint; bits 1 / 2 force 4-wave / 1-wave workgroups (None: by occupancy);
-        # bit 3 compact child lists for non-root nodes
-        flags = (0 if descent_hint else 1) | {None: 0, 4: 2, 1: 4}[wpb] | (8 if layout == "lists" else 0)
+        # bit 3 compact child lists for non-root nodes; bit 4 two waves per game
+        flags = ((0 if descent_hint else 1) | {None: 0, 4: 2, 1: 4}[wpb] | (8 if layout == "lists" else 0)
+                 | (16 if self.pair else 0))
         self.ecfg = _lib.EngineCfg(self.G, c.BOARD_SIZE, c.N_IN_ROW, c.NUM_SIMULATIONS, c.NUM_TOP_ACTIONS, self.mode,
                                    int(c.C_VISIT), flags, float(c.C_SCALE),
                                    float(c.VALUE_MINMAX_DELTA), float(c.DISCOUNT), int(game_offset))
@@ -340,7 +345,7 @@ class SplitSelfPlayEngine:
     all G games whatever layout each side picks.  Calls fork from the caller's stream and join back."""
 
     def __init__(self, cfg=None, num_games=2, net=None, device="cuda", seed=0, parts=2, max_grid=None,
-                 descent_hint=None, layout=None, **overrides):
+                 descent_hint=None, layout=None, pair=None, **overrides):
         self.cfg = from_any(cfg, **overrides)
         c = self.cfg
         G = int(num_games)
@@ -363,7 +368,7 @@ class SplitSelfPlayEngine:
         if layout is None:
             layout = default_layout(g)
         self.engines = [BatchedSelfPlayEngine(c, g, nets[i], device, seed, descent_hint, game_offset=i * g,
-                                              layout=layout) for i in range(parts)]
+                                              layout=layout, pair=pair) for i in range(parts)]
         self.streams = engine_streams(self.device, parts)
         dev = self.device
         self.policy = torch.zeros(G, self.A, dtype=torch.float64, device=dev)
@@ -512,6 +517,16 @@ def default_layout(num_games):
     or less, below 4,096 games), the lists from 4,096 (fewer bytes and instructions per tree level).
     Results are identical either way (tests/test_tree_lists_gpu.py)."""
     return "lists" if num_games >= 4096 else "dense"
+
+
+def default_pair(num_games):
+    """Two waves per game in the fused expand/select kernel (k_expand_select_pair) when one wave per game
+    would leave the SIMDs at one wave or fewer: as measured."""
+    return PAIR_DEFAULT and num_games <= PAIR_MAX_GAMES
+
+
+PAIR_DEFAULT = False
+PAIR_MAX_GAMES = 2048
 
 
 def default_streams(cfg, num_games):

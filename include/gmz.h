@@ -83,7 +83,10 @@ typedef struct gmz_engine_cfg {
                                workgroups of the fused expand/select kernel (default: 1-wave workgroups once the
                                games outnumber the variant's resident waves); results identical either way;
                                bit 3: compact child lists — a non-root node stores only its visited children's
-                               edges (needs num_simulations + 2 <= 65535); results identical to the dense rows */
+                               edges (needs num_simulations + 2 <= 65535); results identical to the dense rows;
+                               bit 4: two waves per game in the fused expand/select launch (MuZero, dense rows
+                               with the hint, 129..256 actions; other configurations ignore it): the same
+                               searches, the softmax sum formed from two half-row partial sums */
   double c_scale;           /* config.C_SCALE */
   double minmax_delta;      /* config.VALUE_MINMAX_DELTA */
   double discount;          /* config.DISCOUNT */
