@@ -89,17 +89,22 @@ __global__ void __launch_bounds__(BN_THREADS) k_bn_stats(const T *__restrict__ x
   }
 }
 
-// per-channel finalisation of the split partials ws[(c * cs + t * ts) * 3 + k], t < ns: one wave per
-// channel, lanes stride the splits (f64), then a wave sum.
+// per-channel finalisation of the split partials ws[(c * cs + t * ts) * 3 + k], t < ns: one workgroup per
+// channel of FIN_THREADS (a multiple of 64) threads striding the splits (f64; the splits of one channel are
+// 3 KB apart in the NHWC layout, so every load is its own round trip: 4 waves cut the one-wave version's 8
+// dependent trips per lane at 512 splits to 2), then wave sums and the waves' sums in wave order.
 //  forward : save = (mean, invstd), running-stat update (nn.BatchNorm training: unbiased variance)
 //  backward: dgamma = sum dz*xhat, dbeta = sum dz, coef = (mean dz, mean dz*xhat) over the masked rows
-__global__ void __launch_bounds__(WAVE) k_bn_finalize(const double *__restrict__ ws, int C, int ns, int cs, int ts,
-                                                      int backward, float eps, float momentum, float *save,
-                                                      float *running_mean, float *running_var, int64_t *num_batches,
-                                                      float *dgamma, float *dbeta, float *coef) {
-  const int c = blockIdx.x;
+constexpr int FIN_MAX_WAVES = 4;
+__global__ void __launch_bounds__(WAVE * FIN_MAX_WAVES) k_bn_finalize(const double *__restrict__ ws, int C, int ns, int cs,
+                                                                      int ts, int backward, float eps, float momentum,
+                                                                      float *save, float *running_mean,
+                                                                      float *running_var, int64_t *num_batches,
+                                                                      float *dgamma, float *dbeta, float *coef) {
+  const int c = blockIdx.x, nt = blockDim.x;
   double a = 0.0, b = 0.0, n = 0.0;
-  for (int t = threadIdx.x; t < ns; t += WAVE) {
+#pragma unroll 2
+  for (int t = threadIdx.x; t < ns; t += nt) {
     const double *p = ws + ((size_t)c * cs + (size_t)t * ts) * 3;
     a += p[0];
     b += p[1];
@@ -108,6 +113,22 @@ __global__ void __launch_bounds__(WAVE) k_bn_finalize(const double *__restrict__
   a = wave_sum_d(a);
   b = wave_sum_d(b);
   n = wave_sum_d(n);
+  if (nt > WAVE) {
+    __shared__ double red[FIN_MAX_WAVES][3];
+    const int w = threadIdx.x / WAVE;
+    if ((threadIdx.x & (WAVE - 1)) == 0) {
+      red[w][0] = a;
+      red[w][1] = b;
+      red[w][2] = n;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0)
+      for (int i = 1; i < nt / WAVE; ++i) {
+        a += red[i][0];
+        b += red[i][1];
+        n += red[i][2];
+      }
+  }
   if (threadIdx.x != 0) return;
   if (!backward) {
     const double nn = n > 0.0 ? n : 1.0;
@@ -422,6 +443,17 @@ __global__ void __launch_bounds__(BN_THREADS) k_bnl_bwd_apply(const T *__restric
   }
 }
 
+// threads per channel of k_bn_finalize: 256 (GMZ_BN_FIN_THREADS=64: the one-wave version, for A/B)
+static int fin_threads() {
+  static int t = 0;
+  if (!t) {
+    const char *e = getenv("GMZ_BN_FIN_THREADS");
+    const int v = e ? atoi(e) : WAVE * FIN_MAX_WAVES;
+    t = (v == WAVE || v == 2 * WAVE || v == 4 * WAVE) ? v : WAVE * FIN_MAX_WAVES;
+  }
+  return t;
+}
+
 int splits_for(int B, int C, int S, int nhwc) {
   // NCHW: (C x ns) workgroups, enough to cover the 256 CUs (>= ~2048), never more splits than rows;
   // NHWC: ns pixel ranges of all channels, 2 per CU, at least one block step (16 positions at C=128) each.
@@ -472,7 +504,7 @@ int bn_forward(int nhwc, const void *x, const void *res, const uint8_t *mask, in
                        (double *)ws);
   }
   GMZ_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_bn_finalize, dim3(C), dim3(WAVE), 0, st, (const double *)ws, C, ns, nhwc ? 1 : ns,
+  hipLaunchKernelGGL(k_bn_finalize, dim3(C), dim3(fin_threads()), 0, st, (const double *)ws, C, ns, nhwc ? 1 : ns,
                      nhwc ? C : 1, 0, eps, momentum, save, rm, rv, nb, (float *)nullptr, (float *)nullptr,
                      (float *)nullptr);
   GMZ_LAUNCH_CHECK();
@@ -511,7 +543,7 @@ int bn_backward(int nhwc, const void *x, const void *y, const void *dy, const ui
                        (const T *)dy, mask, B, C, S, save, relu, (double *)ws);
   }
   GMZ_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_bn_finalize, dim3(C), dim3(WAVE), 0, st, (const double *)ws, C, ns, nhwc ? 1 : ns,
+  hipLaunchKernelGGL(k_bn_finalize, dim3(C), dim3(fin_threads()), 0, st, (const double *)ws, C, ns, nhwc ? 1 : ns,
                      nhwc ? C : 1, accumulate ? 2 : 1, 0.f, 0.f, (float *)nullptr, (float *)nullptr, (float *)nullptr,
                      (int64_t *)nullptr, dgamma, dbeta, coef);
   GMZ_LAUNCH_CHECK();
@@ -537,7 +569,7 @@ template <typename T>
 int bn_forward_stats(const void *x, const void *res, int B, int C, int S, const float *gamma, const float *beta,
                      float eps, float momentum, float *rm, float *rv, int64_t *nb, int relu, void *y, float *save,
                      const double *stats, int ns, hipStream_t st) {
-  hipLaunchKernelGGL(k_bn_finalize, dim3(C), dim3(WAVE), 0, st, stats, C, ns, 1, C, 0, eps, momentum, save, rm, rv, nb,
+  hipLaunchKernelGGL(k_bn_finalize, dim3(C), dim3(fin_threads()), 0, st, stats, C, ns, 1, C, 0, eps, momentum, save, rm, rv, nb,
                      (float *)nullptr, (float *)nullptr, (float *)nullptr);
   GMZ_LAUNCH_CHECK();
   const int V = nhwc_vec(C, sizeof(T), {x, res, y});
