@@ -40,7 +40,7 @@ Prints ONE JSON line on rank 0 (schema: the driver contract) including
                   C5 = 19x19, 800 sims, 16 blocks (G games); C1 = 9x9 AlphaZero, 50 sims (G games), each with
                   moves/s and the tower's and tree kernel's roofline fractions (one stream: every launch alone);
                   g8192 = config 2's search on 8,192 trees as one engine (the tree kernel alone at SURVEY §8(d)'s
-                  measurement point; skipped, and said so, on a GPU without ~230 GiB free);
+                  measurement point; skipped, and said so, on a GPU without ~100 GiB free);
   worker        : the drop-in worker (worker.gpu_selfplay_worker) over torch.multiprocessing queues with a
                   consumer process unpickling every payload (the reference's process graph): moves/s over
                   the steady-state moves including every per-move and per-game record, and its ratio to
@@ -142,7 +142,9 @@ def parse(argv=None):
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--cpu-baseline-sec", type=float, default=20.0)
     ap.add_argument("--cpu-baseline-procs", type=int, default=16,
-                    help="single-threaded oracle processes (capped by the cores this process may use)")
+                    help="single-threaded oracle processes (capped by the cores this process may use); 16 = the "
+                         "reference's process graph size: NUM_WORKERS = 15 self-play workers (config.py:13) + its "
+                         "inference server, each a CPU process")
     ap.add_argument("--sublines", default="empty_board,c5,c1,g8192",
                     help="measured besides the headline: c5 (BASELINE config 5: 19x19/800/16 blocks), c1 (config 1: 9x9 "
                          "AlphaZero/50), g8192 (config 2's search on 8,192 trees, one engine: the tree kernel's "
@@ -351,8 +353,9 @@ def cpu_baseline(args):
     slowest = max(r["seconds"] for r in res)
     stones = sorted(x for r in res for x in r["stones"])
     return {"value": moves / slowest, "unit": "moves/s", "cores": P, "kind": "port",
-            "sample": "%d moves over %d single-threaded processes (one per core used; %d cores available to the "
-                      "process), each one %dx%d game from a random opening (%d..%d stones at the searched positions), "
+            "sample": "%d moves over %d single-threaded processes (one per core used, as many as the reference's "
+                      "process graph runs: NUM_WORKERS = 15 self-play workers + 1 inference server, config.py:13; "
+                      "%d cores available to the process), each one %dx%d game from a random opening (%d..%d stones at the searched positions), "
                       "%d sims (%s), %d NN rows (the reference's duplicate-leaf batches kept); slowest process %.1f s, "
                       "wall %.1f s; C oracle search + numpy fp32 GomokuNetEZ (oracle/cpu_baseline.py)"
                       % (moves, P, avail, args.size, args.size, stones[0], stones[-1], args.sims, args.mode, rows,
@@ -635,7 +638,7 @@ SUBLINES = {  # BASELINE.json configs run on the GPU besides the headline (C2)
     # SURVEY §8(d)'s tree-kernel measurement point (>= 8,192 trees): config C2's search with 8,192 games as ONE
     # engine on one stream (compact child lists, engine.default_layout), so roofline_tree is the kernel alone
     "g8192": dict(size=15, sims=400, mode="MuZero", blocks=8, games=8192, streams=1, steps=2, warmup=1,
-                  min_free_gb=230,
+                  min_free_gb=100,
                   name="C2's search at 8,192 trees on one GPU (one engine, one stream): the tree kernel at SURVEY "
                        "8(d)'s >= 8,192-tree measurement point"),
 }

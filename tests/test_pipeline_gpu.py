@@ -215,3 +215,38 @@ def test_c4_loop_at_its_own_workload(concurrent):
     torch.cuda.synchronize()
     assert isinstance(done, list)
     sp.close()
+
+
+def test_c2_at_8192_games_and_the_c4_trainer_share_one_card():
+    """Config C2's search at 8,192 concurrent games (its two-stream engine, hidden-state pool sized by the
+    waves a search can use: engine.hidden_slots) and config C4's trainer (B = 360, 15x15, 8 blocks, PER
+    shard) resident on one MI355X together: one self-play move of every game and trainer steps run, and
+    the card's used memory stays well inside its 288 GB (the hidden pool alone was 190 GB at 402 slots
+    per game before round 4)."""
+    from datou_gomoku_muzero_amd import engine as E, loop as LP, trainer as T, weights as W
+    from datou_gomoku_muzero_amd.config import GmzConfig
+    free0, total = torch.cuda.mem_get_info()
+    G = 8192
+    cfg = GmzConfig(BOARD_SIZE=15, NUM_SIMULATIONS=400, NUM_RES_BLOCKS=8)
+    tcfg = T.TrainConfig(BOARD_SIZE=15, NUM_RES_BLOCKS=8, PHYSICAL_BATCH_SIZE=360, TRAIN_BUFFER_SIZE=65536,
+                         ENABLE_PER=True)
+    tr = T.Trainer(tcfg, device="cuda")
+    sp = LP.SelfPlay(cfg, G, tr.state_dict_cpu(), seed=3)
+    pool_gb = sp.net.pool.numel() * 2 / 2 ** 30
+    assert sp.net.pool.numel() == E.hidden_slots(cfg, G) * 225 * 128 and pool_gb < 50
+    rb = T.ReplayBuffer(tcfg, device="cuda")
+    rb.add_arrays(*W.synthetic_slices(2048, 15, tcfg.NUM_UNROLL_STEPS, np.random.RandomState(0)))
+    rs = np.random.RandomState(1)
+    for _ in range(2):
+        sp.step()
+        batch, idx, w = rb.sample(360, rs)
+        logs, td = tr.step(batch, w)
+        rb.update_priorities(idx, td)
+        assert np.isfinite(logs[0])
+    torch.cuda.synchronize()
+    free1, _ = torch.cuda.mem_get_info()
+    used_gb = (free0 - free1) / 2 ** 30
+    print("C2 x 8192 games + C4 trainer: %.1f GiB used on the card (hidden pool %.1f GiB) of %.0f GiB"
+          % (used_gb, pool_gb, total / 2 ** 30))
+    assert used_gb < 0.5 * total / 2 ** 30
+    sp.close()

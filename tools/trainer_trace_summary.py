@@ -29,7 +29,7 @@ peak = 2500.0
 res = {"source": "rocprofv3 --kernel-trace of tools/bench_trainer.py --per (B=360, 15x15, 8 blocks, graph-replayed "
                  "step), last %.0f ms = %.1f steps at %.2f ms per step under the tracer" % (win, steps, step_ms),
        "launches_per_step": n / steps, "kernels": {}}
-for k, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:12]:
+for k, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:40]:
     res["kernels"][k[:90]] = {"launches_per_step": c / steps, "mean_us": t / c / 1e3, "ms_per_step": t / 1e6 / steps}
 conv = [(k, v) for k, v in agg.items() if "k_conv3<" in k]
 if conv:
