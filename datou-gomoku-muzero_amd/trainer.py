@@ -731,12 +731,16 @@ class TrainNet(nn.Module):
             return self.projection_net(h, mask)
 
     @torch.no_grad()
-    def initial_value(self, obs):
-        """initial_inference's value scalar (network.py:137-143), eval mode."""
+    def initial_value(self, obs, f16=False):
+        """initial_inference's value scalar (network.py:137-143), eval mode.  ``f16``: the convolutions and
+        linears with f16 operands and f32 accumulation (autocast; the residual convs on the HIP kernels):
+        the 10-bit mantissa the reference's float32 target forward gets from its CUDA GPU's default TF32
+        convolutions (loss.py:54-55 runs outside autocast; torch.backends.cudnn.allow_tf32 = True)."""
         self.eval()
-        _, vl = self.prediction(self.representation(obs))
+        with torch.autocast("cuda", dtype=torch.float16, enabled=bool(f16) and obs.is_cuda):
+            _, vl = self.prediction(self.representation(obs))
         c = self.cfg
-        return support_to_scalar(vl, c.VALUE_SUPPORT_MIN, c.VALUE_SUPPORT_MAX, c.VALUE_SUPPORT_BINS)
+        return support_to_scalar(vl.float(), c.VALUE_SUPPORT_MIN, c.VALUE_SUPPORT_MAX, c.VALUE_SUPPORT_BINS)
 
 
 # ------------------------------------------------------------------------------ loss
@@ -833,6 +837,9 @@ AUTOCAST_CACHE = True  # autocast's weight casts once per step (and per graph re
 # obs[s+1] (loss.py:104), overlapping the unroll's dynamics chain; results are identical (same
 # kernels; every BatchNorm's running statistics are updated in the same order)
 CONCURRENT_FORWARD = True
+# the target network's value (loss.py:54-55) with f16 operands and f32 accumulation (TrainNet.initial_value
+# f16=True; False: float32 on MIOpen, A/B)
+TARGET_F16 = False
 # the unroll steps' cross-entropies and Barlow losses batched over the steps after the unroll (one call
 # each over the stacked [U, B, .] head outputs) instead of per step (False: per step, for A/B)
 BATCHED_LOSS = True
@@ -878,11 +885,11 @@ def muzero_loss(model, target_model, batch, is_weights, cfg, k=None, flip=None, 
         main = torch.cuda.current_stream(obs.device)
         side[0].wait_stream(main)
         with torch.cuda.stream(side[0]), torch.no_grad():
-            last_v = target_model.initial_value(obs[:, -1])[:, 0]
+            last_v = target_model.initial_value(obs[:, -1], f16=TARGET_F16)[:, 0]
             z = value_targets(rew, mval, last_v, c)
     else:
         with torch.no_grad():
-            last_v = target_model.initial_value(obs[:, -1])[:, 0]
+            last_v = target_model.initial_value(obs[:, -1], f16=TARGET_F16)[:, 0]
             z = value_targets(rew, mval, last_v, c)
     dev_type = obs.device.type
     zero = torch.zeros((), device=obs.device)
@@ -1145,7 +1152,7 @@ class Trainer:
             # takes 0.19 ms per 360-board conv (128 TFLOP/s, fp32 MFMA), so the target goes channels-last
             # too; without Find MIOpen's immediate-mode NHWC fp32 pick takes 0.51 ms and its NCHW fp32
             # Winograd 0.26 ms, so the target stays NCHW
-            if torch.backends.cudnn.benchmark:
+            if torch.backends.cudnn.benchmark or TARGET_F16:  # (f16: the HIP residual convs need NHWC)
                 self.target = self.target.to(memory_format=torch.channels_last)
                 self.target.channels_last = True
         import torch.distributed as dist

@@ -128,3 +128,58 @@ def test_headline_composed_path_at_its_own_size(mods):
             assert np.abs(mv["pol"][g] - opol).max() <= 1e-12, (m, g)
             checked += 1
     assert checked == 16
+
+
+def test_c5_composed_path_at_its_own_size(mods):
+    """BASELINE config 5 as bench.py's c5 sub-line runs it: 19x19, 800 simulations, GomokuNetEZ 16 blocks,
+    1,024 games, engine.make_engine's default (one engine, one stream at 19x19: the single-image tower with
+    its global residual scratch), from the headline's kind of start positions; 8 of its searches equal the
+    C oracle driving the SAME HIP network row by row (mcts.py:288-362, network.py:137-152)."""
+    import oracle
+    E, N, W, GmzConfig = mods
+    size, sims, G = 19, 800, 1024
+    A = size * size
+    cfg = GmzConfig(BOARD_SIZE=size, NUM_SIMULATIONS=sims, MCTS_IMPLEMENTATION="MuZero", NUM_RES_BLOCKS=16)
+    sd = W.synthetic_state_dict(cfg, seed=77, with_projection=False)
+    net = N.GomokuNetHip(sd, cfg, num_slots=E.hidden_slots(cfg, G), max_rows=G)
+    eng = E.make_engine(cfg, num_games=G, net=net, seed=7)
+    assert isinstance(eng, E.BatchedSelfPlayEngine)
+    eng.reset_games()
+    eng.set_positions(*E.seeded_openings(range(G), size, 77, stagger=80))
+    noise = np.random.RandomState(5).gumbel(0, 1, (G, A))
+    mv = _play(eng, [noise])[0]
+    eng.close()
+    del eng, net
+    torch.cuda.empty_cache()
+    onet = N.GomokuNetHip(sd, cfg, num_slots=4096, max_rows=16)
+    nxt = [0]
+
+    def alloc(n):
+        s = list(range(nxt[0], nxt[0] + n))
+        nxt[0] += n
+        assert nxt[0] <= 4096
+        return s
+
+    def init(obs):
+        s = alloc(obs.shape[0])
+        lg, v, _ = onet.initial_inference(obs, slots=s)
+        torch.cuda.synchronize()
+        return lg.cpu().numpy(), v.cpu().numpy(), s
+
+    def rec(hs, acts):
+        s = alloc(len(hs))
+        lg, v, r = onet.recurrent_inference(hs, acts, s)
+        torch.cuda.synchronize()
+        return lg.cpu().numpy(), v.cpu().numpy(), r.cpu().numpy(), s
+
+    cb = oracle.CallbackNet(A, size, init, rec)
+    ocfg = oracle.make_cfg(size, sims, "MuZero", hashnet=False)
+    boards, players, lastm, counts = mv["pos"]
+    for g in np.linspace(3, G - 5, 8).astype(int):
+        nxt[0] = 0
+        cb.reset()
+        lm = int(lastm[g])
+        opol, oval, oact, orv, _ = oracle.search(ocfg, boards[g].reshape(-1), int(players[g]), None if lm < 0 else lm,
+                                                 int(counts[g]), noise[g], net=cb)
+        assert mv["act"][g] == oact and mv["val"][g] == oval and (mv["visits"][g] == orv).all(), g
+        assert np.abs(mv["pol"][g] - opol).max() <= 1e-12, g
