@@ -732,13 +732,15 @@ class TrainNet(nn.Module):
 
     @torch.no_grad()
     def initial_value(self, obs, f16=False):
-        """initial_inference's value scalar (network.py:137-143), eval mode.  ``f16``: the convolutions and
-        linears with f16 operands and f32 accumulation (autocast; the residual convs on the HIP kernels):
-        the 10-bit mantissa the reference's float32 target forward gets from its CUDA GPU's default TF32
-        convolutions (loss.py:54-55 runs outside autocast; torch.backends.cudnn.allow_tf32 = True)."""
+        """initial_inference's value scalar (network.py:137-143), eval mode.  ``f16``: the representation
+        trunk's convolutions with f16 operands and f32 accumulation (autocast; the residual convs on the HIP
+        kernels): the 10-bit mantissa the reference's float32 target forward gets from its CUDA GPU's
+        default TF32 convolutions (loss.py:54-55 runs outside autocast; torch.backends.cudnn.allow_tf32 =
+        True); the prediction heads stay float32."""
         self.eval()
         with torch.autocast("cuda", dtype=torch.float16, enabled=bool(f16) and obs.is_cuda):
-            _, vl = self.prediction(self.representation(obs))
+            h = self.representation(obs)
+        _, vl = self.prediction(h.float())  # the heads' linears in float32, as matmuls on CUDA (no TF32 default)
         c = self.cfg
         return support_to_scalar(vl.float(), c.VALUE_SUPPORT_MIN, c.VALUE_SUPPORT_MAX, c.VALUE_SUPPORT_BINS)
 

@@ -222,3 +222,41 @@ def test_isolated_phases_keep_the_headline_when_a_later_phase_fails(tmp_path):
     ranks = d["phases"]["detail"]["trainer"]["ranks"]
     assert ranks[0]["status"].startswith("stopped") and ranks[0]["seconds"] < 60
     assert took < 150
+
+
+def test_isolated_phases_under_torch_distributed_run(tmp_path):
+    """The driver's N > 1 launch: `python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1`
+    makes the rank processes (their process group on the launcher's agent store,
+    TORCHELASTIC_USE_AGENT_STORE set); bench.orchestrate's phase processes then host their own stores on new
+    ports.  Scripted phase processes as above: the one line carries the headline and the phases' errors."""
+    import json
+    import subprocess
+    import time
+    child = tmp_path / "child.py"
+    child.write_text(_PHASE_CHILD)
+    parent = tmp_path / "parent_run.py"
+    parent.write_text("import os, sys\nsys.path.insert(0, %r)\nimport bench\n"
+                      "argv = ['--gpus', '2', '--phase-timeout-loop', '6', '--sublines', 'c1', '--worker-moves', '1']\n"
+                      "assert os.environ.get('TORCHELASTIC_USE_AGENT_STORE') == 'True'\n"
+                      "sys.exit(bench.orchestrate(bench.parse(argv), argv, int(os.environ['RANK']), 2, script=%r))\n"
+                      % (REPO, str(child)))
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT", "MASTER_ADDR"):
+        env.pop(k, None)
+    p = subprocess.Popen([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                          "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(parent)],
+                         env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, start_new_session=True)
+    t0 = time.time()
+    try:
+        out, err = p.communicate(timeout=240)
+    finally:
+        if p.poll() is None:
+            os.killpg(p.pid, 9)  # this test's own process group
+            out, err = p.communicate()
+    assert p.returncode == 0, err[-3000:]
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out
+    d = json.loads(lines[0])
+    assert d["value"] == 10.0 and "error" in d["trainer"] and "error" in d["loop_c4"]
+    assert d["sublines"] == {"c1": {"value": 1.0}}
+    assert time.time() - t0 < 200
