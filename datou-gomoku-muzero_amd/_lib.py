@@ -66,6 +66,8 @@ _SIGS = {
     "gmz_conv3x3_stats_slots": ([I, ctypes.POINTER(ctypes.c_int)], I),
     "gmz_conv3x3_wgrad_workspace_bytes": ([I, ctypes.POINTER(ctypes.c_size_t)], I),
     "gmz_conv3x3_wgrad": ([I, I, P, P, I, P, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, I, P, P], I),
+    "gmz_conv3x3_wgrad_segments": ([I, I, P, P, I, I, P, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                                    I, P, P], I),
     "gmz_conv3x3_forward_stats": ([I, I, P, P, P, I, P, P, P], I),
     "gmz_grad_add_t": ([I, P, I, I, I, P, P], I),
     "gmz_bn_forward_stats": ([I, P, P, I, I, I, P, P, ctypes.c_float, ctypes.c_float, P, P, P, I, P, P, P, I, P], I),

@@ -305,9 +305,18 @@ __device__ __forceinline__ s16x4_t tr_read(const uint8_t *lds_base, int off) {
 #ifndef WGRAD_ABL
 #define WGRAD_ABL 0  // timing ablations (tools only): 1 = no DMA, 2 = k-loop twice per board
 #endif
+// the boards of one weight-gradient launch: up to 8 segments of nps boards each (board b of the launch is
+// board b % nps of segment b / nps), so the gradient contributions of one weight over several uses (the
+// dynamics trunk's convs in every unroll step) are one launch and one partial-sum reduction
+constexpr int WG_MAX_SEGS = 8;
+struct WgSrc {
+  const uint16_t *x[WG_MAX_SEGS];
+  const uint16_t *dy[WG_MAX_SEGS];
+  int nps;
+};
+
 template <int H, typename T>
-__global__ void __launch_bounds__(512, 1) k_conv3_wgrad(const uint16_t *__restrict__ x, const uint16_t *__restrict__ dy,
-                                                        int N, int nch, float *__restrict__ part) {
+__global__ void __launch_bounds__(512, 1) k_conv3_wgrad(WgSrc src, int N, int nch, float *__restrict__ part) {
   using L = WgLds<H>;
   using M = Mfma<T>;
   typedef typename M::V V;
@@ -338,8 +347,9 @@ __global__ void __launch_bounds__(512, 1) k_conv3_wgrad(const uint16_t *__restri
 
   for (int b = chunk; b < N; b += nch) {
     // ---- dy rows 0..A-1 and the x image interior: LDS-linear 1 KB pieces, row pads skipped
-    const uint8_t *sd = (const uint8_t *)(dy + (size_t)b * A * CC);
-    const uint8_t *sx = (const uint8_t *)(x + (size_t)b * A * CC);
+    const int sg = b / src.nps, lb = b - sg * src.nps;
+    const uint8_t *sd = (const uint8_t *)(src.dy[sg] + (size_t)lb * A * CC);
+    const uint8_t *sx = (const uint8_t *)(src.x[sg] + (size_t)lb * A * CC);
     for (int j = w; j < ((WGRAD_ABL & 1) ? 0 : L::NPD + H * L::RUN_DMA); j += 8) {
       if (j < L::NPD) {
         const int o = j * 1024 + lane * 16;
@@ -469,10 +479,9 @@ int wgrad_chunks(int N) {
 }
 
 template <int H, typename T>
-int launch_wgrad(const void *x, const void *dy, int N, float *part, hipStream_t st) {
+int launch_wgrad(const WgSrc &src, int N, float *part, hipStream_t st) {
   const int nch = wgrad_chunks(N);
-  hipLaunchKernelGGL((k_conv3_wgrad<H, T>), dim3(3 * nch), dim3(512), 0, st, (const uint16_t *)x, (const uint16_t *)dy,
-                     N, nch, part);
+  hipLaunchKernelGGL((k_conv3_wgrad<H, T>), dim3(3 * nch), dim3(512), 0, st, src, N, nch, part);
   GMZ_LAUNCH_CHECK();
   return 0;
 }
@@ -537,19 +546,15 @@ GMZ_EXPORT int gmz_conv3x3_wgrad_workspace_bytes(int N, size_t *out) {
   return 0;
 }
 
-GMZ_EXPORT int gmz_conv3x3_wgrad(int dtype, int H, const void *x, const void *dy, int N, float *dw, int64_t s0,
-                                 int64_t s1, int64_t s2, int64_t s3, int accumulate, void *workspace, void *stream) {
-  if (!x || !dy || !dw || !workspace) return fail("gmz_conv3x3_wgrad: null operand");
-  if (N <= 0) return fail("gmz_conv3x3_wgrad: N must be positive");
-  if (((uintptr_t)x | (uintptr_t)dy) & 15) return fail("gmz_conv3x3_wgrad: operands must be 16-B aligned");
-  hipStream_t st = (hipStream_t)stream;
+static int wgrad_launch(int dtype, int H, const WgSrc &src, int N, float *dw, int64_t s0, int64_t s1, int64_t s2,
+                        int64_t s3, int accumulate, void *workspace, hipStream_t st) {
   float *part = (float *)workspace;
   int rc;
   if (dtype == 1)
-    rc = H == 15 ? launch_wgrad<15, __half>(x, dy, N, part, st) : H == 9 ? launch_wgrad<9, __half>(x, dy, N, part, st) : -2;
+    rc = H == 15 ? launch_wgrad<15, __half>(src, N, part, st) : H == 9 ? launch_wgrad<9, __half>(src, N, part, st) : -2;
   else if (dtype == 2)
-    rc = H == 15 ? launch_wgrad<15, __hip_bfloat16>(x, dy, N, part, st)
-                 : H == 9 ? launch_wgrad<9, __hip_bfloat16>(x, dy, N, part, st) : -2;
+    rc = H == 15 ? launch_wgrad<15, __hip_bfloat16>(src, N, part, st)
+                 : H == 9 ? launch_wgrad<9, __hip_bfloat16>(src, N, part, st) : -2;
   else return fail("gmz_conv3x3_wgrad: dtype must be 1 (f16) or 2 (bf16)");
   if (rc == -2) return fail("gmz_conv3x3_wgrad: board size must be 9 or 15");
   if (rc) return rc;
@@ -557,4 +562,34 @@ GMZ_EXPORT int gmz_conv3x3_wgrad(int dtype, int H, const void *x, const void *dy
                      wgrad_chunks(N), dw, (long)s0, (long)s1, (long)s2, (long)s3, accumulate);
   GMZ_LAUNCH_CHECK();
   return 0;
+}
+
+GMZ_EXPORT int gmz_conv3x3_wgrad(int dtype, int H, const void *x, const void *dy, int N, float *dw, int64_t s0,
+                                 int64_t s1, int64_t s2, int64_t s3, int accumulate, void *workspace, void *stream) {
+  if (!x || !dy || !dw || !workspace) return fail("gmz_conv3x3_wgrad: null operand");
+  if (N <= 0) return fail("gmz_conv3x3_wgrad: N must be positive");
+  if (((uintptr_t)x | (uintptr_t)dy) & 15) return fail("gmz_conv3x3_wgrad: operands must be 16-B aligned");
+  WgSrc src = {};
+  src.x[0] = (const uint16_t *)x;
+  src.dy[0] = (const uint16_t *)dy;
+  src.nps = N;
+  return wgrad_launch(dtype, H, src, N, dw, s0, s1, s2, s3, accumulate, workspace, (hipStream_t)stream);
+}
+
+GMZ_EXPORT int gmz_conv3x3_wgrad_segments(int dtype, int H, const void *const *x_segs, const void *const *dy_segs,
+                                          int nseg, int n_per_seg, float *dw, int64_t s0, int64_t s1, int64_t s2,
+                                          int64_t s3, int accumulate, void *workspace, void *stream) {
+  if (!x_segs || !dy_segs || !dw || !workspace) return fail("gmz_conv3x3_wgrad_segments: null operand");
+  if (nseg < 1 || nseg > WG_MAX_SEGS || n_per_seg <= 0)
+    return fail("gmz_conv3x3_wgrad_segments: need 1 <= nseg <= 8 segments of n_per_seg > 0 boards");
+  WgSrc src = {};
+  for (int i = 0; i < nseg; ++i) {
+    if (!x_segs[i] || !dy_segs[i]) return fail("gmz_conv3x3_wgrad_segments: null segment");
+    if (((uintptr_t)x_segs[i] | (uintptr_t)dy_segs[i]) & 15)
+      return fail("gmz_conv3x3_wgrad_segments: operands must be 16-B aligned");
+    src.x[i] = (const uint16_t *)x_segs[i];
+    src.dy[i] = (const uint16_t *)dy_segs[i];
+  }
+  src.nps = n_per_seg;
+  return wgrad_launch(dtype, H, src, nseg * n_per_seg, dw, s0, s1, s2, s3, accumulate, workspace, (hipStream_t)stream);
 }

@@ -422,6 +422,41 @@ _DIRECT_GRAD = [False]
 _WGRAD_WS = {}
 
 
+# the 3x3 weight gradients of Trainer's backward deferred to its end: one multi-segment launch per weight
+# over every use of it (the dynamics trunk's convs run in all unroll steps: 5 launches and 5 partial-sum
+# reductions -> 1), gmz_conv3x3_wgrad_segments
+DEFER_WGRAD = True
+_PENDING_WGRAD = {}
+
+
+def flush_wgrads():
+    """Run the deferred weight gradients (DEFER_WGRAD) into their parameters' f32 .grad."""
+    import ctypes
+    from . import _lib
+    L = _lib.load()
+    for w, uses in _PENDING_WGRAD.items():
+        groups = {}
+        for x, gy in uses:
+            groups.setdefault((x.shape[0], x.dtype, x.shape[2]), []).append((x, gy))
+        for (N, dt, H), lst in groups.items():
+            for i in range(0, len(lst), 8):
+                seg = lst[i:i + 8]
+                n = len(seg) * N
+                if n not in _WGRAD_WS:
+                    nb = ctypes.c_size_t()
+                    _lib.check(L.gmz_conv3x3_wgrad_workspace_bytes(n, ctypes.byref(nb)))
+                    _WGRAD_WS[n] = nb.value
+                ws = torch.empty(_WGRAD_WS[n] // 4, dtype=torch.float32, device=w.device)
+                xs = (ctypes.c_void_p * len(seg))(*[x.data_ptr() for x, _ in seg])
+                gs = (ctypes.c_void_p * len(seg))(*[g.data_ptr() for _, g in seg])
+                st = w.grad.stride()
+                _lib.check(L.gmz_conv3x3_wgrad_segments(_CONV_DTYPES[dt], H, ctypes.cast(xs, ctypes.c_void_p),
+                                                        ctypes.cast(gs, ctypes.c_void_p), len(seg), N,
+                                                        _lib.ptr(w.grad), st[0], st[1], st[2], st[3], 1, _lib.ptr(ws),
+                                                        _lib.stream_ptr()))
+    _PENDING_WGRAD.clear()
+
+
 def _conv3x3_wgrad_hip(x, gy, grad):
     """grad (f32, any strides) += weight gradient of the 128->128 conv from channels-last x, gy."""
     import ctypes
@@ -476,8 +511,12 @@ class _Conv3x3NHWC(torch.autograd.Function):
             if HIP_WGRAD:
                 if _DIRECT_GRAD[0] and w.grad is not None and w.grad.dtype == torch.float32:
                     # inside Trainer's backward: accumulated straight into the f32 .grad (the flat-bucket
-                    # view): no f16 gradient tensor, no cast, no AccumulateGrad add
-                    _conv3x3_wgrad_hip(x, gy, w.grad)
+                    # view): no f16 gradient tensor, no cast, no AccumulateGrad add.  DEFER_WGRAD: after the
+                    # backward, one launch per weight over all its uses (flush_wgrads)
+                    if DEFER_WGRAD:
+                        _PENDING_WGRAD.setdefault(w, []).append((x, gy))
+                    else:
+                        _conv3x3_wgrad_hip(x, gy, w.grad)
                 else:  # any other caller: the gradient goes back through autograd
                     gw = torch.zeros_like(w, dtype=torch.float32)
                     _conv3x3_wgrad_hip(x, gy, gw)
@@ -1193,8 +1232,10 @@ class Trainer:
         _DIRECT_GRAD[0] = True
         try:
             self.scaler.scale(loss / acc).backward()
+            flush_wgrads()
         finally:
             _DIRECT_GRAD[0] = False
+            _PENDING_WGRAD.clear()
         return logs, td
 
     def _allreduce(self):

@@ -334,6 +334,13 @@ int gmz_conv3x3_stats_slots(int N, int *slots);
 int gmz_conv3x3_wgrad_workspace_bytes(int N, size_t *out);
 int gmz_conv3x3_wgrad(int dtype, int H, const void *x_dev, const void *dy_dev, int N, float *dw_dev, int64_t s0,
                       int64_t s1, int64_t s2, int64_t s3, int accumulate, void *workspace_dev, void *stream);
+/* gmz_conv3x3_wgrad over the boards of nseg (<= 8) segments of n_per_seg boards each (host arrays of device
+ * pointers x_segs[i], dy_segs[i]): the summed weight gradient of one convolution's several uses (the
+ * dynamics trunk in every unroll step, loss.py:86-107) in one launch and one partial-sum reduction;
+ * workspace: gmz_conv3x3_wgrad_workspace_bytes(nseg * n_per_seg). */
+int gmz_conv3x3_wgrad_segments(int dtype, int H, const void *const *x_segs, const void *const *dy_segs, int nseg,
+                               int n_per_seg, float *dw_dev, int64_t s0, int64_t s1, int64_t s2, int64_t s3,
+                               int accumulate, void *workspace_dev, void *stream);
 int gmz_conv3x3_forward_stats(int dtype, int H, const void *x_dev, const void *packed_dev, void *y_dev, int N,
                               const uint8_t *mask_dev, double *stats_dev, void *stream);
 /* dst_dev[o][c][p] += src_dev[(p*C + c)*O + o] (f32 accumulate; src dtype 0 = f32, 1 = f16, 2 = bf16):
