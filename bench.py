@@ -940,20 +940,25 @@ def orchestrate(args, argv, rank, world, script=None):
     import datetime
     import torch.distributed as dist
     caps = phase_plan(args)
-    dist.init_process_group("gloo", init_method="env://",
-                            timeout=datetime.timedelta(seconds=max(c for _, c in caps) + 300))
     store = None
-    try:
-        from torch.distributed import distributed_c10d as c10d
-        store = c10d._get_default_store()
-    except Exception:
-        store = None
-    box = [[_free_port() for _ in caps] if rank == 0 else None]
-    dist.broadcast_object_list(box, src=0)
-    ports = box[0]
+    if world > 1:
+        dist.init_process_group("gloo", init_method="env://",
+                                timeout=datetime.timedelta(seconds=max(c for _, c in caps) + 300))
+        try:
+            from torch.distributed import distributed_c10d as c10d
+            store = c10d._get_default_store()
+        except Exception:
+            store = None
+        box = [[_free_port() for _ in caps] if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        ports = box[0]
+    else:  # --isolate on with one GPU: the phases run one after the other as single processes
+        ports = [None for _ in caps]
     out, phases = None, {}
     for (name, cap), port in zip(caps, ports):
-        env = dict(os.environ, MASTER_PORT=str(port), **{PHASE_ENV: name})
+        env = dict(os.environ, **{PHASE_ENV: name})
+        if port is not None:
+            env["MASTER_PORT"] = str(port)
         env.pop("TORCHELASTIC_USE_AGENT_STORE", None)  # the phase group hosts its own store
         if out is not None and out.get("value"):
             env["GMZ_BENCH_HEADLINE_VALUE"] = repr(out["value"])
@@ -998,7 +1003,11 @@ def orchestrate(args, argv, rank, world, script=None):
             except Exception:
                 pass
         every = [None] * world
-        dist.all_gather_object(every, {"status": status, "seconds": round(time.time() - t0, 1)})
+        mine = {"status": status, "seconds": round(time.time() - t0, 1)}
+        if world > 1:
+            dist.all_gather_object(every, mine)
+        else:
+            every = [mine]
         if rank == 0:
             frag = _parse_fragment(text)
             failed = [i for i, e in enumerate(every) if e["status"] != "ok"]
@@ -1025,8 +1034,12 @@ def orchestrate(args, argv, rank, world, script=None):
     if rank == 0:
         out["phases"] = {"isolated": True, "detail": phases,
                          "note": "each phase ran as fresh rank processes with a wall-time cap (bench.orchestrate)"}
+        if world == 1 and not args.no_cpu_baseline and args.net == "hip":
+            log("cpu baseline (bounded sample ~%.0f s)..." % args.cpu_baseline_sec)
+            out["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(out), flush=True)
-    dist.destroy_process_group()
+    if world > 1:
+        dist.destroy_process_group()
     return 0 if (rank != 0 or out.get("value")) else 1
 
 

@@ -148,7 +148,7 @@ def test_ranks_per_gpu_counts_ranks_sharing_a_device():
 
 _PHASE_CHILD = r'''
 import json, os, sys, time
-phase, rank = os.environ["GMZ_BENCH_PHASE"], int(os.environ["RANK"])
+phase, rank = os.environ["GMZ_BENCH_PHASE"], int(os.environ.get("RANK", "0"))
 assert "TORCHELASTIC_USE_AGENT_STORE" not in os.environ
 frag = {"selfplay": {"metric": "m", "value": 10.0 + rank, "port": os.environ["MASTER_PORT"]},
         "extras": {"sublines": {"c1": {"value": 1.0}}, "worker": {"value": 2.0}},
@@ -260,3 +260,20 @@ def test_isolated_phases_under_torch_distributed_run(tmp_path):
     assert d["value"] == 10.0 and "error" in d["trainer"] and "error" in d["loop_c4"]
     assert d["sublines"] == {"c1": {"value": 1.0}}
     assert time.time() - t0 < 200
+
+
+def test_isolated_phases_with_one_gpu(tmp_path, capsys):
+    """bench.py --isolate on at N = 1: the phases run one after another as single fresh processes (no
+    process group); the line is assembled the same way (here rank 0's trainer phase succeeds)."""
+    import json
+    import bench
+    child = tmp_path / "child.py"
+    child.write_text(_PHASE_CHILD)
+    argv = ["--gpus", "1", "--isolate", "on", "--sublines", "c1", "--worker-moves", "1", "--loop-iters", "0",
+            "--no-cpu-baseline"]
+    for k in ("WORLD_SIZE", "RANK"):
+        os.environ.pop(k, None)
+    assert bench.orchestrate(bench.parse(argv), argv, 0, 1, script=str(child)) == 0
+    d = json.loads([l for l in capsys.readouterr().out.splitlines() if l.startswith("{")][-1])
+    assert d["value"] == 10.0 and d["trainer"] == {"value": 3.0} and "loop_c4" not in d
+    assert set(d["phases"]["detail"]) == {"selfplay", "extras", "trainer"}
