@@ -150,7 +150,7 @@ _PHASE_CHILD = r'''
 import json, os, sys, time
 phase, rank = os.environ["GMZ_BENCH_PHASE"], int(os.environ.get("RANK", "0"))
 assert "TORCHELASTIC_USE_AGENT_STORE" not in os.environ
-frag = {"selfplay": {"metric": "m", "value": 10.0 + rank, "port": os.environ["MASTER_PORT"]},
+frag = {"selfplay": {"metric": "m", "value": 10.0 + rank, "port": os.environ.get("MASTER_PORT")},
         "extras": {"sublines": {"c1": {"value": 1.0}}, "worker": {"value": 2.0}},
         "trainer": {"trainer": {"value": 3.0}}, "loop": {"loop_c4": {"moves_per_s": 4.0}}}[phase]
 if phase == "trainer" and rank == 1:
