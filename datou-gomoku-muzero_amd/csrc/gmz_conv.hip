@@ -95,7 +95,10 @@ __global__ void __launch_bounds__(256) k_pack_conv(const float *__restrict__ w, 
   *(uint4 *)(out + (size_t)i * 8) = r;
 }
 
-template <int H, typename T, int PG>
+// HALVES = 2: one workgroup per board computes both halves of the output channels from ONE DMA of the
+// board image (the k-loop twice, the weight ring reloaded for the second half's n-tiles): N workgroups
+// instead of 2N, one board DMA instead of two (gmz_conv3x3 A/B: GMZ_CONV_HALVES)
+template <int H, typename T, int PG, int HALVES = 1>
 __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restrict__ x, const uint16_t *__restrict__ wpk,
                                                   uint16_t *__restrict__ y, int N, const uint8_t *__restrict__ mask,
                                                   double *__restrict__ stats, const uint16_t *__restrict__ addend) {
@@ -116,9 +119,11 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
   // XCD-aware items: workgroups are dealt to the 8 XCDs round-robin by index, so workgroup i runs on
   // XCD i % 8; the two halves of a board are workgroups i and i ^ 8 (same XCD, dispatched together),
   // and the second one's board DMA is served by that XCD's L2 instead of HBM
-  const int half = (blockIdx.x >> 3) & 1;
-  const int b0 = (blockIdx.x >> 4) * 8 + (blockIdx.x & 7);  // first board; also the statistics slot
-  const int ntile0 = half * 4 + nq * NTW;  // this wave's first n-tile (of 8)
+  const int half0 = HALVES == 2 ? 0 : (blockIdx.x >> 3) & 1;
+  // first board; also the statistics slot
+  const int b0 = HALVES == 2 ? (int)blockIdx.x : (int)((blockIdx.x >> 4) * 8 + (blockIdx.x & 7));
+  const int bstride = HALVES == 2 ? (int)gridDim.x : (int)(gridDim.x >> 1);
+  int ntile0 = half0 * 4 + nq * NTW;  // this wave's first n-tile (of 8)
 
   for (int i = tid; i < I::BYTES / 16; i += NTHR) *(uint4 *)(img + i * 16) = make_uint4(0, 0, 0, 0);
 
@@ -130,7 +135,7 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
     pos[i] = (pt < NPT && p < A) ? (p / H) * RS + (p % H) * PS : -1;
   }
   const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc((void *)wpk, (short)0, FRAG_BYTES, 0x00020000);
-  const int wvoff = ntile0 * 1024 + lane * 16;
+  int wvoff = ntile0 * 1024 + lane * 16;
   V ar[RD][NTW];
   auto loadA = [&](int slot, int st) {
     const int soff = (st < CKSTEPS ? st : st - CKSTEPS) * 8192;
@@ -143,14 +148,16 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
   __syncthreads();  // zeroed image before the first DMA
   // BatchNorm statistics of the (rounded) output over the boards in the mask: per lane, its 4
   // channels of each n-tile summed over its positions and boards
-  float s1[NTW][4], s2[NTW][4];
+  float s1[HALVES][NTW][4], s2[HALVES][NTW][4];
 #pragma unroll
-  for (int nt = 0; nt < NTW; ++nt)
+  for (int hh = 0; hh < HALVES; ++hh)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) s1[nt][e] = s2[nt][e] = 0.f;
+    for (int nt = 0; nt < NTW; ++nt)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s1[hh][nt][e] = s2[hh][nt][e] = 0.f;
   int nvalid = 0;
 
-  for (int b = b0; b < N; b += gridDim.x >> 1) {
+  for (int b = b0; b < N; b += bstride) {
     // ---- board b -> image interior: 1 KB pieces of each board row's run of cells
     const uint8_t *src = (const uint8_t *)(x + (size_t)b * A * CC);
     for (int j = w; j < H * I::RUN_DMA; j += NW) {
@@ -164,7 +171,18 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    const bool counted = stats && (!mask || mask[b]);
+    nvalid += counted;
 
+#pragma unroll
+    for (int hh = 0; hh < HALVES; ++hh) {
+    if (HALVES == 2) {  // this half's n-tiles: the weight ring restarts on them
+      ntile0 = hh * 4 + nq * NTW;
+      wvoff = ntile0 * 1024 + lane * 16;
+      if (hh == 1)
+#pragma unroll
+        for (int k = 0; k < RD - 1; ++k) loadA(k, k);
+    }
     f32x4_t acc[NTW][PTW];
     int bb[PTW];
 #pragma unroll
@@ -203,8 +221,6 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
     // ---- epilogue: 4 consecutive output channels of one position per lane -> 8-byte store
     uint16_t *dst = y + (size_t)b * A * CC;
     const uint16_t *add = addend ? addend + (size_t)b * A * CC : nullptr;  // + addend, rounded once
-    const bool counted = stats && (!mask || mask[b]);
-    nvalid += counted;
 #pragma unroll
     for (int i = 0; i < PTW; ++i) {
       const int pt = pg + PG * i;
@@ -227,15 +243,26 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const float v = M::value(o[e]);
-            s1[nt][e] += v;
-            s2[nt][e] = fmaf(v, v, s2[nt][e]);
+            s1[hh][nt][e] += v;
+            s2[hh][nt][e] = fmaf(v, v, s2[hh][nt][e]);
           }
         }
       }
     }
+    }  // halves
+    if (HALVES == 2)  // the next board's first k-steps for half 0 (the ring holds half 1's)
+#pragma unroll
+      for (int k = 0; k < RD - 1; ++k) {
+        wvoff = nq * NTW * 1024 + lane * 16;
+        loadA(k, k);
+      }
     __syncthreads();  // every wave is done reading the image before the next board's DMA
   }
   if (!stats) return;
+#pragma unroll
+  for (int hh = 0; hh < HALVES; ++hh) {
+  const int half = HALVES == 2 ? hh : half0;
+  if (hh > 0) __syncthreads();  // the previous half's partials have left the LDS scratch
   // ---- per-workgroup partials: the 16 lanes of a lane group hold the same 4 channels at different
   // positions; then the PG position-group waves of a channel group meet in LDS (the image is free)
 #pragma unroll
@@ -244,8 +271,8 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
     for (int e = 0; e < 4; ++e)
 #pragma unroll
       for (int o = 1; o < 16; o <<= 1) {
-        s1[nt][e] += __shfl_xor(s1[nt][e], o, 64);
-        s2[nt][e] += __shfl_xor(s2[nt][e], o, 64);
+        s1[hh][nt][e] += __shfl_xor(s1[hh][nt][e], o, 64);
+        s2[hh][nt][e] += __shfl_xor(s2[hh][nt][e], o, 64);
       }
   float *red = (float *)img;  // [PG][64 channels of this half][2]
   if ((lane & 15) == 0) {
@@ -254,8 +281,8 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int cl = (nq * NTW + nt) * 16 + g4 * 4 + e;  // channel within this half
-        red[(pg * 64 + cl) * 2] = s1[nt][e];
-        red[(pg * 64 + cl) * 2 + 1] = s2[nt][e];
+        red[(pg * 64 + cl) * 2] = s1[hh][nt][e];
+        red[(pg * 64 + cl) * 2 + 1] = s2[hh][nt][e];
       }
   }
   __syncthreads();
@@ -271,6 +298,7 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
     out[1] = q;
     out[2] = (double)nvalid * A;
   }
+  }  // halves
 }
 
 // ---- weight gradient: dW[o][c][t] = sum over boards n and positions p of dy[n][p][o] * x[n][p + d(t)][c]
@@ -446,16 +474,38 @@ static int cu_count_conv() {
 
 constexpr int CONV_PG = 2;  // position groups per workgroup: 2 -> 4 waves, 8|7 tiles per wave
 
+// halves of the output channels per workgroup: 1 (two workgroups per board, the product since round 3) or
+// 2 (one per board, one DMA); GMZ_CONV_HALVES=2 selects the second (A/B)
+static int conv_halves() {
+  static int h = 0;
+  if (!h) {
+    const char *e = getenv("GMZ_CONV_HALVES");
+    h = (e && atoi(e) == 2) ? 2 : 1;
+  }
+  return h;
+}
+
 int conv3_grid(int N) {  // a multiple of 16 (whole XCD pairs; workgroups past the boards do nothing)
+  if (conv_halves() == 2) {  // one workgroup per board, at most two per CU
+    const long cap = 2L * cu_count_conv();
+    return (int)(N < cap ? N : cap);
+  }
   const long items = (2L * N + 15) / 16 * 16, cap = 2L * 2 * cu_count_conv() / 16 * 16;
   return (int)(items < cap ? items : cap);
 }
 
+// statistics slots (partials) of gmz_conv3x3_forward_stats: one per board pair of workgroups, or per workgroup
+int conv3_stats_slots(int N) { return conv_halves() == 2 ? conv3_grid(N) : conv3_grid(N) / 2; }
+
 template <int H, typename T>
 int launch_conv3(const void *x, const void *wpk, void *y, int N, const uint8_t *mask, double *stats, const void *addend,
                  hipStream_t st) {
-  hipLaunchKernelGGL((k_conv3<H, T, CONV_PG>), dim3(conv3_grid(N)), dim3(128 * CONV_PG), 0, st, (const uint16_t *)x,
-                     (const uint16_t *)wpk, (uint16_t *)y, N, mask, stats, (const uint16_t *)addend);
+  if (conv_halves() == 2)
+    hipLaunchKernelGGL((k_conv3<H, T, CONV_PG, 2>), dim3(conv3_grid(N)), dim3(128 * CONV_PG), 0, st, (const uint16_t *)x,
+                       (const uint16_t *)wpk, (uint16_t *)y, N, mask, stats, (const uint16_t *)addend);
+  else
+    hipLaunchKernelGGL((k_conv3<H, T, CONV_PG, 1>), dim3(conv3_grid(N)), dim3(128 * CONV_PG), 0, st, (const uint16_t *)x,
+                       (const uint16_t *)wpk, (uint16_t *)y, N, mask, stats, (const uint16_t *)addend);
   GMZ_LAUNCH_CHECK();
   return 0;
 }
@@ -509,7 +559,7 @@ GMZ_EXPORT int gmz_conv3x3_pack(int dtype, const float *w, int64_t s0, int64_t s
 
 GMZ_EXPORT int gmz_conv3x3_stats_slots(int N, int *slots) {
   if (N <= 0 || !slots) return fail("gmz_conv3x3_stats_slots: bad arguments");
-  *slots = conv3_grid(N) / 2;
+  *slots = conv3_stats_slots(N);
   return 0;
 }
 
