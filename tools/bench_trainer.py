@@ -34,7 +34,7 @@ ap.add_argument("--sequential-forward", action="store_true", help="no side strea
 ap.add_argument("--nchw-flatten", action="store_true", help="K = 28,800 Linears on an NCHW copy of the hidden state (trainer.FLAT_NHWC off)")
 ap.add_argument("--no-res-fold", action="store_true", help="autograd sums the residual blocks' input gradients (trainer.FUSED_RES_GRAD off)")
 ap.add_argument("--no-defer-wgrad", action="store_true", help="3x3 weight gradients at each use (trainer.DEFER_WGRAD off)")
-ap.add_argument("--target-f16", action="store_true", help="the target network's value in f16 operands (trainer.TARGET_F16)")
+ap.add_argument("--target-f32", action="store_true", help="the target network's value in float32 on MIOpen (trainer.TARGET_F16 off)")
 ap.add_argument("--per-step-loss", action="store_true", help="loss terms per unroll step (trainer.BATCHED_LOSS off)")
 ap.add_argument("--no-benchmark", action="store_true", help="no torch.backends.cudnn.benchmark (MIOpen Find per shape)")
 a = ap.parse_args()
@@ -56,7 +56,7 @@ T.CONCURRENT_FORWARD = T.CONCURRENT_FORWARD and not a.sequential_forward
 T.FLAT_NHWC = T.FLAT_NHWC and not a.nchw_flatten
 T.FUSED_RES_GRAD = T.FUSED_RES_GRAD and not a.no_res_fold
 T.BATCHED_LOSS = T.BATCHED_LOSS and not a.per_step_loss
-T.TARGET_F16 = T.TARGET_F16 or a.target_f16
+T.TARGET_F16 = T.TARGET_F16 and not a.target_f32
 T.DEFER_WGRAD = T.DEFER_WGRAD and not a.no_defer_wgrad
 
 cfg = T.TrainConfig(BOARD_SIZE=a.size, NUM_RES_BLOCKS=a.blocks, PHYSICAL_BATCH_SIZE=a.batch,

@@ -1,5 +1,5 @@
 #!/bin/bash
-# trainer A/Bs, same box, alternating: defaults | per-use weight gradients | target value with an f16 trunk |
+# trainer A/Bs, same box, alternating: defaults | per-use weight gradients | target value in float32 |
 # one workgroup per board in the 3x3 conv (GMZ_CONV_HALVES=2); conv kernel alone both ways; then the new
 # trainer GPU tests (and the conv tests under GMZ_CONV_HALVES=2) -> gpurun_out/tgt/
 set -o pipefail
@@ -10,8 +10,8 @@ for hv in 1 2; do
   echo "== GMZ_CONV_HALVES=$hv"; grep -v Warning $OUT/conv_h$hv.txt | tail -4
 done
 for round in 1 2; do
-  for v in base nodefer tgt16 halves2; do
-    flag=""; [ $v = nodefer ] && flag="--no-defer-wgrad"; [ $v = tgt16 ] && flag="--target-f16"
+  for v in base nodefer tgt32 halves2; do
+    flag=""; [ $v = nodefer ] && flag="--no-defer-wgrad"; [ $v = tgt32 ] && flag="--target-f32"
     hv=1; [ $v = halves2 ] && hv=2
     GMZ_CONV_HALVES=$hv timeout -k 10 200 python3 tools/bench_trainer.py --steps 30 --per $flag > $OUT/${v}_$round.json 2> $OUT/${v}_$round.err \
       || { echo "$v failed"; tail -5 $OUT/${v}_$round.err; exit 1; }
