@@ -487,13 +487,14 @@ def selfplay_leg(args, rank, world, dist, backend, size, sims, mode, blocks, G, 
            parts[0].descent_hint))
 
     finished = torch.zeros((), dtype=torch.int64, device="cuda")
-    count = [False]
 
     def step():
         eng.search()
         st = eng.play(reset_finished=True)
-        if count[0]:  # +1 / -1 winner or 0 draw: the game ended on this move (and restarts from the empty board)
-            finished.add_(((st == 1) | (st == -1) | (st == 0)).sum())
+        # +1 / -1 winner or 0 draw: the game ended on this move (and restarts from the empty board).  Counted
+        # in the warm-up moves too, so the first use of these kernels (a lazy code-object load, ~0.1 s on a
+        # fresh box) is not inside the timed moves; zeroed before them
+        finished.add_(((st == 1) | (st == -1) | (st == 0)).sum())
 
     for i in range(warmup):
         step()
@@ -512,6 +513,7 @@ def selfplay_leg(args, rank, world, dist, backend, size, sims, mode, blocks, G, 
         e.tree_timer = N.KernelTimer(st)
         tree_timers.append(e.tree_timer)
     eng.tree_counters(reset=True)
+    finished.zero_()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -519,10 +521,11 @@ def selfplay_leg(args, rank, world, dist, backend, size, sims, mode, blocks, G, 
     base.record()
     t0 = time.perf_counter()
     waves = 0
-    count[0] = True
+    marks = [t0]
     for i in range(steps):
         step()
         waves += eng.waves_last
+        marks.append(time.perf_counter())  # host clock per move (the host reads each move's status)
         if (i + 1) % max(1, steps // 5) == 0:
             log("%sstep %d/%d" % (log_prefix, i + 1, steps))
     torch.cuda.synchronize()
@@ -531,7 +534,8 @@ def selfplay_leg(args, rank, world, dist, backend, size, sims, mode, blocks, G, 
     own = time.perf_counter() - t0
     dt = collective_max(own, dist, backend)
     res = {"dt": dt, "waves": waves, "streams": streams, "rank_dt": collective_gather(own, dist, backend),
-           "finished_games": int(collective_sum(float(finished.item()), dist, backend))}
+           "finished_games": int(collective_sum(float(finished.item()), dist, backend)),
+           "step_ms": [round((b - a) * 1e3, 2) for a, b in zip(marks, marks[1:])]}
     ctr = eng.tree_counters()
     traffic_note = "from the committed builder PMC pass %s (not measured in this run)"
     fpr = (repr_flop_per_row if az else tower_flop_per_row)(size, blocks)
@@ -830,6 +834,7 @@ def run_phase(phase, args, rank, world, dist, backend, consumer=None, out=None):
         frag = result_line(args, world, r["dt"], r["waves"], G, backend)
         frag["finished_games"] = r["finished_games"]
         frag["rank_values"] = [G * args.steps / t if t > 0 else None for t in r["rank_dt"]]
+        frag["step_ms"] = r["step_ms"]  # rank 0's host time per timed move
         for k in ("roofline", "roofline_tree", "single_stream_kernels"):
             if k in r:
                 frag[k] = r[k]

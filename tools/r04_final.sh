@@ -16,3 +16,4 @@ timeout -k 10 500 python -u bench.py --steps 20 --warmup 2 > $OUT/bench.json 2> 
 python3 tools/summarize_bench.py $OUT/bench.json
 bash tools/gpu.sh trace r04f_trace || exit 1
 bash tools/gpu.sh pmc r04f_pmc || exit 1
+bash tools/r04_tprof.sh || exit 1
