@@ -42,11 +42,17 @@ if conv:
                        "launches_per_step": c / steps, "ms_per_step": t / 1e6 / steps}
 wg = [(k, v) for k, v in agg.items() if "k_conv3_wgrad<" in k]
 if wg:
+    # one weight gradient per residual-conv USE: 16 convs x (representation + 5 unroll steps) = 96 per step; with
+    # trainer.DEFER_WGRAD one launch covers several uses (segments), so the rate is per use, not per launch
+    uses = 2 * 8 * (1 + 5)
     c = sum(v[0] for _, v in wg)
     t = sum(v[1] for _, v in wg)
-    us = t / c / 1e3
-    ach = flop / (us * 1e-6) / 1e12
-    res["weight_gradient"] = {"kernel": "gmz_conv3x3_wgrad (k_conv3_wgrad, partials; + k_conv3_wgrad_reduce)",
-                              "mean_us_in_step": us, "achieved": ach, "frac": ach / peak, "launches_per_step": c / steps}
+    red = sum(v[1] for k, v in agg.items() if "k_conv3_wgrad_reduce" in k)
+    ms = t / 1e6 / steps
+    ach = uses * flop / (ms * 1e-3) / 1e12
+    res["weight_gradient"] = {"kernel": "gmz_conv3x3_wgrad (k_conv3_wgrad partials; k_conv3_wgrad_reduce separate)",
+                              "uses_per_step": uses, "launches_per_step": c / steps, "ms_per_step": ms,
+                              "reduce_ms_per_step": red / 1e6 / steps, "achieved": ach, "unit": "TFLOP/s",
+                              "frac": ach / peak}
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res, indent=1)[:2500])
