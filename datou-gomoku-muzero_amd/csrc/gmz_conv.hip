@@ -293,7 +293,7 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
       a += (double)red[(g * 64 + tid) * 2];
       q += (double)red[(g * 64 + tid) * 2 + 1];
     }
-    double *out = stats + ((size_t)b0 * CC + half * 64 + tid) * 3;
+    double *out = stats + ((size_t)(half * 64 + tid) * bstride + b0) * 3;  // channel-major [C][slots][3]
     out[0] = a;
     out[1] = q;
     out[2] = (double)nvalid * A;

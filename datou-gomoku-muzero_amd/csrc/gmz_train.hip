@@ -90,9 +90,10 @@ __global__ void __launch_bounds__(BN_THREADS) k_bn_stats(const T *__restrict__ x
 }
 
 // per-channel finalisation of the split partials ws[(c * cs + t * ts) * 3 + k], t < ns: one workgroup per
-// channel of FIN_THREADS (a multiple of 64) threads striding the splits (f64; the splits of one channel are
-// 3 KB apart in the NHWC layout, so every load is its own round trip: 4 waves cut the one-wave version's 8
-// dependent trips per lane at 512 splits to 2), then wave sums and the waves' sums in wave order.
+// channel of FIN_THREADS (a multiple of 64) threads striding the splits (f64; every producer writes its
+// partials channel-major, cs = ns and ts = 1, so a channel's splits are one contiguous run: 4 waves cut
+// the one-wave version's 8 trips per lane at 512 splits to 2), then wave sums and the waves' sums in
+// wave order.
 //  forward : save = (mean, invstd), running-stat update (nn.BatchNorm training: unbiased variance)
 //  backward: dgamma = sum dz*xhat, dbeta = sum dz, coef = (mean dz, mean dz*xhat) over the masked rows
 constexpr int FIN_MAX_WAVES = 4;
@@ -239,8 +240,9 @@ __global__ void __launch_bounds__(BN_THREADS) k_bn_bwd_apply(const T *__restrict
 // for f16/bf16; V = 2 when C % 8 != 0 or an operand is not 16-B aligned), C/V threads cover one
 // position, BN_THREADS / (C/V) positions per block step.  The reductions give each of ns workgroups a
 // contiguous pixel range (pixel = b*S + s, ranges cross rows), accumulate per thread in f32 over the
-// ~10 pixels it sees and combine the position groups in f64; partials ws[t][C][3] (sum, sum of
-// squares | sum dz, sum dz*xhat, valid pixels).
+// ~10 pixels it sees and combine the position groups in f64; partials ws[C][ns][3] (sum, sum of
+// squares | sum dz, sum dz*xhat, valid pixels), channel-major like the NCHW kernels' so that
+// k_bn_finalize reads each channel's partials as one contiguous run.
 template <typename T, int V>
 struct alignas(sizeof(T) * V) VecT {
   T v[V];
@@ -352,7 +354,7 @@ __global__ void __launch_bounds__(BN_THREADS) k_bnl_red(const T *__restrict__ x,
       sa += (double)red[(size_t)g * 2 * C + ch];
       sq += (double)red[(size_t)g * 2 * C + C + ch];
     }
-    double *o = ws + ((size_t)t * C + ch) * 3;
+    double *o = ws + ((size_t)ch * ns + t) * 3;
     o[0] = sa;
     o[1] = sq;
     o[2] = cnt;
@@ -504,9 +506,8 @@ int bn_forward(int nhwc, const void *x, const void *res, const uint8_t *mask, in
                        (double *)ws);
   }
   GMZ_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_bn_finalize, dim3(C), dim3(fin_threads()), 0, st, (const double *)ws, C, ns, nhwc ? 1 : ns,
-                     nhwc ? C : 1, 0, eps, momentum, save, rm, rv, nb, (float *)nullptr, (float *)nullptr,
-                     (float *)nullptr);
+  hipLaunchKernelGGL(k_bn_finalize, dim3(C), dim3(fin_threads()), 0, st, (const double *)ws, C, ns, ns, 1, 0, eps,
+                     momentum, save, rm, rv, nb, (float *)nullptr, (float *)nullptr, (float *)nullptr);
   GMZ_LAUNCH_CHECK();
   if (nhwc) {
     const long P = (long)B * S;
@@ -543,8 +544,8 @@ int bn_backward(int nhwc, const void *x, const void *y, const void *dy, const ui
                        (const T *)dy, mask, B, C, S, save, relu, (double *)ws);
   }
   GMZ_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_bn_finalize, dim3(C), dim3(fin_threads()), 0, st, (const double *)ws, C, ns, nhwc ? 1 : ns,
-                     nhwc ? C : 1, accumulate ? 2 : 1, 0.f, 0.f, (float *)nullptr, (float *)nullptr, (float *)nullptr,
+  hipLaunchKernelGGL(k_bn_finalize, dim3(C), dim3(fin_threads()), 0, st, (const double *)ws, C, ns, ns, 1,
+                     accumulate ? 2 : 1, 0.f, 0.f, (float *)nullptr, (float *)nullptr, (float *)nullptr,
                      (int64_t *)nullptr, dgamma, dbeta, coef);
   GMZ_LAUNCH_CHECK();
   if (nhwc) {
@@ -569,8 +570,8 @@ template <typename T>
 int bn_forward_stats(const void *x, const void *res, int B, int C, int S, const float *gamma, const float *beta,
                      float eps, float momentum, float *rm, float *rv, int64_t *nb, int relu, void *y, float *save,
                      const double *stats, int ns, hipStream_t st) {
-  hipLaunchKernelGGL(k_bn_finalize, dim3(C), dim3(fin_threads()), 0, st, stats, C, ns, 1, C, 0, eps, momentum, save, rm, rv, nb,
-                     (float *)nullptr, (float *)nullptr, (float *)nullptr);
+  hipLaunchKernelGGL(k_bn_finalize, dim3(C), dim3(fin_threads()), 0, st, stats, C, ns, ns, 1, 0, eps, momentum, save, rm,
+                     rv, nb, (float *)nullptr, (float *)nullptr, (float *)nullptr);
   GMZ_LAUNCH_CHECK();
   const int V = nhwc_vec(C, sizeof(T), {x, res, y});
   const long P = (long)B * S;

@@ -474,7 +474,7 @@ def _conv3x3_wgrad_hip(x, gy, grad):
 
 
 def _conv_stats_buffer(N, device):
-    """f64 [slots][128][3] partials for gmz_conv3x3_forward_stats -> (tensor, slots)."""
+    """f64 [128][slots][3] partials (channel-major) for gmz_conv3x3_forward_stats -> (tensor, slots)."""
     import ctypes
     from . import _lib
     if N not in _STATS_SLOTS:

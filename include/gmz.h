@@ -294,7 +294,7 @@ int gmz_bn_backward_acc(int dtype, int layout, const void *x_dev, const void *y_
                         int relu, void *dx_dev, void *dres_dev, float *dgamma_dev, float *dbeta_dev,
                         void *workspace_dev, void *stream, int accumulate);
 /* gmz_bn_forward with the statistics already reduced to partials (e.g. by gmz_conv3x3_forward_stats):
- * stats_dev f64 [ns][C][3] (sum, sum of squares, counted elements); channels-last (layout 1) only. */
+ * stats_dev f64 [C][ns][3] (sum, sum of squares, counted elements); channels-last (layout 1) only. */
 int gmz_bn_forward_stats(int dtype, const void *x_dev, const void *res_dev, int B, int C, int S, const float *gamma_dev,
                          const float *beta_dev, float eps, float momentum, float *running_mean_dev,
                          float *running_var_dev, int64_t *num_batches_dev, int relu, void *y_dev, float *save_dev,
@@ -323,7 +323,7 @@ int gmz_conv3x3_forward(int dtype, int H, const void *x_dev, const void *packed_
 int gmz_conv3x3_forward_add(int dtype, int H, const void *x_dev, const void *packed_dev, const void *addend_dev,
                             void *y_dev, int N, void *stream);
 /* The same convolution, also writing the BatchNorm statistics of the (rounded) output over the boards
- * whose mask_dev byte is nonzero (NULL: all): stats_dev f64 [slots][128][3] = (sum, sum of squares,
+ * whose mask_dev byte is nonzero (NULL: all): stats_dev f64 [128][slots][3] = (sum, sum of squares,
  * counted positions) per slot, slots from gmz_conv3x3_stats_slots(N) — the partials layout
  * gmz_bn_forward_stats consumes (channels-last, ns = slots). */
 int gmz_conv3x3_stats_slots(int N, int *slots);
