@@ -298,6 +298,56 @@ def headline_openings(args, rank, G, size, n_in_row=5):
                              n_in_row=n_in_row)
 
 
+_PEAKS = {}
+
+
+def achievable_peaks():
+    """SURVEY §8(d) 'Peak references', measured live on this GPU after the timed region (once per process):
+    the dense f16 GEMM rate hipBLASLt delivers (torch.matmul, 16384^3, f32 accumulation — the tower's operand
+    type) and device-to-device copy bandwidth (2 GiB, read + write bytes), so that each roofline ``frac``
+    (against the vendor peaks, 2.5 PF and 8 TB/s) can also be read against what this chip delivers."""
+    if _PEAKS:
+        return _PEAKS
+
+    def timed(fn, reps):
+        fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) * 1e-3 / reps
+
+    m = 16384
+    g = torch.Generator(device="cuda").manual_seed(5)
+    x = torch.randn(m, m, dtype=torch.float16, device="cuda", generator=g)  # random data: the clock it holds
+    y = torch.randn(m, m, dtype=torch.float16, device="cuda", generator=g)
+    t = timed(lambda: torch.matmul(x, y), 4)
+    _PEAKS["gemm_f16_tflops"] = 2.0 * m ** 3 / t / 1e12
+    del x, y
+    n = 2 << 30
+    a = torch.empty(n, dtype=torch.uint8, device="cuda")
+    b = torch.empty_like(a)
+    t = timed(lambda: b.copy_(a), 8)
+    _PEAKS["copy_gbs"] = 2.0 * n / t / 1e9
+    del a, b
+    torch.cuda.empty_cache()
+    _PEAKS["how"] = ("measured after the timed region: torch.matmul f16 16384^3 on random data (hipBLASLt), "
+                     "device copy of 2 GiB (read + write bytes)")
+    return _PEAKS
+
+
+def with_achievable(roof, key):
+    """``roof`` (a roofline dict) plus the live achievable peak of its unit and the fraction of it."""
+    pk = achievable_peaks()
+    v = pk[key]
+    roof["achievable"] = {"peak": v, "unit": roof.get("unit"), "frac": roof["achieved"] / v if v else None,
+                          "how": pk["how"]}
+    return roof
+
+
 def timer_stats(timers, base):
     """Launch statistics of KernelTimers (one per stream): (launches, mean launch ms, busy ms) where
     busy = the union of the launch intervals over all streams (ms, from HIP events against ``base``)."""
@@ -838,6 +888,10 @@ def run_phase(phase, args, rank, world, dist, backend, consumer=None, out=None):
         for k in ("roofline", "roofline_tree", "single_stream_kernels"):
             if k in r:
                 frag[k] = r[k]
+        if rank == 0 and args.net == "hip" and "roofline" in frag:  # after every timed region of this phase
+            with_achievable(frag["roofline"], "gemm_f16_tflops")
+            if "roofline_tree" in frag:
+                with_achievable(frag["roofline_tree"], "copy_gbs")
         return frag
     inject_failure(phase, rank)
     if phase == "extras":
