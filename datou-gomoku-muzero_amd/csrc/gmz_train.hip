@@ -292,7 +292,7 @@ __global__ void __launch_bounds__(BN_THREADS) k_bnl_red(const T *__restrict__ x,
   if (grp < pl) {
     // U positions per thread per trip, every load of a trip issued before any arithmetic (the
     // loop is latency-bound otherwise: one HBM round trip per position)
-    constexpr int U = BWD ? 4 : 8;
+    constexpr int U = BWD ? 2 : 8;  // measured (tools/ab_bn.sh): backward 34.4 vs 35.7 us at U = 4, 36.8 at 8
     using VT = VecT<T, V>;
     for (long p = p0 + grp; p < p1; p += (long)U * pl) {
       VT rx[U], rd[U], ry[U];
