@@ -11,7 +11,7 @@ import torch  # noqa: F401  (must precede the CDLL load: shared HIP runtime)
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GMZ_LIB") or os.path.join(PKG_DIR, "libgmz.so")  # GMZ_LIB: A/B builds (tools)
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -69,6 +69,8 @@ _SIGS = {
     "gmz_conv3x3_wgrad_segments": ([I, I, P, P, I, I, P, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
                                     I, P, P], I),
     "gmz_conv3x3_forward_stats": ([I, I, P, P, P, I, P, P, P], I),
+    "gmz_conv3x3_forward_bwdstats": ([I, I, P, P, P, P, I, P, P, P, P, I, P, P], I),
+    "gmz_bn_backward_stats": ([I, P, P, P, P, I, I, I, P, P, I, P, P, P, P, P, I, P, P, I], I),
     "gmz_grad_add_t": ([I, P, I, I, I, P, P], I),
     "gmz_bn_forward_stats": ([I, P, P, I, I, I, P, P, ctypes.c_float, ctypes.c_float, P, P, P, I, P, P, P, I, P], I),
 }

@@ -95,13 +95,25 @@ __global__ void __launch_bounds__(256) k_pack_conv(const float *__restrict__ w, 
   *(uint4 *)(out + (size_t)i * 8) = r;
 }
 
+// The BatchNorm whose backward the output feeds (BWD statistics, gmz_conv3x3_forward_bwdstats): its input
+// x, its output y (after its ReLU) and its saved (mean, invstd) f32 [2][128]
+struct BnBwd {
+  const uint16_t *x, *y;
+  const float *save;
+  int relu;
+};
+
 // HALVES = 2: one workgroup per board computes both halves of the output channels from ONE DMA of the
 // board image (the k-loop twice, the weight ring reloaded for the second half's n-tiles): N workgroups
-// instead of 2N, one board DMA instead of two (gmz_conv3x3 A/B: GMZ_CONV_HALVES)
-template <int H, typename T, int PG, int HALVES = 1>
+// instead of 2N, one board DMA instead of two (gmz_conv3x3 A/B: GMZ_CONV_HALVES).
+// BWD: the epilogue's statistics are the BatchNorm BACKWARD sums of the output taken as that BN's output
+// gradient dy — sum dz and sum dz * xhat, dz = dy * [y > 0], xhat = (x - mean) * invstd (what k_bnl_red<.., 1, ..>
+// reduces in a pass of its own) — instead of the forward sums of the output.
+template <int H, typename T, int PG, int HALVES = 1, bool BWD = false>
 __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restrict__ x, const uint16_t *__restrict__ wpk,
                                                   uint16_t *__restrict__ y, int N, const uint8_t *__restrict__ mask,
-                                                  double *__restrict__ stats, const uint16_t *__restrict__ addend) {
+                                                  double *__restrict__ stats, const uint16_t *__restrict__ addend,
+                                                  BnBwd bn) {
   using I = CImg<H>;
   using M = Mfma<T>;
   typedef typename M::V V;
@@ -221,6 +233,17 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
     // ---- epilogue: 4 consecutive output channels of one position per lane -> 8-byte store
     uint16_t *dst = y + (size_t)b * A * CC;
     const uint16_t *add = addend ? addend + (size_t)b * A * CC : nullptr;  // + addend, rounded once
+    float mu[NTW][4], isd[NTW][4];  // BWD: the BatchNorm's mean / invstd of this lane's channels
+    if constexpr (BWD) {
+#pragma unroll
+      for (int nt = 0; nt < NTW; ++nt)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c = (ntile0 + nt) * 16 + g4 * 4 + e;
+          mu[nt][e] = bn.save[c];
+          isd[nt][e] = bn.save[CC + c];
+        }
+    }
 #pragma unroll
     for (int i = 0; i < PTW; ++i) {
       const int pt = pg + PG * i;
@@ -240,11 +263,23 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
         }
         *(u16x4_t *)(dst + (size_t)p * CC + n0) = o;
         if (counted) {
+          if constexpr (BWD) {  // the rounded output is the BatchNorm's dy
+            const size_t k = ((size_t)b * A + p) * CC + n0;
+            const u16x4_t xv = *(const u16x4_t *)(bn.x + k), yv = *(const u16x4_t *)(bn.y + k);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float v = M::value(o[e]);
-            s1[hh][nt][e] += v;
-            s2[hh][nt][e] = fmaf(v, v, s2[hh][nt][e]);
+            for (int e = 0; e < 4; ++e) {
+              float g = M::value(o[e]);
+              if (bn.relu && !(M::value(yv[e]) > 0.f)) g = 0.f;
+              s1[hh][nt][e] += g;
+              s2[hh][nt][e] = fmaf(g, (M::value(xv[e]) - mu[nt][e]) * isd[nt][e], s2[hh][nt][e]);
+            }
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float v = M::value(o[e]);
+              s1[hh][nt][e] += v;
+              s2[hh][nt][e] = fmaf(v, v, s2[hh][nt][e]);
+            }
           }
         }
       }
@@ -497,25 +532,34 @@ int conv3_grid(int N) {  // a multiple of 16 (whole XCD pairs; workgroups past t
 // statistics slots (partials) of gmz_conv3x3_forward_stats: one per board pair of workgroups, or per workgroup
 int conv3_stats_slots(int N) { return conv_halves() == 2 ? conv3_grid(N) : conv3_grid(N) / 2; }
 
+template <int H, typename T, int HV, bool BWD>
+void launch_conv3_k(const void *x, const void *wpk, void *y, int N, const uint8_t *mask, double *stats, const void *addend,
+                    const BnBwd &bn, hipStream_t st) {
+  hipLaunchKernelGGL((k_conv3<H, T, CONV_PG, HV, BWD>), dim3(conv3_grid(N)), dim3(128 * CONV_PG), 0, st,
+                     (const uint16_t *)x, (const uint16_t *)wpk, (uint16_t *)y, N, mask, stats, (const uint16_t *)addend, bn);
+}
+
 template <int H, typename T>
 int launch_conv3(const void *x, const void *wpk, void *y, int N, const uint8_t *mask, double *stats, const void *addend,
-                 hipStream_t st) {
-  if (conv_halves() == 2)
-    hipLaunchKernelGGL((k_conv3<H, T, CONV_PG, 2>), dim3(conv3_grid(N)), dim3(128 * CONV_PG), 0, st, (const uint16_t *)x,
-                       (const uint16_t *)wpk, (uint16_t *)y, N, mask, stats, (const uint16_t *)addend);
-  else
-    hipLaunchKernelGGL((k_conv3<H, T, CONV_PG, 1>), dim3(conv3_grid(N)), dim3(128 * CONV_PG), 0, st, (const uint16_t *)x,
-                       (const uint16_t *)wpk, (uint16_t *)y, N, mask, stats, (const uint16_t *)addend);
+                 const BnBwd &bn, hipStream_t st) {
+  const bool bwd = bn.x != nullptr;
+  if (conv_halves() == 2) {
+    if (bwd) launch_conv3_k<H, T, 2, true>(x, wpk, y, N, mask, stats, addend, bn, st);
+    else launch_conv3_k<H, T, 2, false>(x, wpk, y, N, mask, stats, addend, bn, st);
+  } else {
+    if (bwd) launch_conv3_k<H, T, 1, true>(x, wpk, y, N, mask, stats, addend, bn, st);
+    else launch_conv3_k<H, T, 1, false>(x, wpk, y, N, mask, stats, addend, bn, st);
+  }
   GMZ_LAUNCH_CHECK();
   return 0;
 }
 
 template <typename T>
 int conv3_dispatch(int H, const void *x, const void *wpk, void *y, int N, const uint8_t *mask, double *stats, const void *addend,
-                   hipStream_t st) {
+                   hipStream_t st, const BnBwd &bn = BnBwd{}) {
   switch (H) {
-    case 9: return launch_conv3<9, T>(x, wpk, y, N, mask, stats, addend, st);
-    case 15: return launch_conv3<15, T>(x, wpk, y, N, mask, stats, addend, st);
+    case 9: return launch_conv3<9, T>(x, wpk, y, N, mask, stats, addend, bn, st);
+    case 15: return launch_conv3<15, T>(x, wpk, y, N, mask, stats, addend, bn, st);
   }
   return fail("gmz_conv3x3: board size must be 9 or 15");
 }
@@ -588,6 +632,21 @@ GMZ_EXPORT int gmz_conv3x3_forward_add(int dtype, int H, const void *x, const vo
   if (dtype == 1) return conv3_dispatch<__half>(H, x, packed, y, N, nullptr, nullptr, addend, st);
   if (dtype == 2) return conv3_dispatch<__hip_bfloat16>(H, x, packed, y, N, nullptr, nullptr, addend, st);
   return fail("gmz_conv3x3_forward_add: dtype must be 1 (f16) or 2 (bf16)");
+}
+
+GMZ_EXPORT int gmz_conv3x3_forward_bwdstats(int dtype, int H, const void *x, const void *packed, const void *addend,
+                                            void *y, int N, const uint8_t *mask, const void *bn_x, const void *bn_y,
+                                            const float *bn_save, int relu, double *stats, void *stream) {
+  if (!x || !packed || !y || !bn_x || !bn_y || !bn_save || !stats) return fail("gmz_conv3x3_forward_bwdstats: null operand");
+  if (N <= 0) return fail("gmz_conv3x3_forward_bwdstats: N must be positive");
+  if (((uintptr_t)x | (uintptr_t)packed | (uintptr_t)y | (uintptr_t)addend) & 15)
+    return fail("gmz_conv3x3_forward_bwdstats: operands must be 16-B aligned");
+  if (((uintptr_t)bn_x | (uintptr_t)bn_y) & 7) return fail("gmz_conv3x3_forward_bwdstats: BN operands must be 8-B aligned");
+  hipStream_t st = (hipStream_t)stream;
+  const BnBwd bn = {(const uint16_t *)bn_x, (const uint16_t *)bn_y, bn_save, relu};
+  if (dtype == 1) return conv3_dispatch<__half>(H, x, packed, y, N, mask, stats, addend, st, bn);
+  if (dtype == 2) return conv3_dispatch<__hip_bfloat16>(H, x, packed, y, N, mask, stats, addend, st, bn);
+  return fail("gmz_conv3x3_forward_bwdstats: dtype must be 1 (f16) or 2 (bf16)");
 }
 
 GMZ_EXPORT int gmz_conv3x3_wgrad_workspace_bytes(int N, size_t *out) {

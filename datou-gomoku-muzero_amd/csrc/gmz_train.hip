@@ -566,6 +566,30 @@ int bn_backward(int nhwc, const void *x, const void *y, const void *dy, const ui
   return 0;
 }
 
+// backward with the dz sums already reduced to channel-major partials by the producer of dy (the
+// k_conv3 epilogue, gmz_conv3x3_forward_bwdstats): finalise + apply, no reduction pass
+template <typename T>
+int bn_backward_stats(const void *x, const void *y, const void *dy, const uint8_t *mask, int B, int C, int S,
+                      const float *gamma, const float *save, int relu, void *dx, void *dres, float *dgamma,
+                      float *dbeta, const double *stats, int ns, float *coef, hipStream_t st, int accumulate) {
+  hipLaunchKernelGGL(k_bn_finalize, dim3(C), dim3(fin_threads()), 0, st, stats, C, ns, ns, 1, accumulate ? 2 : 1, 0.f,
+                     0.f, (float *)nullptr, (float *)nullptr, (float *)nullptr, (int64_t *)nullptr, dgamma, dbeta,
+                     coef);
+  GMZ_LAUNCH_CHECK();
+  const int V = nhwc_vec(C, sizeof(T), {x, y, dy, dx, dres});
+  const long P = (long)B * S;
+  if (V == 8)
+    hipLaunchKernelGGL((k_bnl_bwd_apply<T, 8>), dim3(elementwise_blocks(P, C, 8)), dim3(BN_THREADS), 0, st,
+                       (const T *)x, (const T *)y, (const T *)dy, mask, P, C, S, gamma, save, relu, (T *)dx, (T *)dres,
+                       coef);
+  else
+    hipLaunchKernelGGL((k_bnl_bwd_apply<T, 2>), dim3(elementwise_blocks(P, C, 2)), dim3(BN_THREADS), 0, st,
+                       (const T *)x, (const T *)y, (const T *)dy, mask, P, C, S, gamma, save, relu, (T *)dx, (T *)dres,
+                       coef);
+  GMZ_LAUNCH_CHECK();
+  return 0;
+}
+
 template <typename T>
 int bn_forward_stats(const void *x, const void *res, int B, int C, int S, const float *gamma, const float *beta,
                      float eps, float momentum, float *rm, float *rv, int64_t *nb, int relu, void *y, float *save,
@@ -737,6 +761,27 @@ GMZ_EXPORT int gmz_bn_eval(int dtype, int layout, const void *x, const void *res
                                      st);
   }
   return fail("gmz_bn_eval: dtype must be 0 (f32), 1 (f16) or 2 (bf16)");
+}
+
+GMZ_EXPORT int gmz_bn_backward_stats(int dtype, const void *x, const void *y, const void *dy, const uint8_t *mask,
+                                     int B, int C, int S, const float *gamma, const float *save, int relu, void *dx,
+                                     void *dres, float *dgamma, float *dbeta, const double *stats, int ns, void *ws,
+                                     void *stream, int accumulate) {
+  if (B <= 0 || C <= 0 || S <= 0 || ns <= 0 || (size_t)B * C * S >= (1ull << 31)) return fail("gmz_bn_backward_stats: bad shape");
+  if (check_layout(1, C)) return -1;
+  if (!x || !dy || !dx || !gamma || !save || !dgamma || !dbeta || !stats || !ws || (relu && !y))
+    return fail("gmz_bn_backward_stats: null operand");
+  hipStream_t st = (hipStream_t)stream;
+  float *coef = (float *)((double *)ws + ws_doubles(B, C, S, 1));  // where gmz_bn_backward keeps them
+  switch (dtype) {
+    case 0: return bn_backward_stats<float>(x, y, dy, mask, B, C, S, gamma, save, relu, dx, dres, dgamma, dbeta, stats,
+                                            ns, coef, st, accumulate);
+    case 1: return bn_backward_stats<__half>(x, y, dy, mask, B, C, S, gamma, save, relu, dx, dres, dgamma, dbeta, stats,
+                                             ns, coef, st, accumulate);
+    case 2: return bn_backward_stats<__hip_bfloat16>(x, y, dy, mask, B, C, S, gamma, save, relu, dx, dres, dgamma, dbeta,
+                                                     stats, ns, coef, st, accumulate);
+  }
+  return fail("gmz_bn_backward_stats: dtype must be 0 (f32), 1 (f16) or 2 (bf16)");
 }
 
 GMZ_EXPORT int gmz_bn_forward_stats(int dtype, const void *x, const void *res, int B, int C, int S, const float *gamma,

@@ -149,6 +149,22 @@ def _bn(mod, x, mask=None):
 SUBBATCH_BN = False
 _BN_DTYPES = {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2}
 FUSED_BN = True  # device BatchNorm layers of a training-mode model run the HIP kernels (gmz_train.hip)
+# the backward's dz sums of a channels-last BatchNorm whose output feeds a HIP 3x3 conv reduced in that conv's
+# input-gradient epilogue (gmz_conv3x3_forward_bwdstats -> gmz_bn_backward_stats): no reduction pass of its own.
+# Measured (profiles/r04_bn_bwd_fused_ab.txt): the BatchNorm backward 34.6 -> 20.8 us, but the conv's epilogue
+# loads of the BN's x and y (not overlapped with its MFMAs) 35.0 -> 48.9 us, and the step 35.0-35.7 vs
+# 36.3-36.8 steps/s; off (A/B switch, tested)
+FUSED_BN_BWD_STATS = False
+
+
+class _BnBwdLink:
+    """Hand-off from a training-mode BatchNorm (+ReLU) to the HIP conv that consumes its output y: the BN's
+    input x, row mask, saved (mean, invstd) and ReLU flag (the conv saved y itself), and back from that conv's
+    backward the dz partials of the gradient it produced for y, ``bwd`` = (stats, slots, that gradient)."""
+    __slots__ = ("x", "mask", "save", "relu", "bwd")
+
+    def __init__(self, x, mask, save, relu):
+        self.x, self.mask, self.save, self.relu, self.bwd = x, mask, save, relu, None
 
 
 def _bn_layout(x):
@@ -173,7 +189,7 @@ class _FusedMaskedBN(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, gamma, beta, res, mask, running_mean, running_var, num_batches, eps, momentum, relu,
-                stats=None, link=None):
+                stats=None, link=None, bwd_link=False):
         from . import _lib
         L = _lib.load()
         layout = _bn_layout(x)
@@ -201,6 +217,10 @@ class _FusedMaskedBN(torch.autograd.Function):
         ctx.relu, ctx.has_res, ctx.layout = relu, res is not None, layout
         ctx.beta = beta
         ctx.link = link
+        ctx.bwd_link = None
+        if bwd_link and layout == 1 and x.dtype in _CONV_DTYPES:  # a HIP conv consuming y may reduce our dz sums
+            ctx.bwd_link = _BnBwdLink(x, mask, save, relu)
+            y._gmz_bnsrc = ctx.bwd_link
         return y
 
     @staticmethod
@@ -225,17 +245,29 @@ class _FusedMaskedBN(torch.autograd.Function):
             dgamma = torch.empty(C, dtype=torch.float32, device=x.device)
             dbeta = torch.empty(C, dtype=torch.float32, device=x.device)
         ws = _bn_workspace(layout, B, C, S, x.device)
-        _lib.check(L.gmz_bn_backward_acc(_BN_DTYPES[x.dtype], layout, _lib.ptr(x), _lib.ptr(y), _lib.ptr(dy),
-                                         _lib.ptr(mask), B, C, S, _lib.ptr(gamma), _lib.ptr(save), int(ctx.relu),
-                                         _lib.ptr(dx), _lib.ptr(dres), _lib.ptr(dgamma), _lib.ptr(dbeta),
-                                         _lib.ptr(ws), _lib.stream_ptr(), int(acc)))
+        bl = ctx.bwd_link
+        pre = bl.bwd if bl is not None else None
+        if bl is not None:
+            bl.bwd = None
+        if pre is not None and (pre[2] is dy or (pre[2].data_ptr() == dy.data_ptr() and pre[2].stride() == dy.stride()
+                                                 and pre[2].dtype == dy.dtype)):
+            # dz sums already reduced by the conv that produced dy (gmz_conv3x3_forward_bwdstats)
+            _lib.check(L.gmz_bn_backward_stats(_BN_DTYPES[x.dtype], _lib.ptr(x), _lib.ptr(y), _lib.ptr(dy),
+                                               _lib.ptr(mask), B, C, S, _lib.ptr(gamma), _lib.ptr(save), int(ctx.relu),
+                                               _lib.ptr(dx), _lib.ptr(dres), _lib.ptr(dgamma), _lib.ptr(dbeta),
+                                               _lib.ptr(pre[0]), int(pre[1]), _lib.ptr(ws), _lib.stream_ptr(), int(acc)))
+        else:
+            _lib.check(L.gmz_bn_backward_acc(_BN_DTYPES[x.dtype], layout, _lib.ptr(x), _lib.ptr(y), _lib.ptr(dy),
+                                             _lib.ptr(mask), B, C, S, _lib.ptr(gamma), _lib.ptr(save), int(ctx.relu),
+                                             _lib.ptr(dx), _lib.ptr(dres), _lib.ptr(dgamma), _lib.ptr(dbeta),
+                                             _lib.ptr(ws), _lib.stream_ptr(), int(acc)))
         if ctx.link is not None and dres is not None:
             # the residual's gradient goes to the block's first conv, whose input-gradient epilogue adds it
             # (_ResLink): autograd then has one gradient for the block input, no accumulation pass
             ctx.link.dres, dres = dres, None
         if acc:
-            return dx, None, None, dres, None, None, None, None, None, None, None, None, None
-        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None
+            return dx, None, None, dres, None, None, None, None, None, None, None, None, None, None
+        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None, None
 
 
 _WS_BYTES = {}
@@ -261,9 +293,10 @@ def _bn_act(mod, x, mask=None, res=None, relu=True, link=None):
             res = res.to(x.dtype)
         m = None if mask is None else mask.contiguous().view(torch.uint8)
         use = link if (link is not None and res is not None and link.xin is res) else None
+        want = FUSED_BN_BWD_STATS and torch.is_grad_enabled() and (x.requires_grad or mod.weight.requires_grad)
         return _FusedMaskedBN.apply(x, mod.weight, mod.bias, res, m, mod.running_mean, mod.running_var,
                                     mod.num_batches_tracked, mod.eps, mod.momentum, relu,
-                                    getattr(x, "_gmz_bnstats", None), use)
+                                    getattr(x, "_gmz_bnstats", None), use, want)
     if (FUSED_BN and not mod.training and x.is_cuda and x.dtype in _BN_DTYPES and _bn_layout(x) is not None
             and not (torch.is_grad_enabled() and (x.requires_grad or mod.weight.requires_grad))):
         return _bn_eval(mod, x, res, relu)
@@ -380,9 +413,21 @@ def _packed_conv_weight(w, dtype, transpose):
 _STATS_SLOTS = {}
 
 
-def _conv3x3_hip(x, packed, mask=None, stats=None, addend=None):
+def _conv3x3_hip(x, packed, mask=None, stats=None, addend=None, bnb=None, bn_y=None):
+    """``bnb``: a _BnBwdLink whose BatchNorm output ``bn_y`` fed the forward conv: the output (its dy) also
+    gets that BatchNorm's backward dz sums, returned as ``bnb.bwd``."""
     from . import _lib
     y = torch.empty_like(x, memory_format=torch.channels_last)
+    if bnb is not None:
+        if addend is not None:
+            addend = addend.to(x.dtype).contiguous(memory_format=torch.channels_last)
+        st, ns = _conv_stats_buffer(x.shape[0], x.device)
+        _lib.check(_lib.load().gmz_conv3x3_forward_bwdstats(
+            _CONV_DTYPES[x.dtype], x.shape[2], _lib.ptr(x), _lib.ptr(packed), _lib.ptr(addend), _lib.ptr(y), x.shape[0],
+            _lib.ptr(bnb.mask), _lib.ptr(bnb.x), _lib.ptr(bn_y), _lib.ptr(bnb.save), int(bnb.relu), _lib.ptr(st),
+            _lib.stream_ptr()))
+        bnb.bwd = (st, ns, y)
+        return y
     if addend is not None:  # y = round(conv + addend) (the residual gradient folded into the input gradient)
         addend = addend.to(x.dtype).contiguous(memory_format=torch.channels_last)
         _lib.check(_lib.load().gmz_conv3x3_forward_add(_CONV_DTYPES[x.dtype], x.shape[2], _lib.ptr(x), _lib.ptr(packed),
@@ -493,9 +538,10 @@ class _Conv3x3NHWC(torch.autograd.Function):
     converts it (what autocast's cast would do)."""
 
     @staticmethod
-    def forward(ctx, x, w, mask=None, stats=None, link=None):
+    def forward(ctx, x, w, mask=None, stats=None, link=None, bnsrc=None):
         ctx.save_for_backward(x, w)
         ctx.link = link
+        ctx.bnsrc = bnsrc  # the _BnBwdLink of the BatchNorm whose output x is (FUSED_BN_BWD_STATS)
         return _conv3x3_hip(x, _packed_conv_weight(w, x.dtype, 0), mask, stats)
 
     @staticmethod
@@ -505,7 +551,10 @@ class _Conv3x3NHWC(torch.autograd.Function):
         add = None
         if ctx.link is not None:
             add, ctx.link.dres = ctx.link.dres, None
-        gx = _conv3x3_hip(gy, _packed_conv_weight(w, x.dtype, 1), addend=add) if ctx.needs_input_grad[0] else None
+        gx = None
+        if ctx.needs_input_grad[0]:
+            bnb = ctx.bnsrc if (FUSED_BN_BWD_STATS and ctx.bnsrc is not None and ctx.bnsrc.x.dtype == x.dtype) else None
+            gx = _conv3x3_hip(gy, _packed_conv_weight(w, x.dtype, 1), addend=add, bnb=bnb, bn_y=x)
         gw = None
         if ctx.needs_input_grad[1]:
             if HIP_WGRAD:
@@ -530,7 +579,7 @@ class _Conv3x3NHWC(torch.autograd.Function):
                     gw = None
                 else:
                     gw = gw.to(w.dtype)
-        return gx, gw, None, None, None
+        return gx, gw, None, None, None, None
 
 
 def _conv3(cin, cout):
@@ -550,7 +599,8 @@ def _conv3_apply(conv, x, bn=None, mask=None, link=None):
                 st = _conv_stats_buffer(x.shape[0], x.device)
             m = None if mask is None else mask.contiguous().view(torch.uint8)
             xin = x.to(dt)
-            y = _Conv3x3NHWC.apply(xin, conv.weight, m, None if st is None else st[0], link)
+            bnsrc = getattr(xin, "_gmz_bnsrc", None) if xin is x else None  # x = a BatchNorm's output, as is
+            y = _Conv3x3NHWC.apply(xin, conv.weight, m, None if st is None else st[0], link, bnsrc)
             if link is not None:
                 link.xin = xin
             if st is not None:

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define GMZ_ABI_VERSION 6
+#define GMZ_ABI_VERSION 7
 
 /* ------------------------------------------------------------------ misc */
 const char *gmz_last_error(void);
@@ -299,6 +299,13 @@ int gmz_bn_forward_stats(int dtype, const void *x_dev, const void *res_dev, int 
                          const float *beta_dev, float eps, float momentum, float *running_mean_dev,
                          float *running_var_dev, int64_t *num_batches_dev, int relu, void *y_dev, float *save_dev,
                          const double *stats_dev, int ns, void *stream);
+/* gmz_bn_backward_acc (channels-last) with its dz sums already reduced to partials stats_dev f64 [C][ns][3]
+ * (sum dz, sum dz * xhat, counted elements) by the producer of dy_dev (gmz_conv3x3_forward_bwdstats): the
+ * finalisation and the elementwise pass only.  workspace_dev: gmz_bn_workspace_bytes(1, B, C, S).  (ABI 7) */
+int gmz_bn_backward_stats(int dtype, const void *x_dev, const void *y_dev, const void *dy_dev, const uint8_t *mask_dev,
+                          int B, int C, int S, const float *gamma_dev, const float *save_dev, int relu, void *dx_dev,
+                          void *dres_dev, float *dgamma_dev, float *dbeta_dev, const double *stats_dev, int ns,
+                          void *workspace_dev, void *stream, int accumulate);
 /* Eval-mode BatchNorm (running statistics) + residual + ReLU, same layouts/dtypes as gmz_bn_forward:
  * y = relu?(gamma*(x-running_mean)/sqrt(running_var+eps) + beta (+ res)) — nn.BatchNorm2d/1d in eval()
  * (the target network's value of loss.py:54-55).  workspace_dev: gmz_bn_workspace_bytes bytes. */
@@ -343,6 +350,16 @@ int gmz_conv3x3_wgrad_segments(int dtype, int H, const void *const *x_segs, cons
                                int accumulate, void *workspace_dev, void *stream);
 int gmz_conv3x3_forward_stats(int dtype, int H, const void *x_dev, const void *packed_dev, void *y_dev, int N,
                               const uint8_t *mask_dev, double *stats_dev, void *stream);
+/* The convolution as an input gradient (transposed packing; addend_dev optional, as gmz_conv3x3_forward_add)
+ * whose output y is the output gradient dy of a channels-last BatchNorm (+ReLU) below it — bn_x_dev its input,
+ * bn_y_dev its output, bn_save_dev its saved (mean, invstd) f32 [2][128], same [N][H*H][128] layout and dtype —
+ * also writing that BatchNorm's BACKWARD sums over the boards whose mask_dev byte is nonzero: stats_dev f64
+ * [128][slots][3] = (sum dz, sum dz * xhat, counted positions), dz = y * [bn_y > 0] (relu) or y,
+ * xhat = (bn_x - mean) * invstd — the partials gmz_bn_backward_stats consumes instead of its reduction pass.
+ * bn_x_dev / bn_y_dev 8-B aligned.  (ABI 7) */
+int gmz_conv3x3_forward_bwdstats(int dtype, int H, const void *x_dev, const void *packed_dev, const void *addend_dev,
+                                 void *y_dev, int N, const uint8_t *mask_dev, const void *bn_x_dev, const void *bn_y_dev,
+                                 const float *bn_save_dev, int relu, double *stats_dev, void *stream);
 /* dst_dev[o][c][p] += src_dev[(p*C + c)*O + o] (f32 accumulate; src dtype 0 = f32, 1 = f16, 2 = bf16):
  * the weight gradient x^T dy of a K = C*P Linear whose input was a channels-last [N][P][C] hidden state
  * flattened in (p, c) order, added into the f32 .grad of W [O][C*P] (the reference's NCHW flatten,

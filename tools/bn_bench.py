@@ -59,4 +59,12 @@ def timed(fn):
 
 
 out = {"forward_us": timed(fwd), "backward_us": timed(bwd), "reps": reps}
+if hasattr(L, "gmz_bn_backward_stats"):  # ABI 7: the dz sums already reduced (by the conv epilogue)
+    ns = 360  # gmz_conv3x3_stats_slots(360)
+    stats = torch.rand(C * ns * 3, dtype=torch.float64, device="cuda")
+
+    def bwd_stats():
+        _lib.check(L.gmz_bn_backward_stats(1, P(x), P(y), P(dy), P(mask), B, C, S, P(gamma), P(save), 1, P(dx), P(dres),
+                                           P(dg), P(db), P(stats), ns, P(ws), _lib.stream_ptr(), 1))
+    out["backward_given_sums_us"] = timed(bwd_stats)
 print(json.dumps(out))

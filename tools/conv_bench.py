@@ -17,6 +17,9 @@ wh = w.half()
 pk, pkt = T._packed_conv_weight(w, torch.float16, 0), T._packed_conv_weight(w, torch.float16, 1)
 fl = 2.0 * N * H * H * 128 * 128 * 9
 gacc = torch.zeros_like(w)
+# a BatchNorm (+ReLU) whose output fed this conv: dgrad with its backward dz sums in the epilogue
+bnb = T._BnBwdLink(x, (torch.rand(N, device="cuda") < 0.7).to(torch.uint8),
+                   torch.stack([torch.zeros(128), torch.ones(128)]).cuda(), 1)
 
 
 def tm(fn, n=50):
@@ -35,6 +38,7 @@ def tm(fn, n=50):
 res = {
     "hip fwd": tm(lambda: T._conv3x3_hip(x, pk)),
     "hip dgrad": tm(lambda: T._conv3x3_hip(x, pkt)),
+    "hip dgrad+bnsums": tm(lambda: T._conv3x3_hip(x, pkt, bnb=bnb, bn_y=x)),
     "miopen fwd": tm(lambda: torch.nn.functional.conv2d(x, wh, padding=1)),
     "miopen dgrad": tm(lambda: torch.ops.aten.convolution_backward(x, x, wh, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [True, False, False])),
     "miopen wgrad": tm(lambda: torch.ops.aten.convolution_backward(x, x, wh, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False])),
@@ -50,4 +54,4 @@ gwr = torch.ops.aten.convolution_backward(x.float(), x.float(), wh.float(), None
 werr = float((gw - gwr).abs().max() / gwr.abs().max())
 print("N=%d H=%d  rel err %.2e  wgrad rel err %.2e" % (N, H, err, werr))
 for k, v in res.items():
-    print("%-14s %8.1f us  %6.0f TFLOP/s" % (k, v, fl / v / 1e6))
+    print("%-17s %8.1f us  %6.0f TFLOP/s" % (k, v, fl / v / 1e6))
