@@ -135,6 +135,9 @@ def parse(argv=None):
                          "or compact lists of the visited children (identical results)")
     ap.add_argument("--hint", default=None, choices=["on", "off"],
                     help="descent prefetch hint / cached exp rows of the tree kernels (default: by game count)")
+    ap.add_argument("--kernel-timers", default="on", choices=["on", "off"],
+                    help="HIP events around every tower / tree launch in the timed moves (off: A/B of their cost; the "
+                         "line then has no roofline)")
     ap.add_argument("--pair", default=None, choices=["on", "off"],
                     help="two waves per game in the fused tree kernel (engine.default_pair when omitted)")
     ap.add_argument("--precision", default="fp16", choices=["fp16", "bf16"],
@@ -553,6 +556,8 @@ def selfplay_leg(args, rank, world, dist, backend, size, sims, mode, blocks, G, 
     az = mode == "AlphaZero"  # AlphaZero searches run the representation tower per wave
     timers, tree_timers = [], []
     for e, st in zip(parts, pstreams):  # HIP events on each part's launch stream
+        if getattr(args, "kernel_timers", "on") == "off":  # (A/B of the events' own cost; no roofline then)
+            break
         if args.net == "hip":
             t = N.KernelTimer(st)
             timers.append(t)
