@@ -155,7 +155,9 @@ def parse(argv=None):
     ap.add_argument("--subline-games", type=int, default=1024)
     ap.add_argument("--c5-steps", type=int, default=3)
     ap.add_argument("--c1-steps", type=int, default=10)
-    ap.add_argument("--worker-moves", type=int, default=20, help="timed moves of the drop-in worker leg (0: skip)")
+    ap.add_argument("--worker-moves", type=int, default=40,
+                    help="timed moves of the drop-in worker leg (0: skip); 40 so the one-move drain at the end of the "
+                         "timed region (the last move's records) weighs ~2.5 %, not 5 %")
     ap.add_argument("--worker-warmup", type=int, default=4, help="untimed worker moves first")
     ap.add_argument("--worker-openings", type=int, default=80,
                     help="staggered starts: each slot's first game from a random opening of 0..N stones "
