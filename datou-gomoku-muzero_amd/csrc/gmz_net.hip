@@ -158,7 +158,9 @@ struct Img3 {
 // k_tower3 ablation bits (0 in the product; timing-only variants in tools/tower_ablate.hip):
 // 1 = A fragments from one k-step (L1-resident), 2 = no weight loads, 32 = no per-board I/O,
 // 128 = s_memtime phase stamps -> pv_feat, 256 = pin the last k-step, 512 = no epilogue,
-// 1024 = no per-layer barrier
+// 1024 = no per-layer barrier, 2048 = weight k-steps past ABL_ALIAS_KS aliased back onto the first ones
+// (the streamed set <= 3.5 MB fits a 4 MB XCD L2), 4096 = k-steps past ABL_ALIAS_KS loaded non-temporal
+constexpr int ABL_ALIAS_KS = 12 * 36;
 template <int H, bool DYN, int ABL = 0, int RD = 4, int NQ = 2, int PG = 4, int NB = 1, typename E = F16>
 __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
   using G = Geo<H>;
@@ -311,7 +313,15 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
   V8 ar[RD][NTW];
   auto loadA = [&](int slot, int gs) {
     if constexpr ((ABL & 2) != 0) if (gs >= 2) return;  // ablation: no weight stream in the loop
-    const int soff = (ABL & 1) ? 0 : (gs < total_ks ? gs : gs - total_ks) * 8192;  // ablation: L1-resident
+    int g = gs < total_ks ? gs : gs - total_ks;
+    if constexpr ((ABL & 2048) != 0) if (g >= ABL_ALIAS_KS) g -= ABL_ALIAS_KS;  // ablation: weight set <= 3.5 MB
+    const int soff = (ABL & 1) ? 0 : g * 8192;  // ablation 1: L1-resident
+    if ((ABL & 4096) != 0 && g >= ABL_ALIAS_KS) {  // ablation: the tail past 3.5 MB streamed non-temporal
+#pragma unroll
+      for (int nt = 0; nt < NTW; ++nt)
+        ar[slot][nt] = __builtin_bit_cast(V8, __builtin_amdgcn_raw_buffer_load_b128(wrsrc, wvoff + nt * 1024, soff, 2));
+      return;
+    }
 #pragma unroll
     for (int nt = 0; nt < NTW; ++nt) {
       const auto v = __builtin_amdgcn_raw_buffer_load_b128(wrsrc, wvoff + nt * 1024, soff, 0);

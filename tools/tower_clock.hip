@@ -91,13 +91,27 @@ int main(int argc, char **argv) {
     printf("warm-up: %d launches, %.2f ms each\n", n, ms / n);
   }
   const int reps = 100;
+  // variants (argv[3]: a comma list of indices, default all): 0 product, 1 weights aliased onto <= 3.5 MB
+  // (ABL 2048, ablation only), 2 the k-steps past 3.5 MB loaded non-temporal (ABL 4096)
+  const char *names[3] = {"product", "alias<=3.5MB", "nt-tail"};
+  std::vector<int> vars;
+  if (argc > 3) { for (const char *p = argv[3]; *p; ++p) if (*p >= '0' && *p <= '2') vars.push_back(*p - '0'); }
+  else vars = {0, 1, 2};
+  auto run = [&](int v, bool stamped) {
+    for (int i = 0; i < reps; ++i) {
+      if (v == 0) { if (stamped) launch<128>(a, grid, ++gen); else launch<0>(a, grid, ++gen); }
+      else if (v == 1) { if (stamped) launch<2048 | 128>(a, grid, ++gen); else launch<2048>(a, grid, ++gen); }
+      else { if (stamped) launch<4096 | 128>(a, grid, ++gen); else launch<4096>(a, grid, ++gen); }
+    }
+  };
   for (int round = 0; round < 3; ++round) {
+    for (int v : vars) {
     float ms0 = 0.f, ms1 = 0.f;
     CK(hipEventRecord(e0, 0));
-    for (int i = 0; i < reps; ++i) launch<0>(a, grid, ++gen);
+    run(v, false);
     CK(hipEventRecord(e1, 0)); CK(hipEventSynchronize(e1)); CK(hipEventElapsedTime(&ms0, e0, e1));
     CK(hipEventRecord(e0, 0));
-    for (int i = 0; i < reps; ++i) launch<128>(a, grid, ++gen);
+    run(v, true);
     CK(hipEventRecord(e1, 0)); CK(hipEventSynchronize(e1)); CK(hipEventElapsedTime(&ms1, e0, e1));
     std::vector<float> st((size_t)grid * NW * 4);
     CK(hipMemcpy(st.data(), dpv, st.size() * 4, hipMemcpyDeviceToHost));  // the last stamped launch
@@ -108,11 +122,12 @@ int main(int argc, char **argv) {
     }
     const double nw = grid * NW, wall1 = ms1 / reps * 1e-3;
     const double flop = 1136505600.0 * rows;
-    printf("round %d: product %.4f ms (%.0f TFLOP/s, %.3f of 2.5 PF) | stamped %.4f ms | per wave: k-loop %.0f, "
+    printf("round %d %-13s: %.4f ms (%.0f TFLOP/s, %.3f of 2.5 PF) | stamped %.4f ms | per wave: k-loop %.0f, "
            "epilogue %.0f, barrier %.0f, lifetime %.0f (max %.0f) cycles | in-kernel clock %.3f GHz | "
            "k-loop share %.3f, epilogue %.3f, barrier %.3f\n",
-           round, ms0 / reps, flop / (ms0 / reps * 1e-3) / 1e12, flop / (ms0 / reps * 1e-3) / 2.5e15, ms1 / reps,
+           round, names[v], ms0 / reps, flop / (ms0 / reps * 1e-3) / 1e12, flop / (ms0 / reps * 1e-3) / 2.5e15, ms1 / reps,
            loop / nw, epi / nw, bar / nw, tot / nw, tmax, tmax / wall1 / 1e9, loop / tot, epi / tot, bar / tot);
+    }
   }
   CK(hipDeviceSynchronize());
   return 0;
