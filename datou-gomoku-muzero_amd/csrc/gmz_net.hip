@@ -161,7 +161,16 @@ struct Img3 {
 // 1024 = no per-layer barrier, 2048 = weight k-steps past ABL_ALIAS_KS aliased back onto the first ones
 // (the streamed set <= 3.5 MB fits a 4 MB XCD L2), 4096 = k-steps past ABL_ALIAS_KS loaded non-temporal
 constexpr int ABL_ALIAS_KS = 12 * 36;
-template <int H, bool DYN, int ABL = 0, int RD = 4, int NQ = 2, int PG = 4, int NB = 1, typename E = F16>
+// PIPE (15x15 two-image configuration, 8 waves = 4 channel quarters x 2 position groups): 0 = one workgroup barrier
+// per layer; 1 = the layer hand-off split into two channel halves that run as a pipeline: half h = the waves of
+// channel quarters h and h + 2, whose output chunks {0-3, 8-11} / {4-7, 12-15} are exactly the input chunks of
+// k-steps {0, 1} / {2, 3} (the LDS chunk pairing {2s, 2s+8, 2s+1, 2s+9}).  A half runs its own k-steps of every tap
+// first (they read only its own previous epilogue) and the other half's second, so it waits for its own half's
+// epilogue before a layer and for the other half's only half way through it: one half's epilogue runs under the
+// other half's MFMAs.  The two waves of a SIMD belong to different halves (and different position groups, so every
+// SIMD keeps 15 tiles).  Hand-offs are LDS counters (epilogues done per half); the board's last layer still ends in
+// a workgroup barrier.  2 = 1 with half 0 at a raised issue priority (it leads, half 1 fills its epilogues).
+template <int H, bool DYN, int ABL = 0, int RD = 4, int NQ = 2, int PG = 4, int NB = 1, typename E = F16, int PIPE = 0>
 __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
   using G = Geo<H>;
   using I = Img3<H>;
@@ -236,10 +245,17 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
     finish_launch();
     return;
   }
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  constexpr bool PP = PIPE != 0;
+  static_assert(!PP || (NB == 1 && !ONE && NQ == 4 && PG == 2), "the half pipeline is the 15x15 8-wave two-image tower's");
   // wave w -> (channel group nh, position group pg) = (w % NQ, w / NQ): the waves sharing a SIMD
-  // (w, w+4, ...) get different position groups, so a short last group does not load one SIMD less
-  const int nh = w % NQ, pg = w / NQ;
+  // (w, w+4, ...) get different position groups, so a short last group does not load one SIMD less.
+  // PIPE: w -> half hh = w / 4, quarter hh + 2 (w & 1), position group (w >> 1) & 1 (half 0) or its complement
+  // (half 1): SIMD j hosts one wave of each half and of each position group
+  const int hh = PP ? (w >> 2) : 0;
+  const int nh = PP ? hh + 2 * (w & 1) : w % NQ;
+  const int pg = PP ? (hh == 0 ? ((w >> 1) & 1) : 1 - ((w >> 1) & 1)) : w / NQ;
+  if constexpr (PIPE == 2) if (hh == 0) __builtin_amdgcn_s_setprio(1);
   const int g4 = lane >> 4;
   const int cg = (g4 & 1) * 8 + (g4 >> 1);  // {0, 8, 1, 9}
   auto cell = [&](int p) { return (p / H + 1) * RS + (p % H + 1) * PS; };
@@ -260,16 +276,34 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
                                          16, 0, 0);
     }
   };
-  // ---- bias of layer L -> sbias[slot]: one 512 B LDS-DMA by wave 0 (32 lanes)
+  // ---- bias of layer L -> sbias[slot]: one 512 B LDS-DMA by wave 0 (32 lanes); PIPE: each half's first wave
+  //      DMAs its own half's channels (quarters hh and hh + 2: 2 x 128 B), the only ones its half reads
   auto issue_bias = [&](int L, int slot) {
-    if (w == 0 && lane < 32)
+    if constexpr (PP) {
+      if ((w & 3) == 0 && lane < 8) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+          __builtin_amdgcn_global_load_lds((const void *)(t.bias + L * C + (hh + 2 * q) * 32 + lane * 4),
+                                           (__attribute__((address_space(3))) void *)(sbias + slot * C + (hh + 2 * q) * 32),
+                                           16, 0, 0);
+      }
+    } else if (w == 0 && lane < 32) {
       __builtin_amdgcn_global_load_lds((const void *)(t.bias + L * C + lane * 4),
                                        (__attribute__((address_space(3))) void *)(sbias + slot * C), 16, 0, 0);
+    }
+  };
+  // ---- PIPE hand-offs: s_cnt[h] = epilogues finished by half h's 4 waves (cumulative over this workgroup's layers)
+  __shared__ int s_cnt[2];
+  auto wait_cnt = [&](int h, int target) {
+    volatile int *c = s_cnt + h;
+    while (*c < target) __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
   };
 
   // ---- zero both images (borders and pads), biases of layer 0, action term
   for (int i = tid; i < NB * BB / 16; i += NTHR) *(uint4 *)(smem + i * 16) = make_uint4(0, 0, 0, 0);
   if (tid < C) sbias[tid] = t.bias[tid];
+  if (tid < 2) s_cnt[tid] = 0;
   if (DYN)
     for (int i = tid; i < 9 * C; i += NTHR) saction[i] = t.action_term[i];
   __syncthreads();  // zeroing done before the DMA writes the interior
@@ -328,8 +362,22 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
       ar[slot][nt] = __builtin_bit_cast(V8, v);
     }
   };
+  // PIPE: k-step s of layer Lk in the half's order: s < 18 -> tap s / 2, k-step 2 hh + (s & 1) (own half's input
+  // chunks), s >= 18 -> tap (s - 18) / 2, k-step 2 (1 - hh) + (s & 1); Lk = n_layers is the next board's layer 0
+  const int hown = hh * 16384, hoth = (1 - hh) * 16384;
+  auto loadAp = [&](int slot, int Lk, int s) {
+    const int Lw = Lk < t.n_layers ? Lk : Lk - t.n_layers;
+    const int tap = (s < 18 ? s : s - 18) >> 1;
+    const int soff = (Lw * KSTEPS + tap * 4 + (s & 1)) * 8192 + (s < 18 ? hown : hoth);
 #pragma unroll
-  for (int k = 0; k < RD - 1; ++k) loadA(k, k);
+    for (int nt = 0; nt < NTW; ++nt)
+      ar[slot][nt] = __builtin_bit_cast(V8, __builtin_amdgcn_raw_buffer_load_b128(wrsrc, wvoff + nt * 1024, soff, 0));
+  };
+#pragma unroll
+  for (int k = 0; k < RD - 1; ++k) {
+    if constexpr (PP) loadAp(k, 0, k);
+    else loadA(k, k);
+  }
   int gl = 0;  // layers run by this workgroup so far: bias slot = gl & 1
   uint64_t st_loop = 0, st_epi = 0, st_bar = 0, st_t0 = 0, st_t1 = 0, st_t2 = 0;  // ABL & 128 stamps
   const uint64_t st_start = (ABL & 128) ? __builtin_amdgcn_s_memtime() : 0;
@@ -392,6 +440,11 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
     for (int L = 0; L < t.n_layers; ++L, ++gl) {
       const uint8_t *img = smem + (ONE ? 0 : (L & 1) * IMG);
       uint8_t *nimg = smem + (ONE ? 0 : ((L + 1) & 1) * IMG);
+      if constexpr (PP) {  // own half's epilogues of the previous layer (its bias DMA landed before them)
+        if (ABL & 128) st_t2 = __builtin_amdgcn_s_memtime();
+        wait_cnt(hh, 4 * gl);
+        if (ABL & 128) st_bar += __builtin_amdgcn_s_memtime() - st_t2;
+      }
       // the next layer's bias (for the last layer: the next board's layer 0) -> the other slot;
       // that slot was last read by the previous layer's epilogue, which the barrier has closed
       issue_bias(L + 1 < t.n_layers ? L + 1 : 0, (gl + 1) & 1);
@@ -405,7 +458,7 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
       int bb[PTW];
 #pragma unroll
       for (int i = 0; i < PTW; ++i) {
-        bb[i] = (pos[i] < 0 ? 0 : pos[i] + cg * 16) + (int)(size_t)(img - smem);
+        bb[i] = (pos[i] < 0 ? 0 : pos[i] + cg * 16) + (int)(size_t)(img - smem) + (PP ? 64 * hh : 0);
         asm volatile("" : "+v"(bb[i]));  // one base VGPR per tile and layer; all else immediates
       }
       // k-loop over the NTL tiles this wave owns (NTL = PTW, or PTW - 1 for a short last position
@@ -418,12 +471,41 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
           for (int nt = 0; nt < NTW; ++nt) acc[nt][i] = bv[nt];  // the empty slot (never stored)
         V8 b[2][NTL];
         auto readB = [&](int buf, int st) {
-          const int tap = st >> 2, ks = st & 3;
+          const int tap = PP ? (st < 18 ? st : st - 18) >> 1 : st >> 2, ks = PP ? (st & 1) : st & 3;
           const int off = (tap / 3) * RS + (tap % 3) * PS + ks * 32;
 #pragma unroll
           for (int i = 0; i < NTL; ++i) b[buf][i] = *(const V8 *)(smem + bb[i] + off);
         };
         readB(0, 0);
+        if constexpr (PP) {
+          if (ABL & 128) st_t0 = __builtin_amdgcn_s_memtime();
+#pragma unroll
+          for (int st = 0; st < KSTEPS; ++st) {
+            const int sn = st + RD - 1;
+            if (sn < KSTEPS) loadAp(sn % RD, L, sn);
+            else loadAp(sn % RD, L + 1, sn - KSTEPS);
+            if (st + 1 < KSTEPS && st + 1 != 18) readB((st + 1) & 1, st + 1);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < NTL; ++i)
+#pragma unroll
+              for (int nt = 0; nt < NTW; ++nt)
+                acc[nt][i] = E::mfma(ar[st % RD][nt], b[st & 1][i], st == 0 ? bv[nt] : acc[nt][i]);
+            if (st == 17) {  // half way: the other half's chunks, written by its epilogues of the previous layer
+              __builtin_amdgcn_sched_barrier(0);
+              uint64_t tw = 0;
+              if (ABL & 128) tw = __builtin_amdgcn_s_memtime();
+              wait_cnt(1 - hh, 4 * gl);
+              if (ABL & 128) st_bar += __builtin_amdgcn_s_memtime() - tw;
+              const int dsw = 64 - 128 * hh;
+#pragma unroll
+              for (int i = 0; i < NTL; ++i) bb[i] += dsw;
+              readB(0, 18);
+            }
+            if ((ABL & 256) || st + 1 < KSTEPS) __builtin_amdgcn_sched_barrier(0);
+          }
+          return;
+        }
         if (ABL & 128) st_t0 = __builtin_amdgcn_s_memtime();
         const int gs0 = L * KSTEPS;
 #pragma unroll
@@ -519,10 +601,20 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
       else epilogue(std::integral_constant<int, 2>{});
       // the bias DMA (issued before this layer's 36 k-steps) is older than the (RD-1)*NTW ring loads
       // still in flight: this count retires it before the barrier publishes the slot
-      if (w == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((RD - 1) * NTW) : "memory");
+      if (w == 0 || (PP && w == 4)) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((RD - 1) * NTW) : "memory");
       if (ABL & 128) { st_t2 = __builtin_amdgcn_s_memtime(); st_epi += st_t2 - st_t1; }
-      if constexpr (!(ABL & 1024)) __syncthreads();  // ablation 1024: no per-layer barrier (timing only)
-      if (ABL & 128) st_bar += __builtin_amdgcn_s_memtime() - st_t2;
+      if constexpr (PP) {
+        // this wave's epilogue stores (and, for the half's first wave, the bias DMA) are complete: count it
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_fetch_add(s_cnt + hh, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (L == t.n_layers - 1) {
+          __syncthreads();  // the board's output stage reads every channel
+          if (ABL & 128) st_bar += __builtin_amdgcn_s_memtime() - st_t2;
+        }
+      } else {
+        if constexpr (!(ABL & 1024)) __syncthreads();  // ablation 1024: no per-layer barrier (timing only)
+        if (ABL & 128) st_bar += __builtin_amdgcn_s_memtime() - st_t2;
+      }
     }
 
     // ---- next boards' input -> the free images, overlapped with these boards' output stage

@@ -7,6 +7,7 @@
 // Build: hipcc -O3 --offload-arch=gfx950 -std=c++17 -ffp-contract=off -Iinclude tools/tower_clock.hip -o tools/tower_clock.bin
 #include "../datou-gomoku-muzero_amd/csrc/gmz_net.hip"
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <random>
@@ -20,12 +21,12 @@ using namespace gmz;
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
 
-template <int ABL>
+template <int ABL, int PIPE = 0>
 static void launch(TowerArgs a, int grid, unsigned long long gen) {
   using T = TowerCfg<15>;
   a.gen = gen;
-  hipLaunchKernelGGL((k_tower3<15, true, ABL, T::RD, T::NQ, T::PG, T::NB, F16>), dim3(grid), dim3(64 * T::NQ * T::PG), 0, 0,
-                     a);
+  hipLaunchKernelGGL((k_tower3<15, true, ABL, T::RD, T::NQ, T::PG, T::NB, F16, PIPE>), dim3(grid), dim3(64 * T::NQ * T::PG), 0,
+                     0, a);
 }
 
 static uint16_t half_bits(float f) {
@@ -78,6 +79,26 @@ int main(int argc, char **argv) {
   unsigned long long gen = 0;
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  // the pipelined variants against the product on the same input (k-step order differs: f32 summation order only)
+  {
+    std::vector<uint16_t> o0((size_t)rows * A * 128), o1(o0.size());
+    launch<0>(a, grid, ++gen);
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(o0.data(), dpool + (size_t)rows * A * 128, o0.size() * 2, hipMemcpyDeviceToHost));
+    for (int pv = 1; pv <= 2; ++pv) {
+      CK(hipMemset(dpool + (size_t)rows * A * 128, 0, o0.size() * 2));
+      if (pv == 1) launch<0, 1>(a, grid, ++gen); else launch<0, 2>(a, grid, ++gen);
+      CK(hipDeviceSynchronize());
+      CK(hipMemcpy(o1.data(), dpool + (size_t)rows * A * 128, o1.size() * 2, hipMemcpyDeviceToHost));
+      double md = 0, mx = 0; size_t ndiff = 0;
+      for (size_t i = 0; i < o0.size(); ++i) {
+        _Float16 x, y; memcpy(&x, &o0[i], 2); memcpy(&y, &o1[i], 2);
+        const double d = fabs((double)x - (double)y);
+        md = std::max(md, d); mx = std::max(mx, fabs((double)x)); ndiff += o0[i] != o1[i];
+      }
+      printf("PIPE %d vs product: max |d| %.4g (max |x| %.4g), %zu of %zu values differ\n", pv, md, mx, ndiff, o0.size());
+    }
+  }
   // warm-up: >= `seconds` s of back-to-back product launches (the clock the chip settles at under this load)
   {
     float ms = 0.f;
@@ -92,16 +113,22 @@ int main(int argc, char **argv) {
   }
   const int reps = 100;
   // variants (argv[3]: a comma list of indices, default all): 0 product, 1 weights aliased onto <= 3.5 MB
-  // (ABL 2048, ablation only), 2 the k-steps past 3.5 MB loaded non-temporal (ABL 4096)
-  const char *names[3] = {"product", "alias<=3.5MB", "nt-tail"};
+  // (ABL 2048, ablation only), 2 the k-steps past 3.5 MB loaded non-temporal (ABL 4096), 3 no per-layer barrier
+  // (ABL 1024, ablation: the bound of a barrier-free layer hand-off), 4 no barrier and no epilogue (ABL 1536),
+  // 5 the channel-half pipeline (PIPE 1), 6 the same with half 0 at raised priority (PIPE 2)
+  const char *names[7] = {"product", "alias<=3.5MB", "nt-tail", "no-barrier", "no-bar+no-epi", "pipe-halves", "pipe+prio"};
   std::vector<int> vars;
-  if (argc > 3) { for (const char *p = argv[3]; *p; ++p) if (*p >= '0' && *p <= '2') vars.push_back(*p - '0'); }
+  if (argc > 3) { for (const char *p = argv[3]; *p; ++p) if (*p >= '0' && *p <= '6') vars.push_back(*p - '0'); }
   else vars = {0, 1, 2};
   auto run = [&](int v, bool stamped) {
     for (int i = 0; i < reps; ++i) {
       if (v == 0) { if (stamped) launch<128>(a, grid, ++gen); else launch<0>(a, grid, ++gen); }
       else if (v == 1) { if (stamped) launch<2048 | 128>(a, grid, ++gen); else launch<2048>(a, grid, ++gen); }
-      else { if (stamped) launch<4096 | 128>(a, grid, ++gen); else launch<4096>(a, grid, ++gen); }
+      else if (v == 2) { if (stamped) launch<4096 | 128>(a, grid, ++gen); else launch<4096>(a, grid, ++gen); }
+      else if (v == 3) { if (stamped) launch<1024 | 128>(a, grid, ++gen); else launch<1024>(a, grid, ++gen); }
+      else if (v == 4) { if (stamped) launch<1536 | 128>(a, grid, ++gen); else launch<1536>(a, grid, ++gen); }
+      else if (v == 5) { if (stamped) launch<128, 1>(a, grid, ++gen); else launch<0, 1>(a, grid, ++gen); }
+      else { if (stamped) launch<128, 2>(a, grid, ++gen); else launch<0, 2>(a, grid, ++gen); }
     }
   };
   for (int round = 0; round < 3; ++round) {
