@@ -11,7 +11,7 @@ import torch  # noqa: F401  (must precede the CDLL load: shared HIP runtime)
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GMZ_LIB") or os.path.join(PKG_DIR, "libgmz.so")  # GMZ_LIB: A/B builds (tools)
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -53,6 +53,8 @@ _SIGS = {
     "gmz_engine_wave_depth": ([P, P, P], I),
     "gmz_engine_tree_counters": ([P, P, I, P], I),
     "gmz_engine_set_hidden_bases": ([P, P, P], I),
+    "gmz_engine_set_hidden_budget": ([P, P, P], I),
+    "gmz_engine_errors": ([P, ctypes.POINTER(ctypes.c_int32), I], I),
     "gmz_hashnet_initial": ([P, I, I, P, P, P, P, P], I),
     "gmz_hashnet_recurrent": ([P, P, P, P, I, I, P, P, P, P], I),
     "gmz_bn_workspace_bytes": ([I, I, I, I, ctypes.POINTER(ctypes.c_size_t)], I),

@@ -97,6 +97,10 @@ struct Dev {
   int32_t *ctr;        // [G][4] k_expand_select work counters (gmz_engine_tree_counters)
   int32_t *hbase;      // [G] hidden-state slot of game g's node 0: node u's hidden state is pool slot hbase[g] + u
                        //     (gmz_engine_set_hidden_bases; default g * S)
+  int32_t *hbud;       // [G] hidden-state slots game g owns from hbase[g] (gmz_engine_set_hidden_budget; default S):
+                       //     a selection whose new node would pass it raises err bit 0 and writes the game's last
+                       //     slot instead, never the next game's
+  int32_t *err;        // [1] sticky error bits (gmz_engine_errors)
   GameState *gs;
   uint64_t *legal;  // [G][NJ]
   int16_t *set_rank;
@@ -110,6 +114,16 @@ struct Dev {
   double c_scale;
   float disc_f, delta_f;
 };
+
+// node `leaf` of game g -> its hidden-state slot offset from hbase[g]; a node past the game's budget (the
+// caller sized the pool too small for this search) raises error bit 0 and takes the game's last slot, so the
+// fault stays inside the game (its search result is void) instead of overwriting the next game's states
+__device__ __forceinline__ int hidden_slot_in_budget(const Dev &D, int g, int leaf) {
+  const int bud = D.hbud[g];
+  if (leaf < bud) return leaf;
+  atomicOr(D.err, 1);
+  return bud > 0 ? bud - 1 : 0;
+}
 
 // waves per SIMD the hint kernel is compiled for: 2 (<= 256 VGPRs) measured faster than 4 (128 VGPRs,
 // spills) at 1,024 games per engine (36.4 vs 46.9 us, profiles/r02_tree_expl_variants.txt)
@@ -1183,7 +1197,7 @@ __device__ __forceinline__ void select_game(const Dev &D, int g, int lane, int32
     D.gs[g] = st;
     in_slot[g] = hb + u;
     act_out[g] = a;
-    out_slot[g] = hb + leaf;
+    out_slot[g] = hb + hidden_slot_in_budget(D, g, leaf);
   }
   if (AZ && obs) {  // observation of the replayed board (mcts.py:251)
     float *o = obs + (size_t)g * 3 * A;
@@ -1709,7 +1723,7 @@ __device__ void select_game_pair(const Dev &D, int g, int h, int lane, int32_t *
     D.gs[g] = st;
     in_slot[g] = hb + u;
     act_out[g] = a;
-    out_slot[g] = hb + leaf;
+    out_slot[g] = hb + hidden_slot_in_budget(D, g, leaf);
   }
 }
 
@@ -1909,6 +1923,8 @@ GMZ_EXPORT int gmz_engine_create(const gmz_engine_cfg *cfg, gmz_engine **out) {
   rc |= dalloc(e, &D.hdr, G * S);
   rc |= dalloc(e, &D.ctr, G * 4);
   rc |= dalloc(e, &D.hbase, G);
+  rc |= dalloc(e, &D.hbud, G);
+  rc |= dalloc(e, &D.err, 1);
   rc |= dalloc(e, &D.path_u, G * S);
   rc |= dalloc(e, &D.path_a, G * S);
   rc |= dalloc(e, &D.path_e, G * S);
@@ -1929,10 +1945,12 @@ GMZ_EXPORT int gmz_engine_create(const gmz_engine_cfg *cfg, gmz_engine **out) {
     gmz_engine_destroy(e);
     return fail("gmz_engine_create: hipMemset failed");
   }
-  {  // default hidden-state slots: game g's nodes at g * S + u (a pool of G * S slots)
-    std::vector<int32_t> hb(G);
+  {  // default hidden-state slots: game g's nodes at g * S + u (a pool of G * S slots), S of them each
+    std::vector<int32_t> hb(G), bud(G, (int32_t)S);
     for (size_t g = 0; g < G; ++g) hb[g] = (int32_t)(g * S);
-    if (hipMemcpy(D.hbase, hb.data(), G * sizeof(int32_t), hipMemcpyHostToDevice) != hipSuccess) {
+    if (hipMemcpy(D.hbase, hb.data(), G * sizeof(int32_t), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(D.hbud, bud.data(), G * sizeof(int32_t), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemset(D.err, 0, sizeof(int32_t)) != hipSuccess) {
       gmz_engine_destroy(e);
       return fail("gmz_engine_create: hipMemcpy failed");
     }
@@ -2206,6 +2224,21 @@ GMZ_EXPORT int gmz_engine_set_hidden_bases(gmz_engine *e, const int32_t *hbase_d
   if (!e || !hbase_dev) return fail("gmz_engine_set_hidden_bases: null argument");
   GMZ_HIP(hipMemcpyAsync(e->D.hbase, hbase_dev, (size_t)e->D.G * sizeof(int32_t), hipMemcpyDeviceToDevice,
                          (hipStream_t)stream));
+  return 0;
+}
+
+GMZ_EXPORT int gmz_engine_set_hidden_budget(gmz_engine *e, const int32_t *budget_dev, void *stream) {
+  if (!e || !budget_dev) return fail("gmz_engine_set_hidden_budget: null argument");
+  GMZ_HIP(hipMemcpyAsync(e->D.hbud, budget_dev, (size_t)e->D.G * sizeof(int32_t), hipMemcpyDeviceToDevice,
+                         (hipStream_t)stream));
+  return 0;
+}
+
+GMZ_EXPORT int gmz_engine_errors(gmz_engine *e, int32_t *out, int reset) {
+  if (!e || !out) return fail("gmz_engine_errors: null argument");
+  GMZ_HIP(hipDeviceSynchronize());
+  GMZ_HIP(hipMemcpy(out, e->D.err, sizeof(int32_t), hipMemcpyDeviceToHost));
+  if (reset) GMZ_HIP(hipMemset(e->D.err, 0, sizeof(int32_t)));
   return 0;
 }
 

@@ -31,10 +31,11 @@ class HashNetBackend:
         self.A = action_space
         self.pool = torch.zeros(num_slots, dtype=torch.int32, device=device)  # uint32 ids
 
-    def ensure_slots(self, n):
-        """At least ``n`` hidden-state slots (a larger pool, contents not kept: called between moves)."""
+    def ensure_slots(self, n, stream=None):
+        """At least ``n`` hidden-state slots (a larger pool, contents not kept: called between moves); the old
+        pool is recorded on ``stream`` (default: the current one), the stream that used it."""
         if n > self.pool.numel():
-            torch.cuda.synchronize(self.pool.device)
+            self.pool.record_stream(stream if stream is not None else torch.cuda.current_stream(self.pool.device))
             self.pool = torch.zeros(int(n * 1.25) + 1, dtype=torch.int32, device=self.pool.device)
 
     def split(self, parts, max_grid=0):
@@ -114,9 +115,14 @@ class BatchedSelfPlayEngine:
         self.in_slot = torch.zeros(G, dtype=i32, device=dev)
         self.out_slot = torch.zeros(G, dtype=i32, device=dev)
         self.act_req = torch.zeros(G, dtype=i32, device=dev)
-        # hidden-state slot of each game's root (= its node 0): hbase[g], rewritten when the bases move
-        self.root_slot = torch.arange(G, dtype=i32, device=dev) * self.slots_per_game
-        self._hb_host = [torch.zeros(G, dtype=i32).pin_memory() for _ in range(2)]
+        # hidden-state slot of each game's root (= its node 0): hbase[g], rewritten when the bases move, and
+        # beside it each game's slot budget (gmz_engine_set_hidden_budget): one device buffer [2G]
+        self._hb_dev = torch.empty(2 * G, dtype=i32, device=dev)
+        self.root_slot = self._hb_dev[:G]
+        self.hidden_budget = self._hb_dev[G:]
+        self.root_slot.copy_(torch.arange(G, dtype=i32, device=dev) * self.slots_per_game)
+        self.hidden_budget.fill_(self.slots_per_game)
+        self._hb_host = [torch.zeros(2 * G, dtype=i32).pin_memory() for _ in range(2)]
         self._hb_events = [None, None]
         self._hb_flip = 0
         self._hb_last = None  # the bases last handed to the engine (host copy)
@@ -131,6 +137,9 @@ class BatchedSelfPlayEngine:
         self._last_reset = True
         self.waves_last = 0
         self.tree_timer = None  # optional network.KernelTimer around the fused expand/backup+select launches
+        # the packed per-game hidden-state bases and budgets from the start, so a direct ABI caller
+        # (begin_move / select without search_steps) already uses slots inside the network's pool
+        self._place_hidden(self._stream())
 
     # ------------------------------------------------------------------ lifecycle
     def close(self):
@@ -210,25 +219,37 @@ class BatchedSelfPlayEngine:
         base = np.zeros(self.G, np.int64)
         np.cumsum(need[:-1], out=base[1:])
         total = int(base[-1] + need[-1])
-        if self._hb_last is not None and np.array_equal(base, self._hb_last):
+        key = np.concatenate([base, need])
+        if self._hb_last is not None and np.array_equal(key, self._hb_last):
             return
         if total >= 2 ** 31:
             raise ValueError("hidden-state pool: %d slots exceed the int32 slot index" % total)
         if hasattr(self.net, "ensure_slots"):
-            self.net.ensure_slots(total)
+            self.net.ensure_slots(total, stream)
         i = self._hb_flip
         self._hb_flip ^= 1
         if self._hb_events[i] is not None:
             self._hb_events[i].synchronize()  # (a copy two placements ago: long done)
-        self._hb_host[i].numpy()[:] = base
+        hb = self._hb_host[i].numpy()
+        hb[:self.G] = base
+        hb[self.G:] = need
         with torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext():
-            self.root_slot.copy_(self._hb_host[i], non_blocking=True)  # on the search's stream
+            self._hb_dev.copy_(self._hb_host[i], non_blocking=True)  # on the search's stream
             ev = torch.cuda.Event()
             ev.record()
         self._hb_events[i] = ev
         check(self.lib.gmz_engine_set_hidden_bases(self.handle, ptr(self.root_slot), s))
-        self._hb_last = base
+        check(self.lib.gmz_engine_set_hidden_budget(self.handle, ptr(self.hidden_budget), s))
+        self._hb_last = key
         self.hidden_slots_used = total
+
+    def errors(self, reset=False):
+        """Sticky error bits of the engine's kernels (synchronises the device; gmz_engine_errors): bit 0 = a
+        search created more nodes than its game's hidden-state budget (its result is void; no other game's
+        states were touched)."""
+        out = ctypes.c_int32()
+        check(self.lib.gmz_engine_errors(self.handle, ctypes.byref(out), 1 if reset else 0))
+        return out.value
 
     def waves_needed(self):
         out = ctypes.c_int32()

@@ -267,12 +267,15 @@ class GomokuNetHip:
             q.w.max_grid = keep
             q._tensors = self._tensors
 
-    def ensure_slots(self, n):
+    def ensure_slots(self, n, stream=None):
         """At least ``n`` hidden-state slots in ``self.pool`` (engine._place_hidden, between moves: the
-        contents are not kept).  A split() view that outgrows its slice gets a pool of its own."""
+        contents are not kept).  A split() view that outgrows its slice gets a pool of its own.  ``stream``:
+        the (torch) stream whose launches use the pool (default: the current one); the old pool's memory is
+        recorded on it, so the caching allocator reuses it only after that stream's queued launches, and no
+        other stream (the other engine half, a concurrent trainer) is waited for."""
         per = self.A * C
         if n * per > self.pool.numel():
-            torch.cuda.synchronize(self.device)  # no launch still reads or writes the old pool
+            self.pool.record_stream(stream if stream is not None else torch.cuda.current_stream(self.device))
             self.pool = torch.empty(int(n * 1.25 + 1) * per, dtype=torch.int16, device=self.device)
 
     def split(self, parts, max_grid=0):

@@ -1133,7 +1133,10 @@ class ReplayBuffer:
             obs, act, rew, pol, val = obs[-self.N:], act[-self.N:], rew[-self.N:], pol[-self.N:], val[-self.N:]
             n = self.N
         idx = ((torch.arange(n) + self.ptr) % self.N).to(self.device)
-        dv = lambda x, dt: torch.as_tensor(x).to(self.device, dt)  # noqa: E731
+        def dv(x, dt):
+            if isinstance(x, np.ndarray) and not x.flags.writeable:
+                x = np.array(x)  # torch.as_tensor warns on (and would alias) a read-only numpy array
+            return torch.as_tensor(x).to(self.device, dt)
         self.obs[idx] = dv(obs, torch.uint8)
         self.act[idx] = dv(act, torch.int32)
         self.rew[idx] = dv(rew, torch.float32)

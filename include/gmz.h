@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define GMZ_ABI_VERSION 7
+#define GMZ_ABI_VERSION 8
 
 /* ------------------------------------------------------------------ misc */
 const char *gmz_last_error(void);
@@ -123,6 +123,13 @@ int gmz_engine_set_root(gmz_engine *e, const float *logits_dev, const float *val
  * + 2 slots (engine.py sizes the pool per move this way); the root's slot hbase[g] is the
  * initial_inference output slot. */
 int gmz_engine_set_hidden_bases(gmz_engine *e, const int32_t *hbase_dev, void *stream);
+/* Slots game g owns from hbase[g] (budget_dev int32[G], copied stream-ordered; default num_simulations + 2).
+ * A selection whose new node would pass its game's budget sets error bit 0 (gmz_engine_errors) and writes
+ * that game's last slot instead of the next game's.  (ABI 8) */
+int gmz_engine_set_hidden_budget(gmz_engine *e, const int32_t *budget_dev, void *stream);
+/* Sticky error bits of the engine's kernels into *out (synchronises the device); reset != 0 clears them.
+ * Bit 0: a hidden-state slot past a game's budget (gmz_engine_set_hidden_budget).  (ABI 8) */
+int gmz_engine_errors(gmz_engine *e, int32_t *out, int reset);
 /* Step 3 (mcts.py:326-336 / 233-253): one wave.  For each game with an unfinished search:
  * descend to the leaf, allocate its node, and emit the network request
  *   MuZero:    in_slot_dev[g] = hbase[g] + parent node, action_dev[g] = leaf action,
