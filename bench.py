@@ -195,6 +195,10 @@ def parse(argv=None):
     ap.add_argument("--phase-timeout-extras", type=float, default=200.0)
     ap.add_argument("--phase-timeout-trainer", type=float, default=150.0)
     ap.add_argument("--phase-timeout-loop", type=float, default=180.0)
+    ap.add_argument("--deadline", type=float, default=540.0,
+                    help="isolated phases (N > 1): wall-time budget of the whole run in s; each phase's cap shrinks to "
+                         "what is left of it (a later phase with < 15 s left is skipped), so the sum of the caps never "
+                         "exceeds it (0: the per-phase caps only)")
     ap.add_argument("--pmc-file", default=os.path.join(REPO, "profiles", "pmc_tower_latest.json"))
     ap.add_argument("--pmc-tree-file", default=os.path.join(REPO, "profiles", "pmc_tree_latest.json"))
     return ap.parse_args(argv)
@@ -995,6 +999,9 @@ def _parse_fragment(text):
     return None
 
 
+MIN_PHASE_S = 15.0  # a later phase with less of the deadline left is skipped, not started
+
+
 def orchestrate(args, argv, rank, world, script=None):
     """N > 1: this rank process never touches the GPU.  Every phase runs as a FRESH set of rank processes
     (one per rank, a process group of their own on a new port) under a wall-time cap, so a failure or hang
@@ -1005,6 +1012,7 @@ def orchestrate(args, argv, rank, world, script=None):
     fragment, then each later phase's, or {"error": ...} in the keys of a phase that failed or timed out."""
     import datetime
     import torch.distributed as dist
+    t_start = time.time()
     caps = phase_plan(args)
     store = None
     if world > 1:
@@ -1021,7 +1029,30 @@ def orchestrate(args, argv, rank, world, script=None):
     else:  # --isolate on with one GPU: the phases run one after the other as single processes
         ports = [None for _ in caps]
     out, phases = None, {}
+    # what the deadline leaves after the phases: the per-phase status exchange and the line (+ the CPU baseline
+    # sample with one rank)
+    reserve = 10.0 + ((args.cpu_baseline_sec + 15.0) if (world == 1 and not args.no_cpu_baseline) else 0.0)
     for (name, cap), port in zip(caps, ports):
+        left = None
+        if args.deadline > 0:  # rank 0's clock decides every rank's cap (the ranks' phase processes must agree)
+            left = args.deadline - (time.time() - t_start) - reserve
+            if name == "selfplay":
+                left = max(left, 60.0)
+            if world > 1:
+                box = [left]
+                dist.broadcast_object_list(box, src=0)
+                left = box[0]
+            cap = min(cap, left)
+        if left is not None and left < MIN_PHASE_S:  # too little of the deadline left: skipped, its keys say so
+            every = [{"status": "skipped: %.0f s of the %.0f s deadline left" % (max(left, 0.0), args.deadline),
+                      "seconds": 0.0}] * world
+            if rank == 0:
+                phases[name] = {"ranks": every, "cap_s": 0.0}
+                log("phase %s: skipped (deadline)" % name)
+                err = {"error": "phase %s skipped: %s" % (name, every[0]["status"]), "n_gpus": world}
+                for k in phase_keys(name, args):
+                    out[k] = err
+            continue
         env = dict(os.environ, **{PHASE_ENV: name})
         if port is not None:
             env["MASTER_PORT"] = str(port)
@@ -1077,7 +1108,7 @@ def orchestrate(args, argv, rank, world, script=None):
         if rank == 0:
             frag = _parse_fragment(text)
             failed = [i for i, e in enumerate(every) if e["status"] != "ok"]
-            phases[name] = {"ranks": every, "cap_s": cap}
+            phases[name] = {"ranks": every, "cap_s": round(cap, 1)}
             log("phase %s: %s" % (name, ", ".join("rank %d %s (%.1f s)" % (i, e["status"], e["seconds"])
                                                   for i, e in enumerate(every))))
             if name == "selfplay":
@@ -1098,8 +1129,10 @@ def orchestrate(args, argv, rank, world, script=None):
                     for k in phase_keys(name, args):  # rank 0's numbers, if any, kept but flagged
                         out[k] = dict((frag or {}).get(k) or {}, **err)
     if rank == 0:
-        out["phases"] = {"isolated": True, "detail": phases,
-                         "note": "each phase ran as fresh rank processes with a wall-time cap (bench.orchestrate)"}
+        out["phases"] = {"isolated": True, "detail": phases, "deadline_s": args.deadline,
+                         "seconds": round(time.time() - t_start, 1),
+                         "note": "each phase ran as fresh rank processes with a wall-time cap (bench.orchestrate), "
+                                 "the caps shrunk to what the deadline left"}
         if world == 1 and not args.no_cpu_baseline and args.net == "hip":
             log("cpu baseline (bounded sample ~%.0f s)..." % args.cpu_baseline_sec)
             out["cpu_baseline"] = cpu_baseline(args)

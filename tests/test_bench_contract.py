@@ -277,3 +277,93 @@ def test_isolated_phases_with_one_gpu(tmp_path, capsys):
     d = json.loads([l for l in capsys.readouterr().out.splitlines() if l.startswith("{")][-1])
     assert d["value"] == 10.0 and d["trainer"] == {"value": 3.0} and "loop_c4" not in d
     assert set(d["phases"]["detail"]) == {"selfplay", "extras", "trainer"}
+
+
+_PHASE_CHILD_8 = r'''
+import json, os, sys, time
+phase, rank = os.environ["GMZ_BENCH_PHASE"], int(os.environ.get("RANK", "0"))
+world = int(os.environ.get("WORLD_SIZE", "1"))
+frag = {"selfplay": {"metric": "m", "value": 100.0, "world": world},
+        "extras": {"sublines": {"c1": {"value": 1.0}}, "worker": {"value": 2.0}},
+        "trainer": {"trainer": {"value": 3.0}}, "loop": {"loop_c4": {"moves_per_s": 4.0}}}[phase]
+hang, fail = os.environ.get("T_HANG", ""), os.environ.get("T_FAIL", "")
+if hang == "%s:%d" % (phase, rank):
+    time.sleep(300)                  # a rank stuck in the phase: killed at the (deadline-shrunk) cap
+if fail == "%s:%d" % (phase, rank):
+    sys.exit(3)                      # a rank whose phase fails
+if fail.startswith(phase + ":"):
+    time.sleep(300)                  # its peers, waiting in a collective: stopped by the failure flag
+if rank == 0:
+    print("GMZ_PHASE_RESULT " + json.dumps(frag), flush=True)
+'''
+
+_PHASE_PARENT_N = r'''
+import os, sys
+sys.path.insert(0, %r)
+import bench
+N = %d
+argv = %r
+if "RANK" not in os.environ:
+    sys.exit(bench.spawn_ranks(N, [], script=os.path.abspath(__file__)))
+args = bench.parse(argv)
+sys.exit(bench.orchestrate(args, argv, int(os.environ["RANK"]), N, script=%r))
+'''
+
+
+def _run_orchestrated(tmp_path, n, argv, hang, fail, timeout):
+    import json
+    import subprocess
+    import time
+    child = tmp_path / "child8.py"
+    child.write_text(_PHASE_CHILD_8)
+    parent = tmp_path / ("parent%d.py" % n)
+    parent.write_text(_PHASE_PARENT_N % (REPO, n, argv, str(child)))
+    env = dict(os.environ, T_HANG=hang, T_FAIL=fail)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT", "MASTER_ADDR"):
+        env.pop(k, None)
+    t0 = time.time()
+    p = subprocess.Popen([sys.executable, str(parent)], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                         text=True, start_new_session=True)
+    try:
+        out, err = p.communicate(timeout=timeout)
+    finally:
+        if p.poll() is None:
+            os.killpg(p.pid, 9)  # this test's own process group (the spawned ranks and phases with it)
+            out, err = p.communicate()
+    assert p.returncode == 0, err[-3000:]
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out
+    return json.loads(lines[0]), time.time() - t0
+
+
+def test_eight_rank_orchestration_inside_the_deadline(tmp_path):
+    """VERDICT r4 item 4: the driver's first N = 8 line.  Eight rank processes (gloo), scripted phases: rank 3
+    hangs in the trainer phase (killed at its cap), rank 5 fails in the loop phase (its seven peers, stuck in
+    a collective, are stopped by the store flag).  The one line arrives inside --deadline with the headline
+    of all 8 ranks' phase intact, the extras merged, and `phases` naming both failures."""
+    argv = ["--gpus", "8", "--deadline", "90", "--phase-timeout-trainer", "8", "--sublines", "c1",
+            "--worker-moves", "1"]
+    d, took = _run_orchestrated(tmp_path, 8, argv, "trainer:3", "loop:5", 200)
+    assert d["value"] == 100.0 and d["world"] == 8
+    assert d["sublines"] == {"c1": {"value": 1.0}} and d["worker"] == {"value": 2.0}
+    det = d["phases"]["detail"]
+    assert len(det["selfplay"]["ranks"]) == 8 and all(r["status"] == "ok" for r in det["selfplay"]["ranks"])
+    assert det["trainer"]["ranks"][3]["status"].startswith("timeout")
+    assert "error" in d["trainer"] and "rank 3 timeout" in d["trainer"]["error"]
+    assert det["loop"]["ranks"][5]["status"] == "exit 3"
+    assert all(r["status"].startswith("stopped") for i, r in enumerate(det["loop"]["ranks"]) if i != 5)
+    assert "error" in d["loop_c4"] and "rank 5 exit 3" in d["loop_c4"]["error"]
+    assert all(p["cap_s"] <= 90 for p in det.values())  # each cap = at most what the deadline had left
+    assert d["phases"]["seconds"] <= 90 and took < 120
+
+
+def test_deadline_shrinks_a_later_phase_and_skips_the_rest(tmp_path):
+    """--deadline: a hung trainer phase is killed at what the deadline leaves (not its own 150 s cap), and the
+    loop phase, with less than 15 s left, is skipped with an error in its keys; the line still arrives in time."""
+    argv = ["--gpus", "2", "--deadline", "32", "--sublines", "c1", "--worker-moves", "1"]
+    d, took = _run_orchestrated(tmp_path, 2, argv, "trainer:1", "", 120)
+    det = d["phases"]["detail"]
+    assert d["value"] == 100.0
+    assert det["trainer"]["cap_s"] < 32 and det["trainer"]["ranks"][1]["status"].startswith("timeout")
+    assert det["loop"]["ranks"][0]["status"].startswith("skipped") and "skipped" in d["loop_c4"]["error"]
+    assert d["phases"]["seconds"] <= 32 + 5 and took < 60
