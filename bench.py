@@ -93,11 +93,13 @@ PEAK_MFMA_TFLOPS = 2500.0   # MI355X dense f16 / bf16 MFMA (MI355X_MICROARCH.md,
 PEAK_HBM_GBS = 8000.0
 
 
-def pmc_traffic(path, args, G, az, streams):
+def pmc_traffic(path, args, G, az, streams, size=None, blocks=None):
     """HBM bytes per launch from a committed PMC summary (tools/gpu.sh pmc -> tools/pmc_summary.py) when it
-    was measured on this configuration (15x15, 8 blocks, MuZero, G = 1024, same precision and the same
-    number of streams as this run resolved to)."""
-    if not os.path.exists(path) or (args.size, args.blocks, G) != (15, 8, 1024) or az:
+    was measured on this configuration (15x15, 8 blocks, MuZero, the same games per GPU — 1,024 unless the
+    summary says otherwise —, precision and number of streams as this run resolved to)."""
+    size = args.size if size is None else size
+    blocks = args.blocks if blocks is None else blocks
+    if not os.path.exists(path) or (size, blocks) != (15, 8) or az:
         return None
     try:
         pm = json.load(open(path))
@@ -105,7 +107,12 @@ def pmc_traffic(path, args, G, az, streams):
         return None
     if pm.get("precision", "bf16") != args.precision or int(pm.get("streams", 1)) != int(streams or 1):
         return None
+    if int(pm.get("games", 1024)) != int(G):
+        return None
     return pm.get("hbm_bytes_per_launch")
+
+
+PMC_TREE_G8192 = os.path.join(REPO, "profiles", "pmc_tree_g8192.json")  # the g8192 sub-line's PMC pass
 
 
 def log(*a):
@@ -628,12 +635,18 @@ def selfplay_leg(args, rank, world, dist, backend, size, sims, mode, blocks, G, 
         A = size * size
         bpl = tree_bytes(ctr, A) / n_tree
         gbs = bpl * n_tree / (busy_tree * 1e-3) / 1e9 if busy_tree > 0 else 0.0
-        is_c2 = (size, blocks, G, mode) == (15, 8, 1024, "MuZero")
-        tr = pmc_traffic(args.pmc_tree_file, args, G, az, streams) if is_c2 else None
+        tfile = {1024: args.pmc_tree_file, 8192: PMC_TREE_G8192}.get(G)
+        tr = (pmc_traffic(tfile, args, G, az, streams, size, blocks)
+              if (tfile and (size, blocks, mode) == (15, 8, "MuZero")) else None)
+        # the same rate on the kernel's MEASURED bytes (PMC FETCH_SIZE x2 + WRITE_SIZE per launch, committed
+        # pass of this configuration) in place of the SURVEY 8(d) model's: the lists move fewer bytes than the
+        # model counts, the dense hint kernel more (its cached exp rows)
+        gbs_m = tr * n_tree / (busy_tree * 1e-3) / 1e9 if (tr and busy_tree > 0) else None
         res["roofline_tree"] = {
             "bound": "hbm", "kernel": "k_expand_select<%d> (backup of wave i + selection of wave i+1)" % ((A + 63) // 64),
             "achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS,
-            "traffic": tr, "traffic_source": (traffic_note % os.path.relpath(args.pmc_tree_file, REPO)) if tr else None,
+            "achieved_measured": gbs_m, "frac_measured": gbs_m / PEAK_HBM_GBS if gbs_m else None,
+            "traffic": tr, "traffic_source": (traffic_note % os.path.relpath(tfile, REPO)) if tr else None,
             "launches": n_tree, "mean_launch_ms": ms_tree, "bytes_per_launch": bpl,
             "mean_backup_levels": ctr["backup_levels"] / max(1, ctr["backups"]),
             "mean_select_levels": ctr["select_levels"] / max(1, ctr["selects"]),
@@ -734,7 +747,8 @@ def subline(args, key, rank, world, dist, backend):
         if k in r:
             q = r[k]
             out[k] = {x: q[x] for x in ("kernel", "achieved", "unit", "frac", "mean_launch_ms", "bytes_per_launch",
-                                        "layout", "games_per_launch", "mean_select_levels") if x in q}
+                                        "layout", "games_per_launch", "mean_select_levels", "traffic",
+                                        "achieved_measured", "frac_measured", "traffic_source") if x in q}
     return out
 
 
