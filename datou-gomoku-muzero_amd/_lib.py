@@ -75,6 +75,8 @@ _SIGS = {
     "gmz_bn_backward_stats": ([I, P, P, P, P, I, I, I, P, P, I, P, P, P, P, P, I, P, P, I], I),
     "gmz_grad_add_t": ([I, P, I, I, I, P, P], I),
     "gmz_bn_forward_stats": ([I, P, P, I, I, I, P, P, ctypes.c_float, ctypes.c_float, P, P, P, I, P, P, P, I, P], I),
+    "gmz_bn_forward_seg": ([I, P, P, P, I, I, I, I, P, P, ctypes.c_float, ctypes.c_float, P, P, P, I, P, P, P, P, P], I),
+    "gmz_conv3x3_forward_board_stats": ([I, I, P, P, P, I, P, P, P], I),
 }
 
 # symbols added by the network kernels (declared in include/gmz.h too)

@@ -109,7 +109,10 @@ struct BnBwd {
 // BWD: the epilogue's statistics are the BatchNorm BACKWARD sums of the output taken as that BN's output
 // gradient dy — sum dz and sum dz * xhat, dz = dy * [y > 0], xhat = (x - mean) * invstd (what k_bnl_red<.., 1, ..>
 // reduces in a pass of its own) — instead of the forward sums of the output.
-template <int H, typename T, int PG, int HALVES = 1, bool BWD = false>
+// PB: the statistics partials per BOARD (stats [C][N][3], slot = board) instead of per workgroup, so a
+// consumer can take them over any board ranges: the trainer's batched consistency trunk (five unroll steps'
+// observations as one launch, each step's BatchNorm statistics over its own boards; gmz_bn_forward_seg).
+template <int H, typename T, int PG, int HALVES = 1, bool BWD = false, bool PB = false>
 __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restrict__ x, const uint16_t *__restrict__ wpk,
                                                   uint16_t *__restrict__ y, int N, const uint8_t *__restrict__ mask,
                                                   double *__restrict__ stats, const uint16_t *__restrict__ addend,
@@ -123,6 +126,8 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
   static_assert(CKSTEPS % RD == 0, "ring slots repeat per item");
   __shared__ __attribute__((aligned(16))) uint8_t img[I::BYTES];
   static_assert(I::BYTES >= PG * 64 * 2 * 4, "stats scratch fits in the image");
+  static_assert(!PB || (HALVES == 1 && !BWD), "per-board statistics: forward sums, one half per workgroup");
+  __shared__ float pbred[PB ? PG * 64 * 2 : 1];  // PB: [PG][64 channels of this half][2], per board
 
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int nq = w & 1, pg = w >> 1;
@@ -285,6 +290,43 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
       }
     }
     }  // halves
+    if constexpr (PB) {  // this board's partials -> slot b, then the accumulators restart
+      if (stats) {
+#pragma unroll
+        for (int nt = 0; nt < NTW; ++nt)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) {
+              s1[0][nt][e] += __shfl_xor(s1[0][nt][e], o, 64);
+              s2[0][nt][e] += __shfl_xor(s2[0][nt][e], o, 64);
+            }
+        if ((lane & 15) == 0) {
+#pragma unroll
+          for (int nt = 0; nt < NTW; ++nt)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int cl = (nq * NTW + nt) * 16 + g4 * 4 + e;
+              pbred[(pg * 64 + cl) * 2] = s1[0][nt][e];
+              pbred[(pg * 64 + cl) * 2 + 1] = s2[0][nt][e];
+              s1[0][nt][e] = s2[0][nt][e] = 0.f;
+            }
+        }
+        __syncthreads();
+        if (tid < 64) {
+          double a = 0.0, q = 0.0;
+#pragma unroll
+          for (int g = 0; g < PG; ++g) {
+            a += (double)pbred[(g * 64 + tid) * 2];
+            q += (double)pbred[(g * 64 + tid) * 2 + 1];
+          }
+          double *out = stats + ((size_t)(half0 * 64 + tid) * N + b) * 3;  // channel-major [C][N][3]
+          out[0] = a;
+          out[1] = q;
+          out[2] = counted ? (double)A : 0.0;
+        }
+      }
+    }
     if (HALVES == 2)  // the next board's first k-steps for half 0 (the ring holds half 1's)
 #pragma unroll
       for (int k = 0; k < RD - 1; ++k) {
@@ -293,7 +335,7 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
       }
     __syncthreads();  // every wave is done reading the image before the next board's DMA
   }
-  if (!stats) return;
+  if (!stats || PB) return;
 #pragma unroll
   for (int hh = 0; hh < HALVES; ++hh) {
   const int half = HALVES == 2 ? hh : half0;
@@ -532,18 +574,24 @@ int conv3_grid(int N) {  // a multiple of 16 (whole XCD pairs; workgroups past t
 // statistics slots (partials) of gmz_conv3x3_forward_stats: one per board pair of workgroups, or per workgroup
 int conv3_stats_slots(int N) { return conv_halves() == 2 ? conv3_grid(N) : conv3_grid(N) / 2; }
 
-template <int H, typename T, int HV, bool BWD>
+template <int H, typename T, int HV, bool BWD, bool PB = false>
 void launch_conv3_k(const void *x, const void *wpk, void *y, int N, const uint8_t *mask, double *stats, const void *addend,
                     const BnBwd &bn, hipStream_t st) {
-  hipLaunchKernelGGL((k_conv3<H, T, CONV_PG, HV, BWD>), dim3(conv3_grid(N)), dim3(128 * CONV_PG), 0, st,
+  // per-board statistics: two workgroups per board (one per half), never the one-workgroup-per-board A/B
+  const int grid = PB ? (int)((2L * N + 15) / 16 * 16 < 2L * 2 * cu_count_conv() / 16 * 16 ? (2L * N + 15) / 16 * 16
+                                                                                             : 2L * 2 * cu_count_conv() / 16 * 16)
+                      : conv3_grid(N);
+  hipLaunchKernelGGL((k_conv3<H, T, CONV_PG, HV, BWD, PB>), dim3(grid), dim3(128 * CONV_PG), 0, st,
                      (const uint16_t *)x, (const uint16_t *)wpk, (uint16_t *)y, N, mask, stats, (const uint16_t *)addend, bn);
 }
 
 template <int H, typename T>
 int launch_conv3(const void *x, const void *wpk, void *y, int N, const uint8_t *mask, double *stats, const void *addend,
-                 const BnBwd &bn, hipStream_t st) {
+                 const BnBwd &bn, hipStream_t st, bool per_board = false) {
   const bool bwd = bn.x != nullptr;
-  if (conv_halves() == 2) {
+  if (per_board) {
+    launch_conv3_k<H, T, 1, false, true>(x, wpk, y, N, mask, stats, addend, bn, st);
+  } else if (conv_halves() == 2) {
     if (bwd) launch_conv3_k<H, T, 2, true>(x, wpk, y, N, mask, stats, addend, bn, st);
     else launch_conv3_k<H, T, 2, false>(x, wpk, y, N, mask, stats, addend, bn, st);
   } else {
@@ -556,10 +604,10 @@ int launch_conv3(const void *x, const void *wpk, void *y, int N, const uint8_t *
 
 template <typename T>
 int conv3_dispatch(int H, const void *x, const void *wpk, void *y, int N, const uint8_t *mask, double *stats, const void *addend,
-                   hipStream_t st, const BnBwd &bn = BnBwd{}) {
+                   hipStream_t st, const BnBwd &bn = BnBwd{}, bool per_board = false) {
   switch (H) {
-    case 9: return launch_conv3<9, T>(x, wpk, y, N, mask, stats, addend, bn, st);
-    case 15: return launch_conv3<15, T>(x, wpk, y, N, mask, stats, addend, bn, st);
+    case 9: return launch_conv3<9, T>(x, wpk, y, N, mask, stats, addend, bn, st, per_board);
+    case 15: return launch_conv3<15, T>(x, wpk, y, N, mask, stats, addend, bn, st, per_board);
   }
   return fail("gmz_conv3x3: board size must be 9 or 15");
 }
@@ -616,6 +664,18 @@ GMZ_EXPORT int gmz_conv3x3_forward_stats(int dtype, int H, const void *x, const 
   if (dtype == 1) return conv3_dispatch<__half>(H, x, packed, y, N, mask, stats, nullptr, st);
   if (dtype == 2) return conv3_dispatch<__hip_bfloat16>(H, x, packed, y, N, mask, stats, nullptr, st);
   return fail("gmz_conv3x3_forward: dtype must be 1 (f16) or 2 (bf16)");
+}
+
+GMZ_EXPORT int gmz_conv3x3_forward_board_stats(int dtype, int H, const void *x, const void *packed, void *y, int N,
+                                               const uint8_t *mask, double *stats, void *stream) {
+  if (!x || !packed || !y || !stats) return fail("gmz_conv3x3_forward_board_stats: null operand");
+  if (N <= 0) return fail("gmz_conv3x3_forward_board_stats: N must be positive");
+  if (((uintptr_t)x | (uintptr_t)packed | (uintptr_t)y) & 15)
+    return fail("gmz_conv3x3_forward_board_stats: operands must be 16-B aligned");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == 1) return conv3_dispatch<__half>(H, x, packed, y, N, mask, stats, nullptr, st, BnBwd{}, true);
+  if (dtype == 2) return conv3_dispatch<__hip_bfloat16>(H, x, packed, y, N, mask, stats, nullptr, st, BnBwd{}, true);
+  return fail("gmz_conv3x3_forward_board_stats: dtype must be 1 (f16) or 2 (bf16)");
 }
 
 GMZ_EXPORT int gmz_conv3x3_forward(int dtype, int H, const void *x, const void *packed, void *y, int N, void *stream) {

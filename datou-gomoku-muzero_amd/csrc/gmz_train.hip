@@ -158,6 +158,66 @@ __global__ void __launch_bounds__(WAVE * FIN_MAX_WAVES) k_bn_finalize(const doub
   }
 }
 
+// the forward finalisation of nseg row segments (gmz_bn_forward_seg): per channel, segment g's statistics from
+// its sps partial slots [g * sps, (g + 1) * sps) -> save[g] = (mean, invstd), and the running statistics updated
+// by the segments in order, exactly as nseg BatchNorm calls one after the other (a segment with no valid row is
+// skipped, like a call on an empty mask)
+__global__ void __launch_bounds__(WAVE * FIN_MAX_WAVES) k_bn_finalize_seg(const double *__restrict__ ws, int C, int nseg,
+                                                                          int sps, float eps, float momentum,
+                                                                          float *save, float *running_mean,
+                                                                          float *running_var, int64_t *num_batches) {
+  const int c = blockIdx.x, nt = blockDim.x, ns = nseg * sps;
+  __shared__ double red[FIN_MAX_WAVES][3];
+  float rm = running_mean ? running_mean[c] : 0.f, rv = running_var ? running_var[c] : 0.f;
+  int live = 0;
+  for (int g = 0; g < nseg; ++g) {
+    double a = 0.0, b = 0.0, n = 0.0;
+#pragma unroll 2
+    for (int t = g * sps + threadIdx.x; t < (g + 1) * sps; t += nt) {
+      const double *p = ws + ((size_t)c * ns + t) * 3;
+      a += p[0];
+      b += p[1];
+      n += p[2];
+    }
+    a = wave_sum_d(a);
+    b = wave_sum_d(b);
+    n = wave_sum_d(n);
+    const int w = threadIdx.x / WAVE;
+    if ((threadIdx.x & (WAVE - 1)) == 0) {
+      red[w][0] = a;
+      red[w][1] = b;
+      red[w][2] = n;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int i = 1; i < nt / WAVE; ++i) {
+        a += red[i][0];
+        b += red[i][1];
+        n += red[i][2];
+      }
+      const double nn = n > 0.0 ? n : 1.0;
+      const double m = a / nn;
+      double v = b / nn - m * m;
+      v = v > 0.0 ? v : 0.0;
+      const float mean = (float)m, var_b = (float)v;
+      save[(size_t)g * 2 * C + c] = mean;
+      save[(size_t)g * 2 * C + C + c] = 1.0f / sqrtf(var_b + eps);
+      if (n > 0.0) {
+        const float unb = (float)(v * n / (n > 1.0 ? n - 1.0 : 1.0));
+        rm = (1.0f - momentum) * rm + momentum * mean;
+        rv = (1.0f - momentum) * rv + momentum * unb;
+        ++live;
+      }
+    }
+    __syncthreads();  // red is reused by the next segment
+  }
+  if (threadIdx.x == 0 && running_mean) {
+    running_mean[c] = rm;
+    running_var[c] = rv;
+    if (c == 0 && num_batches) num_batches[0] += live;
+  }
+}
+
 template <typename T>
 __global__ void __launch_bounds__(BN_THREADS) k_bn_apply(const T *__restrict__ x, const T *__restrict__ res, int B,
                                                          int C, int S, const float *__restrict__ gamma,
@@ -263,19 +323,22 @@ __device__ __forceinline__ void stv(T *p, size_t k, const float *a) {
 
 constexpr int BNL_MAX_SPLITS = 512;
 
-// stats (BWD = 0) or dz sums (BWD = 1) of the masked pixels of workgroup t's pixel range
+// stats (BWD = 0) or dz sums (BWD = 1) of the masked pixels of workgroup t's pixel range.  nseg > 1: the B rows
+// are nseg equal segments (gmz_bn_forward_seg) and the ns = gridDim.x splits nseg equal groups, split group g
+// covering segment g only, so the partials of slots [g * ns / nseg, (g + 1) * ns / nseg) are segment g's
 template <typename T, int BWD, int V>
 __global__ void __launch_bounds__(BN_THREADS) k_bnl_red(const T *__restrict__ x, const T *__restrict__ y,
                                                         const T *__restrict__ dy, const uint8_t *__restrict__ mask,
                                                         int B, int C, int S, const float *__restrict__ save, int relu,
-                                                        double *__restrict__ ws) {
+                                                        double *__restrict__ ws, int nseg = 1) {
   __shared__ float red[BN_THREADS * V * 2];  // [group][2][C]
   const int t = blockIdx.x, ns = gridDim.x;
   const int tpp = C / V, pl = BN_THREADS / tpp;
   const int cp = threadIdx.x % tpp, grp = threadIdx.x / tpp;
   const int c = V * cp;
-  const long P = (long)B * S;
-  const long p0 = P * t / ns, p1 = P * (t + 1) / ns;
+  const int nsps = ns / nseg, sg = t / nsps, tl = t - sg * nsps;
+  const long Ps = (long)(B / nseg) * S, pb = Ps * sg;
+  const long p0 = pb + Ps * tl / nsps, p1 = pb + Ps * (tl + 1) / nsps;
   float a[V], q[V], m[V], is[V];
 #pragma unroll
   for (int j = 0; j < V; ++j) {
@@ -363,15 +426,18 @@ __global__ void __launch_bounds__(BN_THREADS) k_bnl_red(const T *__restrict__ x,
 
 // elementwise passes: a thread keeps its V channels' constants in registers and strides over
 // positions (pl positions per block step, grid-stride over the B*S positions)
+// grid.y = segments (gmz_bn_forward_seg): segment g's positions [g * Pseg, (g + 1) * Pseg) with its own save[g]
 template <typename T, int V>
 __global__ void __launch_bounds__(BN_THREADS) k_bnl_apply(const T *__restrict__ x, const T *__restrict__ res,
-                                                          long P, int C, const float *__restrict__ gamma,
+                                                          long Pseg, int C, const float *__restrict__ gamma,
                                                           const float *__restrict__ beta, int relu,
                                                           T *__restrict__ y, const float *__restrict__ save) {
   const int tpp = C / V, pl = BN_THREADS / tpp;
   const int cp = threadIdx.x % tpp, grp = threadIdx.x / tpp;
   if (grp >= pl) return;
   const int c = V * cp;
+  save += (size_t)blockIdx.y * 2 * C;
+  const long pbeg = Pseg * blockIdx.y, P = pbeg + Pseg;
   float sc[V], sh[V];
 #pragma unroll
   for (int j = 0; j < V; ++j) {
@@ -381,7 +447,7 @@ __global__ void __launch_bounds__(BN_THREADS) k_bnl_apply(const T *__restrict__ 
   float mean[V];
 #pragma unroll
   for (int j = 0; j < V; ++j) mean[j] = save[c + j];
-  for (long p = (long)blockIdx.x * pl + grp; p < P; p += (long)gridDim.x * pl) {
+  for (long p = pbeg + (long)blockIdx.x * pl + grp; p < P; p += (long)gridDim.x * pl) {
     const size_t k = (size_t)p * C + c;
     float v[V], r[V];
     ldv<T, V>(x, k, v);
@@ -609,6 +675,42 @@ int bn_forward_stats(const void *x, const void *res, int B, int C, int S, const 
   return 0;
 }
 
+// training-mode forward of nseg equal row segments at once, channels-last: each segment's statistics over its own
+// masked rows (per-board conv partials board_stats [C][B][3] when given, else a reduction pass with the splits
+// grouped by segment), save [nseg][2][C], the running statistics updated segment after segment
+template <typename T>
+int bn_forward_seg(const void *x, const void *res, const uint8_t *mask, int B, int nseg, int C, int S, const float *gamma,
+                   const float *beta, float eps, float momentum, float *rm, float *rv, int64_t *nb, int relu, void *y,
+                   float *save, void *ws, const double *board_stats, hipStream_t st) {
+  const int V = nhwc_vec(C, sizeof(T), {x, res, y});
+  const double *parts = board_stats;
+  int sps = B / nseg;
+  if (!board_stats) {
+    sps = splits_for(B, C, S, 1) / nseg;
+    if (sps < 1) sps = 1;
+    if (V == 8)
+      hipLaunchKernelGGL((k_bnl_red<T, 0, 8>), dim3(nseg * sps), dim3(BN_THREADS), 0, st, (const T *)x, (const T *)nullptr,
+                         (const T *)nullptr, mask, B, C, S, (const float *)nullptr, 0, (double *)ws, nseg);
+    else
+      hipLaunchKernelGGL((k_bnl_red<T, 0, 2>), dim3(nseg * sps), dim3(BN_THREADS), 0, st, (const T *)x, (const T *)nullptr,
+                         (const T *)nullptr, mask, B, C, S, (const float *)nullptr, 0, (double *)ws, nseg);
+    GMZ_LAUNCH_CHECK();
+    parts = (const double *)ws;
+  }
+  hipLaunchKernelGGL(k_bn_finalize_seg, dim3(C), dim3(WAVE * FIN_MAX_WAVES), 0, st, parts, C, nseg, sps, eps, momentum,
+                     save, rm, rv, nb);
+  GMZ_LAUNCH_CHECK();
+  const long Ps = (long)(B / nseg) * S;
+  if (V == 8)
+    hipLaunchKernelGGL((k_bnl_apply<T, 8>), dim3(elementwise_blocks(Ps, C, 8), nseg), dim3(BN_THREADS), 0, st,
+                       (const T *)x, (const T *)res, Ps, C, gamma, beta, relu, (T *)y, (const float *)save);
+  else
+    hipLaunchKernelGGL((k_bnl_apply<T, 2>), dim3(elementwise_blocks(Ps, C, 2), nseg), dim3(BN_THREADS), 0, st,
+                       (const T *)x, (const T *)res, Ps, C, gamma, beta, relu, (T *)y, (const float *)save);
+  GMZ_LAUNCH_CHECK();
+  return 0;
+}
+
 // eval mode: save = (running_mean, 1/sqrt(running_var + eps))
 __global__ void k_bn_eval_save(const float *__restrict__ rm, const float *__restrict__ rv, int C, float eps,
                                float *__restrict__ save) {
@@ -744,6 +846,27 @@ GMZ_EXPORT int gmz_bn_backward(int dtype, int layout, const void *x, const void 
                                int relu, void *dx, void *dres, float *dgamma, float *dbeta, void *ws, void *stream) {
   return gmz_bn_backward_acc(dtype, layout, x, y, dy, mask, B, C, S, gamma, save, relu, dx, dres, dgamma, dbeta, ws,
                              stream, 0);
+}
+
+GMZ_EXPORT int gmz_bn_forward_seg(int dtype, const void *x, const void *res, const uint8_t *mask, int B, int nseg, int C,
+                                  int S, const float *gamma, const float *beta, float eps, float momentum,
+                                  float *running_mean, float *running_var, int64_t *num_batches, int relu, void *y,
+                                  float *save, void *ws, const double *board_stats, void *stream) {
+  if (B <= 0 || C <= 0 || S <= 0 || nseg <= 0 || B % nseg || (size_t)B * C * S >= (1ull << 31))
+    return fail("gmz_bn_forward_seg: bad shape (B must be a multiple of nseg)");
+  if (check_layout(1, C)) return -1;
+  if (!x || !y || !gamma || !beta || !save || !ws) return fail("gmz_bn_forward_seg: null operand");
+  if ((running_mean == nullptr) != (running_var == nullptr)) return fail("gmz_bn_forward_seg: running stats pair");
+  hipStream_t st = (hipStream_t)stream;
+  switch (dtype) {
+    case 0: return bn_forward_seg<float>(x, res, mask, B, nseg, C, S, gamma, beta, eps, momentum, running_mean,
+                                         running_var, num_batches, relu, y, save, ws, board_stats, st);
+    case 1: return bn_forward_seg<__half>(x, res, mask, B, nseg, C, S, gamma, beta, eps, momentum, running_mean,
+                                          running_var, num_batches, relu, y, save, ws, board_stats, st);
+    case 2: return bn_forward_seg<__hip_bfloat16>(x, res, mask, B, nseg, C, S, gamma, beta, eps, momentum, running_mean,
+                                                  running_var, num_batches, relu, y, save, ws, board_stats, st);
+  }
+  return fail("gmz_bn_forward_seg: dtype must be 0 (f32), 1 (f16) or 2 (bf16)");
 }
 
 GMZ_EXPORT int gmz_bn_eval(int dtype, int layout, const void *x, const void *res, int B, int C, int S,

@@ -104,8 +104,11 @@ def scalar_to_support(x, vmin, vmax, bins):
 
 
 # ------------------------------------------------------------------------------ network
-def _bn(mod, x, mask=None):
-    """BatchNorm whose training-mode statistics (and running-stat update) cover only the rows
+def _bn(mod, x, mask=None, segments=1):
+    """``segments`` > 1: x is that many equal row segments (the batched consistency representations), each
+    normalised with its own statistics and the running statistics updated segment after segment — exactly
+    ``segments`` calls one after the other.
+    BatchNorm whose training-mode statistics (and running-stat update) cover only the rows
     where ``mask`` is set.  The reference runs the unrolled steps on the sub-batch of games still
     in progress (loss.py:89-93); running every step on the FULL batch with row-masked statistics
     gives the same values and gradients with fixed shapes (MIOpen compiles each convolution once
@@ -113,6 +116,10 @@ def _bn(mod, x, mask=None):
     so a whole training step can be captured in one HIP graph.  ``mask``: bool [B].  Computed in
     float32 (as autocast runs BatchNorm).  A mask with no row set leaves the running statistics
     untouched (the reference skips such a step)."""
+    if segments > 1 and mod.training:
+        xs = x.chunk(segments)
+        ms = mask.chunk(segments) if mask is not None else [None] * segments
+        return torch.cat([_bn(mod, a, m) for a, m in zip(xs, ms)])
     if mask is None or not mod.training:
         return mod(x)
     if SUBBATCH_BN:  # diagnostics: the reference's own computation, native BatchNorm on the gathered live rows
@@ -284,10 +291,18 @@ def _bn_workspace(layout, B, C, S, device):
     return torch.empty((_WS_BYTES[key] + 7) // 8, dtype=torch.float64, device=device)
 
 
-def _bn_act(mod, x, mask=None, res=None, relu=True, link=None):
+def _bn_act(mod, x, mask=None, res=None, relu=True, link=None, segments=1):
     """relu?(BatchNorm(x) (+ res)) with row-masked training statistics (see ``_bn``).  Training-mode
     BatchNorm on the GPU runs the fused HIP kernels; eval mode and the CPU use PyTorch ops.  ``link``:
-    the block's _ResLink, used when ``res`` is the very tensor its first HIP conv consumed."""
+    the block's _ResLink, used when ``res`` is the very tensor its first HIP conv consumed.  ``segments``:
+    see ``_bn`` (no autograd: the batched consistency representations run under no_grad)."""
+    if segments > 1 and mod.training:
+        if FUSED_BN and x.is_cuda and x.dtype in _BN_DTYPES and _bn_layout(x) == 1 and not torch.is_grad_enabled():
+            return _bn_seg(mod, x, mask, res, relu, segments)
+        xs = x.chunk(segments)
+        ms = mask.chunk(segments) if mask is not None else [None] * segments
+        rs = res.chunk(segments) if res is not None else [None] * segments
+        return torch.cat([_bn_act(mod, a, m, r, relu) for a, m, r in zip(xs, ms, rs)])
     if FUSED_BN and mod.training and x.is_cuda and x.dtype in _BN_DTYPES:
         if res is not None:
             res = res.to(x.dtype)
@@ -304,6 +319,29 @@ def _bn_act(mod, x, mask=None, res=None, relu=True, link=None):
     if res is not None:
         y = y + res
     return F.relu(y) if relu else y
+
+
+def _bn_seg(mod, x, mask, res, relu, nseg):
+    """Training-mode BatchNorm (+ res, ReLU) of ``nseg`` equal row segments of a channels-last activation in one
+    pass (``gmz_bn_forward_seg``): segment statistics from the producing conv's per-board partials when it left
+    them (``_conv3_apply`` with segments), else one reduction pass; no autograd (no_grad callers only)."""
+    from . import _lib
+    B, C = x.shape[0], x.shape[1]
+    S = x[0, 0].numel()
+    if res is not None:
+        res = _like(res.to(x.dtype), 1)
+    y = torch.empty_like(x)
+    save = torch.empty(nseg * 2 * C, dtype=torch.float32, device=x.device)
+    ws = _bn_workspace(1, B, C, S, x.device)
+    st = getattr(x, "_gmz_bnstats", None)
+    board = st[0] if (st is not None and st[1] == "board") else None
+    m = None if mask is None else mask.contiguous().view(torch.uint8)
+    _lib.check(_lib.load().gmz_bn_forward_seg(_BN_DTYPES[x.dtype], _lib.ptr(x), _lib.ptr(res), _lib.ptr(m), B, nseg, C,
+                                              S, _lib.ptr(mod.weight), _lib.ptr(mod.bias), float(mod.eps),
+                                              float(mod.momentum), _lib.ptr(mod.running_mean), _lib.ptr(mod.running_var),
+                                              _lib.ptr(mod.num_batches_tracked), int(relu), _lib.ptr(y), _lib.ptr(save),
+                                              _lib.ptr(ws), _lib.ptr(board), _lib.stream_ptr()))
+    return y
 
 
 def _bn_eval(mod, x, res, relu):
@@ -586,13 +624,32 @@ def _conv3(cin, cout):
     return nn.Conv2d(cin, cout, 3, padding=1, bias=False)
 
 
-def _conv3_apply(conv, x, bn=None, mask=None, link=None):
+def _conv3_apply(conv, x, bn=None, mask=None, link=None, segments=1):
     """conv(x), on the HIP kernels when they cover the case (see ``_Conv3x3NHWC``).  ``bn``: the
     training-mode BatchNorm that consumes the output — the kernel's epilogue then also reduces its
-    (row-masked) statistics, attached to the output for ``_bn_act`` (no separate reduction pass)."""
+    (row-masked) statistics, attached to the output for ``_bn_act`` (no separate reduction pass).
+    ``segments`` > 1 (no_grad only): the statistics partials per board, for the segmented BatchNorm."""
     if (FUSED_CONV and x.is_cuda and x.dim() == 4 and x.shape[1] == 128 and x.shape[2] == x.shape[3]
             and x.shape[2] in (9, 15) and conv.weight.shape == (128, 128, 3, 3) and conv.bias is None):
         dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x.dtype
+        if (segments > 1 and dt in _CONV_DTYPES and x.is_contiguous(memory_format=torch.channels_last)
+                and not torch.is_grad_enabled()):
+            from . import _lib
+            xin = x.to(dt)
+            N = xin.shape[0]
+            y = torch.empty_like(xin, memory_format=torch.channels_last)
+            packed = _packed_conv_weight(conv.weight, dt, 0)
+            if bn is not None and bn.training and FUSED_BN:
+                st = torch.empty(128 * N * 3, dtype=torch.float64, device=x.device)
+                m = None if mask is None else mask.contiguous().view(torch.uint8)
+                _lib.check(_lib.load().gmz_conv3x3_forward_board_stats(_CONV_DTYPES[dt], xin.shape[2], _lib.ptr(xin),
+                                                                       _lib.ptr(packed), _lib.ptr(y), N, _lib.ptr(m),
+                                                                       _lib.ptr(st), _lib.stream_ptr()))
+                y._gmz_bnstats = (st, "board")
+            else:
+                _lib.check(_lib.load().gmz_conv3x3_forward(_CONV_DTYPES[dt], xin.shape[2], _lib.ptr(xin), _lib.ptr(packed),
+                                                           _lib.ptr(y), N, _lib.stream_ptr()))
+            return y
         if dt in _CONV_DTYPES and x.is_contiguous(memory_format=torch.channels_last):
             st = None
             if bn is not None and bn.training and FUSED_BN:
@@ -617,7 +674,12 @@ class _Block(nn.Module):
         self.conv1, self.bn1 = _conv3(c, c), nn.BatchNorm2d(c, eps=1e-4)
         self.conv2, self.bn2 = _conv3(c, c), nn.BatchNorm2d(c, eps=1e-4)
 
-    def forward(self, x, mask=None):
+    def forward(self, x, mask=None, segments=1):
+        if segments > 1:  # the batched consistency representations (no_grad): per-segment statistics
+            y = _bn_act(self.bn1, _conv3_apply(self.conv1, x, self.bn1, mask, segments=segments), mask,
+                        segments=segments)
+            return _bn_act(self.bn2, _conv3_apply(self.conv2, y, self.bn2, mask, segments=segments), mask, res=x,
+                           segments=segments)
         link = _ResLink() if (FUSED_RES_GRAD and torch.is_grad_enabled() and x.requires_grad) else None
         y = _bn_act(self.bn1, _conv3_apply(self.conv1, x, self.bn1, mask, link=link), mask)
         return _bn_act(self.bn2, _conv3_apply(self.conv2, y, self.bn2, mask), mask, res=x, link=link)
@@ -634,10 +696,10 @@ class _Trunk(nn.Module):
         self.conv, self.bn = _conv3(cin, c), nn.BatchNorm2d(c, eps=1e-4)
         self.resblocks = nn.Sequential(*[_Block(c) for _ in range(blocks)])
 
-    def forward(self, x, mask=None):
-        h = _bn_act(self.bn, self.conv(x), mask)
+    def forward(self, x, mask=None, segments=1):
+        h = _bn_act(self.bn, self.conv(x), mask, segments=segments)
         for blk in self.resblocks:
-            h = blk(h, mask)
+            h = blk(h, mask, segments) if segments > 1 else blk(h, mask)
         return h
 
 
@@ -802,9 +864,13 @@ class TrainNet(nn.Module):
 
     channels_last = False  # set by Trainer(channels_last=True): activations in NHWC memory format
 
-    def representation(self, obs, mask=None):
+    def representation(self, obs, mask=None, segments=1):
+        """``segments`` > 1 (no_grad): obs holds that many equal batches (each with its own BatchNorm statistics
+        and running-statistic update, in order): the five consistency representations as one pass."""
         if self.channels_last:
             obs = obs.contiguous(memory_format=torch.channels_last)
+        if segments > 1:
+            return self.representation_net(obs, mask, segments)
         return self.representation_net(obs, mask)
 
     def prediction(self, h, mask=None):
@@ -937,7 +1003,21 @@ TARGET_F16 = True
 # the unroll steps' cross-entropies and Barlow losses batched over the steps after the unroll (one call
 # each over the stacked [U, B, .] head outputs) instead of per step (False: per step, for A/B)
 BATCHED_LOSS = True
+# the five no-grad consistency representations of obs[1..U] (loss.py:102-104) as ONE trunk pass over the U*B
+# stacked boards, each step's BatchNorm statistics over its own live rows (segmented BatchNorm: per-board conv
+# statistics partials, one finalisation per layer, running statistics updated step after step as the reference's
+# five calls do): 16 conv launches of U*B boards instead of 80 of B, a fifth of the BatchNorm launches
+BATCHED_CONSISTENCY = True
 _SIDE_STREAMS = {}
+
+
+def consistency_representations(model, obs, masks):
+    """[representation(obs[:, s + 1], mask=masks[s]) for s < U] as one segmented pass (BATCHED_CONSISTENCY):
+    the same values as the U separate calls (per-step BatchNorm statistics; running statistics in step order)."""
+    U, B = len(masks), obs.shape[0]
+    o = obs[:, 1:U + 1].transpose(0, 1).reshape(U * B, *obs.shape[2:])  # step-major: segment s = step s
+    th = model.representation(o, mask=torch.stack(masks).reshape(U * B), segments=U)
+    return list(th.split(B))
 
 
 def _side_streams(device):
@@ -1000,13 +1080,22 @@ def muzero_loss(model, target_model, batch, is_weights, cfg, k=None, flip=None, 
             side[1].wait_stream(main)
             tru_h, tru_ev = [], []
             with torch.cuda.stream(side[1]), torch.no_grad():
-                for s in range(c.NUM_UNROLL_STEPS):
-                    tru_h.append(model.representation(obs[:, s + 1], mask=masks[s]))
+                if BATCHED_CONSISTENCY and c.NUM_UNROLL_STEPS > 1:
+                    tru_h = consistency_representations(model, obs, masks)
                     ev = torch.cuda.Event()
                     ev.record(side[1])
-                    tru_ev.append(ev)
+                    tru_ev = [ev] * c.NUM_UNROLL_STEPS
+                else:
+                    for s in range(c.NUM_UNROLL_STEPS):
+                        tru_h.append(model.representation(obs[:, s + 1], mask=masks[s]))
+                        ev = torch.cuda.Event()
+                        ev.record(side[1])
+                        tru_ev.append(ev)
             main.wait_stream(side[0])
             z.record_stream(main)
+        elif BATCHED_CONSISTENCY and c.NUM_UNROLL_STEPS > 1:  # one stream: the batched pass right after obs[0]'s
+            with torch.no_grad():
+                tru_h = consistency_representations(model, obs, [act[:, s] != -1 for s in range(c.NUM_UNROLL_STEPS)])
         pl, vl = model.prediction(h)
         lp = F.cross_entropy(pl.float(), pi[:, 0], reduction="none")
         # the support targets of every step in two calls (the per-step calls were ~10 tiny kernels each)
@@ -1039,7 +1128,9 @@ def muzero_loss(model, target_model, batch, is_weights, cfg, k=None, flip=None, 
                                                            reduction="none"), zero)
             dyn = model.project(hk, with_grad=True, mask=m)
             with torch.no_grad():
-                if tru_h is not None:
+                if tru_h is not None and side is None:
+                    tru = model.project(tru_h[s], with_grad=False, mask=m)
+                elif tru_h is not None:
                     main.wait_event(tru_ev[s])
                     tru_h[s].record_stream(main)
                     tru = model.project(tru_h[s], with_grad=False, mask=m)

@@ -316,6 +316,16 @@ int gmz_bn_backward_stats(int dtype, const void *x_dev, const void *y_dev, const
 /* Eval-mode BatchNorm (running statistics) + residual + ReLU, same layouts/dtypes as gmz_bn_forward:
  * y = relu?(gamma*(x-running_mean)/sqrt(running_var+eps) + beta (+ res)) — nn.BatchNorm2d/1d in eval()
  * (the target network's value of loss.py:54-55).  workspace_dev: gmz_bn_workspace_bytes bytes. */
+/* Training-mode channels-last BatchNorm (+ res, ReLU) of nseg equal row segments at once (the trainer's batched
+ * consistency representations, loss.py:102-104): segment g = rows [g B/nseg, (g+1) B/nseg), its statistics over
+ * its own masked rows, save_dev f32 [nseg][2][C] = per segment (mean, invstd), the running statistics updated by
+ * the segments in order (= nseg gmz_bn_forward calls).  board_stats_dev: per-board partials from
+ * gmz_conv3x3_forward_board_stats (f64 [C][B][3]) or NULL (a reduction pass).  workspace_dev:
+ * gmz_bn_workspace_bytes(1, B, C, S).  (ABI 8) */
+int gmz_bn_forward_seg(int dtype, const void *x_dev, const void *res_dev, const uint8_t *mask_dev, int B, int nseg,
+                       int C, int S, const float *gamma_dev, const float *beta_dev, float eps, float momentum,
+                       float *running_mean_dev, float *running_var_dev, int64_t *num_batches_dev, int relu, void *y_dev,
+                       float *save_dev, void *workspace_dev, const double *board_stats_dev, void *stream);
 int gmz_bn_eval(int dtype, int layout, const void *x_dev, const void *res_dev, int B, int C, int S, const float *gamma_dev,
                 const float *beta_dev, const float *running_mean_dev, const float *running_var_dev, float eps, int relu,
                 void *y_dev, void *workspace_dev, void *stream);
@@ -329,6 +339,10 @@ int gmz_bn_eval(int dtype, int layout, const void *x_dev, const void *res_dev, i
  * gmz_conv3x3_forward: x_dev, packed_dev and y_dev 16-B aligned, N >= 1. */
 int gmz_conv3x3_pack(int dtype, const float *w_dev, int64_t s0, int64_t s1, int64_t s2, int64_t s3, int transpose,
                      void *packed_dev, void *stream);
+/* gmz_conv3x3_forward_stats with the BatchNorm statistics partials per BOARD: stats_dev f64 [128][N][3] (sum,
+ * sum of squares, valid pixels of board n; 0 for a masked-out board), for gmz_bn_forward_seg.  (ABI 8) */
+int gmz_conv3x3_forward_board_stats(int dtype, int H, const void *x_dev, const void *packed_dev, void *y_dev, int N,
+                                    const uint8_t *mask_dev, double *stats_dev, void *stream);
 int gmz_conv3x3_forward(int dtype, int H, const void *x_dev, const void *packed_dev, void *y_dev, int N, void *stream);
 /* The same convolution plus an addend of the output's shape and dtype, rounded once:
  * y = round(conv(x, W) + addend).  The residual blocks' input gradient with the identity path's
