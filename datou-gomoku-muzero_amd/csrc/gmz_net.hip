@@ -177,7 +177,14 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
   using V8 = typename E::v8;
   // NB boards per workgroup at once (small boards): their NB x NPT position tiles form one tile
   // space, so each weight fragment a wave loads feeds NB times the MFMAs
-  constexpr int A = G::A, NPT = G::NPT, NPTB = NB * NPT;
+  constexpr int A = G::A, NPT = G::NPT;
+  // PACKED (small boards, NB > 1): the NB boards' positions form ONE run of NB*A positions cut into 16-position
+  // tiles, a tile straddling two boards (9x9: 162 positions in 11 tiles instead of 2 x 6 = 96 % fill instead of 84 %;
+  // 6x6: 5 tiles instead of 6).  Each lane addresses its own position's board image, and board b's image starts
+  // (b*A mod 16) 16-B slots later, so the bank slot of a position is its global index mod 16 across the board
+  // seam too: the straddling tile's B-fragment reads stay conflict-free
+  constexpr bool PACKED = NB > 1 && (NB * A + 15) / 16 < NB * NPT;
+  constexpr int NPTB = PACKED ? (NB * A + 15) / 16 : NB * NPT;
   constexpr int NW = NQ * PG, NTHR = 64 * NW;       // waves: NQ channel groups x PG position groups
   constexpr int NTW = 8 / NQ, PTW = (NPTB + PG - 1) / PG;  // n-tiles / position tiles per wave
   static_assert(8 % NQ == 0, "channel groups");
@@ -188,9 +195,25 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
   constexpr bool ONE = 2 * IMG + 2 * C * 4 + 9 * C * 4 > 163840;
   constexpr int NIMG = ONE ? 1 : 2, BB = NIMG * IMG;  // BB: LDS bytes per board (its images)
   static_assert(!ONE || NB == 1, "single-image boards run one board per workgroup");
-  static_assert(NB * BB + 2 * C * 4 + 9 * C * 4 <= 163840, "LDS budget");
-  __shared__ __attribute__((aligned(16))) uint8_t smem[NB * BB + 2 * C * 4 + 9 * C * 4];
-  float *sbias = (float *)(smem + NB * BB);  // [2][128] per-layer double buffer
+  constexpr int IMGS = NB * BB + (PACKED ? 256 : 0);  // the board images (+ the packed boards' slot offsets)
+  static_assert(IMGS + 2 * C * 4 + 9 * C * 4 <= 163840, "LDS budget");
+  __shared__ __attribute__((aligned(16))) uint8_t smem[IMGS + 2 * C * 4 + 9 * C * 4];
+  float *sbias = (float *)(smem + IMGS);  // [2][128] per-layer double buffer
+  // board b's image base (bytes): PACKED boards start (b*A mod 16) 16-B slots after b*BB
+  auto bbase = [](int b) { return b * BB + (PACKED ? ((b * A) & 15) * 16 : 0); };
+  // position tile pt, lane column l -> (board slot bsl, position p); p = A: past the boards
+  auto tile_pos = [](int pt, int l, int &bsl, int &p) {
+    if constexpr (PACKED) {
+      const int gp = pt * 16 + sigma16(l & 15);
+      bsl = gp / A;
+      p = gp - bsl * A;
+      if (bsl >= NB) { bsl = NB - 1; p = A; }
+    } else {
+      bsl = pt / NPT;
+      p = (pt - bsl * NPT) * 16 + sigma16(l & 15);
+      if (pt >= NPTB) { bsl = 0; p = A; }
+    }
+  };
   float *saction = sbias + 2 * C;             // DYN: [9][128]
 
   auto next_row = [&](int from) {
@@ -265,7 +288,7 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
   //      run are masked off
   auto issue_input = [&](int row, int bsl) {
     const uint8_t *src = (const uint8_t *)(t.pool + (size_t)t.in_slot[row] * A * C);
-    uint8_t *img0 = smem + bsl * BB;
+    uint8_t *img0 = smem + bbase(bsl);
     for (int j = w; j < H * I::RUN_DMA; j += NW) {
       const int y = j / I::RUN_DMA, piece = j % I::RUN_DMA;
       const int o = piece * 1024 + lane * 16;
@@ -301,7 +324,7 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
   };
 
   // ---- zero both images (borders and pads), biases of layer 0, action term
-  for (int i = tid; i < NB * BB / 16; i += NTHR) *(uint4 *)(smem + i * 16) = make_uint4(0, 0, 0, 0);
+  for (int i = tid; i < IMGS / 16; i += NTHR) *(uint4 *)(smem + i * 16) = make_uint4(0, 0, 0, 0);
   if (tid < C) sbias[tid] = t.bias[tid];
   if (tid < 2) s_cnt[tid] = 0;
   if (DYN)
@@ -316,9 +339,9 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
   int pos[PTW];
 #pragma unroll
   for (int i = 0; i < PTW; ++i) {
-    const int pt = pg + PG * i, bsl = pt / NPT, lt = pt - bsl * NPT;
-    const int p = lt * 16 + sigma16(lane & 15);
-    pos[i] = (pt < NPTB && p < A) ? bsl * BB + (p / H) * RS + (p % H) * PS : -1;
+    int bsl, p;
+    tile_pos(pg + PG * i, lane, bsl, p);
+    pos[i] = p < A ? bbase(bsl) + (p / H) * RS + (p % H) * PS : -1;
   }
   f32x4 acc[NTW][PTW];
   // ONE: this lane's residual tile values, [NTW][PTW][64 lanes] x 4 16-bit values per wave (same lane writes
@@ -396,9 +419,9 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
 #pragma unroll
         for (int nt = 0; nt < NTW; ++nt) acc[nt][i] = f32x4{0.f, 0.f, 0.f, 0.f};
         if (pg + PG * i >= NPTB) continue;
-        const int pt = pg + PG * i, bsl = pt / NPT;
+        int bsl, p;
+        tile_pos(pg + PG * i, ln, bsl, p);
         const float *ob = t.obs + (size_t)rr[bsl] * 3 * A;
-        const int p = (pt - bsl * NPT) * 16 + sigma16(ln & 15);
         const int y = p / H, x = p % H;
         V8 b;
 #pragma unroll
@@ -571,8 +594,8 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
           for (int i = 0; i < PTW; ++i) {
             f32x4 v = acc[nt][i];
             if constexpr (DYN && KIND == 0) {
-              const int pt = pg + PG * i, bsl = pt / NPT;
-              const int p = (pt - bsl * NPT) * 16 + sigma16(lane & 15);
+              int bsl, p;
+              tile_pos(pg + PG * i, lane, bsl, p);
               const int ddy = ay[bsl] - p / H + 1, ddx = ax[bsl] - p % H + 1;
               if (ddy >= 0 && ddy <= 2 && ddx >= 0 && ddx <= 2) v += *(const f32x4 *)(saction + (ddy * 3 + ddx) * C + n0);
             }
@@ -632,7 +655,7 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
     for (int b = 0; b < NB; ++b) {
     if (b > 0 && nrr[b] == nrr[b - 1]) break;  // a repeated row: already stored
     const int r = nrr[b], os = t.out_slot[r];
-    const uint8_t *fin = smem + b * BB + (ONE ? 0 : (t.n_layers & 1) * IMG);
+    const uint8_t *fin = smem + bbase(b) + (ONE ? 0 : (t.n_layers & 1) * IMG);
     if (!(ABL & 32)) {
       uint4 *dst = (uint4 *)(t.pool + (size_t)os * A * C);
       for (int i = tid; i < A * 16; i += NTHR) dst[i] = *(const uint4 *)(fin + cell(i >> 4) + (i & 15) * 16);
