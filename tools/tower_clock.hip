@@ -29,6 +29,13 @@ static void launch(TowerArgs a, int grid, unsigned long long gen) {
                      0, a);
 }
 
+// other wave decompositions of the same tower (A/B): NQ channel groups x PG position groups
+template <int ABL, int NQ, int PG, int RD>
+static void launch_dec(TowerArgs a, int grid, unsigned long long gen) {
+  a.gen = gen;
+  hipLaunchKernelGGL((k_tower3<15, true, ABL, RD, NQ, PG, 1, F16>), dim3(grid), dim3(64 * NQ * PG), 0, 0, a);
+}
+
 static uint16_t half_bits(float f) {
   _Float16 h = (_Float16)f;
   uint16_t u;
@@ -85,9 +92,12 @@ int main(int argc, char **argv) {
     launch<0>(a, grid, ++gen);
     CK(hipDeviceSynchronize());
     CK(hipMemcpy(o0.data(), dpool + (size_t)rows * A * 128, o0.size() * 2, hipMemcpyDeviceToHost));
-    for (int pv = 1; pv <= 2; ++pv) {
+    for (int pv = 1; pv <= 4; ++pv) {
       CK(hipMemset(dpool + (size_t)rows * A * 128, 0, o0.size() * 2));
-      if (pv == 1) launch<0, 1>(a, grid, ++gen); else launch<0, 2>(a, grid, ++gen);
+      if (pv == 1) launch<0, 1>(a, grid, ++gen);
+      else if (pv == 2) launch<0, 2>(a, grid, ++gen);
+      else if (pv == 3) launch_dec<0, 2, 4, 3>(a, grid, ++gen);
+      else launch_dec<0, 2, 4, 2>(a, grid, ++gen);
       CK(hipDeviceSynchronize());
       CK(hipMemcpy(o1.data(), dpool + (size_t)rows * A * 128, o1.size() * 2, hipMemcpyDeviceToHost));
       double md = 0, mx = 0; size_t ndiff = 0;
@@ -96,7 +106,7 @@ int main(int argc, char **argv) {
         const double d = fabs((double)x - (double)y);
         md = std::max(md, d); mx = std::max(mx, fabs((double)x)); ndiff += o0[i] != o1[i];
       }
-      printf("PIPE %d vs product: max |d| %.4g (max |x| %.4g), %zu of %zu values differ\n", pv, md, mx, ndiff, o0.size());
+      printf("variant %d vs product: max |d| %.4g (max |x| %.4g), %zu of %zu values differ\n", pv, md, mx, ndiff, o0.size());
     }
   }
   // warm-up: >= `seconds` s of back-to-back product launches (the clock the chip settles at under this load)
@@ -116,9 +126,10 @@ int main(int argc, char **argv) {
   // (ABL 2048, ablation only), 2 the k-steps past 3.5 MB loaded non-temporal (ABL 4096), 3 no per-layer barrier
   // (ABL 1024, ablation: the bound of a barrier-free layer hand-off), 4 no barrier and no epilogue (ABL 1536),
   // 5 the channel-half pipeline (PIPE 1), 6 the same with half 0 at raised priority (PIPE 2)
-  const char *names[7] = {"product", "alias<=3.5MB", "nt-tail", "no-barrier", "no-bar+no-epi", "pipe-halves", "pipe+prio"};
+  const char *names[9] = {"product", "alias<=3.5MB", "nt-tail", "no-barrier", "no-bar+no-epi", "pipe-halves", "pipe+prio",
+                          "nq2pg4-rd3", "nq2pg4-rd2"};
   std::vector<int> vars;
-  if (argc > 3) { for (const char *p = argv[3]; *p; ++p) if (*p >= '0' && *p <= '6') vars.push_back(*p - '0'); }
+  if (argc > 3) { for (const char *p = argv[3]; *p; ++p) if (*p >= '0' && *p <= '8') vars.push_back(*p - '0'); }
   else vars = {0, 1, 2};
   auto run = [&](int v, bool stamped) {
     for (int i = 0; i < reps; ++i) {
@@ -128,7 +139,9 @@ int main(int argc, char **argv) {
       else if (v == 3) { if (stamped) launch<1024 | 128>(a, grid, ++gen); else launch<1024>(a, grid, ++gen); }
       else if (v == 4) { if (stamped) launch<1536 | 128>(a, grid, ++gen); else launch<1536>(a, grid, ++gen); }
       else if (v == 5) { if (stamped) launch<128, 1>(a, grid, ++gen); else launch<0, 1>(a, grid, ++gen); }
-      else { if (stamped) launch<128, 2>(a, grid, ++gen); else launch<0, 2>(a, grid, ++gen); }
+      else if (v == 6) { if (stamped) launch<128, 2>(a, grid, ++gen); else launch<0, 2>(a, grid, ++gen); }
+      else if (v == 7) { if (stamped) launch_dec<128, 2, 4, 3>(a, grid, ++gen); else launch_dec<0, 2, 4, 3>(a, grid, ++gen); }
+      else { if (stamped) launch_dec<128, 2, 4, 2>(a, grid, ++gen); else launch_dec<0, 2, 4, 2>(a, grid, ++gen); }
     }
   };
   for (int round = 0; round < 3; ++round) {
