@@ -428,6 +428,23 @@ def cpu_baseline(args):
                          slowest, wall)}
 
 
+def trainer_flop_per_step(H, blocks, B, U, C=128, hd=64, proj=512):
+    """Algorithmic FLOP of one training step (loss.py:30-158 at B boards, U unroll steps): the
+    convolutions and Linears of every forward, x3 for the parts with gradients (forward, input and weight
+    gradients), x1 for the no-grad parts (the target network's representation and the U consistency
+    representations).  Elementwise work (BatchNorm, activations, losses) is not counted."""
+    A = H * H
+    conv = 2.0 * A * C * C * 9                      # one 128 -> 128 3x3 conv, one board
+    repr_ = 2 * blocks * conv + 2.0 * A * C * 3 * 9  # representation: stem 3 -> 128 + residual blocks
+    dyn = 2 * blocks * conv + 2.0 * A * C * (C + 16) * 9 + 2.0 * A * 16  # dynamics: embed + 144 -> 128 + blocks
+    pred = 2.0 * A * C * 3 + 2.0 * (2 * A) * A + 2.0 * A * hd + 2.0 * hd * 3   # 1x1 convs, policy_fc, value MLP
+    projection = 2.0 * (A * C) * proj + 2.0 * proj * proj
+    reward = 2.0 * (A * C) * hd + 2.0 * hd * 3
+    grad = repr_ + U * dyn + (U + 1) * pred + U * projection + U * reward
+    nograd = repr_ + U * repr_ + U * projection + pred  # target value, consistency trunks + their projections
+    return B * (3.0 * grad + nograd)
+
+
 def trainer_leg(args, world, rank, dist, backend):
     """Config C4's training step on every rank (DDP when world > 1), timed like the self-play region."""
     from datou_gomoku_muzero_amd import trainer as T, weights as W
@@ -464,6 +481,9 @@ def trainer_leg(args, world, rank, dist, backend):
         dist.barrier()
     dt = collective_max(time.perf_counter() - t0, dist, backend)
     loss = float(pending[0][0]) if pending[0] is not None else None
+    ar_ms = tr.allreduce_ms()
+    step_flop = trainer_flop_per_step(args.size, args.blocks, args.trainer_batch, cfg.NUM_UNROLL_STEPS)
+    step_ach = step_flop * args.trainer_steps / dt / 1e12
     # the dominant HIP kernel of the step: the 128->128 residual-block conv (forward and input gradient),
     # timed standalone at the step's shape (B boards, f16 NHWC) with HIP events
     B, H = args.trainer_batch, args.size
@@ -492,6 +512,13 @@ def trainer_leg(args, world, rank, dist, backend):
             "parallelism": "ddp%d: one flat-bucket gradient all-reduce + sharded-PER syncs per step" % world
             if world > 1 else "single GPU",
             "last_loss": loss,
+            "allreduce_ms": ar_ms,
+            "allreduce_note": ("per step on the compute stream, from bucket A's all-reduce issue (backward done) to both "
+                               "buckets averaged; bucket B's weight gradients run inside it" if ar_ms is not None else
+                               "single GPU: no all-reduce"),
+            "roofline_step": {"bound": "mfma", "achieved": step_ach, "peak": PEAK_MFMA_TFLOPS, "unit": "TFLOP/s",
+                              "frac": step_ach / PEAK_MFMA_TFLOPS, "flop_per_step": step_flop,
+                              "count": "bench.trainer_flop_per_step (DESIGN.md 8): convs + Linears, x3 with gradients"},
             "roofline": {"bound": "mfma", "kernel": "gmz_conv3x3 (128->128 3x3 conv, f16 NHWC, B=%d)" % B,
                          "achieved": ach, "peak": PEAK_MFMA_TFLOPS, "unit": "TFLOP/s", "frac": ach / PEAK_MFMA_TFLOPS,
                          "mean_launch_ms": ms, "timed": "standalone at the step's shape, %d launches" % n,

@@ -1349,13 +1349,22 @@ class Trainer:
             for t in list(self.model.parameters()) + list(self.model.buffers()):
                 self.dist.broadcast(t.data, 0)
             self.target.load_state_dict(self.model.state_dict())
-        # gradients as views of one flat bucket (the all-reduce operand)
+        # gradients as views of one flat buffer, the all-reduce operand, in two buckets: [A | B], B = the residual
+        # blocks' 3x3 conv weights, whose gradients the deferred weight-gradient pass (flush_wgrads, DEFER_WGRAD)
+        # writes after the backward, A = everything else, final when the backward ends.  Data parallel: A's
+        # all-reduce runs while B's weight gradients are computed (workers.py:565-583).  The optimiser
+        # keeps the reference's parameter order (its state_dict indices); only the gradient views are reordered.
         self.params = [p for p in self.model.parameters() if p.requires_grad]
+        late = {id(m.conv1.weight) for m in self.model.modules() if isinstance(m, _Block)}
+        late |= {id(m.conv2.weight) for m in self.model.modules() if isinstance(m, _Block)}
+        layout = [p for p in self.params if id(p) not in late] + [p for p in self.params if id(p) in late]
         self.flat_grad = torch.zeros(sum(p.numel() for p in self.params), dtype=torch.float32, device=self.device)
+        self._bucket_a = sum(p.numel() for p in layout if id(p) not in late)
         off = 0
-        for p in self.params:
+        for p in layout:
             p.grad = self.flat_grad[off:off + p.numel()].as_strided(p.shape, p.stride())  # same layout as p
             off += p.numel()
+        self.comm_events = []  # (start, end) CUDA events around each step's all-reduce window (N > 1)
         cuda = self.device.type == "cuda"
         lr = torch.tensor(c.LEARNING_RATE, device=self.device) if cuda else c.LEARNING_RATE
         self.opt = torch.optim.Adam(self.params, lr=lr, weight_decay=c.WEIGHT_DECAY,
@@ -1373,22 +1382,66 @@ class Trainer:
         self._static = None
 
     # ------------------------------------------------------------------ step pieces
-    def _forward_backward(self, batch, is_weights, acc=1, k=None, flip=None, augmented=False):
+    def _forward_backward(self, batch, is_weights, acc=1, k=None, flip=None, augmented=False, flush=True):
+        """Loss and backward; ``flush`` = False leaves the deferred 3x3 weight gradients queued (bucket B) for
+        ``flush_wgrads`` after bucket A's all-reduce has been issued."""
         loss, logs, td = muzero_loss(self.model, self.target, batch, is_weights, self.cfg, k=k, flip=flip,
                                      amp=self.amp, amp_dtype=self.amp_dtype, sync_logs=False, augmented=augmented)
         _DIRECT_GRAD[0] = True
+        ok = False
         try:
             self.scaler.scale(loss / acc).backward()
-            flush_wgrads()
+            if flush:
+                flush_wgrads()
+            ok = True
         finally:
             _DIRECT_GRAD[0] = False
-            _PENDING_WGRAD.clear()
+            if flush or not ok:
+                _PENDING_WGRAD.clear()
         return logs, td
 
+    def _flush(self):
+        try:
+            flush_wgrads()
+        finally:
+            _PENDING_WGRAD.clear()
+
+    def _allreduce_start(self):
+        """Bucket A's all-reduce, issued asynchronously (RCCL on its own stream, after the backward's kernels)."""
+        if self.dist is None:
+            return None
+        if self.device.type == "cuda":
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            self.comm_events.append([ev, None])
+        return self.dist.all_reduce(self.flat_grad[:self._bucket_a], async_op=True)
+
+    def _allreduce_finish(self, work):
+        """Bucket B's all-reduce (its gradients are final once flush_wgrads ran), then both buckets averaged."""
+        if self.dist is None:
+            return
+        if self._bucket_a < self.flat_grad.numel():
+            self.dist.all_reduce(self.flat_grad[self._bucket_a:])
+        work.wait()
+        self.flat_grad.div_(self.dist.get_world_size())
+        if self.device.type == "cuda" and self.comm_events:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            self.comm_events[-1][1] = ev
+            del self.comm_events[:-64]
+
     def _allreduce(self):
-        if self.dist is not None:  # data parallel: ONE all-reduce of the flat gradient bucket (RCCL)
-            self.dist.all_reduce(self.flat_grad)
-            self.flat_grad.div_(self.dist.get_world_size())
+        if self.dist is not None:  # data parallel: the two buckets' all-reduces (RCCL), A's issued first
+            self._allreduce_finish(self._allreduce_start())
+
+    def allreduce_ms(self):
+        """Mean time (ms) of the recent steps' all-reduce windows on the compute stream: from bucket A's issue (the
+        backward done) to both buckets averaged — with bucket B's weight gradients computed inside it (N > 1)."""
+        done = [(a, b) for a, b in self.comm_events if b is not None]
+        if not done:
+            return None
+        done[-1][1].synchronize()
+        return sum(a.elapsed_time(b) for a, b in done) / len(done)
 
     def _update(self):
         c = self.cfg
@@ -1426,14 +1479,20 @@ class Trainer:
         g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         with torch.cuda.stream(s):
             with torch.cuda.graph(g1, stream=s):
-                self._out = self._forward_backward(st[:6], st[6], augmented=True)
+                self._out = self._forward_backward(st[:6], st[6], augmented=True, flush=self.dist is None)
                 if self.dist is None:
                     self._update()
+            gf = None
             if self.dist is not None:
+                # the deferred weight gradients (bucket B) as a graph of their own, replayed while bucket A's
+                # all-reduce runs; then the update
+                gf = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gf, stream=s, pool=g1.pool()):
+                    self._flush()
                 with torch.cuda.graph(g2, stream=s, pool=g1.pool()):
                     self._update()
         torch.cuda.current_stream(self.device).wait_stream(s)
-        self._graphs = (g1, g2 if self.dist is not None else None)
+        self._graphs = (g1, g2 if self.dist is not None else None, gf)
 
     def step(self, batch, is_weights, k=None, flip=None, sync=True):
         """One training step -> ((total, policy, value, reward, consistency) floats, td errors [B]).
@@ -1445,18 +1504,25 @@ class Trainer:
             self._augment_into_static(batch, is_weights, k, flip)
             if self._graphs is None:
                 self._capture()
-            g1, g2 = self._graphs
+            g1, g2, gf = self._graphs
             g1.replay()
             if g2 is not None:
-                self._allreduce()
+                work = self._allreduce_start()
+                gf.replay()
+                self._allreduce_finish(work)
                 g2.replay()
             logs, td = self._out
             td = td.clone()
             self.sched.step()
         else:
-            logs, td = self._forward_backward(batch, is_weights, acc, k=k, flip=flip)
-            if (self.step_count + 1) % acc == 0:
-                self._allreduce()
+            last = (self.step_count + 1) % acc == 0
+            overlap = self.dist is not None and last
+            logs, td = self._forward_backward(batch, is_weights, acc, k=k, flip=flip, flush=not overlap)
+            if overlap:  # bucket A's all-reduce beside bucket B's weight gradients
+                work = self._allreduce_start()
+                self._flush()
+                self._allreduce_finish(work)
+            if last:
                 self._update()
                 self.sched.step()
         self.step_count += 1
