@@ -309,9 +309,12 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
               const int cl = (nq * NTW + nt) * 16 + g4 * 4 + e;
               pbred[(pg * 64 + cl) * 2] = s1[0][nt][e];
               pbred[(pg * 64 + cl) * 2 + 1] = s2[0][nt][e];
-              s1[0][nt][e] = s2[0][nt][e] = 0.f;
             }
         }
+#pragma unroll
+        for (int nt = 0; nt < NTW; ++nt)  // every lane: its accumulators now hold the group's reduced sums
+#pragma unroll
+          for (int e = 0; e < 4; ++e) s1[0][nt][e] = s2[0][nt][e] = 0.f;
         __syncthreads();
         if (tid < 64) {
           double a = 0.0, q = 0.0;

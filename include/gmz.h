@@ -316,8 +316,9 @@ int gmz_bn_backward_stats(int dtype, const void *x_dev, const void *y_dev, const
 /* Eval-mode BatchNorm (running statistics) + residual + ReLU, same layouts/dtypes as gmz_bn_forward:
  * y = relu?(gamma*(x-running_mean)/sqrt(running_var+eps) + beta (+ res)) — nn.BatchNorm2d/1d in eval()
  * (the target network's value of loss.py:54-55).  workspace_dev: gmz_bn_workspace_bytes bytes. */
-/* Launches of the fused BatchNorm finalisation (the channels-last apply passes, default; GMZ_BN_FUSED_FIN=0 keeps the
- * separate finalisation launch) whose bounded wait for every channel's published constants ran out: must stay 0.
+/* Launches of the fused BatchNorm finalisation (the channels-last apply passes with GMZ_BN_FUSED_FIN=1; default: the
+ * separate finalisation launch, measured faster) whose bounded wait for every channel's published constants ran
+ * out: must stay 0.
  * Synchronises the device; reset != 0 clears the count.  (ABI 8) */
 int gmz_bn_sync_errors(uint32_t *out, int reset);
 /* Training-mode channels-last BatchNorm (+ res, ReLU) of nseg equal row segments at once (the trainer's batched

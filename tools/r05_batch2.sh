@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 5 GPU batch 2: trainer — the batched consistency pass (tests, then a same-box A/B against the per-step
-# representations, and against the separate BatchNorm finalisation launch: nofin), and the NET_FPC library A/B (fp contraction in the net / conv / train kernels) on the trainer
+# representations, and the fused BatchNorm finalisation: fusedfin), and the NET_FPC library A/B (fp contraction in the net / conv / train kernels) on the trainer
 # and the headline.
 set -o pipefail
 OUT=gpurun_out/r05_b2
@@ -11,10 +11,10 @@ rc=$?
 grep -E "PASS|FAIL|^E  " $OUT/tests.log | tail -20
 [ $rc -eq 0 ] || exit $rc
 for i in 1 2; do
-  for V in base perstep nofin fpc; do
+  for V in base perstep fusedfin fpc; do
     ARGS="--steps 30 --per"; ENV=""
     [ $V = perstep ] && ARGS="$ARGS --per-step-consistency"
-    [ $V = nofin ] && ENV="GMZ_BN_FUSED_FIN=0"
+    [ $V = fusedfin ] && ENV="GMZ_BN_FUSED_FIN=1"
     [ $V = fpc ] && ENV="GMZ_LIB=$PWD/datou-gomoku-muzero_amd/_alt/libgmz_fpc.so"
     env $ENV timeout -k 10 200 python3 tools/bench_trainer.py $ARGS > $OUT/tr_${V}_$i.json 2> $OUT/tr_${V}_$i.err \
       || { echo "trainer $V failed"; tail -5 $OUT/tr_${V}_$i.err; exit 1; }
