@@ -78,6 +78,7 @@ _SIGS = {
     "gmz_bn_forward_seg": ([I, P, P, P, I, I, I, I, P, P, ctypes.c_float, ctypes.c_float, P, P, P, I, P, P, P, P, P], I),
     "gmz_conv3x3_forward_board_stats": ([I, I, P, P, P, I, P, P, P], I),
     "gmz_bn_sync_errors": ([ctypes.POINTER(ctypes.c_uint32), I], I),
+    "gmz_conv3x3_forward_stamp": ([I, I, P, P, P, I, P, P, P, P, P], I),
 }
 
 # symbols added by the network kernels (declared in include/gmz.h too)

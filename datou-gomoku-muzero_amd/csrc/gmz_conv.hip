@@ -103,6 +103,15 @@ struct BnBwd {
   int relu;
 };
 
+// The dynamics trunk's first conv (network.py:79-96, 128 hidden + 16 action-embedding planes -> 128): its 16-plane
+// part is the embedding of ONE one-hot action cell per board, so its output is a 3x3 stamp around that cell:
+// out[o][q] += table[tap][o] where tap = (a - q) + (1, 1) in the 3x3 window, table[tap][o] = sum_c W[o][128 + c][tap]
+// * embed[c] (f32).  Added in f32 before the output's single rounding, like the 144-channel conv's accumulation.
+struct ActStamp {
+  const int32_t *action;  // [N] action cell per board (nullptr: no stamp)
+  const float *table;     // [9][128]
+};
+
 // HALVES = 2: one workgroup per board computes both halves of the output channels from ONE DMA of the
 // board image (the k-loop twice, the weight ring reloaded for the second half's n-tiles): N workgroups
 // instead of 2N, one board DMA instead of two (gmz_conv3x3 A/B: GMZ_CONV_HALVES).
@@ -116,7 +125,7 @@ template <int H, typename T, int PG, int HALVES = 1, bool BWD = false, bool PB =
 __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restrict__ x, const uint16_t *__restrict__ wpk,
                                                   uint16_t *__restrict__ y, int N, const uint8_t *__restrict__ mask,
                                                   double *__restrict__ stats, const uint16_t *__restrict__ addend,
-                                                  BnBwd bn) {
+                                                  BnBwd bn, ActStamp as) {
   using I = CImg<H>;
   using M = Mfma<T>;
   typedef typename M::V V;
@@ -237,6 +246,12 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
 
     // ---- epilogue: 4 consecutive output channels of one position per lane -> 8-byte store
     uint16_t *dst = y + (size_t)b * A * CC;
+    int say = -100, sax = -100;  // the action stamp's cell (never within reach when there is none)
+    if (as.action) {
+      const int av = as.action[b];
+      say = av / H;
+      sax = av - say * H;
+    }
     const uint16_t *add = addend ? addend + (size_t)b * A * CC : nullptr;  // + addend, rounded once
     float mu[NTW][4], isd[NTW][4];  // BWD: the BatchNorm's mean / invstd of this lane's channels
     if constexpr (BWD) {
@@ -258,6 +273,14 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
       for (int nt = 0; nt < NTW; ++nt) {
         const int n0 = (ntile0 + nt) * 16 + g4 * 4;
         u16x4_t o;
+        {
+          const int ddy = say - p / H + 1, ddx = sax - p % H + 1;
+          if (ddy >= 0 && ddy <= 2 && ddx >= 0 && ddx <= 2) {
+            const float *tb = as.table + (ddy * 3 + ddx) * CC + n0;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[nt][i][e] += tb[e];
+          }
+        }
         if (add) {
           const u16x4_t ad = *(const u16x4_t *)(add + (size_t)p * CC + n0);
 #pragma unroll
@@ -579,27 +602,28 @@ int conv3_stats_slots(int N) { return conv_halves() == 2 ? conv3_grid(N) : conv3
 
 template <int H, typename T, int HV, bool BWD, bool PB = false>
 void launch_conv3_k(const void *x, const void *wpk, void *y, int N, const uint8_t *mask, double *stats, const void *addend,
-                    const BnBwd &bn, hipStream_t st) {
+                    const BnBwd &bn, hipStream_t st, const ActStamp &as = ActStamp{}) {
   // per-board statistics: two workgroups per board (one per half), never the one-workgroup-per-board A/B
   const int grid = PB ? (int)((2L * N + 15) / 16 * 16 < 2L * 2 * cu_count_conv() / 16 * 16 ? (2L * N + 15) / 16 * 16
                                                                                              : 2L * 2 * cu_count_conv() / 16 * 16)
                       : conv3_grid(N);
   hipLaunchKernelGGL((k_conv3<H, T, CONV_PG, HV, BWD, PB>), dim3(grid), dim3(128 * CONV_PG), 0, st,
-                     (const uint16_t *)x, (const uint16_t *)wpk, (uint16_t *)y, N, mask, stats, (const uint16_t *)addend, bn);
+                     (const uint16_t *)x, (const uint16_t *)wpk, (uint16_t *)y, N, mask, stats, (const uint16_t *)addend, bn,
+                     as);
 }
 
 template <int H, typename T>
 int launch_conv3(const void *x, const void *wpk, void *y, int N, const uint8_t *mask, double *stats, const void *addend,
-                 const BnBwd &bn, hipStream_t st, bool per_board = false) {
+                 const BnBwd &bn, hipStream_t st, bool per_board = false, const ActStamp &as = ActStamp{}) {
   const bool bwd = bn.x != nullptr;
   if (per_board) {
-    launch_conv3_k<H, T, 1, false, true>(x, wpk, y, N, mask, stats, addend, bn, st);
+    launch_conv3_k<H, T, 1, false, true>(x, wpk, y, N, mask, stats, addend, bn, st, as);
   } else if (conv_halves() == 2) {
-    if (bwd) launch_conv3_k<H, T, 2, true>(x, wpk, y, N, mask, stats, addend, bn, st);
-    else launch_conv3_k<H, T, 2, false>(x, wpk, y, N, mask, stats, addend, bn, st);
+    if (bwd) launch_conv3_k<H, T, 2, true>(x, wpk, y, N, mask, stats, addend, bn, st, as);
+    else launch_conv3_k<H, T, 2, false>(x, wpk, y, N, mask, stats, addend, bn, st, as);
   } else {
-    if (bwd) launch_conv3_k<H, T, 1, true>(x, wpk, y, N, mask, stats, addend, bn, st);
-    else launch_conv3_k<H, T, 1, false>(x, wpk, y, N, mask, stats, addend, bn, st);
+    if (bwd) launch_conv3_k<H, T, 1, true>(x, wpk, y, N, mask, stats, addend, bn, st, as);
+    else launch_conv3_k<H, T, 1, false>(x, wpk, y, N, mask, stats, addend, bn, st, as);
   }
   GMZ_LAUNCH_CHECK();
   return 0;
@@ -607,10 +631,10 @@ int launch_conv3(const void *x, const void *wpk, void *y, int N, const uint8_t *
 
 template <typename T>
 int conv3_dispatch(int H, const void *x, const void *wpk, void *y, int N, const uint8_t *mask, double *stats, const void *addend,
-                   hipStream_t st, const BnBwd &bn = BnBwd{}, bool per_board = false) {
+                   hipStream_t st, const BnBwd &bn = BnBwd{}, bool per_board = false, const ActStamp &as = ActStamp{}) {
   switch (H) {
-    case 9: return launch_conv3<9, T>(x, wpk, y, N, mask, stats, addend, bn, st, per_board);
-    case 15: return launch_conv3<15, T>(x, wpk, y, N, mask, stats, addend, bn, st, per_board);
+    case 9: return launch_conv3<9, T>(x, wpk, y, N, mask, stats, addend, bn, st, per_board, as);
+    case 15: return launch_conv3<15, T>(x, wpk, y, N, mask, stats, addend, bn, st, per_board, as);
   }
   return fail("gmz_conv3x3: board size must be 9 or 15");
 }
@@ -679,6 +703,20 @@ GMZ_EXPORT int gmz_conv3x3_forward_board_stats(int dtype, int H, const void *x, 
   if (dtype == 1) return conv3_dispatch<__half>(H, x, packed, y, N, mask, stats, nullptr, st, BnBwd{}, true);
   if (dtype == 2) return conv3_dispatch<__hip_bfloat16>(H, x, packed, y, N, mask, stats, nullptr, st, BnBwd{}, true);
   return fail("gmz_conv3x3_forward_board_stats: dtype must be 1 (f16) or 2 (bf16)");
+}
+
+GMZ_EXPORT int gmz_conv3x3_forward_stamp(int dtype, int H, const void *x, const void *packed, void *y, int N,
+                                         const uint8_t *mask, double *stats, const int32_t *action, const float *table,
+                                         void *stream) {
+  if (!x || !packed || !y || !action || !table) return fail("gmz_conv3x3_forward_stamp: null operand");
+  if (N <= 0) return fail("gmz_conv3x3_forward_stamp: N must be positive");
+  if (((uintptr_t)x | (uintptr_t)packed | (uintptr_t)y) & 15)
+    return fail("gmz_conv3x3_forward_stamp: operands must be 16-B aligned");
+  hipStream_t st = (hipStream_t)stream;
+  const ActStamp as = {action, table};
+  if (dtype == 1) return conv3_dispatch<__half>(H, x, packed, y, N, mask, stats, nullptr, st, BnBwd{}, false, as);
+  if (dtype == 2) return conv3_dispatch<__hip_bfloat16>(H, x, packed, y, N, mask, stats, nullptr, st, BnBwd{}, false, as);
+  return fail("gmz_conv3x3_forward_stamp: dtype must be 1 (f16) or 2 (bf16)");
 }
 
 GMZ_EXPORT int gmz_conv3x3_forward(int dtype, int H, const void *x, const void *packed, void *y, int N, void *stream) {

@@ -430,21 +430,23 @@ FUSED_CONV = True  # 128->128 3x3 convs of f16/bf16 channels-last activations ru
 _CONV_DTYPES = {torch.float16: 1, torch.bfloat16: 2}
 
 
-def _packed_conv_weight(w, dtype, transpose):
+def _packed_conv_weight(w, dtype, transpose, parent=None):
     """gmz_conv3x3_pack of ``w`` (f32 [128,128,3,3], any memory format) for ``dtype``; cached on the
     parameter per (dtype, transpose) and its version counter, so a weight used by several unroll
-    steps is packed once per optimiser step (also inside a captured step: first use packs)."""
+    steps is packed once per optimiser step (also inside a captured step: first use packs).  ``parent``: w is
+    the view W[:, :128] of that larger parameter (the dynamics stem), cached on it."""
     from . import _lib
-    key = (dtype, transpose)
-    cache = w.__dict__.setdefault("_gmz_pack", {})
+    owner = w if parent is None else parent
+    key = (dtype, transpose) if parent is None else ("stem", dtype, transpose)
+    cache = owner.__dict__.setdefault("_gmz_pack", {})
     hit = cache.get(key)
-    if hit is not None and hit[0] == w._version:
+    if hit is not None and hit[0] == owner._version:
         return hit[1]
     out = torch.empty(147456, dtype=torch.int16, device=w.device)
     s = w.stride()
     _lib.check(_lib.load().gmz_conv3x3_pack(_CONV_DTYPES[dtype], _lib.ptr(w.detach()), s[0], s[1], s[2], s[3],
                                             int(transpose), _lib.ptr(out), _lib.stream_ptr()))
-    cache[key] = (w._version, out)
+    cache[key] = (owner._version, out)
     return out
 
 
@@ -620,6 +622,98 @@ class _Conv3x3NHWC(torch.autograd.Function):
         return gx, gw, None, None, None, None
 
 
+# the dynamics trunk's first conv (144 -> 128) on the HIP conv: its 128 hidden planes as a 128 -> 128 conv, its 16
+# action-embedding planes (one one-hot cell per board) as a 3x3 stamp added in the conv's epilogue
+# (gmz_conv3x3_forward_stamp), instead of MIOpen's three 144-channel kernels and the concatenation (False: A/B)
+DYN_STEM_HIP = True
+
+
+class _StemGrad:
+    """flush_wgrads' handle on the stem weight's hidden-plane gradient W.grad[:, :128] (the deferred HIP weight
+    gradient of the 128 -> 128 part; one handle per parameter, so the unroll steps' uses merge into one launch)."""
+    __slots__ = ("grad", "device")
+
+    def __init__(self, device):
+        self.grad, self.device = None, device
+
+
+class _DynStemHIP(torch.autograd.Function):
+    """y = conv3x3(cat(h, embed(a)), W) for channels-last f16/bf16 h [n, 128, H, H], W f32 [128, 144, 3, 3],
+    embed = action_embed_conv (1 -> 16, no bias) of the one-hot plane of a (network.py:79-96, under autocast):
+    the hidden part on gmz_conv3x3 (forward, input and weight gradients), the embedding part as the stamp table
+    T[tap][o] = sum_c W16[o][128 + c][tap] * e16[c] (the 16-bit operands the 144-channel conv multiplies, f32 sums)
+    added before the output's one rounding; its gradients from the 9 output cells around each board's action."""
+
+    @staticmethod
+    def forward(ctx, h, W, w_emb, a, mask, stats):
+        from . import _lib
+        dt = h.dtype
+        n, _, H, _ = h.shape
+        w2 = W.detach()[:, 128:].to(dt).float().reshape(128, 16, 9)
+        e = w_emb.detach().reshape(16).to(dt).float()
+        table = torch.einsum("oct,c->to", w2, e).contiguous()
+        a32 = a.to(torch.int32).contiguous()
+        y = torch.empty_like(h, memory_format=torch.channels_last)
+        _lib.check(_lib.load().gmz_conv3x3_forward_stamp(
+            _CONV_DTYPES[dt], H, _lib.ptr(h), _lib.ptr(_packed_conv_weight(W[:, :128], dt, 0, parent=W)), _lib.ptr(y), n,
+            _lib.ptr(mask), _lib.ptr(stats), _lib.ptr(a32), _lib.ptr(table), _lib.stream_ptr()))
+        ctx.save_for_backward(h, W, w_emb, a32)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        h, W, w_emb, a32 = ctx.saved_tensors
+        dt = h.dtype
+        n, _, H, _ = h.shape
+        A = H * H
+        gy = gy.to(dt).contiguous(memory_format=torch.channels_last)
+        gh = None
+        if ctx.needs_input_grad[0]:
+            gh = _conv3x3_hip(gy, _packed_conv_weight(W[:, :128], dt, 1, parent=W))
+        gW = gemb = None
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+            # the stamp's gradient: dT[tap][o] = sum over boards of gy at the cell q = a - (tap - (1, 1))
+            a = a32.long()
+            ay, ax = a // H, a % H
+            k = torch.arange(9, device=a.device)
+            qy, qx = ay[:, None] - (k // 3 - 1), ax[:, None] - (k % 3 - 1)
+            ok = ((qy >= 0) & (qy < H) & (qx >= 0) & (qx < H)).to(torch.float32)
+            idx = (qy.clamp(0, H - 1) * H + qx.clamp(0, H - 1))
+            g = gy.permute(0, 2, 3, 1).reshape(n, A, 128).gather(1, idx[..., None].expand(n, 9, 128)).float()
+            dT = (g * ok[..., None]).sum(0)  # [9, 128]
+            w2 = W.detach()[:, 128:].to(dt).float().reshape(128, 16, 9)
+            e = w_emb.detach().reshape(16).to(dt).float()
+            dW2 = torch.einsum("to,c->oct", dT, e).reshape(128, 16, 3, 3)
+            gemb = torch.einsum("to,oct->c", dT, w2).reshape(w_emb.shape)
+            if _DIRECT_GRAD[0] and W.grad is not None and W.grad.dtype == torch.float32:
+                W.grad[:, 128:].add_(dW2)
+                hold = W.__dict__.get("_gmz_stem_grad")
+                if hold is None:
+                    hold = W.__dict__.setdefault("_gmz_stem_grad", _StemGrad(W.device))
+                hold.grad = W.grad[:, :128]
+                if DEFER_WGRAD:
+                    _PENDING_WGRAD.setdefault(hold, []).append((h, gy))
+                else:
+                    _conv3x3_wgrad_hip(h, gy, hold.grad)
+            else:
+                gW = torch.zeros(W.shape, dtype=torch.float32, device=W.device)
+                _conv3x3_wgrad_hip(h, gy, gW[:, :128])
+                gW[:, 128:] = dW2
+                gW = gW.to(W.dtype)
+            gemb = gemb.to(w_emb.dtype)
+        return gh, gW, gemb, None, None, None
+
+
+def _dyn_stem_hip_ok(dyn, h):
+    if not (DYN_STEM_HIP and FUSED_CONV and h.is_cuda and h.dim() == 4 and h.shape[1] == 128
+            and h.shape[2] == h.shape[3] and h.shape[2] in (9, 15)):
+        return False
+    if dyn.conv.weight.shape != (128, 128 + dyn.EMB, 3, 3) or dyn.conv.bias is not None:
+        return False
+    dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else h.dtype
+    return dt in _CONV_DTYPES and h.is_contiguous(memory_format=torch.channels_last)
+
+
 def _conv3(cin, cout):
     return nn.Conv2d(cin, cout, 3, padding=1, bias=False)
 
@@ -732,6 +826,19 @@ class _Dynamics(_Trunk):
 
     def forward(self, h, a, mask=None):
         n, _, H, W = h.shape
+        if _dyn_stem_hip_ok(self, h):  # DYN_STEM_HIP: the 144-channel conv as hidden-plane conv + action stamp
+            dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else h.dtype
+            st = _conv_stats_buffer(n, h.device) if (self.bn.training and FUSED_BN) else None
+            m = None if mask is None else mask.contiguous().view(torch.uint8)
+            y = _DynStemHIP.apply(h.to(dt), self.conv.weight, self.action_embed_conv.weight, a, m,
+                                  None if st is None else st[0])
+            if st is not None:
+                y._gmz_bnstats = st
+            x = _bn_act(self.bn, y, mask)
+            for blk in self.resblocks:
+                x = blk(x, mask)
+            fc0, act, fc2 = self.reward_fc
+            return x, fc2(act(_linear_flat(fc0, x)))
         plane = F.one_hot(a, H * W).to(h.dtype).reshape(n, 1, H, W)
         emb = _conv1x1(self.action_embed_conv, plane).to(h.dtype)
         if h.is_contiguous(memory_format=torch.channels_last) and not h.is_contiguous():
@@ -1357,6 +1464,7 @@ class Trainer:
         self.params = [p for p in self.model.parameters() if p.requires_grad]
         late = {id(m.conv1.weight) for m in self.model.modules() if isinstance(m, _Block)}
         late |= {id(m.conv2.weight) for m in self.model.modules() if isinstance(m, _Block)}
+        late |= {id(m.conv.weight) for m in self.model.modules() if isinstance(m, _Dynamics)}  # DYN_STEM_HIP
         layout = [p for p in self.params if id(p) not in late] + [p for p in self.params if id(p) in late]
         self.flat_grad = torch.zeros(sum(p.numel() for p in self.params), dtype=torch.float32, device=self.device)
         self._bucket_a = sum(p.numel() for p in layout if id(p) not in late)

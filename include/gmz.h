@@ -348,6 +348,15 @@ int gmz_conv3x3_pack(int dtype, const float *w_dev, int64_t s0, int64_t s1, int6
  * sum of squares, valid pixels of board n; 0 for a masked-out board), for gmz_bn_forward_seg.  (ABI 8) */
 int gmz_conv3x3_forward_board_stats(int dtype, int H, const void *x_dev, const void *packed_dev, void *y_dev, int N,
                                     const uint8_t *mask_dev, double *stats_dev, void *stream);
+/* The dynamics trunk's first conv (144 -> 128: 128 hidden planes + the 16-plane embedding of one action cell per
+ * board, network.py:79-96) as the 128 -> 128 conv of the hidden planes (packed_dev from gmz_conv3x3_pack of
+ * W[:, :128]) plus a 3x3 stamp around each board's action cell: out[n][q][o] += table_dev[tap][o] for q in the
+ * cell's 3x3 window (tap = (a - q) + (1, 1)), table_dev f32 [9][128] = sum_c W[o][128 + c][tap] * embed[c],
+ * added in f32 before the output's one rounding.  action_dev int32 [N]; stats_dev / mask_dev as
+ * gmz_conv3x3_forward_stats (either may be NULL).  (ABI 8) */
+int gmz_conv3x3_forward_stamp(int dtype, int H, const void *x_dev, const void *packed_dev, void *y_dev, int N,
+                              const uint8_t *mask_dev, double *stats_dev, const int32_t *action_dev,
+                              const float *table_dev, void *stream);
 int gmz_conv3x3_forward(int dtype, int H, const void *x_dev, const void *packed_dev, void *y_dev, int N, void *stream);
 /* The same convolution plus an addend of the output's shape and dtype, rounded once:
  * y = round(conv(x, W) + addend).  The residual blocks' input gradient with the identity path's
