@@ -129,6 +129,8 @@ if rank == 0:
     print(json.dumps({"metric": "trainer steps/sec (config C4)", "value": a.steps / dt, "unit": "steps/s",
                       "n_gpus": world, "samples_per_s": a.steps * a.batch * world / dt, "ms_per_step": dt / a.steps * 1e3,
                       "batch_per_gpu": a.batch, "unroll": U, "board": a.size, "blocks": a.blocks, "amp": ("bf16" if a.bf16 else "fp16") if not a.no_amp else None, "channels_last": a.channels_last, "benchmark": a.benchmark, "graph": tr.graph,
-                      "per": a.per, "sync_logs": a.sync_logs, "last_loss": logs[0], "data": "synthetic slices in a device ReplayBuffer"}))
+                      "per": a.per, "sync_logs": a.sync_logs, "last_loss": logs[0], "data": "synthetic slices in a device ReplayBuffer",
+                      "max_memory_allocated_gb": torch.cuda.max_memory_allocated() / 2 ** 30,
+                      "defer_wgrad": T.DEFER_WGRAD}))
 if dist:
     dist.destroy_process_group()
