@@ -79,6 +79,9 @@ _SIGS = {
     "gmz_conv3x3_forward_board_stats": ([I, I, P, P, P, I, P, P, P], I),
     "gmz_bn_sync_errors": ([ctypes.POINTER(ctypes.c_uint32), I], I),
     "gmz_conv3x3_forward_stamp": ([I, I, P, P, P, I, P, P, P, P, P], I),
+    "gmz_bn_forward_m": ([I, I, P, P, P, I, I, I, P, P, ctypes.c_float, ctypes.c_float, P, P, P, I, P, P, P, P, P], I),
+    "gmz_bn_forward_stats_m": ([I, P, P, I, I, I, P, P, ctypes.c_float, ctypes.c_float, P, P, P, I, P, P, P, I, P, P], I),
+    "gmz_bn_backward_acc_m": ([I, I, P, P, P, P, I, I, I, P, P, I, P, P, P, P, P, P, P, I], I),
 }
 
 # symbols added by the network kernels (declared in include/gmz.h too)

@@ -330,8 +330,12 @@ template <typename T, int BWD, int V>
 __global__ void __launch_bounds__(BN_THREADS) k_bnl_red(const T *__restrict__ x, const T *__restrict__ y,
                                                         const T *__restrict__ dy, const uint8_t *__restrict__ mask,
                                                         int B, int C, int S, const float *__restrict__ save, int relu,
-                                                        double *__restrict__ ws, int nseg = 1) {
+                                                        double *__restrict__ ws, int nseg = 1,
+                                                        const uint8_t *__restrict__ rmask = nullptr) {
   __shared__ float red[BN_THREADS * V * 2];  // [group][2][C]
+  // BWD with rmask (V = 8): the ReLU's mask bits written by the forward (bit j of byte [pixel][c / 8]) instead of
+  // re-reading the output y
+  const bool use_mask = V == 8 && BWD && relu && rmask != nullptr;
   const int t = blockIdx.x, ns = gridDim.x;
   const int tpp = C / V, pl = BN_THREADS / tpp;
   const int cp = threadIdx.x % tpp, grp = threadIdx.x / tpp;
@@ -359,6 +363,7 @@ __global__ void __launch_bounds__(BN_THREADS) k_bnl_red(const T *__restrict__ x,
     using VT = VecT<T, V>;
     for (long p = p0 + grp; p < p1; p += (long)U * pl) {
       VT rx[U], rd[U], ry[U];
+      uint8_t mb[U];
       bool ok[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -368,7 +373,8 @@ __global__ void __launch_bounds__(BN_THREADS) k_bnl_red(const T *__restrict__ x,
         rx[u] = *reinterpret_cast<const VT *>(x + k);
         if (BWD) {
           rd[u] = *reinterpret_cast<const VT *>(dy + k);
-          if (relu) ry[u] = *reinterpret_cast<const VT *>(y + k);
+          if (use_mask) mb[u] = rmask[(size_t)(ok[u] ? pp : p) * (C / 8) + cp];
+          else if (relu) ry[u] = *reinterpret_cast<const VT *>(y + k);
         }
         if (mask && ok[u]) ok[u] = mask[pp / S] != 0;
       }
@@ -386,7 +392,7 @@ __global__ void __launch_bounds__(BN_THREADS) k_bnl_red(const T *__restrict__ x,
 #pragma unroll
           for (int j = 0; j < V; ++j) {
             float g = ld(rd[u].v, j);
-            if (relu && !(ld(ry[u].v, j) > 0.f)) g = 0.f;
+            if (use_mask ? !((mb[u] >> j) & 1) : (relu && !(ld(ry[u].v, j) > 0.f))) g = 0.f;
             a[j] += g;
             q[j] = fmaf(g, (ld(rx[u].v, j) - m[j]) * is[j], q[j]);
           }
@@ -431,7 +437,8 @@ template <typename T, int V>
 __global__ void __launch_bounds__(BN_THREADS) k_bnl_apply(const T *__restrict__ x, const T *__restrict__ res,
                                                           long Pseg, int C, const float *__restrict__ gamma,
                                                           const float *__restrict__ beta, int relu,
-                                                          T *__restrict__ y, const float *__restrict__ save) {
+                                                          T *__restrict__ y, const float *__restrict__ save,
+                                                          uint8_t *__restrict__ rmask = nullptr) {
   const int tpp = C / V, pl = BN_THREADS / tpp;
   const int cp = threadIdx.x % tpp, grp = threadIdx.x / tpp;
   if (grp >= pl) return;
@@ -459,6 +466,16 @@ __global__ void __launch_bounds__(BN_THREADS) k_bnl_apply(const T *__restrict__ 
       if (relu) v[j] = fmaxf(v[j], 0.f);
     }
     stv<T, V>(y, k, v);
+    if (V == 8 && relu && rmask) {  // the ReLU's mask of the STORED (rounded) values: bit j = y > 0
+      uint8_t bits = 0;
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        T t[1];
+        st(t, 0, v[j]);
+        bits |= (ld(t, 0) > 0.f ? 1 : 0) << j;
+      }
+      rmask[(size_t)p * (C / 8) + cp] = bits;
+    }
   }
 }
 
@@ -469,8 +486,10 @@ __global__ void __launch_bounds__(BN_THREADS) k_bnl_bwd_apply(const T *__restric
                                                               int S, const float *__restrict__ gamma,
                                                               const float *__restrict__ save, int relu,
                                                               T *__restrict__ dx, T *__restrict__ dres,
-                                                              const float *__restrict__ coef) {
+                                                              const float *__restrict__ coef,
+                                                              const uint8_t *__restrict__ rmask = nullptr) {
   const int tpp = C / V, pl = BN_THREADS / tpp;
+  const bool use_mask = V == 8 && relu && rmask != nullptr;
   const int cp = threadIdx.x % tpp, grp = threadIdx.x / tpp;
   if (grp >= pl) return;
   const int c = V * cp;
@@ -488,7 +507,12 @@ __global__ void __launch_bounds__(BN_THREADS) k_bnl_bwd_apply(const T *__restric
     const bool in = !mask || mask[p / S];
     float g[V], d[V];
     ldv<T, V>(dy, k, g);
-    if (relu) {
+    if (use_mask) {
+      const uint8_t mb = rmask[(size_t)p * (C / 8) + cp];
+#pragma unroll
+      for (int j = 0; j < V; ++j)
+        if (!((mb >> j) & 1)) g[j] = 0.f;
+    } else if (relu) {
       float yv[V];
       ldv<T, V>(y, k, yv);
 #pragma unroll
@@ -792,9 +816,10 @@ int nhwc_vec(int C, size_t esize, std::initializer_list<const void *> ptrs) {
 template <typename T>
 int bn_forward(int nhwc, const void *x, const void *res, const uint8_t *mask, int B, int C, int S, const float *gamma,
                const float *beta, float eps, float momentum, float *rm, float *rv, int64_t *nb, int relu, void *y,
-               float *save, void *ws, hipStream_t st) {
+               float *save, void *ws, hipStream_t st, uint8_t *rmask = nullptr) {
   const int ns = splits_for(B, C, S, nhwc);
   const int V = nhwc ? nhwc_vec(C, sizeof(T), {x, res, y}) : 0;
+  if (rmask && V != 8) return fail("gmz_bn: relu_mask needs channels-last 16-B aligned operands with C % 8 == 0");
   if (nhwc) {
     if (V == 8)
       hipLaunchKernelGGL((k_bnl_red<T, 0, 8>), dim3(ns), dim3(BN_THREADS), 0, st, (const T *)x, (const T *)nullptr,
@@ -808,7 +833,7 @@ int bn_forward(int nhwc, const void *x, const void *res, const uint8_t *mask, in
   }
   GMZ_LAUNCH_CHECK();
   if (nhwc) {
-    unsigned *sync = fused_fin() ? next_sync_slot() : nullptr;
+    unsigned *sync = (fused_fin() && !rmask) ? next_sync_slot() : nullptr;
     if (sync) {
       const long P = (long)B * S;
       if (V == 8)
@@ -830,7 +855,7 @@ int bn_forward(int nhwc, const void *x, const void *res, const uint8_t *mask, in
     const long P = (long)B * S;
     if (V == 8)
       hipLaunchKernelGGL((k_bnl_apply<T, 8>), dim3(elementwise_blocks(P, C, 8)), dim3(BN_THREADS), 0, st,
-                         (const T *)x, (const T *)res, P, C, gamma, beta, relu, (T *)y, save);
+                         (const T *)x, (const T *)res, P, C, gamma, beta, relu, (T *)y, save, rmask);
     else
       hipLaunchKernelGGL((k_bnl_apply<T, 2>), dim3(elementwise_blocks(P, C, 2)), dim3(BN_THREADS), 0, st,
                          (const T *)x, (const T *)res, P, C, gamma, beta, relu, (T *)y, save);
@@ -845,14 +870,15 @@ int bn_forward(int nhwc, const void *x, const void *res, const uint8_t *mask, in
 template <typename T>
 int bn_backward(int nhwc, const void *x, const void *y, const void *dy, const uint8_t *mask, int B, int C, int S,
                 const float *gamma, const float *save, int relu, void *dx, void *dres, float *dgamma, float *dbeta,
-                void *ws, hipStream_t st, int accumulate) {
+                void *ws, hipStream_t st, int accumulate, const uint8_t *rmask = nullptr) {
   const int ns = splits_for(B, C, S, nhwc);
   const int V = nhwc ? nhwc_vec(C, sizeof(T), {x, y, dy, dx, dres}) : 0;
+  if (rmask && V != 8) return fail("gmz_bn: relu_mask needs channels-last 16-B aligned operands with C % 8 == 0");
   float *coef = (float *)((double *)ws + ws_doubles(B, C, S, nhwc));  // f32 [2][C] after the partials
   if (nhwc) {
     if (V == 8)
       hipLaunchKernelGGL((k_bnl_red<T, 1, 8>), dim3(ns), dim3(BN_THREADS), 0, st, (const T *)x, (const T *)y,
-                         (const T *)dy, mask, B, C, S, save, relu, (double *)ws);
+                         (const T *)dy, mask, B, C, S, save, relu, (double *)ws, 1, rmask);
     else
       hipLaunchKernelGGL((k_bnl_red<T, 1, 2>), dim3(ns), dim3(BN_THREADS), 0, st, (const T *)x, (const T *)y,
                          (const T *)dy, mask, B, C, S, save, relu, (double *)ws);
@@ -862,7 +888,7 @@ int bn_backward(int nhwc, const void *x, const void *y, const void *dy, const ui
   }
   GMZ_LAUNCH_CHECK();
   if (nhwc) {
-    unsigned *sync = fused_fin() ? next_sync_slot() : nullptr;
+    unsigned *sync = (fused_fin() && !rmask) ? next_sync_slot() : nullptr;
     if (sync) {
       const long P = (long)B * S;
       if (V == 8)
@@ -886,7 +912,7 @@ int bn_backward(int nhwc, const void *x, const void *y, const void *dy, const ui
     if (V == 8)
       hipLaunchKernelGGL((k_bnl_bwd_apply<T, 8>), dim3(elementwise_blocks(P, C, 8)), dim3(BN_THREADS), 0, st,
                          (const T *)x, (const T *)y, (const T *)dy, mask, P, C, S, gamma, save, relu, (T *)dx,
-                         (T *)dres, coef);
+                         (T *)dres, coef, rmask);
     else
       hipLaunchKernelGGL((k_bnl_bwd_apply<T, 2>), dim3(elementwise_blocks(P, C, 2)), dim3(BN_THREADS), 0, st,
                          (const T *)x, (const T *)y, (const T *)dy, mask, P, C, S, gamma, save, relu, (T *)dx,
@@ -926,8 +952,10 @@ int bn_backward_stats(const void *x, const void *y, const void *dy, const uint8_
 template <typename T>
 int bn_forward_stats(const void *x, const void *res, int B, int C, int S, const float *gamma, const float *beta,
                      float eps, float momentum, float *rm, float *rv, int64_t *nb, int relu, void *y, float *save,
-                     const double *stats, int ns, hipStream_t st) {
-  if (unsigned *sync = fused_fin() ? next_sync_slot() : nullptr) {
+                     const double *stats, int ns, hipStream_t st, uint8_t *rmask = nullptr) {
+  if (rmask && nhwc_vec(C, sizeof(T), {x, res, y}) != 8)
+    return fail("gmz_bn: relu_mask needs channels-last 16-B aligned operands with C % 8 == 0");
+  if (unsigned *sync = (fused_fin() && !rmask) ? next_sync_slot() : nullptr) {
     const int V = nhwc_vec(C, sizeof(T), {x, res, y});
     const long P = (long)B * S;
     if (V == 8)
@@ -948,7 +976,7 @@ int bn_forward_stats(const void *x, const void *res, int B, int C, int S, const 
   const long P = (long)B * S;
   if (V == 8)
     hipLaunchKernelGGL((k_bnl_apply<T, 8>), dim3(elementwise_blocks(P, C, 8)), dim3(BN_THREADS), 0, st, (const T *)x,
-                       (const T *)res, P, C, gamma, beta, relu, (T *)y, (const float *)save);
+                       (const T *)res, P, C, gamma, beta, relu, (T *)y, (const float *)save, rmask);
   else
     hipLaunchKernelGGL((k_bnl_apply<T, 2>), dim3(elementwise_blocks(P, C, 2)), dim3(BN_THREADS), 0, st, (const T *)x,
                        (const T *)res, P, C, gamma, beta, relu, (T *)y, (const float *)save);
@@ -1120,6 +1148,71 @@ GMZ_EXPORT int gmz_bn_backward_acc(int dtype, int layout, const void *x, const v
                                                dbeta, ws, st, accumulate);
   }
   return fail("gmz_bn_backward: dtype must be 0 (f32), 1 (f16) or 2 (bf16)");
+}
+
+// the same entry points with the ReLU's output mask (relu_mask_dev uint8 [B*S][C/8], bit j of byte [pixel][c/8] =
+// y > 0): written by the forward, read by the backward instead of re-reading y (ABI 8)
+GMZ_EXPORT int gmz_bn_forward_m(int dtype, int layout, const void *x, const void *res, const uint8_t *mask, int B, int C,
+                                int S, const float *gamma, const float *beta, float eps, float momentum,
+                                float *running_mean, float *running_var, int64_t *num_batches, int relu, void *y,
+                                float *save, void *ws, uint8_t *relu_mask, void *stream) {
+  if (B <= 0 || C <= 0 || S <= 0 || (size_t)B * C * S >= (1ull << 31)) return fail("gmz_bn_forward: bad shape");
+  if (check_layout(layout, C)) return -1;
+  if (!x || !y || !gamma || !beta || !save || !ws) return fail("gmz_bn_forward: null operand");
+  if ((running_mean == nullptr) != (running_var == nullptr)) return fail("gmz_bn_forward: running stats pair");
+  if (relu_mask && (!relu || layout != 1)) return fail("gmz_bn_forward_m: relu_mask needs relu and channels-last");
+  hipStream_t st = (hipStream_t)stream;
+  switch (dtype) {
+    case 0: return bn_forward<float>(layout, x, res, mask, B, C, S, gamma, beta, eps, momentum, running_mean,
+                                     running_var, num_batches, relu, y, save, ws, st, relu_mask);
+    case 1: return bn_forward<__half>(layout, x, res, mask, B, C, S, gamma, beta, eps, momentum, running_mean,
+                                      running_var, num_batches, relu, y, save, ws, st, relu_mask);
+    case 2: return bn_forward<__hip_bfloat16>(layout, x, res, mask, B, C, S, gamma, beta, eps, momentum, running_mean,
+                                              running_var, num_batches, relu, y, save, ws, st, relu_mask);
+  }
+  return fail("gmz_bn_forward: dtype must be 0 (f32), 1 (f16) or 2 (bf16)");
+}
+
+GMZ_EXPORT int gmz_bn_backward_acc_m(int dtype, int layout, const void *x, const void *y, const void *dy,
+                                     const uint8_t *mask, int B, int C, int S, const float *gamma, const float *save,
+                                     int relu, void *dx, void *dres, float *dgamma, float *dbeta, void *ws,
+                                     const uint8_t *relu_mask, void *stream, int accumulate) {
+  if (B <= 0 || C <= 0 || S <= 0 || (size_t)B * C * S >= (1ull << 31)) return fail("gmz_bn_backward: bad shape");
+  if (check_layout(layout, C)) return -1;
+  if (!x || !dy || !dx || !gamma || !save || !dgamma || !dbeta || !ws || (relu && !y))
+    return fail("gmz_bn_backward: null operand");
+  if (relu_mask && (!relu || layout != 1)) return fail("gmz_bn_backward_acc_m: relu_mask needs relu and channels-last");
+  hipStream_t st = (hipStream_t)stream;
+  switch (dtype) {
+    case 0: return bn_backward<float>(layout, x, y, dy, mask, B, C, S, gamma, save, relu, dx, dres, dgamma, dbeta, ws,
+                                      st, accumulate, relu_mask);
+    case 1: return bn_backward<__half>(layout, x, y, dy, mask, B, C, S, gamma, save, relu, dx, dres, dgamma, dbeta,
+                                       ws, st, accumulate, relu_mask);
+    case 2: return bn_backward<__hip_bfloat16>(layout, x, y, dy, mask, B, C, S, gamma, save, relu, dx, dres, dgamma,
+                                               dbeta, ws, st, accumulate, relu_mask);
+  }
+  return fail("gmz_bn_backward: dtype must be 0 (f32), 1 (f16) or 2 (bf16)");
+}
+
+GMZ_EXPORT int gmz_bn_forward_stats_m(int dtype, const void *x, const void *res, int B, int C, int S, const float *gamma,
+                                      const float *beta, float eps, float momentum, float *running_mean,
+                                      float *running_var, int64_t *num_batches, int relu, void *y, float *save,
+                                      const double *stats, int ns, uint8_t *relu_mask, void *stream) {
+  if (B <= 0 || C <= 0 || S <= 0 || ns <= 0 || (size_t)B * C * S >= (1ull << 31)) return fail("gmz_bn_forward_stats: bad shape");
+  if (check_layout(1, C)) return -1;
+  if (!x || !y || !gamma || !beta || !save || !stats) return fail("gmz_bn_forward_stats: null operand");
+  if ((running_mean == nullptr) != (running_var == nullptr)) return fail("gmz_bn_forward_stats: running stats pair");
+  if (relu_mask && !relu) return fail("gmz_bn_forward_stats_m: relu_mask needs relu");
+  hipStream_t st = (hipStream_t)stream;
+  switch (dtype) {
+    case 0: return bn_forward_stats<float>(x, res, B, C, S, gamma, beta, eps, momentum, running_mean, running_var,
+                                           num_batches, relu, y, save, stats, ns, st, relu_mask);
+    case 1: return bn_forward_stats<__half>(x, res, B, C, S, gamma, beta, eps, momentum, running_mean, running_var,
+                                            num_batches, relu, y, save, stats, ns, st, relu_mask);
+    case 2: return bn_forward_stats<__hip_bfloat16>(x, res, B, C, S, gamma, beta, eps, momentum, running_mean,
+                                                    running_var, num_batches, relu, y, save, stats, ns, st, relu_mask);
+  }
+  return fail("gmz_bn_forward_stats: dtype must be 0 (f32), 1 (f16) or 2 (bf16)");
 }
 
 GMZ_EXPORT int gmz_bn_backward(int dtype, int layout, const void *x, const void *y, const void *dy,

@@ -162,6 +162,14 @@ FUSED_BN = True  # device BatchNorm layers of a training-mode model run the HIP 
 # loads of the BN's x and y (not overlapped with its MFMAs) 35.0 -> 48.9 us, and the step 35.0-35.7 vs
 # 36.3-36.8 steps/s; off (A/B switch, tested)
 FUSED_BN_BWD_STATS = False
+# the channels-last BatchNorm + ReLU forward also writes its ReLU's output mask (1 bit per element,
+# gmz_bn_forward_m / _stats_m) and the backward reads it instead of re-reading the 16-bit output y in both of its
+# passes (gmz_bn_backward_acc_m): 2 x 20 MB fewer reads per 360-board BatchNorm backward.  A/B switch
+RELU_MASK = False
+
+
+def _aligned16(*ts):
+    return all(t is None or t.data_ptr() % 16 == 0 for t in ts)
 
 
 class _BnBwdLink:
@@ -208,20 +216,40 @@ class _FusedMaskedBN(torch.autograd.Function):
         S = x[0, 0].numel()
         y = torch.empty_like(x)
         save = torch.empty(2, C, dtype=torch.float32, device=x.device)
+        rmask = None
+        if (RELU_MASK and relu and layout == 1 and C % 8 == 0 and x.dtype != torch.float32 and torch.is_grad_enabled()
+                and _aligned16(x, res, y) and not (FUSED_BN_BWD_STATS and bwd_link)):
+            rmask = torch.empty(B * S * (C // 8), dtype=torch.uint8, device=x.device)
         if stats is not None and layout == 1:  # statistics reduced by the producing conv's epilogue
-            _lib.check(L.gmz_bn_forward_stats(_BN_DTYPES[x.dtype], _lib.ptr(x), _lib.ptr(res), B, C, S,
-                                              _lib.ptr(gamma), _lib.ptr(beta), float(eps), float(momentum),
-                                              _lib.ptr(running_mean), _lib.ptr(running_var), _lib.ptr(num_batches),
-                                              int(relu), _lib.ptr(y), _lib.ptr(save), _lib.ptr(stats[0]),
-                                              int(stats[1]), _lib.stream_ptr()))
+            if rmask is not None:
+                _lib.check(L.gmz_bn_forward_stats_m(_BN_DTYPES[x.dtype], _lib.ptr(x), _lib.ptr(res), B, C, S,
+                                                    _lib.ptr(gamma), _lib.ptr(beta), float(eps), float(momentum),
+                                                    _lib.ptr(running_mean), _lib.ptr(running_var),
+                                                    _lib.ptr(num_batches), int(relu), _lib.ptr(y), _lib.ptr(save),
+                                                    _lib.ptr(stats[0]), int(stats[1]), _lib.ptr(rmask),
+                                                    _lib.stream_ptr()))
+            else:
+                _lib.check(L.gmz_bn_forward_stats(_BN_DTYPES[x.dtype], _lib.ptr(x), _lib.ptr(res), B, C, S,
+                                                  _lib.ptr(gamma), _lib.ptr(beta), float(eps), float(momentum),
+                                                  _lib.ptr(running_mean), _lib.ptr(running_var), _lib.ptr(num_batches),
+                                                  int(relu), _lib.ptr(y), _lib.ptr(save), _lib.ptr(stats[0]),
+                                                  int(stats[1]), _lib.stream_ptr()))
         else:
             ws = _bn_workspace(layout, B, C, S, x.device)
-            _lib.check(L.gmz_bn_forward(_BN_DTYPES[x.dtype], layout, _lib.ptr(x), _lib.ptr(res), _lib.ptr(mask), B,
-                                        C, S, _lib.ptr(gamma), _lib.ptr(beta), float(eps), float(momentum),
-                                        _lib.ptr(running_mean), _lib.ptr(running_var), _lib.ptr(num_batches),
-                                        int(relu), _lib.ptr(y), _lib.ptr(save), _lib.ptr(ws), _lib.stream_ptr()))
+            if rmask is not None:
+                _lib.check(L.gmz_bn_forward_m(_BN_DTYPES[x.dtype], layout, _lib.ptr(x), _lib.ptr(res), _lib.ptr(mask),
+                                              B, C, S, _lib.ptr(gamma), _lib.ptr(beta), float(eps), float(momentum),
+                                              _lib.ptr(running_mean), _lib.ptr(running_var), _lib.ptr(num_batches),
+                                              int(relu), _lib.ptr(y), _lib.ptr(save), _lib.ptr(ws), _lib.ptr(rmask),
+                                              _lib.stream_ptr()))
+            else:
+                _lib.check(L.gmz_bn_forward(_BN_DTYPES[x.dtype], layout, _lib.ptr(x), _lib.ptr(res), _lib.ptr(mask), B,
+                                            C, S, _lib.ptr(gamma), _lib.ptr(beta), float(eps), float(momentum),
+                                            _lib.ptr(running_mean), _lib.ptr(running_var), _lib.ptr(num_batches),
+                                            int(relu), _lib.ptr(y), _lib.ptr(save), _lib.ptr(ws), _lib.stream_ptr()))
         ctx.save_for_backward(x, y, mask, gamma, save)
         ctx.relu, ctx.has_res, ctx.layout = relu, res is not None, layout
+        ctx.rmask = rmask
         ctx.beta = beta
         ctx.link = link
         ctx.bwd_link = None
@@ -263,11 +291,17 @@ class _FusedMaskedBN(torch.autograd.Function):
                                                _lib.ptr(mask), B, C, S, _lib.ptr(gamma), _lib.ptr(save), int(ctx.relu),
                                                _lib.ptr(dx), _lib.ptr(dres), _lib.ptr(dgamma), _lib.ptr(dbeta),
                                                _lib.ptr(pre[0]), int(pre[1]), _lib.ptr(ws), _lib.stream_ptr(), int(acc)))
+        elif ctx.rmask is not None and _aligned16(x, y, dy, dx, dres):
+            _lib.check(L.gmz_bn_backward_acc_m(_BN_DTYPES[x.dtype], layout, _lib.ptr(x), _lib.ptr(y), _lib.ptr(dy),
+                                               _lib.ptr(mask), B, C, S, _lib.ptr(gamma), _lib.ptr(save), int(ctx.relu),
+                                               _lib.ptr(dx), _lib.ptr(dres), _lib.ptr(dgamma), _lib.ptr(dbeta),
+                                               _lib.ptr(ws), _lib.ptr(ctx.rmask), _lib.stream_ptr(), int(acc)))
         else:
             _lib.check(L.gmz_bn_backward_acc(_BN_DTYPES[x.dtype], layout, _lib.ptr(x), _lib.ptr(y), _lib.ptr(dy),
                                              _lib.ptr(mask), B, C, S, _lib.ptr(gamma), _lib.ptr(save), int(ctx.relu),
                                              _lib.ptr(dx), _lib.ptr(dres), _lib.ptr(dgamma), _lib.ptr(dbeta),
                                              _lib.ptr(ws), _lib.stream_ptr(), int(acc)))
+        ctx.rmask = None
         if ctx.link is not None and dres is not None:
             # the residual's gradient goes to the block's first conv, whose input-gradient epilogue adds it
             # (_ResLink): autograd then has one gradient for the block input, no accumulation pass

@@ -316,6 +316,22 @@ int gmz_bn_backward_stats(int dtype, const void *x_dev, const void *y_dev, const
 /* Eval-mode BatchNorm (running statistics) + residual + ReLU, same layouts/dtypes as gmz_bn_forward:
  * y = relu?(gamma*(x-running_mean)/sqrt(running_var+eps) + beta (+ res)) — nn.BatchNorm2d/1d in eval()
  * (the target network's value of loss.py:54-55).  workspace_dev: gmz_bn_workspace_bytes bytes. */
+/* gmz_bn_forward / gmz_bn_forward_stats / gmz_bn_backward_acc with the ReLU's output mask: relu_mask_dev uint8
+ * [B*S][C/8] (bit j of byte [pixel][c/8] = y > 0, from the STORED value) written by the forward and read by the
+ * backward instead of re-reading y (16 bits per element -> 1): channels-last, C % 8 == 0, 16-B aligned operands, relu
+ * set (trainer.RELU_MASK).  (ABI 8) */
+int gmz_bn_forward_m(int dtype, int layout, const void *x_dev, const void *res_dev, const uint8_t *mask_dev, int B,
+                     int C, int S, const float *gamma_dev, const float *beta_dev, float eps, float momentum,
+                     float *running_mean_dev, float *running_var_dev, int64_t *num_batches_dev, int relu, void *y_dev,
+                     float *save_dev, void *workspace_dev, uint8_t *relu_mask_dev, void *stream);
+int gmz_bn_forward_stats_m(int dtype, const void *x_dev, const void *res_dev, int B, int C, int S, const float *gamma_dev,
+                           const float *beta_dev, float eps, float momentum, float *running_mean_dev,
+                           float *running_var_dev, int64_t *num_batches_dev, int relu, void *y_dev, float *save_dev,
+                           const double *stats_dev, int slots, uint8_t *relu_mask_dev, void *stream);
+int gmz_bn_backward_acc_m(int dtype, int layout, const void *x_dev, const void *y_dev, const void *dy_dev,
+                          const uint8_t *mask_dev, int B, int C, int S, const float *gamma_dev, const float *save_dev,
+                          int relu, void *dx_dev, void *dres_dev, float *dgamma_dev, float *dbeta_dev,
+                          void *workspace_dev, const uint8_t *relu_mask_dev, void *stream, int accumulate);
 /* Launches of the fused BatchNorm finalisation (the channels-last apply passes with GMZ_BN_FUSED_FIN=1; default: the
  * separate finalisation launch, measured faster) whose bounded wait for every channel's published constants ran
  * out: must stay 0.

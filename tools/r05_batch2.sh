@@ -6,15 +6,16 @@ set -o pipefail
 OUT=gpurun_out/r05_b2
 mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest tests/test_trainer.py -m gpu -x -v --timeout 300 --timeout-method thread \
-  -k "batched_consistency or concurrent_forward or production_training_step or elementwise or fused_bn_finalisation or dynamics_stem" > $OUT/tests.log 2>&1
+  -k "batched_consistency or concurrent_forward or production_training_step or elementwise or fused_bn_finalisation or dynamics_stem or relu_mask" > $OUT/tests.log 2>&1
 rc=$?
 grep -E "PASS|FAIL|^E  " $OUT/tests.log | tail -20
 [ $rc -eq 0 ] || exit $rc
 for i in 1 2; do
-  for V in base perstep miopenstem fusedfin fpc; do
+  for V in base perstep miopenstem relumask fusedfin fpc; do
     ARGS="--steps 30 --per"; ENV=""
     [ $V = perstep ] && ARGS="$ARGS --per-step-consistency"
     [ $V = miopenstem ] && ARGS="$ARGS --miopen-stem"
+    [ $V = relumask ] && ARGS="$ARGS --relu-mask"
     [ $V = fusedfin ] && ENV="GMZ_BN_FUSED_FIN=1"
     [ $V = fpc ] && ENV="GMZ_LIB=$PWD/datou-gomoku-muzero_amd/_alt/libgmz_fpc.so"
     env $ENV timeout -k 10 200 python3 tools/bench_trainer.py $ARGS > $OUT/tr_${V}_$i.json 2> $OUT/tr_${V}_$i.err \
