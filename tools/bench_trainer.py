@@ -37,8 +37,8 @@ ap.add_argument("--no-defer-wgrad", action="store_true", help="3x3 weight gradie
 ap.add_argument("--target-f32", action="store_true", help="the target network's value in float32 on MIOpen (trainer.TARGET_F16 off)")
 ap.add_argument("--per-step-loss", action="store_true", help="loss terms per unroll step (trainer.BATCHED_LOSS off)")
 ap.add_argument("--relu-mask", action="store_true", help="BatchNorm backward reads 1-bit ReLU masks (trainer.RELU_MASK on)")
-ap.add_argument("--miopen-stem", action="store_true",
-                help="the dynamics trunk's 144-channel first conv on MIOpen (trainer.DYN_STEM_HIP off)")
+ap.add_argument("--hip-stem", action="store_true",
+                help="the dynamics trunk's 144-channel first conv on the HIP conv + action stamp (trainer.DYN_STEM_HIP on)")
 ap.add_argument("--per-step-consistency", action="store_true",
                 help="five consistency representations, one per unroll step (trainer.BATCHED_CONSISTENCY off)")
 ap.add_argument("--no-benchmark", action="store_true", help="no torch.backends.cudnn.benchmark (MIOpen Find per shape)")
@@ -62,7 +62,7 @@ T.FLAT_NHWC = T.FLAT_NHWC and not a.nchw_flatten
 T.FUSED_RES_GRAD = T.FUSED_RES_GRAD and not a.no_res_fold
 T.BATCHED_LOSS = T.BATCHED_LOSS and not a.per_step_loss
 T.BATCHED_CONSISTENCY = T.BATCHED_CONSISTENCY and not a.per_step_consistency
-T.DYN_STEM_HIP = T.DYN_STEM_HIP and not a.miopen_stem
+T.DYN_STEM_HIP = T.DYN_STEM_HIP or a.hip_stem
 T.RELU_MASK = T.RELU_MASK or a.relu_mask
 T.TARGET_F16 = T.TARGET_F16 and not a.target_f32
 T.DEFER_WGRAD = T.DEFER_WGRAD and not a.no_defer_wgrad

@@ -11,10 +11,10 @@ rc=$?
 grep -E "PASS|FAIL|^E  " $OUT/tests.log | tail -20
 [ $rc -eq 0 ] || exit $rc
 for i in 1 2; do
-  for V in base perstep miopenstem relumask fusedfin fpc; do
+  for V in base perstep hipstem relumask fusedfin fpc; do
     ARGS="--steps 30 --per"; ENV=""
     [ $V = perstep ] && ARGS="$ARGS --per-step-consistency"
-    [ $V = miopenstem ] && ARGS="$ARGS --miopen-stem"
+    [ $V = hipstem ] && ARGS="$ARGS --hip-stem"
     [ $V = relumask ] && ARGS="$ARGS --relu-mask"
     [ $V = fusedfin ] && ENV="GMZ_BN_FUSED_FIN=1"
     [ $V = fpc ] && ENV="GMZ_LIB=$PWD/datou-gomoku-muzero_amd/_alt/libgmz_fpc.so"
