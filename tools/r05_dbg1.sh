@@ -10,4 +10,10 @@ timeout -k 10 300 python -u -m pytest tests/test_pipeline_gpu.py -m gpu -x -q --
 GMZ_DIST_BACKEND=gloo AMD_SERIALIZE_KERNEL=3 timeout -k 10 240 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
   --master-addr 127.0.0.1 --master-port 29731 tools/bench_trainer.py --size 9 --blocks 1 --batch 16 --steps 4 --warmup 4 \
   --buffer 256 > $OUT/gloo_trainer.json 2> $OUT/gloo_trainer.err; rc=$?
-tail -20 $OUT/gloo_trainer.err; cat $OUT/gloo_trainer.json; exit $rc
+tail -20 $OUT/gloo_trainer.err; cat $OUT/gloo_trainer.json; [ $rc -eq 0 ] || exit $rc
+# the gloo rehearsal's loop phase alone (the phase that aborted in r05_batch1), kernels serialised
+GMZ_DIST_BACKEND=gloo AMD_SERIALIZE_KERNEL=3 timeout -k 10 400 python3 bench.py --gpus 2 --games 64 --size 9 --sims 50 \
+  --blocks 1 --steps 2 --warmup 1 --trainer-steps 0 --trainer-batch 16 --trainer-buffer 64 --loop-iters 4 --loop-warmup 4 \
+  --loop-games 64 --loop-update-interval 2 --loop-prefill 64 --loop-buffer 4096 --sublines= --worker-moves 0 \
+  --dist-timeout 60 --no-cpu-baseline > $OUT/loop2.json 2> $OUT/loop2.err; rc=$?
+grep -iE "fault|error|abort|Traceback" $OUT/loop2.err | head -20; tail -c 1500 $OUT/loop2.json; exit $rc
