@@ -25,7 +25,14 @@ for size in (9, 15):
         y_hip = T._DynStemHIP.apply(h, dyn0.conv.weight, dyn0.action_embed_conv.weight, a, None, None)
         st = T._conv_stats_buffer(B, h.device)
         y_hip2 = T._DynStemHIP.apply(h, dyn0.conv.weight, dyn0.action_embed_conv.weight, a, m8, st[0])
+        W16 = dyn0.conv.weight.detach().half().float()
+        y32 = F.conv2d(x.float(), W16, padding=1)
+        y32h = F.conv2d(h.float(), W16[:, :128], padding=1)
     torch.cuda.synchronize()
+    print("size %d: vs fp32 conv of the same f16 operands: MIOpen %.3g  HIP %.3g  (hidden part only %.3g); emb max %.3g"
+          % (size, rel(y32, y_ref), rel(y32, y_hip), rel(y32, y32h), float(emb.abs().max())))
+    dd = (y_hip.float() - y32).abs()[0].sum(0)
+    print("   board0 action", int(a[0]), "cells where HIP differs:", torch.nonzero(dd > 1e-2).tolist()[:12])
     print("size %d: stem conv rel %.3g (no stats) %.3g (stats)  y_ref %s %s  y_hip %s %s" % (
         size, rel(y_ref, y_hip), rel(y_ref, y_hip2), y_ref.dtype, tuple(y_ref.stride()), y_hip.dtype, tuple(y_hip.stride())))
     d1, d2 = copy.deepcopy(dyn0), copy.deepcopy(dyn0)
