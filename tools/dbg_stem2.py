@@ -45,13 +45,28 @@ for size in (9, 15):
     print("   bn out rel %.3g (masked rows %.3g)  running_mean rel %.3g  var rel %.3g" % (
         rel(b_ref, b_hip), rel(b_ref[mask], b_hip[mask]), rel(d1.bn.running_mean, d2.bn.running_mean),
         rel(d1.bn.running_var, d2.bn.running_var)))
+    outs = {}
     for hip in (False, True):
         T.DYN_STEM_HIP = hip
         d = copy.deepcopy(dyn0)
         d.train()
         with torch.no_grad(), torch.autocast("cuda", dtype=torch.float16):
             nxt, r = d(h, a, mask=mask)
-        if not hip:
-            n0 = nxt
-        else:
-            print("   module out rel %.3g (masked %.3g)" % (rel(n0, nxt), rel(n0[mask], nxt[mask])))
+        outs[hip] = nxt
+    # the same stages composed by hand from each stem output (fresh modules): block input and output
+    stages = {}
+    for name, y in (("ref", y_ref), ("hip", y_hip2)):
+        d = copy.deepcopy(dyn0)
+        d.train()
+        with torch.no_grad(), torch.autocast("cuda", dtype=torch.float16):
+            if name == "hip":
+                y._gmz_bnstats = T._conv_stats_buffer(B, h.device)  # stale on purpose? no: recompute below
+                y = T._DynStemHIP.apply(h, d.conv.weight, d.action_embed_conv.weight, a, m8, y._gmz_bnstats[0])
+                y._gmz_bnstats = stt = None
+            x0 = T._bn_act(d.bn, y, mask)
+            x1 = d.resblocks[0](x0, mask)
+        stages[name] = (x0, x1)
+    torch.cuda.synchronize()
+    print("   module out rel %.3g (masked %.3g) | by hand: stem-bn rel %.3g, block rel %.3g | module-hip vs hand-hip %.3g"
+          % (rel(outs[False], outs[True]), rel(outs[False][mask], outs[True][mask]), rel(stages["ref"][0], stages["hip"][0]),
+             rel(stages["ref"][1], stages["hip"][1]), rel(outs[True], stages["hip"][1])))
