@@ -684,10 +684,17 @@ class _DynStemHIP(torch.autograd.Function):
         from . import _lib
         dt = h.dtype
         n, _, H, _ = h.shape
-        w2 = W.detach()[:, 128:].to(dt).float().reshape(128, 16, 9)
-        e = w_emb.detach().reshape(16).to(dt).float()
-        table = torch.einsum("oct,c->to", w2, e).contiguous()
+        # the table in float32 whatever the caller's autocast state (under autocast einsum would run in f16 and
+        # hand the kernel a half-size f16 buffer it reads as f32: the round-5 GPU fault)
+        with torch.autocast("cuda", enabled=False):
+            w2 = W.detach()[:, 128:].to(dt).float().reshape(128, 16, 9)
+            e = w_emb.detach().reshape(16).to(dt).float()
+            table = torch.einsum("oct,c->to", w2, e).contiguous()
+        if table.dtype != torch.float32 or table.numel() != 9 * 128:
+            raise RuntimeError("_DynStemHIP: stamp table must be f32 [9][128]")
         a32 = a.to(torch.int32).contiguous()
+        if a32.numel() != h.shape[0]:
+            raise RuntimeError("_DynStemHIP: one action per board")
         y = torch.empty_like(h, memory_format=torch.channels_last)
         _lib.check(_lib.load().gmz_conv3x3_forward_stamp(
             _CONV_DTYPES[dt], H, _lib.ptr(h), _lib.ptr(_packed_conv_weight(W[:, :128], dt, 0, parent=W)), _lib.ptr(y), n,
@@ -715,11 +722,12 @@ class _DynStemHIP(torch.autograd.Function):
             ok = ((qy >= 0) & (qy < H) & (qx >= 0) & (qx < H)).to(torch.float32)
             idx = (qy.clamp(0, H - 1) * H + qx.clamp(0, H - 1))
             g = gy.permute(0, 2, 3, 1).reshape(n, A, 128).gather(1, idx[..., None].expand(n, 9, 128)).float()
-            dT = (g * ok[..., None]).sum(0)  # [9, 128]
-            w2 = W.detach()[:, 128:].to(dt).float().reshape(128, 16, 9)
-            e = w_emb.detach().reshape(16).to(dt).float()
-            dW2 = torch.einsum("to,c->oct", dT, e).reshape(128, 16, 3, 3)
-            gemb = torch.einsum("to,oct->c", dT, w2).reshape(w_emb.shape)
+            with torch.autocast("cuda", enabled=False):
+                dT = (g * ok[..., None]).sum(0)  # [9, 128]
+                w2 = W.detach()[:, 128:].to(dt).float().reshape(128, 16, 9)
+                e = w_emb.detach().reshape(16).to(dt).float()
+                dW2 = torch.einsum("to,c->oct", dT, e).reshape(128, 16, 3, 3)
+                gemb = torch.einsum("to,oct->c", dT, w2).reshape(w_emb.shape)
             if _DIRECT_GRAD[0] and W.grad is not None and W.grad.dtype == torch.float32:
                 W.grad[:, 128:].add_(dW2)
                 hold = W.__dict__.get("_gmz_stem_grad")
