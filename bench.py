@@ -530,8 +530,10 @@ def trainer_trace_summary(args):
     """The dominant convolution inside the graph-replayed trainer step and the step's launch count, from the
     committed rocprofv3 trace summary (tools/trainer_profile.sh -> tools/trainer_trace_summary.py; a HIP
     graph's kernels cannot be timed from inside the process): builder-measured, not this run."""
-    path = os.path.join(REPO, "profiles", "r04_trainer_trace.json")
-    if not os.path.exists(path) or (args.size, args.blocks, args.trainer_batch) != (15, 8, 360):
+    import glob
+    paths = sorted(glob.glob(os.path.join(REPO, "profiles", "r[0-9][0-9]_trainer_trace.json")))
+    path = paths[-1] if paths else ""
+    if not path or (args.size, args.blocks, args.trainer_batch) != (15, 8, 360):
         return None
     try:
         d = json.load(open(path))

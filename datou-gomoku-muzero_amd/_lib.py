@@ -11,10 +11,11 @@ import torch  # noqa: F401  (must precede the CDLL load: shared HIP runtime)
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GMZ_LIB") or os.path.join(PKG_DIR, "libgmz.so")  # GMZ_LIB: A/B builds (tools)
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 P = ctypes.c_void_p
 I = ctypes.c_int
+L = ctypes.c_long
 U64 = ctypes.c_uint64
 
 
@@ -74,6 +75,9 @@ _SIGS = {
     "gmz_conv3x3_forward_bwdstats": ([I, I, P, P, P, P, I, P, P, P, P, I, P, P], I),
     "gmz_bn_backward_stats": ([I, P, P, P, P, I, I, I, P, P, I, P, P, P, P, P, I, P, P, I], I),
     "gmz_grad_add_t": ([I, P, I, I, I, P, P], I),
+    "gmz_head_conv1x1_forward": ([I, P, L, I, P, P, I, P, P, I, P, P, P], I),
+    "gmz_head_conv1x1_workspace_bytes": ([L, I, P], I),
+    "gmz_head_conv1x1_backward": ([I, P, L, I, P, I, P, I, P, P, P, P, P, P, P, I, P, P], I),
     "gmz_bn_forward_stats": ([I, P, P, I, I, I, P, P, ctypes.c_float, ctypes.c_float, P, P, P, I, P, P, P, I, P], I),
     "gmz_bn_forward_seg": ([I, P, P, P, I, I, I, I, P, P, ctypes.c_float, ctypes.c_float, P, P, P, I, P, P, P, P, P], I),
     "gmz_conv3x3_forward_board_stats": ([I, I, P, P, P, I, P, P, P], I),

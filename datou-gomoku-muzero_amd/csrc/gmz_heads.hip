@@ -1,0 +1,283 @@
+// gmz_heads.hip — the prediction heads' two 1x1 convolutions (network.py:61,64: policy_conv 128 -> 2, value_conv
+// 128 -> 1, both reading the same hidden state, network.py:69-71) as ONE pass over the channels-last hidden state,
+// forward and backward, for the trainer (trainer._HeadConv1x1; loss.py:70,96 call prediction six times per step).
+//
+// PyTorch ran each head as its own GEMM with K = 128 and N = 1 or 2 (plus a bias add), and its backward as a
+// GEMM for dx, a batched GEMM + reduction for dW and a reduction for db — per head — then an add of the two
+// heads' dx into the hidden state's gradient: ~10 launches and three 20 MB passes per prediction.  Here:
+//   forward : y0[p][o] = round(sum_c x[p][c] W[o][c] + b[o]) for o < O0, y1 likewise for the next O1 rows of W;
+//             one read of x.
+//   backward: dx[p][c] = round(sum_o dy[p][o] W[o][c]) (both heads, one rounding), and per workgroup the
+//             partials of dW[o][c] = sum_p dy[p][o] x[p][c] and db[o] = sum_p dy[p][o] — one read of x, one write
+//             of dx — then k_head1x1_red sums the partials in a fixed order into the f32 parameter gradients.
+// Operands follow autocast: x and dy in the activation dtype, W and b rounded to it, f32 accumulation.
+// HBM-bound (bytes per position: 256 read forward; 256 read + 256 written backward, at C = 128, f16).
+#include "gmz_common.h"
+
+#include <hip/hip_bf16.h>
+#include <hip/hip_fp16.h>
+
+namespace gmz {
+namespace {
+
+constexpr int HC = 128;                  // hidden channels
+constexpr int HV = 8;                    // channels per thread (one 16-B access)
+constexpr int HTPP = HC / HV;            // threads per position
+constexpr int HTHREADS = 256;
+constexpr int HPL = HTHREADS / HTPP;     // positions per block step
+constexpr int HMAXO = 4;                 // O0 + O1
+constexpr int HBLOCKS = 512;             // backward partials (workgroups)
+
+__device__ __forceinline__ float hld(const float *p, size_t i) { return p[i]; }
+__device__ __forceinline__ float hld(const __half *p, size_t i) { return __half2float(p[i]); }
+__device__ __forceinline__ float hld(const __hip_bfloat16 *p, size_t i) { return __bfloat162float(p[i]); }
+__device__ __forceinline__ void hst(float *p, size_t i, float v) { p[i] = v; }
+__device__ __forceinline__ void hst(__half *p, size_t i, float v) { p[i] = __float2half(v); }
+__device__ __forceinline__ void hst(__hip_bfloat16 *p, size_t i, float v) { p[i] = __float2bfloat16(v); }
+template <typename T>
+__device__ __forceinline__ float rnd(float v) {  // v rounded to T (autocast's cast of the f32 parameters)
+  T t[1];
+  hst(t, 0, v);
+  return hld(t, 0);
+}
+
+template <typename T>
+struct alignas(16) Vec8 {
+  T v[HV];
+};
+
+// the O = O0 + O1 weight rows (head 0's O0 rows, then head 1's) rounded to T, this thread's 8 channels
+struct HeadW {
+  const float *w0, *b0, *w1, *b1;  // [O0][HC], [O0] (or null), [O1][HC], [O1] (or null)
+};
+template <typename T, int O>
+__device__ __forceinline__ void load_w(const HeadW &hw, int O0, int c, float (&wr)[O][HV]) {
+#pragma unroll
+  for (int o = 0; o < O; ++o) {
+    const float *row = o < O0 ? hw.w0 + o * HC : hw.w1 + (o - O0) * HC;
+#pragma unroll
+    for (int j = 0; j < HV; ++j) wr[o][j] = rnd<T>(row[c + j]);
+  }
+}
+
+template <typename T, int O>
+__global__ void __launch_bounds__(HTHREADS) k_head1x1_fwd(const T *__restrict__ x, long P, HeadW hw, int O0,
+                                                         T *__restrict__ y0, T *__restrict__ y1) {
+  const int cp = threadIdx.x % HTPP, grp = threadIdx.x / HTPP, c = cp * HV;
+  float wr[O][HV];
+  load_w<T, O>(hw, O0, c, wr);
+  float bb[O];
+#pragma unroll
+  for (int o = 0; o < O; ++o) {
+    const float *b = o < O0 ? hw.b0 : hw.b1;
+    bb[o] = b ? rnd<T>(b[o < O0 ? o : o - O0]) : 0.f;
+  }
+  for (long p = (long)blockIdx.x * HPL + grp; p < P; p += (long)gridDim.x * HPL) {
+    const Vec8<T> r = *reinterpret_cast<const Vec8<T> *>(x + (size_t)p * HC + c);
+    float acc[O];
+#pragma unroll
+    for (int o = 0; o < O; ++o) {
+      acc[o] = 0.f;
+#pragma unroll
+      for (int j = 0; j < HV; ++j) acc[o] = fmaf(hld(r.v, j), wr[o][j], acc[o]);
+    }
+#pragma unroll
+    for (int o = 0; o < O; ++o)
+#pragma unroll
+      for (int s = 1; s < HTPP; s <<= 1) acc[o] += __shfl_xor(acc[o], s, 64);  // the 16 lanes of a position
+    if (cp == 0) {
+#pragma unroll
+      for (int o = 0; o < O; ++o) {
+        if (o < O0) hst(y0, (size_t)p * O0 + o, acc[o] + bb[o]);
+        else hst(y1, (size_t)p * (O - O0) + (o - O0), acc[o] + bb[o]);
+      }
+    }
+  }
+}
+
+// dx, and this workgroup's dW / db partials -> part[blockIdx.x][O * (HC + 1)] (dW rows, then db)
+template <typename T, int O>
+__global__ void __launch_bounds__(HTHREADS) k_head1x1_bwd(const T *__restrict__ x, long P, HeadW hw, int O0,
+                                                         const T *__restrict__ dy0, const T *__restrict__ dy1,
+                                                         T *__restrict__ dx, float *__restrict__ part) {
+  __shared__ float red[HPL][O * (HC + 1)];
+  const int cp = threadIdx.x % HTPP, grp = threadIdx.x / HTPP, c = cp * HV;
+  float wr[O][HV];
+  load_w<T, O>(hw, O0, c, wr);
+  float gw[O][HV], gb[O];
+#pragma unroll
+  for (int o = 0; o < O; ++o) {
+    gb[o] = 0.f;
+#pragma unroll
+    for (int j = 0; j < HV; ++j) gw[o][j] = 0.f;
+  }
+  for (long p = (long)blockIdx.x * HPL + grp; p < P; p += (long)gridDim.x * HPL) {
+    const Vec8<T> r = *reinterpret_cast<const Vec8<T> *>(x + (size_t)p * HC + c);
+    float g[O];
+#pragma unroll
+    for (int o = 0; o < O; ++o)
+      g[o] = o < O0 ? hld(dy0, (size_t)p * O0 + o) : hld(dy1, (size_t)p * (O - O0) + (o - O0));
+    float d[HV];
+#pragma unroll
+    for (int j = 0; j < HV; ++j) {
+      d[j] = 0.f;
+#pragma unroll
+      for (int o = 0; o < O; ++o) d[j] = fmaf(g[o], wr[o][j], d[j]);
+    }
+    Vec8<T> out;
+#pragma unroll
+    for (int j = 0; j < HV; ++j) hst(out.v, j, d[j]);
+    *reinterpret_cast<Vec8<T> *>(dx + (size_t)p * HC + c) = out;
+#pragma unroll
+    for (int o = 0; o < O; ++o) {
+      gb[o] += g[o];
+#pragma unroll
+      for (int j = 0; j < HV; ++j) gw[o][j] = fmaf(g[o], hld(r.v, j), gw[o][j]);
+    }
+  }
+#pragma unroll
+  for (int o = 0; o < O; ++o) {
+#pragma unroll
+    for (int j = 0; j < HV; ++j) red[grp][o * HC + c + j] = gw[o][j];
+    if (cp == 0) red[grp][O * HC + o] = gb[o];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < O * (HC + 1); i += HTHREADS) {
+    float s = 0.f;
+#pragma unroll
+    for (int g2 = 0; g2 < HPL; ++g2) s += red[g2][i];
+    part[(size_t)blockIdx.x * O * (HC + 1) + i] = s;
+  }
+}
+
+// one workgroup per output element i of [O][HC] dW rows + [O] db: the nb partials summed in a fixed tree order,
+// then written or added into the destination (dW0 [O0][HC], db0 [O0], dW1 [O1][HC], db1 [O1])
+__global__ void __launch_bounds__(HTHREADS) k_head1x1_red(const float *__restrict__ part, int nb, int O, int O0,
+                                                         float *__restrict__ dw0, float *__restrict__ db0,
+                                                         float *__restrict__ dw1, float *__restrict__ db1, int acc) {
+  __shared__ float s[HTHREADS];
+  const int i = blockIdx.x, n = O * (HC + 1);
+  float a = 0.f;
+  for (int k = threadIdx.x; k < nb; k += HTHREADS) a += part[(size_t)k * n + i];
+  s[threadIdx.x] = a;
+  __syncthreads();
+  for (int h = HTHREADS / 2; h > 0; h >>= 1) {
+    if (threadIdx.x < h) s[threadIdx.x] += s[threadIdx.x + h];
+    __syncthreads();
+  }
+  if (threadIdx.x != 0) return;
+  float *base;  // a null destination (no bias) is skipped
+  int off;
+  if (i < O * HC) {
+    const int o = i / HC, c = i % HC;
+    base = o < O0 ? dw0 : dw1;
+    off = (o < O0 ? o : o - O0) * HC + c;
+  } else {
+    const int o = i - O * HC;
+    base = o < O0 ? db0 : db1;
+    off = o < O0 ? o : o - O0;
+  }
+  if (!base) return;
+  base[off] = acc ? base[off] + s[0] : s[0];
+}
+
+template <typename T, int O>
+void launch_fwd(const void *x, long P, const HeadW &hw, int O0, void *y0, void *y1, hipStream_t st) {
+  long nb = (P + HPL * 4 - 1) / (HPL * 4);
+  nb = nb < 4096 ? (nb < 1 ? 1 : nb) : 4096;
+  hipLaunchKernelGGL((k_head1x1_fwd<T, O>), dim3((int)nb), dim3(HTHREADS), 0, st, (const T *)x, P, hw, O0, (T *)y0,
+                     (T *)y1);
+}
+
+template <typename T, int O>
+void launch_bwd(const void *x, long P, const HeadW &hw, int O0, const void *dy0, const void *dy1, void *dx, float *part,
+                int nb, hipStream_t st) {
+  hipLaunchKernelGGL((k_head1x1_bwd<T, O>), dim3(nb), dim3(HTHREADS), 0, st, (const T *)x, P, hw, O0, (const T *)dy0,
+                     (const T *)dy1, (T *)dx, part);
+}
+
+template <typename T>
+int head_fwd(const void *x, long P, const HeadW &hw, int O0, int O1, void *y0, void *y1, hipStream_t st) {
+  switch (O0 + O1) {
+    case 1: launch_fwd<T, 1>(x, P, hw, O0, y0, y1, st); break;
+    case 2: launch_fwd<T, 2>(x, P, hw, O0, y0, y1, st); break;
+    case 3: launch_fwd<T, 3>(x, P, hw, O0, y0, y1, st); break;
+    default: launch_fwd<T, 4>(x, P, hw, O0, y0, y1, st); break;
+  }
+  GMZ_LAUNCH_CHECK();
+  return 0;
+}
+
+int head_blocks(long P) {
+  const long nb = (P + HPL - 1) / HPL;
+  return (int)(nb < HBLOCKS ? nb : HBLOCKS);
+}
+
+template <typename T>
+int head_bwd(const void *x, long P, const HeadW &hw, int O0, int O1, const void *dy0, const void *dy1, void *dx,
+             float *dw0, float *db0, float *dw1, float *db1, int acc, float *ws, hipStream_t st) {
+  const int O = O0 + O1, nb = head_blocks(P);
+  switch (O) {
+    case 1: launch_bwd<T, 1>(x, P, hw, O0, dy0, dy1, dx, ws, nb, st); break;
+    case 2: launch_bwd<T, 2>(x, P, hw, O0, dy0, dy1, dx, ws, nb, st); break;
+    case 3: launch_bwd<T, 3>(x, P, hw, O0, dy0, dy1, dx, ws, nb, st); break;
+    default: launch_bwd<T, 4>(x, P, hw, O0, dy0, dy1, dx, ws, nb, st); break;
+  }
+  GMZ_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_head1x1_red, dim3(O * (HC + 1)), dim3(HTHREADS), 0, st, (const float *)ws, nb, O, O0, dw0, db0,
+                     dw1, db1, acc);
+  GMZ_LAUNCH_CHECK();
+  return 0;
+}
+
+int head_check(const char *fn, int C, long P, int O0, int O1, const void *x, const float *w0, const float *w1) {
+  if (C != HC) return fail(std::string(fn) + ": C must be 128");
+  if (P <= 0 || (size_t)P * HC >= (1ull << 31)) return fail(std::string(fn) + ": bad position count");
+  if (O0 < 1 || O1 < 0 || O0 + O1 > HMAXO) return fail(std::string(fn) + ": need 1 <= O0, 0 <= O1, O0 + O1 <= 4");
+  if (!x || !w0 || (O1 > 0 && !w1)) return fail(std::string(fn) + ": null operand");
+  if (((uintptr_t)x) % 16) return fail(std::string(fn) + ": x must be 16-B aligned");
+  return 0;
+}
+
+}  // namespace
+}  // namespace gmz
+
+using namespace gmz;
+
+GMZ_EXPORT int gmz_head_conv1x1_forward(int dtype, const void *x, long P, int C, const float *w0, const float *b0,
+                                        int O0, const float *w1, const float *b1, int O1, void *y0, void *y1,
+                                        void *stream) {
+  if (head_check("gmz_head_conv1x1_forward", C, P, O0, O1, x, w0, w1)) return -1;
+  const HeadW hw{w0, b0, w1, b1};
+  if (!y0 || (O1 > 0 && !y1)) return fail("gmz_head_conv1x1_forward: null output");
+  hipStream_t st = (hipStream_t)stream;
+  switch (dtype) {
+    case 0: return head_fwd<float>(x, P, hw, O0, O1, y0, y1, st);
+    case 1: return head_fwd<__half>(x, P, hw, O0, O1, y0, y1, st);
+    case 2: return head_fwd<__hip_bfloat16>(x, P, hw, O0, O1, y0, y1, st);
+  }
+  return fail("gmz_head_conv1x1_forward: dtype must be 0 (f32), 1 (f16) or 2 (bf16)");
+}
+
+GMZ_EXPORT int gmz_head_conv1x1_workspace_bytes(long P, int O, size_t *out) {
+  if (P <= 0 || O < 1 || O > HMAXO || !out) return fail("gmz_head_conv1x1_workspace_bytes: bad arguments");
+  *out = (size_t)head_blocks(P) * O * (HC + 1) * sizeof(float);
+  return 0;
+}
+
+GMZ_EXPORT int gmz_head_conv1x1_backward(int dtype, const void *x, long P, int C, const float *w0, int O0,
+                                         const float *w1, int O1, const void *dy0, const void *dy1, void *dx, float *dw0, float *db0, float *dw1,
+                                         float *db1, int accumulate, void *ws, void *stream) {
+  if (head_check("gmz_head_conv1x1_backward", C, P, O0, O1, x, w0, w1)) return -1;
+  const HeadW hw{w0, nullptr, w1, nullptr};
+  if (!dy0 || (O1 > 0 && !dy1) || !dx || !ws) return fail("gmz_head_conv1x1_backward: null operand");
+  if (((uintptr_t)dx) % 16) return fail("gmz_head_conv1x1_backward: dx must be 16-B aligned");
+  hipStream_t st = (hipStream_t)stream;
+  switch (dtype) {
+    case 0: return head_bwd<float>(x, P, hw, O0, O1, dy0, dy1, dx, dw0, db0, dw1, db1, accumulate, (float *)ws, st);
+    case 1: return head_bwd<__half>(x, P, hw, O0, O1, dy0, dy1, dx, dw0, db0, dw1, db1, accumulate, (float *)ws, st);
+    case 2:
+      return head_bwd<__hip_bfloat16>(x, P, hw, O0, O1, dy0, dy1, dx, dw0, db0, dw1, db1, accumulate, (float *)ws, st);
+  }
+  return fail("gmz_head_conv1x1_backward: dtype must be 0 (f32), 1 (f16) or 2 (bf16)");
+}

@@ -840,6 +840,80 @@ class _Trunk(nn.Module):
         return h
 
 
+# the prediction heads' two 1x1 convs (policy 128 -> 2, value 128 -> 1, same input) as one HIP pass forward and one
+# backward (gmz_head_conv1x1_*: dx of both heads in one rounding, dW / db reduced in a fixed order) instead of two
+# GEMMs + bias adds forward and two GEMMs + batched GEMMs + reductions + a dx add backward (False: PyTorch, A/B)
+FUSED_HEADS = True
+
+
+class _HeadConv1x1(torch.autograd.Function):
+    """(policy_conv(x), value_conv(x)) for a channels-last f16/bf16 hidden state x [n, 128, H, W] under autocast:
+    y0 [n, O0, H, W] and y1 [n, O1, H, W] channels-last (gmz_head_conv1x1_forward / _backward)."""
+
+    @staticmethod
+    def forward(ctx, x, w0, b0, w1, b1):
+        from . import _lib
+        L = _lib.load()
+        n, C, H, W = x.shape
+        O0, O1 = w0.shape[0], w1.shape[0]
+        P = n * H * W
+        wm = [_head_param(t, (O0, C)) for t in (w0, b0, w1, b1)]  # [O][C] rows / [O]: f32, contiguous views
+        y0 = torch.empty((n, H, W, O0), dtype=x.dtype, device=x.device)
+        y1 = torch.empty((n, H, W, O1), dtype=x.dtype, device=x.device)
+        _lib.check(L.gmz_head_conv1x1_forward(_BN_DTYPES[x.dtype], _lib.ptr(x), P, C, _lib.ptr(wm[0]), _lib.ptr(wm[1]),
+                                              O0, _lib.ptr(wm[2]), _lib.ptr(wm[3]), O1, _lib.ptr(y0), _lib.ptr(y1),
+                                              _lib.stream_ptr()))
+        ctx.save_for_backward(x, wm[0], wm[2], w0, b0, w1, b1)
+        ctx.O = (O0, O1)
+        return y0.permute(0, 3, 1, 2), y1.permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, g0, g1):
+        import ctypes
+        from . import _lib
+        L = _lib.load()
+        x, w0m, w1m, w0, b0, w1, b1 = ctx.saved_tensors
+        O0, O1 = ctx.O
+        n, C, H, W = x.shape
+        P = n * H * W
+        g0 = (g0 if g0 is not None else torch.zeros((n, O0, H, W), dtype=x.dtype, device=x.device))
+        g1 = (g1 if g1 is not None else torch.zeros((n, O1, H, W), dtype=x.dtype, device=x.device))
+        g0 = g0.to(x.dtype).permute(0, 2, 3, 1).contiguous()  # [n, H, W, O]: positions x outputs
+        g1 = g1.to(x.dtype).permute(0, 2, 3, 1).contiguous()
+        dx = torch.empty_like(x)  # channels-last like x
+        nb = ctypes.c_size_t()
+        _lib.check(L.gmz_head_conv1x1_workspace_bytes(P, O0 + O1, ctypes.byref(nb)))
+        ws = torch.empty(nb.value // 4, dtype=torch.float32, device=x.device)
+        params = (w0, b0, w1, b1)
+        # the trainer's own backward (_DIRECT_GRAD): add into the f32 .grad views of its flat bucket
+        direct = _DIRECT_GRAD[0] and all(p.grad is not None and p.grad.dtype == torch.float32
+                                         and p.grad.is_contiguous() for p in params)
+        outs = [p.grad if direct else torch.empty(p.shape, dtype=torch.float32, device=x.device) for p in params]
+        _lib.check(L.gmz_head_conv1x1_backward(_BN_DTYPES[x.dtype], _lib.ptr(x), P, C, _lib.ptr(w0m), O0, _lib.ptr(w1m), O1,
+                                               _lib.ptr(g0), _lib.ptr(g1), _lib.ptr(dx), *[_lib.ptr(t) for t in outs],
+                                               int(direct), _lib.ptr(ws), _lib.stream_ptr()))
+        if direct:
+            return dx, None, None, None, None
+        return (dx,) + tuple(t.to(p.dtype) for t, p in zip(outs, params))
+
+
+def _head_param(t, shape):
+    """a head conv's f32 weight [O, C, 1, 1] as its [O][C] rows (bias: as is), without a copy when it already is"""
+    t = t.detach()
+    t = t.reshape(t.shape[0], -1) if t.dim() > 1 else t
+    if t.dtype != torch.float32 or not t.is_contiguous():
+        t = t.float().contiguous()
+    return t
+
+
+def _head_convs_hip_ok(pred, h):
+    if not (FUSED_HEADS and h.is_cuda and torch.is_autocast_enabled("cuda") and h.dim() == 4 and h.shape[1] == 128):
+        return False
+    dt = torch.get_autocast_dtype("cuda")
+    return (dt in _CONV_DTYPES and h.dtype == dt and h.is_contiguous(memory_format=torch.channels_last)
+            and h.data_ptr() % 16 == 0 and pred.policy_conv.bias is not None and pred.value_conv.bias is not None)
+
+
 class _Prediction(nn.Module):
     def __init__(self, c, H, hd, vbins):
         super().__init__()
@@ -851,8 +925,13 @@ class _Prediction(nn.Module):
 
     def forward(self, h, mask=None):
         n = h.shape[0]
-        pol = self.policy_fc(_bn_act(self.policy_bn, _conv1x1(self.policy_conv, h), mask).reshape(n, -1))
-        v = F.relu(self.value_fc1(_bn_act(self.value_bn, _conv1x1(self.value_conv, h), mask).reshape(n, -1)))
+        if _head_convs_hip_ok(self, h):
+            yp, yv = _HeadConv1x1.apply(h, self.policy_conv.weight, self.policy_conv.bias, self.value_conv.weight,
+                                        self.value_conv.bias)
+        else:
+            yp, yv = _conv1x1(self.policy_conv, h), _conv1x1(self.value_conv, h)
+        pol = self.policy_fc(_bn_act(self.policy_bn, yp, mask).reshape(n, -1))
+        v = F.relu(self.value_fc1(_bn_act(self.value_bn, yv, mask).reshape(n, -1)))
         return pol, self.value_fc2(v)
 
 

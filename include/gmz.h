@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define GMZ_ABI_VERSION 8
+#define GMZ_ABI_VERSION 9
 
 /* ------------------------------------------------------------------ misc */
 const char *gmz_last_error(void);
@@ -416,6 +416,28 @@ int gmz_conv3x3_forward_bwdstats(int dtype, int H, const void *x_dev, const void
  * flattened in (p, c) order, added into the f32 .grad of W [O][C*P] (the reference's NCHW flatten,
  * network.py:95,105; loss.py:70-107 backward).  One add per element: the result is order-independent. */
 int gmz_grad_add_t(int dtype, const void *src_dev, int P, int C, int O, float *dst_dev, void *stream);
+
+/* ------------------------------------------------------------------ prediction heads' 1x1 convs (ABI 9)
+ * The two 1x1 convolutions of the prediction net (network.py:61,64: policy_conv 128 -> 2, value_conv 128 -> 1,
+ * both over the same hidden state, network.py:69-71) in one pass over a channels-last hidden state x_dev
+ * [P][128] (P = boards * H * W positions, 16-B aligned; dtype 0 = f32, 1 = f16, 2 = bf16): head 0's weight
+ * w0_dev f32 [O0][128] and bias b0_dev [O0] (or NULL), head 1's w1_dev [O1][128], b1_dev [O1] (or NULL);
+ * y0_dev [P][O0], y1_dev [P][O1] in x's dtype.
+ * W and b are rounded to x's dtype (autocast), accumulation in f32, one rounding of (sum + b).
+ * 1 <= O0, 0 <= O1, O0 + O1 <= 4.  Replaces torch.nn.Conv2d(128, O, 1) forward of both heads under autocast. */
+int gmz_head_conv1x1_forward(int dtype, const void *x_dev, long P, int C, const float *w0_dev, const float *b0_dev,
+                             int O0, const float *w1_dev, const float *b1_dev, int O1, void *y0_dev, void *y1_dev,
+                             void *stream);
+/* bytes of the backward's workspace for P positions and O = O0 + O1 outputs */
+int gmz_head_conv1x1_workspace_bytes(long P, int O, size_t *out);
+/* The backward of gmz_head_conv1x1_forward: dx_dev [P][128] = round(sum_o dy[p][o] W[o][c]) over BOTH heads
+ * (dy0_dev [P][O0], dy1_dev [P][O1], x's dtype; dx 16-B aligned), and the f32 parameter gradients dW0 [O0][128],
+ * db0 [O0], dW1 [O1][128], db1 [O1] (any may be NULL: skipped) = sum over positions, reduced in a fixed order
+ * (deterministic); accumulate != 0 adds into them.  ws_dev: gmz_head_conv1x1_workspace_bytes. */
+int gmz_head_conv1x1_backward(int dtype, const void *x_dev, long P, int C, const float *w0_dev, int O0,
+                              const float *w1_dev, int O1,
+                              const void *dy0_dev, const void *dy1_dev, void *dx_dev, float *dw0_dev, float *db0_dev,
+                              float *dw1_dev, float *db1_dev, int accumulate, void *ws_dev, void *stream);
 
 #ifdef __cplusplus
 }

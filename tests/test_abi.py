@@ -14,7 +14,7 @@ def test_library_exports_every_header_symbol():
     assert len(names) >= 25
     missing = [n for n in names if not hasattr(lib, n)]
     assert not missing, missing
-    assert lib.gmz_abi_version() == 8
+    assert lib.gmz_abi_version() == 9
 
 
 def test_product_package_never_imports_oracle():
