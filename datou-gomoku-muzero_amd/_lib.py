@@ -75,6 +75,7 @@ _SIGS = {
     "gmz_conv3x3_forward_bwdstats": ([I, I, P, P, P, P, I, P, P, P, P, I, P, P], I),
     "gmz_bn_backward_stats": ([I, P, P, P, P, I, I, I, P, P, I, P, P, P, P, P, I, P, P, I], I),
     "gmz_grad_add_t": ([I, P, I, I, I, P, P], I),
+    "gmz_grad_add_t_cols": ([I, P, I, I, I, I, I, P, P], I),
     "gmz_head_conv1x1_forward": ([I, P, L, I, P, P, I, P, P, I, P, P, P], I),
     "gmz_head_conv1x1_workspace_bytes": ([L, I, P], I),
     "gmz_head_conv1x1_backward": ([I, P, L, I, P, I, P, I, P, P, P, P, P, P, P, I, P, P], I),

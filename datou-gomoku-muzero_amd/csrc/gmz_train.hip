@@ -1057,15 +1057,16 @@ int bn_eval(int nhwc, const void *x, const void *res, int B, int C, int S, const
 // 64 x 64 (p, o) tile goes through LDS: reads coalesced along o, writes along p.  Each dst element
 // takes exactly one add, so the result equals any other order of the same additions.
 constexpr int GT = 64;
+// ldo / col0: src rows of ldo values, this weight's columns from col0 (the shared-input Linears' [K][O1 + O2] x^T dy)
 template <typename T>
 __global__ void __launch_bounds__(256) k_grad_add_t(const T *__restrict__ src, int P, int C, int O,
-                                                    float *__restrict__ dst) {
+                                                    float *__restrict__ dst, int ldo, int col0) {
   __shared__ float tile[GT][GT + 1];
   const int p0 = blockIdx.x * GT, o0 = blockIdx.y * GT, c = blockIdx.z;
   const int tx = threadIdx.x & (GT - 1), ty = threadIdx.x / GT;  // 64 x 4
   for (int r = ty; r < GT; r += 4) {
     const int p = p0 + r, o = o0 + tx;
-    tile[r][tx] = (p < P && o < O) ? ld(src, ((size_t)p * C + c) * O + o) : 0.f;
+    tile[r][tx] = (p < P && o < O) ? ld(src, ((size_t)p * C + c) * ldo + col0 + o) : 0.f;
   }
   __syncthreads();
   for (int r = ty; r < GT; r += 4) {
@@ -1079,22 +1080,32 @@ __global__ void __launch_bounds__(256) k_grad_add_t(const T *__restrict__ src, i
 
 using namespace gmz;
 
-GMZ_EXPORT int gmz_grad_add_t(int dtype, const void *src, int P, int C, int O, float *dst, void *stream) {
-  if (!src || !dst || P <= 0 || C <= 0 || O <= 0 || (size_t)P * C * O >= (1ull << 31))
+GMZ_EXPORT int gmz_grad_add_t_cols(int dtype, const void *src, int P, int C, int O, int ldo, int col0, float *dst,
+                                   void *stream) {
+  if (!src || !dst || P <= 0 || C <= 0 || O <= 0 || col0 < 0 || ldo < col0 + O || (size_t)P * C * ldo >= (1ull << 31))
     return fail("gmz_grad_add_t: bad arguments");
   if (C > 65535) return fail("gmz_grad_add_t: C must be <= 65535 (grid z)");
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid((P + GT - 1) / GT, (O + GT - 1) / GT, C);
   switch (dtype) {
-    case 0: hipLaunchKernelGGL(k_grad_add_t<float>, grid, dim3(256), 0, st, (const float *)src, P, C, O, dst); break;
-    case 1: hipLaunchKernelGGL(k_grad_add_t<__half>, grid, dim3(256), 0, st, (const __half *)src, P, C, O, dst); break;
+    case 0:
+      hipLaunchKernelGGL(k_grad_add_t<float>, grid, dim3(256), 0, st, (const float *)src, P, C, O, dst, ldo, col0);
+      break;
+    case 1:
+      hipLaunchKernelGGL(k_grad_add_t<__half>, grid, dim3(256), 0, st, (const __half *)src, P, C, O, dst, ldo, col0);
+      break;
     case 2:
-      hipLaunchKernelGGL(k_grad_add_t<__hip_bfloat16>, grid, dim3(256), 0, st, (const __hip_bfloat16 *)src, P, C, O, dst);
+      hipLaunchKernelGGL(k_grad_add_t<__hip_bfloat16>, grid, dim3(256), 0, st, (const __hip_bfloat16 *)src, P, C, O,
+                         dst, ldo, col0);
       break;
     default: return fail("gmz_grad_add_t: dtype must be 0 (f32), 1 (f16) or 2 (bf16)");
   }
   GMZ_LAUNCH_CHECK();
   return 0;
+}
+
+GMZ_EXPORT int gmz_grad_add_t(int dtype, const void *src, int P, int C, int O, float *dst, void *stream) {
+  return gmz_grad_add_t_cols(dtype, src, P, C, O, O, 0, dst, stream);
 }
 
 static int check_layout(int layout, int C) {

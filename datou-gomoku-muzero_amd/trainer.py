@@ -946,7 +946,9 @@ class _Dynamics(_Trunk):
         self._build(c + self.EMB, c, blocks)
         self.reward_fc = nn.Sequential(nn.Linear(c * H * H, hd), nn.ReLU(), nn.Linear(hd, rbins))
 
-    def forward(self, h, a, mask=None):
+    def forward(self, h, a, mask=None, reward=True):
+        """(next hidden state, reward logits); ``reward`` False: the trunk only (BATCHED_HEADS takes the reward head
+        of every unroll step after the unroll, in one pass)."""
         n, _, H, W = h.shape
         if _dyn_stem_hip_ok(self, h):  # DYN_STEM_HIP: the 144-channel conv as hidden-plane conv + action stamp
             dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else h.dtype
@@ -959,6 +961,8 @@ class _Dynamics(_Trunk):
             x = _bn_act(self.bn, y, mask)
             for blk in self.resblocks:
                 x = blk(x, mask)
+            if not reward:
+                return x, None
             fc0, act, fc2 = self.reward_fc
             return x, fc2(act(_linear_flat(fc0, x)))
         plane = F.one_hot(a, H * W).to(h.dtype).reshape(n, 1, H, W)
@@ -966,6 +970,8 @@ class _Dynamics(_Trunk):
         if h.is_contiguous(memory_format=torch.channels_last) and not h.is_contiguous():
             emb = emb.contiguous(memory_format=torch.channels_last)   # cat keeps channels-last
         nxt = super().forward(torch.cat((h, emb), dim=1), mask)
+        if not reward:
+            return nxt, None
         fc0, act, fc2 = self.reward_fc
         return nxt, fc2(act(_linear_flat(fc0, nxt)))
 
@@ -1042,6 +1048,85 @@ class _BigKLinear(torch.autograd.Function):
         return gx, gw, gb, None, None
 
 
+def _bigk_weight_cat(w1, w2, dt, perm):
+    """[w1; w2] in the autocast dtype and channels-last column order (_bigk_weight of each), cached on w1 per
+    optimiser step of both (version counters; inside a captured step the first use converts)."""
+    key = ("bigkcat", dt, perm, id(w2))
+    cache = w1.__dict__.setdefault("_gmz_pack", {})
+    hit = cache.get(key)
+    if hit is not None and hit[0] == (w1._version, w2._version):
+        return hit[1]
+    out = torch.cat((_bigk_weight(w1, dt, perm), _bigk_weight(w2, dt, perm)))
+    cache[key] = ((w1._version, w2._version), out)
+    return out
+
+
+class _BigKLinear2(torch.autograd.Function):
+    """(x W1^T + b1, x W2^T + b2) for two K = 28,800 Linears that read the same flattened hidden state — the
+    projection's fc1 (network.py:95) and the reward head's first Linear (network.py:105) of every unroll step — as
+    ONE split-K GEMM against [W1; W2] (_BigKLinear's arithmetic: f32 partial sums, one rounding).  Backward: one
+    dx GEMM against [W1; W2] (no add of two input gradients), one x^T dy GEMM whose two column ranges go into the
+    two weights' f32 .grad (gmz_grad_add_t_cols)."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, dt, perm=None):
+        xs, ws = x.to(dt), _bigk_weight_cat(w1, w2, dt, perm)
+        n, K = xs.shape
+        S = _BigKLinear.SPLIT if n <= 1024 else 4
+        y = torch.bmm(xs.view(n, S, K // S).transpose(0, 1), ws.view(-1, S, K // S).permute(1, 2, 0),
+                      out_dtype=torch.float32).sum(0)
+        y = (y + torch.cat((b1, b2)).float()).to(dt)
+        O1 = w1.shape[0]
+        ctx.save_for_backward(xs, ws, w1, w2)
+        ctx.perm, ctx.O1 = perm, O1
+        return y[:, :O1].contiguous(), y[:, O1:].contiguous()
+
+    @staticmethod
+    def backward(ctx, g1, g2):
+        xs, ws, w1, w2 = ctx.saved_tensors
+        n, O1 = xs.shape[0], ctx.O1
+        O2 = ws.shape[0] - O1
+        g1 = torch.zeros((n, O1), dtype=xs.dtype, device=xs.device) if g1 is None else g1.to(xs.dtype)
+        g2 = torch.zeros((n, O2), dtype=xs.dtype, device=xs.device) if g2 is None else g2.to(xs.dtype)
+        gy = torch.cat((g1, g2), 1)
+        gx = gy @ ws if ctx.needs_input_grad[0] else None
+        outs = [None, None, None, None]
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[3]:
+            gwt = xs.t() @ gy  # [K, O1 + O2] in x's column order
+            for i, (w, c0, O) in enumerate(((w1, 0, O1), (w2, O1, O2))):
+                if not ctx.needs_input_grad[1 + 2 * i]:
+                    continue
+                acc = (_DIRECT_GRAD[0] and w.grad is not None and w.grad.dtype == torch.float32
+                       and w.grad.is_contiguous())
+                if ctx.perm is None:
+                    outs[2 * i] = gwt[:, c0:c0 + O].t().to(w.dtype)
+                    continue
+                from . import _lib
+                C, HW = ctx.perm
+                dst = w.grad if acc else torch.zeros(w.shape, dtype=torch.float32, device=w.device)
+                _lib.check(_lib.load().gmz_grad_add_t_cols(_BN_DTYPES[gwt.dtype], _lib.ptr(gwt), HW, C, O, O1 + O2, c0,
+                                                          _lib.ptr(dst), _lib.stream_ptr()))
+                if not acc:
+                    outs[2 * i] = dst
+        if ctx.needs_input_grad[2] or ctx.needs_input_grad[4]:
+            gb = gy.sum(0, dtype=torch.float32)
+            outs[1], outs[3] = gb[:O1], gb[O1:]
+        return (gx, outs[0], outs[1], outs[2], outs[3], None, None)
+
+
+def _linear_flat_pair(lin1, lin2, h):
+    """(lin1(flat h), lin2(flat h)) — one _BigKLinear2 GEMM on the channels-last flatten under GPU autocast."""
+    n = h.shape[0]
+    if (FLAT_NHWC and h.is_cuda and torch.is_autocast_enabled("cuda") and h.dim() == 4 and not h.is_contiguous()
+            and h.is_contiguous(memory_format=torch.channels_last) and lin1.bias is not None and lin2.bias is not None):
+        C, HW = h.shape[1], h.shape[2] * h.shape[3]
+        K = C * HW
+        if (K >= 4096 and K % _BigKLinear.SPLIT == 0 and lin1.weight.shape[1] == K and lin2.weight.shape[1] == K):
+            return _BigKLinear2.apply(h.permute(0, 2, 3, 1).reshape(n, K), lin1.weight, lin1.bias, lin2.weight,
+                                      lin2.bias, torch.get_autocast_dtype("cuda"), (C, HW))
+    return _linear_flat(lin1, h), _linear_flat(lin2, h)
+
+
 def _linear(lin, x):
     """lin(x), with K = 28,800 Linears under GPU autocast on ``_BigKLinear``."""
     if (x.is_cuda and torch.is_autocast_enabled("cuda") and x.dim() == 2 and x.shape[1] >= 4096
@@ -1105,8 +1190,8 @@ class TrainNet(nn.Module):
     def prediction(self, h, mask=None):
         return self.prediction_net(h, mask)
 
-    def dynamics(self, h, a, mask=None):
-        return self.dynamics_net(h, a, mask)
+    def dynamics(self, h, a, mask=None, reward=True):
+        return self.dynamics_net(h, a, mask, reward)
 
     def project(self, h, with_grad=True, mask=None):
         if with_grad:
@@ -1249,6 +1334,93 @@ def consistency_representations(model, obs, masks):
     return list(th.split(B))
 
 
+# the heads of every unroll step taken after the unroll, each as ONE pass over the stacked steps (loss.py:70,96-106
+# call prediction / reward / projection once per step): the six predictions over [(U+1)B] rows, the five reward
+# heads and the five projections of the dynamics states over [UB] rows through one shared-input GEMM
+# (_BigKLinear2), the five consistency targets' projections over [UB] rows.  Every BatchNorm in them normalises each
+# step over ITS OWN live rows (_bn_seg_grad) and the running statistics are updated in the reference's call order
+# (the projection's: dynamics step s, then target s, step after step; _bn_running_update).  The heads only feed the
+# losses, so nothing in the unroll waits on them.  (False: per step, A/B)
+BATCHED_HEADS = True
+
+
+def _bn_seg_grad(mod, x, ms):
+    """Training-mode BatchNorm of ``ms.shape[0]`` equal row segments of x [(nseg*B), C(, H, W)] (autograd allowed),
+    segment s over its rows where ms[s] (bool [nseg, B]) is set — ``_bn`` of each segment, in float32 — WITHOUT the
+    running-statistics update: returns (y float32 shaped like x, (mean [nseg, C], unbiased var [nseg, C], ok [nseg]))
+    for ``_bn_running_update``."""
+    nseg, B = ms.shape
+    C = x.shape[1]
+    xv = x.float().reshape(nseg, B, C, -1)  # a view for channels-last 4-D (H, W merge)
+    S = xv.shape[3]
+    w = ms.to(torch.float32)[:, :, None, None]
+    nv = ms.sum(1)
+    n = nv.to(torch.float32) * S
+    ns = n.clamp(min=1.0)[:, None, None, None]
+    mean = (xv * w).sum((1, 3), keepdim=True) / ns
+    xc = xv - mean
+    var = (xc * xc * w).sum((1, 3), keepdim=True) / ns
+    y = xc * (torch.rsqrt(var + mod.eps) * mod.weight[:, None]) + mod.bias[:, None]
+    y = y.reshape(x.shape)
+    with torch.no_grad():
+        unb = var.reshape(nseg, C) * (n / (n - 1).clamp(min=1.0))[:, None]
+        st = (mean.reshape(nseg, C).detach(), unb.detach(), nv > 0)
+    return y, st
+
+
+def _bn_running_update(mod, stats):
+    """The running-statistics updates of a sequence of training-mode BatchNorm calls (``stats``: a list of
+    _bn_seg_grad results, applied in list order, segment by segment; a segment with no live row is skipped, as the
+    reference skips that step) in closed form: r <- r * prod_k f_k + sum_k m ok_k v_k prod_{j>k} f_j with
+    f_k = 1 - m ok_k — the sequential r <- (1 - m) r + m v_k of each call."""
+    with torch.no_grad():
+        mean = torch.cat([s[0] for s in stats])
+        var = torch.cat([s[1] for s in stats])
+        ok = torch.cat([s[2] for s in stats]).to(torch.float32)
+        m = mod.momentum
+        f = 1.0 - m * ok
+        suf = torch.flip(torch.cumprod(torch.flip(f, (0,)), 0), (0,))  # prod_{j >= k}
+        excl = torch.cat((suf[1:], torch.ones_like(suf[:1])))        # prod_{j > k}
+        a = (m * ok * excl)[:, None]
+        rm, rv = mod.running_mean.data, mod.running_var.data
+        rm.copy_(rm * suf[0] + (a * mean).sum(0))
+        rv.copy_(rv * suf[0] + (a * var).sum(0))
+        mod.num_batches_tracked.data += ok.sum().to(mod.num_batches_tracked.dtype)
+
+
+def _prediction_seg(pred, h, ms):
+    """prediction (network.py:67-73) of nseg stacked steps h [(nseg*B), 128, H, W], each step's BatchNorms over
+    its own rows ms [nseg, B]; returns (policy logits, value logits, [policy_bn stats, value_bn stats])."""
+    n = h.shape[0]
+    if _head_convs_hip_ok(pred, h):
+        yp, yv = _HeadConv1x1.apply(h, pred.policy_conv.weight, pred.policy_conv.bias, pred.value_conv.weight,
+                                    pred.value_conv.bias)
+    else:
+        yp, yv = _conv1x1(pred.policy_conv, h), _conv1x1(pred.value_conv, h)
+    bp, sp = _bn_seg_grad(pred.policy_bn, yp, ms)
+    bv, sv = _bn_seg_grad(pred.value_bn, yv, ms)
+    pol = pred.policy_fc(F.relu(bp).reshape(n, -1))
+    v = F.relu(pred.value_fc1(F.relu(bv).reshape(n, -1)))
+    return pol, pred.value_fc2(v), (sp, sv)
+
+
+def _reward_projection_seg(model, h, ms):
+    """The reward head (network.py:105-106) and the projection (loss.py:97: project(h, with_grad=True)) of U stacked
+    dynamics states h [(U*B), ...]: their first Linears in one GEMM (_linear_flat_pair), the projection's
+    BatchNorm per step over ms [U, B]; returns (reward logits, projection, bn1 stats)."""
+    proj = model.projection_net
+    fc0, act, fc2 = model.dynamics_net.reward_fc
+    a, r = _linear_flat_pair(proj.fc1, fc0, h)
+    b, st = _bn_seg_grad(proj.bn1, a, ms)
+    return fc2(act(r)), proj.fc2(F.relu(b)), st
+
+
+def _projection_seg(proj, h, ms):
+    """projection (loss.py:104: with_grad=False) of U stacked steps, BatchNorm per step; returns (z, bn1 stats)."""
+    b, st = _bn_seg_grad(proj.bn1, _linear_flat(proj.fc1, h), ms)
+    return proj.fc2(F.relu(b)), st
+
+
 def _side_streams(device):
     if device not in _SIDE_STREAMS:
         _SIDE_STREAMS[device] = (torch.cuda.Stream(device), torch.cuda.Stream(device))
@@ -1325,66 +1497,120 @@ def muzero_loss(model, target_model, batch, is_weights, cfg, k=None, flip=None, 
         elif BATCHED_CONSISTENCY and c.NUM_UNROLL_STEPS > 1:  # one stream: the batched pass right after obs[0]'s
             with torch.no_grad():
                 tru_h = consistency_representations(model, obs, [act[:, s] != -1 for s in range(c.NUM_UNROLL_STEPS)])
-        pl, vl = model.prediction(h)
-        lp = F.cross_entropy(pl.float(), pi[:, 0], reduction="none")
-        # the support targets of every step in two calls (the per-step calls were ~10 tiny kernels each)
-        # (step-major, so each step's [B, bins] block is contiguous)
-        zsup = scalar_to_support(z.t().contiguous(), *vsup)       # [U+1, B, bins]
-        rsupt = scalar_to_support(rew.t().contiguous(), *rsup)    # [U, B, bins]
-        lv = F.cross_entropy(vl.float(), zsup[0], reduction="none")
-        # loss.py:78 passes softmax(logits) to support_to_scalar, which applies softmax again:
-        # the PER priority is computed from that doubly-softmaxed value (kept as the reference does)
-        v0 = support_to_scalar(F.softmax(vl.float(), dim=1), *vsup)
-        td = (v0.detach()[:, 0] - z[:, 0]).abs()
-        lr_ = torch.zeros(obs.shape[0], device=obs.device)
-        steps = zero
-        cons = zero
         U = c.NUM_UNROLL_STEPS
-        per_step = []  # BATCHED_LOSS: each step's head outputs, their loss terms taken after the unroll
-        for s in range(U):
-            m = act[:, s] != -1
-            live = m.any().to(torch.float32)   # 0: the reference's `continue` (loss.py:90-91)
-            steps = steps + live
-            # full-batch step, row-masked BatchNorm statistics and losses (== the reference's
-            # sub-batch h[m] computation, loss.py:89-107, with fixed shapes)
-            hk, rl = model.dynamics(h, torch.where(m, act_aug[:, s], torch.zeros_like(act_aug[:, s])), mask=m)
-            plk, vlk = model.prediction(hk, mask=m)
-            if not BATCHED_LOSS:
-                lp = lp + torch.where(m, F.cross_entropy(plk.float(), pi[:, s + 1], reduction="none"), zero)
-                lv = lv + torch.where(m, F.cross_entropy(vlk.float(), zsup[s + 1],
-                                                         reduction="none"), zero)
-                lr_ = lr_ + torch.where(m, F.cross_entropy(rl.float(), rsupt[s],
-                                                           reduction="none"), zero)
-            dyn = model.project(hk, with_grad=True, mask=m)
-            with torch.no_grad():
-                if tru_h is not None and side is None:
-                    tru = model.project(tru_h[s], with_grad=False, mask=m)
-                elif tru_h is not None:
-                    main.wait_event(tru_ev[s])
-                    tru_h[s].record_stream(main)
-                    tru = model.project(tru_h[s], with_grad=False, mask=m)
-                else:
-                    tru = model.project(model.representation(obs[:, s + 1], mask=m), with_grad=False, mask=m)
-            if BATCHED_LOSS:
-                per_step.append((m, plk, vlk, rl, dyn, tru))
-            else:
-                cons = cons + live * barlow_loss(dyn, tru, c.BARLOW_LAMBDA, m)
-            h = _HalveGrad.apply(torch.where(m[:, None, None, None], hk, h))
-        if BATCHED_LOSS and U > 0:
-            # the U steps' cross-entropies and consistency losses as one call each over the stacked
-            # [U, B, .] outputs (masked rows zeroed, summed over the steps): the same per-row values as
-            # the per-step calls, ~5x fewer kernels in the forward and the backward
-            ms, pls, vls, rls, dyns, trus = (torch.stack(x) for x in zip(*per_step))
+        if BATCHED_HEADS and BATCHED_LOSS and not SUBBATCH_BN and U > 0:
+            # the unroll's dynamics chain first (trunks only), then every head over the stacked steps
+            zsup = scalar_to_support(z.t().contiguous(), *vsup)       # [U+1, B, bins]
+            rsupt = scalar_to_support(rew.t().contiguous(), *rsup)    # [U, B, bins]
+            h0, hks, mks = h, [], []
+            steps = zero
+            for s in range(U):
+                m = act[:, s] != -1
+                steps = steps + m.any().to(torch.float32)   # a step with no live row counts nothing (loss.py:90-91)
+                hk, _ = model.dynamics(h, torch.where(m, act_aug[:, s], torch.zeros_like(act_aug[:, s])), mask=m,
+                                       reward=False)
+                hks.append(hk)
+                mks.append(m)
+                h = _HalveGrad.apply(torch.where(m[:, None, None, None], hk, h))
+            ms = torch.stack(mks)                                      # [U, B]
             B = ms.shape[1]
+            hp = torch.cat([h0] + hks)                                 # [(U+1)B]: step-major, step 0 = obs[0]'s
+            pred = model.prediction_net
+            pls_all, vls_all, (sp, sv) = _prediction_seg(pred, hp, torch.cat((torch.ones_like(ms[:1]), ms)))
+            _bn_running_update(pred.policy_bn, [sp])
+            _bn_running_update(pred.value_bn, [sv])
+            rl_all, dyn_all, sdyn = _reward_projection_seg(model, hp[B:], ms)
+            with torch.no_grad():
+                if tru_h is None:
+                    tru_h = [model.representation(obs[:, s + 1], mask=mks[s]) for s in range(U)]
+                elif side is not None:
+                    main.wait_event(tru_ev[-1])
+                th = tru_h[0] if len(tru_h) == 1 else torch.cat(tru_h)
+                if side is not None:
+                    th.record_stream(main)
+                tru_all, stru = _projection_seg(model.projection_net, th, ms)
+            # the projection BatchNorm's running statistics in the reference's order: dynamics s, then target s
+            _bn_running_update(model.projection_net.bn1,
+                               [tuple(torch.stack((a, b), 1).reshape(2 * U, *a.shape[1:]) for a, b in zip(sdyn, stru))])
+            pl, vl = pls_all[:B], vls_all[:B]
+            lp = F.cross_entropy(pl.float(), pi[:, 0], reduction="none")
+            lv = F.cross_entropy(vl.float(), zsup[0], reduction="none")
+            # loss.py:78 passes softmax(logits) to support_to_scalar, which applies softmax again:
+            # the PER priority is computed from that doubly-softmaxed value (kept as the reference does)
+            v0 = support_to_scalar(F.softmax(vl.float(), dim=1), *vsup)
+            td = (v0.detach()[:, 0] - z[:, 0]).abs()
+            pls, vls = pls_all[B:].view(U, B, -1), vls_all[B:].view(U, B, -1)
+            rls, dyns, trus = rl_all.view(U, B, -1), dyn_all.view(U, B, -1), tru_all.view(U, B, -1)
 
             def ce(logits, target):
                 x = logits.float().reshape(U * B, -1)
                 return F.cross_entropy(x, target.reshape(U * B, -1), reduction="none").view(U, B)
             lp = lp + torch.where(ms, ce(pls, pi[:, 1:].transpose(0, 1)), zero).sum(0)
             lv = lv + torch.where(ms, ce(vls, zsup[1:]), zero).sum(0)
-            lr_ = lr_ + torch.where(ms, ce(rls, rsupt), zero).sum(0)
+            lr_ = torch.where(ms, ce(rls, rsupt), zero).sum(0)
             live_s = ms.any(1).to(torch.float32)
             cons = (live_s * barlow_loss_steps(dyns, trus, c.BARLOW_LAMBDA, ms)).sum()
+        else:
+            pl, vl = model.prediction(h)
+            lp = F.cross_entropy(pl.float(), pi[:, 0], reduction="none")
+            # the support targets of every step in two calls (the per-step calls were ~10 tiny kernels each)
+            # (step-major, so each step's [B, bins] block is contiguous)
+            zsup = scalar_to_support(z.t().contiguous(), *vsup)       # [U+1, B, bins]
+            rsupt = scalar_to_support(rew.t().contiguous(), *rsup)    # [U, B, bins]
+            lv = F.cross_entropy(vl.float(), zsup[0], reduction="none")
+            # loss.py:78 passes softmax(logits) to support_to_scalar, which applies softmax again:
+            # the PER priority is computed from that doubly-softmaxed value (kept as the reference does)
+            v0 = support_to_scalar(F.softmax(vl.float(), dim=1), *vsup)
+            td = (v0.detach()[:, 0] - z[:, 0]).abs()
+            lr_ = torch.zeros(obs.shape[0], device=obs.device)
+            steps = zero
+            cons = zero
+            U = c.NUM_UNROLL_STEPS
+            per_step = []  # BATCHED_LOSS: each step's head outputs, their loss terms taken after the unroll
+            for s in range(U):
+                m = act[:, s] != -1
+                live = m.any().to(torch.float32)   # 0: the reference's `continue` (loss.py:90-91)
+                steps = steps + live
+                # full-batch step, row-masked BatchNorm statistics and losses (== the reference's
+                # sub-batch h[m] computation, loss.py:89-107, with fixed shapes)
+                hk, rl = model.dynamics(h, torch.where(m, act_aug[:, s], torch.zeros_like(act_aug[:, s])), mask=m)
+                plk, vlk = model.prediction(hk, mask=m)
+                if not BATCHED_LOSS:
+                    lp = lp + torch.where(m, F.cross_entropy(plk.float(), pi[:, s + 1], reduction="none"), zero)
+                    lv = lv + torch.where(m, F.cross_entropy(vlk.float(), zsup[s + 1],
+                                                             reduction="none"), zero)
+                    lr_ = lr_ + torch.where(m, F.cross_entropy(rl.float(), rsupt[s],
+                                                               reduction="none"), zero)
+                dyn = model.project(hk, with_grad=True, mask=m)
+                with torch.no_grad():
+                    if tru_h is not None and side is None:
+                        tru = model.project(tru_h[s], with_grad=False, mask=m)
+                    elif tru_h is not None:
+                        main.wait_event(tru_ev[s])
+                        tru_h[s].record_stream(main)
+                        tru = model.project(tru_h[s], with_grad=False, mask=m)
+                    else:
+                        tru = model.project(model.representation(obs[:, s + 1], mask=m), with_grad=False, mask=m)
+                if BATCHED_LOSS:
+                    per_step.append((m, plk, vlk, rl, dyn, tru))
+                else:
+                    cons = cons + live * barlow_loss(dyn, tru, c.BARLOW_LAMBDA, m)
+                h = _HalveGrad.apply(torch.where(m[:, None, None, None], hk, h))
+            if BATCHED_LOSS and U > 0:
+                # the U steps' cross-entropies and consistency losses as one call each over the stacked
+                # [U, B, .] outputs (masked rows zeroed, summed over the steps): the same per-row values as
+                # the per-step calls, ~5x fewer kernels in the forward and the backward
+                ms, pls, vls, rls, dyns, trus = (torch.stack(x) for x in zip(*per_step))
+                B = ms.shape[1]
+
+                def ce(logits, target):
+                    x = logits.float().reshape(U * B, -1)
+                    return F.cross_entropy(x, target.reshape(U * B, -1), reduction="none").view(U, B)
+                lp = lp + torch.where(ms, ce(pls, pi[:, 1:].transpose(0, 1)), zero).sum(0)
+                lv = lv + torch.where(ms, ce(vls, zsup[1:]), zero).sum(0)
+                lr_ = lr_ + torch.where(ms, ce(rls, rsupt), zero).sum(0)
+                live_s = ms.any(1).to(torch.float32)
+                cons = (live_s * barlow_loss_steps(dyns, trus, c.BARLOW_LAMBDA, ms)).sum()
     lp = lp / (steps + 1)
     lv = lv / (steps + 1)
     lr_ = lr_ / steps.clamp(min=1.0)

@@ -416,6 +416,11 @@ int gmz_conv3x3_forward_bwdstats(int dtype, int H, const void *x_dev, const void
  * flattened in (p, c) order, added into the f32 .grad of W [O][C*P] (the reference's NCHW flatten,
  * network.py:95,105; loss.py:70-107 backward).  One add per element: the result is order-independent. */
 int gmz_grad_add_t(int dtype, const void *src_dev, int P, int C, int O, float *dst_dev, void *stream);
+/* gmz_grad_add_t over columns [col0, col0 + O) of src rows of ldo values: dst_dev[o][c][p] += src_dev[(p*C + c)*ldo
+ * + col0 + o] — one weight's share of the x^T dy of Linears that share their input (projection fc1 and reward_fc.0
+ * read the same flattened hidden state, network.py:95,105: one GEMM, [K][O1 + O2]).  (ABI 9) */
+int gmz_grad_add_t_cols(int dtype, const void *src_dev, int P, int C, int O, int ldo, int col0, float *dst_dev,
+                        void *stream);
 
 /* ------------------------------------------------------------------ prediction heads' 1x1 convs (ABI 9)
  * The two 1x1 convolutions of the prediction net (network.py:61,64: policy_conv 128 -> 2, value_conv 128 -> 1,

@@ -41,6 +41,10 @@ ap.add_argument("--hip-stem", action="store_true",
                 help="the dynamics trunk's 144-channel first conv on the HIP conv + action stamp (trainer.DYN_STEM_HIP on)")
 ap.add_argument("--per-step-consistency", action="store_true",
                 help="five consistency representations, one per unroll step (trainer.BATCHED_CONSISTENCY off)")
+ap.add_argument("--per-step-heads", action="store_true",
+                help="prediction / reward / projection heads once per unroll step (trainer.BATCHED_HEADS off)")
+ap.add_argument("--torch-head-convs", action="store_true",
+                help="the prediction heads' 1x1 convs on PyTorch GEMMs (trainer.FUSED_HEADS off)")
 ap.add_argument("--no-benchmark", action="store_true", help="no torch.backends.cudnn.benchmark (MIOpen Find per shape)")
 a = ap.parse_args()
 a.channels_last, a.benchmark = not a.nchw, not a.no_benchmark
@@ -62,6 +66,8 @@ T.FLAT_NHWC = T.FLAT_NHWC and not a.nchw_flatten
 T.FUSED_RES_GRAD = T.FUSED_RES_GRAD and not a.no_res_fold
 T.BATCHED_LOSS = T.BATCHED_LOSS and not a.per_step_loss
 T.BATCHED_CONSISTENCY = T.BATCHED_CONSISTENCY and not a.per_step_consistency
+T.BATCHED_HEADS = T.BATCHED_HEADS and not a.per_step_heads
+T.FUSED_HEADS = T.FUSED_HEADS and not a.torch_head_convs
 T.DYN_STEM_HIP = T.DYN_STEM_HIP or a.hip_stem
 T.RELU_MASK = T.RELU_MASK or a.relu_mask
 T.TARGET_F16 = T.TARGET_F16 and not a.target_f32
@@ -133,6 +139,7 @@ if rank == 0:
                       "batch_per_gpu": a.batch, "unroll": U, "board": a.size, "blocks": a.blocks, "amp": ("bf16" if a.bf16 else "fp16") if not a.no_amp else None, "channels_last": a.channels_last, "benchmark": a.benchmark, "graph": tr.graph,
                       "per": a.per, "sync_logs": a.sync_logs, "last_loss": logs[0], "data": "synthetic slices in a device ReplayBuffer",
                       "max_memory_allocated_gb": torch.cuda.max_memory_allocated() / 2 ** 30,
-                      "defer_wgrad": T.DEFER_WGRAD}))
+                      "defer_wgrad": T.DEFER_WGRAD, "batched_heads": T.BATCHED_HEADS, "fused_heads": T.FUSED_HEADS,
+                      "dyn_stem_hip": T.DYN_STEM_HIP, "relu_mask": T.RELU_MASK}))
 if dist:
     dist.destroy_process_group()

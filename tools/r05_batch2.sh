@@ -1,22 +1,22 @@
 #!/bin/bash
-# round 5 GPU batch 2: trainer — the batched consistency pass (tests, then a same-box A/B against the per-step
-# representations, and the fused BatchNorm finalisation: fusedfin), and the NET_FPC library A/B (fp contraction in the net / conv / train kernels) on the trainer
-# and the headline.
+# round 5 GPU batch 2: trainer — the batched heads and the fused head convs (tests, then a same-box A/B against the
+# per-step heads / PyTorch head convs), the HIP dynamics stem, the 1-bit ReLU masks, and the NET_FPC library A/B
+# (fp contraction in the net / conv / train kernels) on the trainer and the headline.
 set -o pipefail
 OUT=gpurun_out/r05_b2
 mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest tests/test_trainer.py -m gpu -x -v --timeout 300 --timeout-method thread \
-  -k "batched_consistency or concurrent_forward or production_training_step or elementwise or fused_bn_finalisation or relu_mask" > $OUT/tests.log 2>&1
+  -k "batched_consistency or concurrent_forward or production_training_step or elementwise or fused_bn_finalisation or relu_mask or head_conv1x1 or prediction_heads or bigk_linear or gpu_loss_and_gradients" > $OUT/tests.log 2>&1
 rc=$?
 grep -E "PASS|FAIL|^E  " $OUT/tests.log | tail -20
 [ $rc -eq 0 ] || exit $rc
 for i in 1 2; do
-  for V in base perstep hipstem relumask fusedfin fpc; do
+  for V in base perheads torchheads hipstem relumask fpc; do
     ARGS="--steps 30 --per"; ENV=""
-    [ $V = perstep ] && ARGS="$ARGS --per-step-consistency"
+    [ $V = perheads ] && ARGS="$ARGS --per-step-heads"
+    [ $V = torchheads ] && ARGS="$ARGS --torch-head-convs"
     [ $V = hipstem ] && ARGS="$ARGS --hip-stem"
     [ $V = relumask ] && ARGS="$ARGS --relu-mask"
-    [ $V = fusedfin ] && ENV="GMZ_BN_FUSED_FIN=1"
     [ $V = fpc ] && ENV="GMZ_LIB=$PWD/datou-gomoku-muzero_amd/_alt/libgmz_fpc.so"
     env $ENV timeout -k 10 200 python3 tools/bench_trainer.py $ARGS > $OUT/tr_${V}_$i.json 2> $OUT/tr_${V}_$i.err \
       || { echo "trainer $V failed"; tail -5 $OUT/tr_${V}_$i.err; exit 1; }
