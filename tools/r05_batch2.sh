@@ -6,7 +6,7 @@ set -o pipefail
 OUT=gpurun_out/r05_b2
 mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest tests/test_trainer.py -m gpu -x -v --timeout 300 --timeout-method thread \
-  -k "batched_consistency or concurrent_forward or production_training_step or elementwise or fused_bn_finalisation or relu_mask or head_conv1x1 or prediction_heads or bigk_linear or gpu_loss_and_gradients" > $OUT/tests.log 2>&1
+  -k "relu_mask or head_conv1x1 or prediction_heads or bigk_linear_pair" > $OUT/tests.log 2>&1
 rc=$?
 grep -E "PASS|FAIL|^E  " $OUT/tests.log | tail -20
 [ $rc -eq 0 ] || exit $rc
