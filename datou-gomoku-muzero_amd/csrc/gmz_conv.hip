@@ -32,6 +32,10 @@ typedef __bf16 b16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 typedef uint16_t u16x4_t __attribute__((ext_vector_type(4)));
 
+// depth of the weight-fragment register ring (k-steps in flight from L2): 3, the product; an A/B build sets 4 or 6
+#ifndef GMZ_CONV_RD
+#define GMZ_CONV_RD 3
+#endif
 constexpr int CC = 128;         // channels in and out
 constexpr int CKSTEPS = 36;     // 9 taps x 4 k-steps of 32 input channels
 constexpr int FRAG_BYTES = 294912;  // 36 k-steps x 8 n-tiles x 64 lanes x 16 B
@@ -130,7 +134,7 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
   using M = Mfma<T>;
   typedef typename M::V V;
   constexpr int A = H * H, NPT = (A + 15) / 16;
-  constexpr int NTW = 2, PTW = (NPT + PG - 1) / PG, RD = 3, NW = 2 * PG, NTHR = 64 * NW;
+  constexpr int NTW = 2, PTW = (NPT + PG - 1) / PG, RD = GMZ_CONV_RD, NW = 2 * PG, NTHR = 64 * NW;
   constexpr int PS = I::PS, RS = I::RS;
   static_assert(CKSTEPS % RD == 0, "ring slots repeat per item");
   __shared__ __attribute__((aligned(16))) uint8_t img[I::BYTES];

@@ -5,7 +5,7 @@ OUT=gpurun_out/r05_b4
 mkdir -p $OUT
 ( while sleep 60; do date >> $OUT/heartbeat; done ) &
 HB=$!
-timeout -k 10 900 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err
+timeout -k 10 700 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err
 rc=$?
 kill $HB
 tail -3 $OUT/bench.err
