@@ -946,9 +946,20 @@ class _Dynamics(_Trunk):
         self._build(c + self.EMB, c, blocks)
         self.reward_fc = nn.Sequential(nn.Linear(c * H * H, hd), nn.ReLU(), nn.Linear(hd, rbins))
 
-    def forward(self, h, a, mask=None, reward=True):
+    def embed(self, a, like):
+        """the action planes' embedding (network.py:88-90: one-hot plane -> 1x1 conv to 16 planes) for actions a
+        [n], in like's dtype and memory format"""
+        n, (H, W) = a.shape[0], like.shape[2:]
+        plane = F.one_hot(a, H * W).to(like.dtype).reshape(n, 1, H, W)
+        emb = _conv1x1(self.action_embed_conv, plane).to(like.dtype)
+        if like.is_contiguous(memory_format=torch.channels_last) and not like.is_contiguous():
+            emb = emb.contiguous(memory_format=torch.channels_last)   # cat keeps channels-last
+        return emb
+
+    def forward(self, h, a, mask=None, reward=True, emb=None):
         """(next hidden state, reward logits); ``reward`` False: the trunk only (BATCHED_HEADS takes the reward head
-        of every unroll step after the unroll, in one pass)."""
+        of every unroll step after the unroll, in one pass).  ``emb``: this step's action embedding, already computed
+        (BATCHED_HEADS embeds every step's action in one pass before the unroll)."""
         n, _, H, W = h.shape
         if _dyn_stem_hip_ok(self, h):  # DYN_STEM_HIP: the 144-channel conv as hidden-plane conv + action stamp
             dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else h.dtype
@@ -965,11 +976,9 @@ class _Dynamics(_Trunk):
                 return x, None
             fc0, act, fc2 = self.reward_fc
             return x, fc2(act(_linear_flat(fc0, x)))
-        plane = F.one_hot(a, H * W).to(h.dtype).reshape(n, 1, H, W)
-        emb = _conv1x1(self.action_embed_conv, plane).to(h.dtype)
-        if h.is_contiguous(memory_format=torch.channels_last) and not h.is_contiguous():
-            emb = emb.contiguous(memory_format=torch.channels_last)   # cat keeps channels-last
-        nxt = super().forward(torch.cat((h, emb), dim=1), mask)
+        if emb is None:
+            emb = self.embed(a, h)
+        nxt = super().forward(torch.cat((h, emb.to(h.dtype)), dim=1), mask)
         if not reward:
             return nxt, None
         fc0, act, fc2 = self.reward_fc
@@ -1190,8 +1199,8 @@ class TrainNet(nn.Module):
     def prediction(self, h, mask=None):
         return self.prediction_net(h, mask)
 
-    def dynamics(self, h, a, mask=None, reward=True):
-        return self.dynamics_net(h, a, mask, reward)
+    def dynamics(self, h, a, mask=None, reward=True, emb=None):
+        return self.dynamics_net(h, a, mask, reward, emb)
 
     def project(self, h, with_grad=True, mask=None):
         if with_grad:
@@ -1504,11 +1513,16 @@ def muzero_loss(model, target_model, batch, is_weights, cfg, k=None, flip=None, 
             rsupt = scalar_to_support(rew.t().contiguous(), *rsup)    # [U, B, bins]
             h0, hks, mks = h, [], []
             steps = zero
+            live_act = act != -1                                        # [B, U]
+            a_all = torch.where(live_act, act_aug, torch.zeros_like(act_aug)).t().reshape(-1)  # step-major [U*B]
+            dyn_net = model.dynamics_net
+            emb_all = None if _dyn_stem_hip_ok(dyn_net, h) else dyn_net.embed(a_all, h)  # every step's embedding
+            B0 = h.shape[0]
             for s in range(U):
-                m = act[:, s] != -1
+                m = live_act[:, s]
                 steps = steps + m.any().to(torch.float32)   # a step with no live row counts nothing (loss.py:90-91)
-                hk, _ = model.dynamics(h, torch.where(m, act_aug[:, s], torch.zeros_like(act_aug[:, s])), mask=m,
-                                       reward=False)
+                hk, _ = model.dynamics(h, a_all[s * B0:(s + 1) * B0], mask=m, reward=False,
+                                       emb=None if emb_all is None else emb_all[s * B0:(s + 1) * B0])
                 hks.append(hk)
                 mks.append(m)
                 h = _HalveGrad.apply(torch.where(m[:, None, None, None], hk, h))
