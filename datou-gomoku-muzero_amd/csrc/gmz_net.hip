@@ -268,8 +268,10 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
     finish_launch();
     return;
   }
-  const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   constexpr bool PP = PIPE != 0;
+  // PIPE branches per half on w: a scalar there.  Elsewhere w stays a VGPR value: a scalar w changed the product
+  // kernels' register allocation (19x19: 39 instead of 12 scratch reloads; 15x15: +3 % instructions)
+  const int tid = threadIdx.x, w = PP ? __builtin_amdgcn_readfirstlane(tid >> 6) : tid >> 6, lane = tid & 63;
   static_assert(!PP || (NB == 1 && !ONE && NQ == 4 && PG == 2), "the half pipeline is the 15x15 8-wave two-image tower's");
   // wave w -> (channel group nh, position group pg) = (w % NQ, w / NQ): the waves sharing a SIMD
   // (w, w+4, ...) get different position groups, so a short last group does not load one SIMD less.

@@ -846,55 +846,68 @@ class _Trunk(nn.Module):
 FUSED_HEADS = True
 
 
+def _headconv_forward(x, w0, b0, w1, b1):
+    """gmz_head_conv1x1_forward of the channels-last x: (y0, y1) channels-last [n, O, H, W] and what the backward
+    needs"""
+    from . import _lib
+    L = _lib.load()
+    n, C, H, W = x.shape
+    O0, O1 = w0.shape[0], w1.shape[0]
+    P = n * H * W
+    wm = [_head_param(t, (O0, C)) for t in (w0, b0, w1, b1)]  # [O][C] rows / [O]: f32, contiguous views
+    y0 = torch.empty((n, H, W, O0), dtype=x.dtype, device=x.device)
+    y1 = torch.empty((n, H, W, O1), dtype=x.dtype, device=x.device)
+    _lib.check(L.gmz_head_conv1x1_forward(_BN_DTYPES[x.dtype], _lib.ptr(x), P, C, _lib.ptr(wm[0]), _lib.ptr(wm[1]),
+                                          O0, _lib.ptr(wm[2]), _lib.ptr(wm[3]), O1, _lib.ptr(y0), _lib.ptr(y1),
+                                          _lib.stream_ptr()))
+    return y0.permute(0, 3, 1, 2), y1.permute(0, 3, 1, 2), (wm[0], wm[2], (O0, O1))
+
+
+def _headconv_backward(x, saved, params, g0, g1):
+    """gmz_head_conv1x1_backward: (dx channels-last like x, the four parameter gradients — None when they went
+    straight into the trainer's f32 .grad, _DIRECT_GRAD)"""
+    import ctypes
+    from . import _lib
+    L = _lib.load()
+    w0m, w1m, (O0, O1) = saved
+    n, C, H, W = x.shape
+    P = n * H * W
+    g0 = (g0 if g0 is not None else torch.zeros((n, O0, H, W), dtype=x.dtype, device=x.device))
+    g1 = (g1 if g1 is not None else torch.zeros((n, O1, H, W), dtype=x.dtype, device=x.device))
+    g0 = g0.to(x.dtype).permute(0, 2, 3, 1).contiguous()  # [n, H, W, O]: positions x outputs
+    g1 = g1.to(x.dtype).permute(0, 2, 3, 1).contiguous()
+    dx = torch.empty_like(x)  # channels-last like x
+    nb = ctypes.c_size_t()
+    _lib.check(L.gmz_head_conv1x1_workspace_bytes(P, O0 + O1, ctypes.byref(nb)))
+    ws = torch.empty(nb.value // 4, dtype=torch.float32, device=x.device)
+    # the trainer's own backward (_DIRECT_GRAD): add into the f32 .grad views of its flat bucket
+    direct = _DIRECT_GRAD[0] and all(p.grad is not None and p.grad.dtype == torch.float32
+                                     and p.grad.is_contiguous() for p in params)
+    outs = [p.grad if direct else torch.empty(p.shape, dtype=torch.float32, device=x.device) for p in params]
+    _lib.check(L.gmz_head_conv1x1_backward(_BN_DTYPES[x.dtype], _lib.ptr(x), P, C, _lib.ptr(w0m), O0, _lib.ptr(w1m), O1,
+                                           _lib.ptr(g0), _lib.ptr(g1), _lib.ptr(dx), *[_lib.ptr(t) for t in outs],
+                                           int(direct), _lib.ptr(ws), _lib.stream_ptr()))
+    if direct:
+        return dx, [None] * 4
+    return dx, [t.to(p.dtype) for t, p in zip(outs, params)]
+
+
 class _HeadConv1x1(torch.autograd.Function):
     """(policy_conv(x), value_conv(x)) for a channels-last f16/bf16 hidden state x [n, 128, H, W] under autocast:
     y0 [n, O0, H, W] and y1 [n, O1, H, W] channels-last (gmz_head_conv1x1_forward / _backward)."""
 
     @staticmethod
     def forward(ctx, x, w0, b0, w1, b1):
-        from . import _lib
-        L = _lib.load()
-        n, C, H, W = x.shape
-        O0, O1 = w0.shape[0], w1.shape[0]
-        P = n * H * W
-        wm = [_head_param(t, (O0, C)) for t in (w0, b0, w1, b1)]  # [O][C] rows / [O]: f32, contiguous views
-        y0 = torch.empty((n, H, W, O0), dtype=x.dtype, device=x.device)
-        y1 = torch.empty((n, H, W, O1), dtype=x.dtype, device=x.device)
-        _lib.check(L.gmz_head_conv1x1_forward(_BN_DTYPES[x.dtype], _lib.ptr(x), P, C, _lib.ptr(wm[0]), _lib.ptr(wm[1]),
-                                              O0, _lib.ptr(wm[2]), _lib.ptr(wm[3]), O1, _lib.ptr(y0), _lib.ptr(y1),
-                                              _lib.stream_ptr()))
-        ctx.save_for_backward(x, wm[0], wm[2], w0, b0, w1, b1)
-        ctx.O = (O0, O1)
-        return y0.permute(0, 3, 1, 2), y1.permute(0, 3, 1, 2)
+        y0, y1, saved = _headconv_forward(x, w0, b0, w1, b1)
+        ctx.save_for_backward(x, saved[0], saved[1], w0, b0, w1, b1)
+        ctx.O = saved[2]
+        return y0, y1
 
     @staticmethod
     def backward(ctx, g0, g1):
-        import ctypes
-        from . import _lib
-        L = _lib.load()
         x, w0m, w1m, w0, b0, w1, b1 = ctx.saved_tensors
-        O0, O1 = ctx.O
-        n, C, H, W = x.shape
-        P = n * H * W
-        g0 = (g0 if g0 is not None else torch.zeros((n, O0, H, W), dtype=x.dtype, device=x.device))
-        g1 = (g1 if g1 is not None else torch.zeros((n, O1, H, W), dtype=x.dtype, device=x.device))
-        g0 = g0.to(x.dtype).permute(0, 2, 3, 1).contiguous()  # [n, H, W, O]: positions x outputs
-        g1 = g1.to(x.dtype).permute(0, 2, 3, 1).contiguous()
-        dx = torch.empty_like(x)  # channels-last like x
-        nb = ctypes.c_size_t()
-        _lib.check(L.gmz_head_conv1x1_workspace_bytes(P, O0 + O1, ctypes.byref(nb)))
-        ws = torch.empty(nb.value // 4, dtype=torch.float32, device=x.device)
-        params = (w0, b0, w1, b1)
-        # the trainer's own backward (_DIRECT_GRAD): add into the f32 .grad views of its flat bucket
-        direct = _DIRECT_GRAD[0] and all(p.grad is not None and p.grad.dtype == torch.float32
-                                         and p.grad.is_contiguous() for p in params)
-        outs = [p.grad if direct else torch.empty(p.shape, dtype=torch.float32, device=x.device) for p in params]
-        _lib.check(L.gmz_head_conv1x1_backward(_BN_DTYPES[x.dtype], _lib.ptr(x), P, C, _lib.ptr(w0m), O0, _lib.ptr(w1m), O1,
-                                               _lib.ptr(g0), _lib.ptr(g1), _lib.ptr(dx), *[_lib.ptr(t) for t in outs],
-                                               int(direct), _lib.ptr(ws), _lib.stream_ptr()))
-        if direct:
-            return dx, None, None, None, None
-        return (dx,) + tuple(t.to(p.dtype) for t, p in zip(outs, params))
+        dx, gp = _headconv_backward(x, (w0m, w1m, ctx.O), (w0, b0, w1, b1), g0, g1)
+        return (dx, *gp)
 
 
 def _head_param(t, shape):
@@ -1070,6 +1083,57 @@ def _bigk_weight_cat(w1, w2, dt, perm):
     return out
 
 
+def _bigk2_forward(x, w1, b1, w2, b2, dt, perm):
+    """(x W1^T + b1, x W2^T + b2) as one split-K GEMM against [W1; W2] (x [n, K] in the flatten order of perm)."""
+    xs, ws = x.to(dt), _bigk_weight_cat(w1, w2, dt, perm)
+    n, K = xs.shape
+    S = _BigKLinear.SPLIT if n <= 1024 else 4
+    y = torch.bmm(xs.view(n, S, K // S).transpose(0, 1), ws.view(-1, S, K // S).permute(1, 2, 0),
+                  out_dtype=torch.float32).sum(0)
+    y = (y + torch.cat((b1, b2)).float()).to(dt)
+    O1 = w1.shape[0]
+    return y[:, :O1].contiguous(), y[:, O1:].contiguous(), xs, ws
+
+
+def _bigk2_backward(xs, ws, w1, w2, perm, g1, g2, needs, gx_acc=None):
+    """The backward of _bigk2_forward: gx = [g1 g2] [W1; W2] — returned, or added in place into gx_acc (a [n, K]
+    view of a gradient that another consumer of x already wrote: one GEMM with beta = 1 instead of a GEMM and an
+    add) — and the four parameter gradients (needs: which of w1, b1, w2, b2; the weights' go straight into their
+    f32 .grad under _DIRECT_GRAD, as None)."""
+    n, O1 = xs.shape[0], w1.shape[0]
+    O2 = ws.shape[0] - O1
+    g1 = torch.zeros((n, O1), dtype=xs.dtype, device=xs.device) if g1 is None else g1.to(xs.dtype)
+    g2 = torch.zeros((n, O2), dtype=xs.dtype, device=xs.device) if g2 is None else g2.to(xs.dtype)
+    gy = torch.cat((g1, g2), 1)
+    gx = None
+    if gx_acc is not None:
+        gx_acc.addmm_(gy, ws)
+    elif needs[0]:
+        gx = gy @ ws
+    outs = [None, None, None, None]
+    if needs[1] or needs[3]:
+        gwt = xs.t() @ gy  # [K, O1 + O2] in x's column order
+        for i, (w, c0, O) in enumerate(((w1, 0, O1), (w2, O1, O2))):
+            if not needs[1 + 2 * i]:
+                continue
+            acc = (_DIRECT_GRAD[0] and w.grad is not None and w.grad.dtype == torch.float32
+                   and w.grad.is_contiguous())
+            if perm is None:
+                outs[2 * i] = gwt[:, c0:c0 + O].t().to(w.dtype)
+                continue
+            from . import _lib
+            C, HW = perm
+            dst = w.grad if acc else torch.zeros(w.shape, dtype=torch.float32, device=w.device)
+            _lib.check(_lib.load().gmz_grad_add_t_cols(_BN_DTYPES[gwt.dtype], _lib.ptr(gwt), HW, C, O, O1 + O2, c0,
+                                                      _lib.ptr(dst), _lib.stream_ptr()))
+            if not acc:
+                outs[2 * i] = dst
+    if needs[2] or needs[4]:
+        gb = gy.sum(0, dtype=torch.float32)
+        outs[1], outs[3] = gb[:O1], gb[O1:]
+    return gx, outs
+
+
 class _BigKLinear2(torch.autograd.Function):
     """(x W1^T + b1, x W2^T + b2) for two K = 28,800 Linears that read the same flattened hidden state — the
     projection's fc1 (network.py:95) and the reward head's first Linear (network.py:105) of every unroll step — as
@@ -1079,48 +1143,45 @@ class _BigKLinear2(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w1, b1, w2, b2, dt, perm=None):
-        xs, ws = x.to(dt), _bigk_weight_cat(w1, w2, dt, perm)
-        n, K = xs.shape
-        S = _BigKLinear.SPLIT if n <= 1024 else 4
-        y = torch.bmm(xs.view(n, S, K // S).transpose(0, 1), ws.view(-1, S, K // S).permute(1, 2, 0),
-                      out_dtype=torch.float32).sum(0)
-        y = (y + torch.cat((b1, b2)).float()).to(dt)
-        O1 = w1.shape[0]
+        y1, y2, xs, ws = _bigk2_forward(x, w1, b1, w2, b2, dt, perm)
         ctx.save_for_backward(xs, ws, w1, w2)
-        ctx.perm, ctx.O1 = perm, O1
-        return y[:, :O1].contiguous(), y[:, O1:].contiguous()
+        ctx.perm = perm
+        return y1, y2
 
     @staticmethod
     def backward(ctx, g1, g2):
         xs, ws, w1, w2 = ctx.saved_tensors
-        n, O1 = xs.shape[0], ctx.O1
-        O2 = ws.shape[0] - O1
-        g1 = torch.zeros((n, O1), dtype=xs.dtype, device=xs.device) if g1 is None else g1.to(xs.dtype)
-        g2 = torch.zeros((n, O2), dtype=xs.dtype, device=xs.device) if g2 is None else g2.to(xs.dtype)
-        gy = torch.cat((g1, g2), 1)
-        gx = gy @ ws if ctx.needs_input_grad[0] else None
-        outs = [None, None, None, None]
-        if ctx.needs_input_grad[1] or ctx.needs_input_grad[3]:
-            gwt = xs.t() @ gy  # [K, O1 + O2] in x's column order
-            for i, (w, c0, O) in enumerate(((w1, 0, O1), (w2, O1, O2))):
-                if not ctx.needs_input_grad[1 + 2 * i]:
-                    continue
-                acc = (_DIRECT_GRAD[0] and w.grad is not None and w.grad.dtype == torch.float32
-                       and w.grad.is_contiguous())
-                if ctx.perm is None:
-                    outs[2 * i] = gwt[:, c0:c0 + O].t().to(w.dtype)
-                    continue
-                from . import _lib
-                C, HW = ctx.perm
-                dst = w.grad if acc else torch.zeros(w.shape, dtype=torch.float32, device=w.device)
-                _lib.check(_lib.load().gmz_grad_add_t_cols(_BN_DTYPES[gwt.dtype], _lib.ptr(gwt), HW, C, O, O1 + O2, c0,
-                                                          _lib.ptr(dst), _lib.stream_ptr()))
-                if not acc:
-                    outs[2 * i] = dst
-        if ctx.needs_input_grad[2] or ctx.needs_input_grad[4]:
-            gb = gy.sum(0, dtype=torch.float32)
-            outs[1], outs[3] = gb[:O1], gb[O1:]
-        return (gx, outs[0], outs[1], outs[2], outs[3], None, None)
+        gx, outs = _bigk2_backward(xs, ws, w1, w2, ctx.perm, g1, g2, ctx.needs_input_grad[:5])
+        return (gx, *outs, None, None)
+
+
+class _HeadsInput(torch.autograd.Function):
+    """The first layer of every head that reads the stacked hidden states hp [(U+1)*B, 128, H, W] (BATCHED_HEADS):
+    the prediction's two 1x1 convs over all U+1 steps (gmz_head_conv1x1) and the projection fc1 + reward fc0 GEMM
+    over the U dynamics steps hp[B:] (_bigk2_forward) — in ONE autograd node, so hp's gradient is the convs' dx with
+    the GEMM's dx added in place into its last U*B rows (addmm_, beta = 1) instead of autograd padding the slice's
+    gradient to hp's shape and adding the two (a 124 MB zero fill, copy and add per step)."""
+
+    @staticmethod
+    def forward(ctx, hp, B, wp, bp, wv, bv, w1, b1, w2, b2, dt, perm):
+        yp, yv, hsaved = _headconv_forward(hp, wp, bp, wv, bv)
+        n, C, H, W = hp.shape
+        a, r, xs, ws = _bigk2_forward(hp[B:].permute(0, 2, 3, 1).reshape(n - B, C * H * W), w1, b1, w2, b2, dt, perm)
+        ctx.save_for_backward(hp, hsaved[0], hsaved[1], wp, bp, wv, bv, ws, w1, w2)
+        ctx.O, ctx.B, ctx.perm = hsaved[2], B, perm
+        return yp, yv, a, r
+
+    @staticmethod
+    def backward(ctx, gyp, gyv, ga, gr):
+        hp, w0m, w1m, wp, bp, wv, bv, ws, w1, w2 = ctx.saved_tensors
+        B = ctx.B
+        dx, gh = _headconv_backward(hp, (w0m, w1m, ctx.O), (wp, bp, wv, bv), gyp, gyv)
+        n, C, H, W = hp.shape
+        xs = hp[B:].permute(0, 2, 3, 1).reshape(n - B, C * H * W)
+        gview = dx[B:].permute(0, 2, 3, 1).view(n - B, C * H * W)  # channels-last rows: a view of dx
+        needs = ctx.needs_input_grad
+        _, gb = _bigk2_backward(xs, ws, w1, w2, ctx.perm, ga, gr, (False,) + tuple(needs[6:10]), gx_acc=gview)
+        return (dx, None, *gh, *gb, None, None)
 
 
 def _linear_flat_pair(lin1, lin2, h):
@@ -1397,11 +1458,30 @@ def _bn_running_update(mod, stats):
         mod.num_batches_tracked.data += ok.sum().to(mod.num_batches_tracked.dtype)
 
 
-def _prediction_seg(pred, h, ms):
+def _heads_input(model, hp, B):
+    """_HeadsInput (the prediction convs and the projection fc1 + reward fc0 GEMM as one autograd node) when both
+    fast paths apply, else None."""
+    pred, proj = model.prediction_net, model.projection_net
+    fc0 = model.dynamics_net.reward_fc[0]
+    if not (_head_convs_hip_ok(pred, hp) and FLAT_NHWC and fc0.bias is not None and proj.fc1.bias is not None):
+        return None
+    C, HW = hp.shape[1], hp.shape[2] * hp.shape[3]
+    K = C * HW
+    if not (K % _BigKLinear.SPLIT == 0 and proj.fc1.weight.shape[1] == K and fc0.weight.shape[1] == K):
+        return None
+    return _HeadsInput.apply(hp, B, pred.policy_conv.weight, pred.policy_conv.bias, pred.value_conv.weight,
+                             pred.value_conv.bias, proj.fc1.weight, proj.fc1.bias, fc0.weight, fc0.bias,
+                             torch.get_autocast_dtype("cuda"), (C, HW))
+
+
+def _prediction_seg(pred, h, ms, convs=None):
     """prediction (network.py:67-73) of nseg stacked steps h [(nseg*B), 128, H, W], each step's BatchNorms over
-    its own rows ms [nseg, B]; returns (policy logits, value logits, [policy_bn stats, value_bn stats])."""
+    its own rows ms [nseg, B]; returns (policy logits, value logits, [policy_bn stats, value_bn stats]).
+    ``convs``: the two 1x1 convs' outputs, already computed (_HeadsInput)."""
     n = h.shape[0]
-    if _head_convs_hip_ok(pred, h):
+    if convs is not None:
+        yp, yv = convs
+    elif _head_convs_hip_ok(pred, h):
         yp, yv = _HeadConv1x1.apply(h, pred.policy_conv.weight, pred.policy_conv.bias, pred.value_conv.weight,
                                     pred.value_conv.bias)
     else:
@@ -1413,13 +1493,14 @@ def _prediction_seg(pred, h, ms):
     return pol, pred.value_fc2(v), (sp, sv)
 
 
-def _reward_projection_seg(model, h, ms):
+def _reward_projection_seg(model, h, ms, first=None):
     """The reward head (network.py:105-106) and the projection (loss.py:97: project(h, with_grad=True)) of U stacked
     dynamics states h [(U*B), ...]: their first Linears in one GEMM (_linear_flat_pair), the projection's
-    BatchNorm per step over ms [U, B]; returns (reward logits, projection, bn1 stats)."""
+    BatchNorm per step over ms [U, B]; returns (reward logits, projection, bn1 stats).  ``first``: the two first
+    Linears' outputs, already computed (_HeadsInput)."""
     proj = model.projection_net
     fc0, act, fc2 = model.dynamics_net.reward_fc
-    a, r = _linear_flat_pair(proj.fc1, fc0, h)
+    a, r = first if first is not None else _linear_flat_pair(proj.fc1, fc0, h)
     b, st = _bn_seg_grad(proj.bn1, a, ms)
     return fc2(act(r)), proj.fc2(F.relu(b)), st
 
@@ -1513,13 +1594,13 @@ def muzero_loss(model, target_model, batch, is_weights, cfg, k=None, flip=None, 
             rsupt = scalar_to_support(rew.t().contiguous(), *rsup)    # [U, B, bins]
             h0, hks, mks = h, [], []
             steps = zero
-            live_act = act != -1                                        # [B, U]
-            a_all = torch.where(live_act, act_aug, torch.zeros_like(act_aug)).t().reshape(-1)  # step-major [U*B]
+            live_act = (act != -1).t().contiguous()                     # [U, B]: each step's mask a contiguous row
+            a_all = torch.where(live_act, act_aug.t(), torch.zeros_like(act_aug.t())).reshape(-1)  # step-major [U*B]
             dyn_net = model.dynamics_net
             emb_all = None if _dyn_stem_hip_ok(dyn_net, h) else dyn_net.embed(a_all, h)  # every step's embedding
             B0 = h.shape[0]
             for s in range(U):
-                m = live_act[:, s]
+                m = live_act[s]
                 steps = steps + m.any().to(torch.float32)   # a step with no live row counts nothing (loss.py:90-91)
                 hk, _ = model.dynamics(h, a_all[s * B0:(s + 1) * B0], mask=m, reward=False,
                                        emb=None if emb_all is None else emb_all[s * B0:(s + 1) * B0])
@@ -1530,10 +1611,12 @@ def muzero_loss(model, target_model, batch, is_weights, cfg, k=None, flip=None, 
             B = ms.shape[1]
             hp = torch.cat([h0] + hks)                                 # [(U+1)B]: step-major, step 0 = obs[0]'s
             pred = model.prediction_net
-            pls_all, vls_all, (sp, sv) = _prediction_seg(pred, hp, torch.cat((torch.ones_like(ms[:1]), ms)))
+            msp = torch.cat((torch.ones_like(ms[:1]), ms))
+            first = _heads_input(model, hp, B)  # the heads' first layers in one node (None: no fused path)
+            pls_all, vls_all, (sp, sv) = _prediction_seg(pred, hp, msp, None if first is None else first[:2])
             _bn_running_update(pred.policy_bn, [sp])
             _bn_running_update(pred.value_bn, [sv])
-            rl_all, dyn_all, sdyn = _reward_projection_seg(model, hp[B:], ms)
+            rl_all, dyn_all, sdyn = _reward_projection_seg(model, hp[B:], ms, None if first is None else first[2:])
             with torch.no_grad():
                 if tru_h is None:
                     tru_h = [model.representation(obs[:, s + 1], mask=mks[s]) for s in range(U)]
