@@ -1401,7 +1401,14 @@ def consistency_representations(model, obs, masks):
     U, B = len(masks), obs.shape[0]
     o = obs[:, 1:U + 1].transpose(0, 1).reshape(U * B, *obs.shape[2:])  # step-major: segment s = step s
     th = model.representation(o, mask=torch.stack(masks).reshape(U * B), segments=U)
-    return list(th.split(B))
+    out = _StepList(th.split(B))
+    out.stacked = th  # the batched heads take the U steps as this one tensor (no re-concatenation)
+    return out
+
+
+class _StepList(list):
+    """per-step tensors that are consecutive row blocks of one tensor, ``stacked``"""
+    stacked = None
 
 
 # the heads of every unroll step taken after the unroll, each as ONE pass over the stacked steps (loss.py:70,96-106
@@ -1622,7 +1629,9 @@ def muzero_loss(model, target_model, batch, is_weights, cfg, k=None, flip=None, 
                     tru_h = [model.representation(obs[:, s + 1], mask=mks[s]) for s in range(U)]
                 elif side is not None:
                     main.wait_event(tru_ev[-1])
-                th = tru_h[0] if len(tru_h) == 1 else torch.cat(tru_h)
+                th = getattr(tru_h, "stacked", None)
+                if th is None:
+                    th = tru_h[0] if len(tru_h) == 1 else torch.cat(tru_h)
                 if side is not None:
                     th.record_stream(main)
                 tru_all, stru = _projection_seg(model.projection_net, th, ms)
