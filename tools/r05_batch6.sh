@@ -23,7 +23,7 @@ for i in 1 2; do
     python3 -c "import json; d=json.load(open('$OUT/tr_${V}_$i.json')); print('trainer %-8s %d %.2f steps/s' % ('$V', $i, d['value']))" | tee -a $OUT/summary.txt
   done
 done
-for i in 1 2; do
+for i in 1; do
   for V in base rd4 rd6; do
     ENV=""; [ $V != base ] && ENV="GMZ_LIB=$PWD/datou-gomoku-muzero_amd/_alt/libgmz_$V.so"
     for N in 360 1800; do
@@ -39,3 +39,4 @@ import json; d=json.load(open('$OUT/hl.json'))
 print('headline %.1f moves/s tower %.4f ms frac %.3f' % (d['value'], d['roofline']['mean_launch_ms'], d['roofline']['frac']))
 for k, v in d['sublines'].items(): print('  %s %.1f moves/s tower %.4f ms frac %.3f' % (k, v['value'], v['roofline']['mean_launch_ms'], v['roofline']['frac']))
 " | tee -a $OUT/summary.txt
+bash tools/r05_pmc_tree.sh r05_b6/pmc_tree
