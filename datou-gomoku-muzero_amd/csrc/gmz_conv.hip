@@ -36,6 +36,11 @@ typedef uint16_t u16x4_t __attribute__((ext_vector_type(4)));
 #ifndef GMZ_CONV_RD
 #define GMZ_CONV_RD 3
 #endif
+// timing ablations of k_conv3 (A/B builds only, results wrong): 1 = each workgroup DMAs only its first board,
+// 2 = no epilogue stores (kept behind a never-true runtime test), 4 = no MFMAs in the k-loop (operand loads kept)
+#ifndef GMZ_CONV_ABL
+#define GMZ_CONV_ABL 0
+#endif
 constexpr int CC = 128;         // channels in and out
 constexpr int CKSTEPS = 36;     // 9 taps x 4 k-steps of 32 input channels
 constexpr int FRAG_BYTES = 294912;  // 36 k-steps x 8 n-tiles x 64 lanes x 16 B
@@ -190,7 +195,7 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
   for (int b = b0; b < N; b += bstride) {
     // ---- board b -> image interior: 1 KB pieces of each board row's run of cells
     const uint8_t *src = (const uint8_t *)(x + (size_t)b * A * CC);
-    for (int j = w; j < H * I::RUN_DMA; j += NW) {
+    for (int j = w; j < (((GMZ_CONV_ABL & 1) && b != b0) ? 0 : H * I::RUN_DMA); j += NW) {
       const int yy = j / I::RUN_DMA, piece = j % I::RUN_DMA;
       const int o = piece * 1024 + lane * 16;
       const int xx = o / PS, ch = (o % PS) >> 4;
@@ -235,8 +240,14 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
 #pragma unroll
         for (int i = 0; i < NTL; ++i)
 #pragma unroll
-          for (int nt = 0; nt < NTW; ++nt)
-            acc[nt][i] = M::run(ar[st % RD][nt], bf[st & 1][i], st == 0 ? f32x4_t{0.f, 0.f, 0.f, 0.f} : acc[nt][i]);
+          for (int nt = 0; nt < NTW; ++nt) {
+            if constexpr ((GMZ_CONV_ABL & 4) != 0) {  // ablation: operands consumed by one VALU op, no MFMA
+              if (st == 0) acc[nt][i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+              acc[nt][i][0] += __builtin_bit_cast(f32x4_t, ar[st % RD][nt])[0] + __builtin_bit_cast(f32x4_t, bf[st & 1][i])[0];
+            } else {
+              acc[nt][i] = M::run(ar[st % RD][nt], bf[st & 1][i], st == 0 ? f32x4_t{0.f, 0.f, 0.f, 0.f} : acc[nt][i]);
+            }
+          }
         if (st + 1 < CKSTEPS) __builtin_amdgcn_sched_barrier(0);
       }
 #pragma unroll
@@ -293,7 +304,7 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
 #pragma unroll
           for (int e = 0; e < 4; ++e) o[e] = M::bits(acc[nt][i][e]);
         }
-        *(u16x4_t *)(dst + (size_t)p * CC + n0) = o;
+        if ((GMZ_CONV_ABL & 2) == 0 || o[0] == 0x7c01) *(u16x4_t *)(dst + (size_t)p * CC + n0) = o;
         if (counted) {
           if constexpr (BWD) {  // the rounded output is the BatchNorm's dy
             const size_t k = ((size_t)b * A + p) * CC + n0;
