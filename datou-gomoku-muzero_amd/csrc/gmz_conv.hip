@@ -41,6 +41,11 @@ typedef uint16_t u16x4_t __attribute__((ext_vector_type(4)));
 #ifndef GMZ_CONV_ABL
 #define GMZ_CONV_ABL 0
 #endif
+// EARLY (one half per workgroup): the next board's DMA is issued as soon as every wave has left the k-loop, and
+// completes under this board's epilogue, instead of after it (A/B build switch)
+#ifndef GMZ_CONV_EARLY
+#define GMZ_CONV_EARLY 0
+#endif
 constexpr int CC = 128;         // channels in and out
 constexpr int CKSTEPS = 36;     // 9 taps x 4 k-steps of 32 input channels
 constexpr int FRAG_BYTES = 294912;  // 36 k-steps x 8 n-tiles x 64 lanes x 16 B
@@ -192,10 +197,11 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
       for (int e = 0; e < 4; ++e) s1[hh][nt][e] = s2[hh][nt][e] = 0.f;
   int nvalid = 0;
 
-  for (int b = b0; b < N; b += bstride) {
-    // ---- board b -> image interior: 1 KB pieces of each board row's run of cells
-    const uint8_t *src = (const uint8_t *)(x + (size_t)b * A * CC);
-    for (int j = w; j < (((GMZ_CONV_ABL & 1) && b != b0) ? 0 : H * I::RUN_DMA); j += NW) {
+  constexpr bool EARLY = GMZ_CONV_EARLY && HALVES == 1;
+  // ---- board bd -> image interior: 1 KB pieces of each board row's run of cells
+  auto dma = [&](int bd) {
+    const uint8_t *src = (const uint8_t *)(x + (size_t)bd * A * CC);
+    for (int j = w; j < (((GMZ_CONV_ABL & 1) && bd != b0) ? 0 : H * I::RUN_DMA); j += NW) {
       const int yy = j / I::RUN_DMA, piece = j % I::RUN_DMA;
       const int o = piece * 1024 + lane * 16;
       const int xx = o / PS, ch = (o % PS) >> 4;
@@ -204,8 +210,18 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
                                          (__attribute__((address_space(3))) void *)(img + (yy + 1) * RS + PS + piece * 1024),
                                          16, 0, 0);
     }
+  };
+  if (EARLY && b0 < N) {
+    dma(b0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+  }
+  for (int b = b0; b < N; b += bstride) {
+    if (!EARLY) {
+      dma(b);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
     const bool counted = stats && (!mask || mask[b]);
     nvalid += counted;
 
@@ -258,6 +274,10 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
     if constexpr (PTW * PG == NPT) kloop(std::integral_constant<int, PTW>{});
     else if (pg + PG * (PTW - 1) < NPT) kloop(std::integral_constant<int, PTW>{});
     else kloop(std::integral_constant<int, PTW - 1>{});
+    if constexpr (EARLY) {  // every wave has read its last B fragments: the image is free for the next board
+      __syncthreads();
+      if (b + bstride < N) dma(b + bstride);
+    }
 
     // ---- epilogue: 4 consecutive output channels of one position per lane -> 8-byte store
     uint16_t *dst = y + (size_t)b * A * CC;
@@ -374,7 +394,8 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
         wvoff = nq * NTW * 1024 + lane * 16;
         loadA(k, k);
       }
-    __syncthreads();  // every wave is done reading the image before the next board's DMA
+    if constexpr (EARLY) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next board has landed
+    __syncthreads();  // every wave is done reading the image before the next board's DMA (EARLY: it is in)
   }
   if (!stats || PB) return;
 #pragma unroll
