@@ -37,7 +37,9 @@ typedef uint16_t u16x4_t __attribute__((ext_vector_type(4)));
 #define GMZ_CONV_RD 3
 #endif
 // timing ablations of k_conv3 (A/B builds only, results wrong): 1 = each workgroup DMAs only its first board,
-// 2 = no epilogue stores (kept behind a never-true runtime test), 4 = no MFMAs in the k-loop (operand loads kept)
+// 2 = no epilogue stores (kept behind a never-true runtime test), 4 = no MFMAs in the k-loop (operand loads kept),
+// 8 = no weight-fragment loads in the k-loop (the ring keeps its first fragments), 16 = no B-fragment LDS reads in
+// the k-loop (the first step's fragments reused)
 #ifndef GMZ_CONV_ABL
 #define GMZ_CONV_ABL 0
 #endif
@@ -250,8 +252,12 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
       readB(0, 0);
 #pragma unroll
       for (int st = 0; st < CKSTEPS; ++st) {
-        loadA((st + RD - 1) % RD, st + RD - 1);
-        if (st + 1 < CKSTEPS) readB((st + 1) & 1, st + 1);
+        if constexpr ((GMZ_CONV_ABL & 8) == 0) loadA((st + RD - 1) % RD, st + RD - 1);
+        if constexpr ((GMZ_CONV_ABL & 16) == 0) {
+          if (st + 1 < CKSTEPS) readB((st + 1) & 1, st + 1);
+        } else if (st == 0) {
+          readB(1, 1);
+        }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int i = 0; i < NTL; ++i)

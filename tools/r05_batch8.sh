@@ -25,3 +25,10 @@ for i in 1 2; do
     python3 -c "import json; d=json.load(open('$OUT/tr_${V}_$i.json')); print('trainer %-6s %d %.2f steps/s' % ('$V', $i, d['value']))" | tee -a $OUT/summary.txt
   done
 done
+for V in abl8 abl16 abl28; do
+  for N in 360 1800; do
+    GMZ_LIB=$PWD/datou-gomoku-muzero_amd/_alt/libgmz_$V.so timeout -k 10 120 python3 tools/conv_bench.py $N > $OUT/conv_${V}_${N}.txt 2>&1 || { echo "conv $V failed"; tail -3 $OUT/conv_${V}_${N}.txt; exit 1; }
+    echo "conv $V N=$N: $(grep -E '^(hip fwd|hip dgrad) ' $OUT/conv_${V}_${N}.txt | tr -s ' ' | tr '\n' ';')" | tee -a $OUT/summary.txt
+  done
+done
+bash tools/r05_pmc_tree.sh r05_b8/pmc_tree

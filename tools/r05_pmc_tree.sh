@@ -12,6 +12,7 @@ SP="--no-cpu-baseline --trainer-steps 0 --loop-iters 0 --sublines= --worker-move
 for CFG in "1024 2" "8192 1"; do
   set -- $CFG
   G=$1; S=$2
+  mkdir -p $OUT/G${G}
   for CTR in FETCH_SIZE WRITE_SIZE; do
     D=$OUT/G${G}/$CTR
     timeout -s KILL 240 rocprofv3 --pmc $CTR --kernel-include-regex "k_expand_select" --output-format csv -d $D -o pmc -- \
