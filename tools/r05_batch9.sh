@@ -1,0 +1,27 @@
+#!/bin/bash
+# round 5 GPU batch 9: the persistent two-image conv (k_conv3db, GMZ_CONV_DB=1): its conv tests, then conv and
+# trainer A/B against k_conv3 on the same box; then the tree kernel's PMC bytes.
+set -o pipefail
+OUT=gpurun_out/r05_b9
+mkdir -p $OUT
+( while sleep 60; do date >> $OUT/heartbeat; done ) &
+HB=$!
+trap "kill $HB" EXIT
+GMZ_CONV_DB=1 timeout -k 10 600 python -u -m pytest tests/test_trainer.py -m gpu -x -v --timeout 300 --timeout-method thread \
+  -k "hip_conv3x3 or conv_epilogue_bn_statistics or conv3x3_forward_add or batched_consistency_kernels or residual_gradient_fold" > $OUT/tests.log 2>&1
+rc=$?
+grep -E "PASS|FAIL|^E  " $OUT/tests.log | tail -30
+[ $rc -eq 0 ] || exit $rc
+for i in 1 2; do
+  for V in base db; do
+    ENV=""; [ $V = db ] && ENV="GMZ_CONV_DB=1"
+    for N in 360 1800; do
+      env $ENV timeout -k 10 120 python3 tools/conv_bench.py $N > $OUT/conv_${V}_${N}_$i.txt 2>&1 || { echo "conv $V failed"; tail -3 $OUT/conv_${V}_${N}_$i.txt; exit 1; }
+      echo "conv $V N=$N $i: $(grep -E '^(hip fwd|hip dgrad) ' $OUT/conv_${V}_${N}_$i.txt | tr -s ' ' | tr '\n' ';') $(grep 'rel err' $OUT/conv_${V}_${N}_$i.txt)" | tee -a $OUT/summary.txt
+    done
+    env $ENV timeout -k 10 200 python3 tools/bench_trainer.py --steps 30 --per > $OUT/tr_${V}_$i.json 2> $OUT/tr_${V}_$i.err \
+      || { echo "trainer $V failed"; tail -5 $OUT/tr_${V}_$i.err; exit 1; }
+    python3 -c "import json; d=json.load(open('$OUT/tr_${V}_$i.json')); print('trainer %-6s %d %.2f steps/s' % ('$V', $i, d['value']))" | tee -a $OUT/summary.txt
+  done
+done
+bash tools/r05_pmc_tree.sh r05_b9/pmc_tree
