@@ -446,251 +446,6 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
   }  // halves
 }
 
-// ---- k_conv3db: the same convolution as k_conv3 (forward statistics, addend, per-board statistics; not the stamp),
-// persistent with ONE workgroup per CU and TWO board images in LDS.  The timing ablations of k_conv3
-// (profiles/r05_conv_ablations.txt) put 45 % of its time outside the k-loop: the board DMA, the epilogue and the
-// barriers around them (13 of 29 us at 360 boards), which the two half-board workgroups of a CU, running in phase,
-// do not hide from each other.  Here the 8 waves cover both halves of the output channels of one board
-// (half = w / 4; waves w and w + 4 share a SIMD and take complementary position groups), and the NEXT board's DMA
-// into the other image is issued right after the k-loop's last weight-fragment load: it lands under this board's
-// epilogue, and no wait for a weight fragment (in-order vmcnt) waits for it before the next board's third k-step.
-// No barrier between the k-loop and the DMA: the other image was released by every wave at the previous board's end.
-// (Spreading the pieces over the k-loop kept their addresses live through it: 300 VGPRs, spills.)
-constexpr int DB_THREADS = 512, DB_RD = 3;
-
-template <int H, typename T, bool PB>
-__global__ void __launch_bounds__(DB_THREADS, 1) k_conv3db(const uint16_t *__restrict__ x, const uint16_t *__restrict__ wpk,
-                                                        uint16_t *__restrict__ y, int N, const uint8_t *__restrict__ mask,
-                                                        double *__restrict__ stats, const uint16_t *__restrict__ addend,
-                                                        ActStamp as) {
-  using I = CImg<H>;
-  using M = Mfma<T>;
-  typedef typename M::V V;
-  constexpr int A = H * H, NPT = (A + 15) / 16, PG = 2, NTW = 2, PTW = (NPT + PG - 1) / PG, RD = DB_RD, NW = 8;
-  constexpr int PS = I::PS, RS = I::RS;
-  constexpr int NPIECE = H * I::RUN_DMA, PPW = (NPIECE + NW - 1) / NW;  // 1 KB DMA pieces per board / per wave
-  static_assert(CKSTEPS % RD == 0 && PPW <= CKSTEPS, "ring slots repeat per board; pieces fit the k-loop");
-  static_assert(2 * I::BYTES + (PB ? 2 * PG * 64 * 2 * 4 : 4) <= 163840, "LDS budget: two images");
-  static_assert(2 * I::BYTES >= 2 * PG * 64 * 2 * 4, "statistics scratch fits in the images");
-  __shared__ __attribute__((aligned(16))) uint8_t img2[2 * I::BYTES];
-  __shared__ float pbred[PB ? 2 * PG * 64 * 2 : 1];  // PB: [half][PG][64 channels][2], per board
-
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  const int half = w >> 2, nq = w & 1, pg = ((w >> 1) ^ (w >> 2)) & 1;  // waves w, w + 4: complementary groups
-  const int g4 = lane >> 4;
-  const int cg = (g4 & 1) * 8 + (g4 >> 1);
-  const int ntile0 = half * 4 + nq * NTW;
-  const int b0 = blockIdx.x, bstride = gridDim.x;
-
-  for (int i = tid; i < 2 * I::BYTES / 16; i += DB_THREADS) *(uint4 *)(img2 + i * 16) = make_uint4(0, 0, 0, 0);
-
-  const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc((void *)wpk, (short)0, FRAG_BYTES, 0x00020000);
-  const int wvoff = ntile0 * 1024 + lane * 16;
-  V ar[RD][NTW];
-  auto loadA = [&](int slot, int st) {
-    const int soff = (st < CKSTEPS ? st : st - CKSTEPS) * 8192;
-#pragma unroll
-    for (int nt = 0; nt < NTW; ++nt)
-      ar[slot][nt] = __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(wrsrc, wvoff + nt * 1024, soff, 0));
-  };
-  // piece k of this wave: j = w + 8k -> board row yy = j / RUN_DMA, LDS piece p = j % RUN_DMA of that row's run.
-  // A lane's source offset within a row depends only on p: computed once per p (at most 4 VGPRs); rows past the
-  // board are clamped to the last one (a duplicate write of the same bytes by two waves).  Board bd's rows are
-  // scalar offsets, so no per-piece address stays live across the k-loop.
-  auto dma_piece = [&](int bd, int k, uint8_t *im) {
-    const int j = w + NW * k;
-    int yy = j / I::RUN_DMA;
-    const int pc = j - yy * I::RUN_DMA;
-    yy = yy < H ? yy : H - 1;
-    int lo = lane * 16;
-    asm volatile("" : "+v"(lo));  // computed here, not hoisted out of the board loop (live across it: spills)
-    const int o = pc * 1024 + lo;
-    const int xx = o / PS, ch = (o % PS) >> 4;
-    const uint8_t *src = (const uint8_t *)(x + (size_t)bd * A * CC) + yy * H * 256;
-    uint8_t *dst = im + (yy + 1) * RS + PS + pc * 1024;
-    if (o < I::RUN && ch < 16)
-      __builtin_amdgcn_global_load_lds((const void *)(src + xx * 256 + ch * 16), (__attribute__((address_space(3))) void *)dst,
-                                       16, 0, 0);
-  };
-  __syncthreads();  // zeroed images before the first DMA
-  if (b0 < N) {
-#pragma unroll
-    for (int k = 0; k < PPW; ++k) dma_piece(b0, k, img2);
-  }
-#pragma unroll
-  for (int k = 0; k < RD - 1; ++k) loadA(k, k);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  float s1[NTW][4], s2[NTW][4];
-#pragma unroll
-  for (int nt = 0; nt < NTW; ++nt)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) s1[nt][e] = s2[nt][e] = 0.f;
-  int nvalid = 0;
-
-  int it = 0;
-  for (int b = b0; b < N; b += bstride, ++it) {
-    const int boff = (it & 1) * I::BYTES;  // this board's image; the next one goes to the other
-    const bool counted = stats && (!mask || mask[b]);
-    nvalid += counted;
-    f32x4_t acc[NTW][PTW];
-    int bb[PTW];
-#pragma unroll
-    for (int i = 0; i < PTW; ++i) {  // tile position -> its cell in this board's image (past the board: cell 0)
-      const int pt = pg + PG * i;
-      int p = pt * 16 + csigma16(lane & 15);
-      asm volatile("" : "+v"(p));  // recomputed per board rather than kept live through the k-loop
-      bb[i] = ((pt < NPT && p < A) ? (p / H) * RS + (p % H) * PS : 0) + cg * 16 + boff;
-    }
-    auto kloop = [&](auto ntl_c) {
-      constexpr int NTL = decltype(ntl_c)::value;
-      V bf[2][NTL];
-      auto readB = [&](int buf, int st) {
-        const int tap = st >> 2, ks = st & 3;
-        const int off = (tap / 3) * RS + (tap % 3) * PS + ks * 32;
-#pragma unroll
-        for (int i = 0; i < NTL; ++i) bf[buf][i] = *(const V *)(img2 + bb[i] + off);
-      };
-      readB(0, 0);
-#pragma unroll
-      for (int st = 0; st < CKSTEPS; ++st) {
-        loadA((st + RD - 1) % RD, st + RD - 1);
-        if (st + 1 < CKSTEPS) readB((st + 1) & 1, st + 1);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int i = 0; i < NTL; ++i)
-#pragma unroll
-          for (int nt = 0; nt < NTW; ++nt)
-            acc[nt][i] = M::run(ar[st % RD][nt], bf[st & 1][i], st == 0 ? f32x4_t{0.f, 0.f, 0.f, 0.f} : acc[nt][i]);
-        if (st + 1 < CKSTEPS) __builtin_amdgcn_sched_barrier(0);
-      }
-#pragma unroll
-      for (int i = NTL; i < PTW; ++i)
-#pragma unroll
-        for (int nt = 0; nt < NTW; ++nt) acc[nt][i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    };
-    if constexpr (PTW * PG == NPT) kloop(std::integral_constant<int, PTW>{});
-    else if (pg + PG * (PTW - 1) < NPT) kloop(std::integral_constant<int, PTW>{});
-    else kloop(std::integral_constant<int, PTW - 1>{});
-    if (b + bstride < N) {  // the next board -> the other image, under this board's epilogue
-#pragma unroll
-      for (int k = 0; k < PPW; ++k) dma_piece(b + bstride, k, img2 + (I::BYTES - boff));
-    }
-
-    // ---- epilogue (k_conv3's): 4 consecutive output channels of one position per lane -> 8-byte store
-    uint16_t *dst = y + (size_t)b * A * CC;
-    const uint16_t *add = addend ? addend + (size_t)b * A * CC : nullptr;
-#pragma unroll
-    for (int i = 0; i < PTW; ++i) {
-      const int pt = pg + PG * i;
-      const int p = pt * 16 + csigma16(lane & 15);
-      if (pt >= NPT || p >= A) continue;
-#pragma unroll
-      for (int nt = 0; nt < NTW; ++nt) {
-        const int n0 = (ntile0 + nt) * 16 + g4 * 4;
-        u16x4_t o;
-        if (add) {
-          const u16x4_t ad = *(const u16x4_t *)(add + (size_t)p * CC + n0);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] = M::bits(acc[nt][i][e] + M::value(ad[e]));
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] = M::bits(acc[nt][i][e]);
-        }
-        *(u16x4_t *)(dst + (size_t)p * CC + n0) = o;
-        if (counted) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float v = M::value(o[e]);
-            s1[nt][e] += v;
-            s2[nt][e] = fmaf(v, v, s2[nt][e]);
-          }
-        }
-      }
-    }
-    if constexpr (PB) {  // this board's partials -> slot b, then the accumulators restart
-      if (stats) {
-#pragma unroll
-        for (int nt = 0; nt < NTW; ++nt)
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-#pragma unroll
-            for (int o = 1; o < 16; o <<= 1) {
-              s1[nt][e] += __shfl_xor(s1[nt][e], o, 64);
-              s2[nt][e] += __shfl_xor(s2[nt][e], o, 64);
-            }
-        if ((lane & 15) == 0) {
-#pragma unroll
-          for (int nt = 0; nt < NTW; ++nt)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const int cl = (nq * NTW + nt) * 16 + g4 * 4 + e;
-              pbred[((half * PG + pg) * 64 + cl) * 2] = s1[nt][e];
-              pbred[((half * PG + pg) * 64 + cl) * 2 + 1] = s2[nt][e];
-            }
-        }
-#pragma unroll
-        for (int nt = 0; nt < NTW; ++nt)  // every lane: its accumulators restart for the next board
-#pragma unroll
-          for (int e = 0; e < 4; ++e) s1[nt][e] = s2[nt][e] = 0.f;
-        __syncthreads();
-        if (tid < 128) {
-          const int hf = tid >> 6, cl = tid & 63;
-          double a = 0.0, q = 0.0;
-#pragma unroll
-          for (int g = 0; g < PG; ++g) {
-            a += (double)pbred[((hf * PG + g) * 64 + cl) * 2];
-            q += (double)pbred[((hf * PG + g) * 64 + cl) * 2 + 1];
-          }
-          double *out = stats + ((size_t)(hf * 64 + cl) * N + b) * 3;  // channel-major [C][N][3]
-          out[0] = a;
-          out[1] = q;
-          out[2] = counted ? (double)A : 0.0;
-        }
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of the next board have landed
-    __syncthreads();  // ... every wave's; and every wave is done reading cur, the board after next's target
-  }
-  if (!stats || PB) return;
-  // ---- per-workgroup partials (slot = blockIdx.x) of all 128 channels: 16 lanes of a group hold the same 4 channels
-#pragma unroll
-  for (int nt = 0; nt < NTW; ++nt)
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) {
-        s1[nt][e] += __shfl_xor(s1[nt][e], o, 64);
-        s2[nt][e] += __shfl_xor(s2[nt][e], o, 64);
-      }
-  float *red = (float *)img2;  // [half][PG][64][2]
-  if ((lane & 15) == 0) {
-#pragma unroll
-    for (int nt = 0; nt < NTW; ++nt)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int cl = (nq * NTW + nt) * 16 + g4 * 4 + e;
-        red[((half * PG + pg) * 64 + cl) * 2] = s1[nt][e];
-        red[((half * PG + pg) * 64 + cl) * 2 + 1] = s2[nt][e];
-      }
-  }
-  __syncthreads();
-  if (tid < 128) {
-    const int hf = tid >> 6, cl = tid & 63;
-    double a = 0.0, q = 0.0;
-#pragma unroll
-    for (int g = 0; g < PG; ++g) {
-      a += (double)red[((hf * PG + g) * 64 + cl) * 2];
-      q += (double)red[((hf * PG + g) * 64 + cl) * 2 + 1];
-    }
-    double *out = stats + ((size_t)(hf * 64 + cl) * bstride + b0) * 3;  // channel-major [C][slots][3]
-    out[0] = a;
-    out[1] = q;
-    out[2] = (double)nvalid * A;
-  }
-}
-
 // ---- weight gradient: dW[o][c][t] = sum over boards n and positions p of dy[n][p][o] * x[n][p + d(t)][c]
 // (d(t) = (t/3 - 1, t%3 - 1), zero outside the board), the GEMM M = o, N = c, K = (n, p) per tap.
 // Workgroup = (tap row ty, chunk of boards): 8 waves = 4 (32 o) x 2 (64 c), accumulating the three taps
@@ -875,22 +630,6 @@ static int conv_halves() {
   return h;
 }
 
-// the persistent two-image kernel (k_conv3db) for the forward-statistics, addend, stamp and per-board-statistics
-// convolutions: GMZ_CONV_DB=1 (A/B)
-static int conv_db() {
-  static int d = -1;
-  if (d < 0) {
-    const char *e = getenv("GMZ_CONV_DB");
-    d = (e && atoi(e) == 1) ? 1 : 0;
-  }
-  return d;
-}
-
-static int conv3db_grid(int N) {
-  const int cus = cu_count_conv();
-  return N < cus ? N : cus;
-}
-
 int conv3_grid(int N) {  // a multiple of 16 (whole XCD pairs; workgroups past the boards do nothing)
   if (conv_halves() == 2) {  // one workgroup per board, at most two per CU
     const long cap = 2L * cu_count_conv();
@@ -901,10 +640,7 @@ int conv3_grid(int N) {  // a multiple of 16 (whole XCD pairs; workgroups past t
 }
 
 // statistics slots (partials) of gmz_conv3x3_forward_stats: one per board pair of workgroups, or per workgroup
-int conv3_stats_slots(int N) {
-  if (conv_db()) return conv3db_grid(N);
-  return conv_halves() == 2 ? conv3_grid(N) : conv3_grid(N) / 2;
-}
+int conv3_stats_slots(int N) { return conv_halves() == 2 ? conv3_grid(N) : conv3_grid(N) / 2; }
 
 template <int H, typename T, int HV, bool BWD, bool PB = false>
 void launch_conv3_k(const void *x, const void *wpk, void *y, int N, const uint8_t *mask, double *stats, const void *addend,
@@ -922,14 +658,7 @@ template <int H, typename T>
 int launch_conv3(const void *x, const void *wpk, void *y, int N, const uint8_t *mask, double *stats, const void *addend,
                  const BnBwd &bn, hipStream_t st, bool per_board = false, const ActStamp &as = ActStamp{}) {
   const bool bwd = bn.x != nullptr;
-  if (conv_db() && !bwd && !as.action) {  // (the action stamp, an A/B path, stays on k_conv3)
-    if (per_board)
-      hipLaunchKernelGGL((k_conv3db<H, T, true>), dim3(conv3db_grid(N)), dim3(DB_THREADS), 0, st, (const uint16_t *)x,
-                         (const uint16_t *)wpk, (uint16_t *)y, N, mask, stats, (const uint16_t *)addend, as);
-    else
-      hipLaunchKernelGGL((k_conv3db<H, T, false>), dim3(conv3db_grid(N)), dim3(DB_THREADS), 0, st, (const uint16_t *)x,
-                         (const uint16_t *)wpk, (uint16_t *)y, N, mask, stats, (const uint16_t *)addend, as);
-  } else if (per_board) {
+  if (per_board) {
     launch_conv3_k<H, T, 1, false, true>(x, wpk, y, N, mask, stats, addend, bn, st, as);
   } else if (conv_halves() == 2) {
     if (bwd) launch_conv3_k<H, T, 2, true>(x, wpk, y, N, mask, stats, addend, bn, st, as);
