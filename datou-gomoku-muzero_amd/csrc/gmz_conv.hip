@@ -586,158 +586,6 @@ __global__ void __launch_bounds__(512, 1) k_conv3_wgrad(WgSrc src, int N, int nc
         }
 }
 
-// ---- k_conv3_wgrad2: k_conv3_wgrad with its board DMA overlapped.  The k-loop of the weight gradient issues no
-// global loads (both operands come from LDS), so a DMA in flight never stalls it — what k_conv3_wgrad lacks is LDS
-// room for a second board (157 KB for one: the dy tile and the padded x image).  Here a board is cut into stages of
-// SK = 3 k-steps (96 positions): a stage holds those positions' dy rows and only the x rows they reach for this
-// workgroup's tap row (7 of the 17 padded rows at 15x15), 62 KB, so two stages fit (124 KB) and the next stage
-// (of this board or the next) is DMA'd into the other one while this one is computed.  Rows outside the board and
-// dy rows past the last position are zero-filled by the workgroup into the stage being loaded; the images' border
-// columns are never written after the initial fill.  Same operands, MFMA order and partials as k_conv3_wgrad.
-template <int H>
-struct WgStage {
-  static constexpr int A = H * H, KS = (A + 31) / 32, SK = 3, NS = (KS + SK - 1) / SK, NPS = SK * 32, RB = 288;
-  static constexpr int HP = H + 2;
-  static constexpr int xrows() {  // the most board rows one stage's positions span
-    int m = 0;
-    for (int s = 0; s < NS; ++s) {
-      const int lo = (s * NPS) / H;
-      int hp = s * NPS + NPS - 1;
-      if (hp > A - 1) hp = A - 1;
-      const int r = hp / H - lo + 1;
-      if (r > m) m = r;
-    }
-    return m;
-  }
-  static constexpr int XR = xrows();
-  static constexpr int DY_BYTES = NPS * RB, X_BYTES = XR * HP * RB, STAGE = DY_BYTES + X_BYTES;
-  static constexpr int RUN = (H - 1) * RB + 256, RUN_DMA = (RUN + 1023) / 1024;  // one board row of x
-};
-
-template <int H, typename T>
-__global__ void __launch_bounds__(512, 1) k_conv3_wgrad2(WgSrc src, int N, int nch, float *__restrict__ part) {
-  using L = WgStage<H>;
-  using M = Mfma<T>;
-  typedef typename M::V V;
-  constexpr int A = H * H, KS = L::KS, SK = L::SK, NS = L::NS, NPS = L::NPS, RB = L::RB, HP = L::HP;
-  static_assert(2 * L::STAGE <= 163840, "LDS budget: two stages");
-  static_assert(L::STAGE % 16 == 0 && L::DY_BYTES % 16 == 0 && (HP * RB) % 16 == 0, "16-B zero fills");
-  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * L::STAGE];
-
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;  // as k_conv3_wgrad: a chunk's tap rows on one XCD
-  const int ty = slot % 3, chunk = (slot / 3) * 8 + xcd;
-  const int wo = w & 3, wc = w >> 2;
-  const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
-  const int ocol = (wo * 32 + 4 * pp) * 2, ccol = (wc * 64 + 4 * pp) * 2;
-
-  for (int i = tid; i < 2 * L::STAGE / 16; i += 512) *(uint4 *)(smem + i * 16) = make_uint4(0, 0, 0, 0);
-  __syncthreads();
-
-  f32x4_t acc[3][2][4];
-#pragma unroll
-  for (int tx = 0; tx < 3; ++tx)
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) acc[tx][mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-  // stage s of board b -> stage buffer buf: its dy rows, its x rows (zero rows outside the board), zero dy rows
-  // past the last position.  DMA pieces are LDS-linear 1 KB runs (row pads skipped), as k_conv3_wgrad's.
-  auto load_stage = [&](int b, int s, int buf) {
-    uint8_t *ld = smem + buf * L::STAGE, *lx = ld + L::DY_BYTES;
-    const int sg = b / src.nps, lb = b - sg * src.nps;
-    const uint8_t *sd = (const uint8_t *)(src.dy[sg] + (size_t)lb * A * CC);
-    const uint8_t *sx = (const uint8_t *)(src.x[sg] + (size_t)lb * A * CC);
-    const int p0 = s * NPS;
-    const int nrows = A - p0 < NPS ? A - p0 : NPS;
-    const int ndy = (nrows * RB + 1023) / 1024;
-    for (int j = w; j < ndy; j += 8) {
-      const int o = j * 1024 + lane * 16;
-      const int row = o / RB, ch = (o % RB) >> 4;
-      if (row < nrows && ch < 16)
-        __builtin_amdgcn_global_load_lds((const void *)(sd + (size_t)(p0 + row) * 256 + ch * 16),
-                                         (__attribute__((address_space(3))) void *)(ld + j * 1024), 16, 0, 0);
-    }
-    for (int i = nrows * RB / 16 + tid; i < L::DY_BYTES / 16; i += 512)  // positions past the board: dy = 0
-      *(uint4 *)(ld + i * 16) = make_uint4(0, 0, 0, 0);
-    const int ylo = p0 / H, yhi = (p0 + nrows - 1) / H, nx = yhi - ylo + 1;
-    for (int j = w; j < nx * L::RUN_DMA; j += 8) {
-      const int lr = j / L::RUN_DMA, piece = j - lr * L::RUN_DMA;
-      const int r = ylo + ty + lr;  // padded row: board row r - 1
-      if (r < 1 || r > H) continue;
-      const int o = piece * 1024 + lane * 16;
-      const int xx = o / RB, ch = (o % RB) >> 4;
-      if (o < L::RUN && ch < 16)
-        __builtin_amdgcn_global_load_lds((const void *)(sx + ((size_t)(r - 1) * H + xx) * 256 + ch * 16),
-                                         (__attribute__((address_space(3))) void *)(lx + (lr * HP + 1) * RB + piece * 1024),
-                                         16, 0, 0);
-    }
-    for (int lr = 0; lr < nx; ++lr) {  // rows outside the board (the top / bottom padding row) are zero
-      const int r = ylo + ty + lr;
-      if (r >= 1 && r <= H) continue;
-      for (int i = tid; i < HP * RB / 16; i += 512) *(uint4 *)(lx + lr * HP * RB + i * 16) = make_uint4(0, 0, 0, 0);
-    }
-  };
-
-  int b = chunk, s = 0, it = 0;
-  if (b < N) load_stage(b, 0, 0);
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  __syncthreads();
-  while (b < N) {
-    const int buf = it & 1;
-    int nb = b, ns = s + 1;  // the next stage: of this board, or the next board's first
-    if (ns == NS) {
-      nb = b + nch;
-      ns = 0;
-    }
-    if (nb < N) load_stage(nb, ns, buf ^ 1);  // lands while this stage is computed
-    const uint8_t *ld = smem + buf * L::STAGE, *lx = ld + L::DY_BYTES;
-    const int p0s = s * NPS, ylo = p0s / H;
-    const int nks = KS - s * SK < SK ? KS - s * SK : SK;
-    for (int kk = 0; kk < nks; ++kk) {
-      const int ks = s * SK + kk;
-      const int p0 = ks * 32 + 4 * g + q, p1 = p0 + 16;
-      const int c0 = p0 < A ? p0 : A - 1, c1 = p1 < A ? p1 : A - 1;
-      const int xb0 = ((c0 / H - ylo) * HP + c0 % H) * RB + ccol, xb1 = ((c1 / H - ylo) * HP + c1 % H) * RB + ccol;
-      const int ab0 = (p0 - p0s) * RB + ocol, ab1 = (p1 - p0s) * RB + ocol;
-      V af[2];
-#pragma unroll
-      for (int mt = 0; mt < 2; ++mt) {
-        const s16x4_t lo = tr_read(ld, ab0 + mt * 32), hi = tr_read(ld, ab1 + mt * 32);
-        af[mt] = __builtin_bit_cast(V, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-      }
-#pragma unroll
-      for (int tx = 0; tx < 3; ++tx) {
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) {
-          const s16x4_t lo = tr_read(lx, xb0 + tx * RB + nt * 32), hi = tr_read(lx, xb1 + tx * RB + nt * 32);
-          const V bf = __builtin_bit_cast(V, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-#pragma unroll
-          for (int mt = 0; mt < 2; ++mt) acc[tx][mt][nt] = M::run(af[mt], bf, acc[tx][mt][nt]);
-        }
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // the next stage (DMA and zero fills) is in
-    __syncthreads();  // ... for every wave; and every wave is done with this stage's buffer
-    b = nb;
-    s = ns;
-    ++it;
-  }
-  float *pc = part + (size_t)chunk * 9 * CC * CC;
-#pragma unroll
-  for (int tx = 0; tx < 3; ++tx)
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int o = wo * 32 + 16 * mt + 4 * g + e, c = wc * 64 + 16 * nt + (lane & 15);
-          pc[((size_t)(ty * 3 + tx) * CC + o) * CC + c] = acc[tx][mt][nt][e];
-        }
-}
-
 // dW[o][c][ky][kx] (+)= sum over chunks of part[chunk][t][o][c], dW at element strides (s0, s1, s2, s3);
 // 8 independent partial sums per thread keep 8 loads in flight
 __global__ void __launch_bounds__(256) k_conv3_wgrad_reduce(const float *__restrict__ part, int nch, float *dw, long s0,
@@ -841,23 +689,10 @@ int wgrad_chunks(int N) {
   return n < cap ? n : cap;
 }
 
-// the staged weight gradient (k_conv3_wgrad2, DMA overlapped): GMZ_WGRAD_STAGED=1 (A/B); same grid and partials
-static int wgrad_staged() {
-  static int d = -1;
-  if (d < 0) {
-    const char *e = getenv("GMZ_WGRAD_STAGED");
-    d = (e && atoi(e) == 1) ? 1 : 0;
-  }
-  return d;
-}
-
 template <int H, typename T>
 int launch_wgrad(const WgSrc &src, int N, float *part, hipStream_t st) {
   const int nch = wgrad_chunks(N);
-  if (wgrad_staged())
-    hipLaunchKernelGGL((k_conv3_wgrad2<H, T>), dim3(3 * nch), dim3(512), 0, st, src, N, nch, part);
-  else
-    hipLaunchKernelGGL((k_conv3_wgrad<H, T>), dim3(3 * nch), dim3(512), 0, st, src, N, nch, part);
+  hipLaunchKernelGGL((k_conv3_wgrad<H, T>), dim3(3 * nch), dim3(512), 0, st, src, N, nch, part);
   GMZ_LAUNCH_CHECK();
   return 0;
 }
