@@ -78,6 +78,8 @@ _SIGS = {
     "gmz_grad_add_t_cols": ([I, P, I, I, I, I, I, P, P], I),
     "gmz_head_conv1x1_forward": ([I, P, L, I, P, P, I, P, P, I, P, P, P], I),
     "gmz_head_conv1x1_workspace_bytes": ([L, I, P], I),
+    "gmz_seg_bn_forward": ([I, P, P, I, I, I, I, P, P, ctypes.c_float, P, P, I, ctypes.c_float, P, P, P, P, P], I),
+    "gmz_seg_bn_backward": ([I, P, P, P, I, I, I, I, P, P, P, P, P, I, P], I),
     "gmz_head_conv1x1_backward": ([I, P, L, I, P, I, P, I, P, P, P, P, P, P, P, I, P, P], I),
     "gmz_bn_forward_stats": ([I, P, P, I, I, I, P, P, ctypes.c_float, ctypes.c_float, P, P, P, I, P, P, P, I, P], I),
     "gmz_bn_forward_seg": ([I, P, P, P, I, I, I, I, P, P, ctypes.c_float, ctypes.c_float, P, P, P, I, P, P, P, P, P], I),

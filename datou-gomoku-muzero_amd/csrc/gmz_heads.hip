@@ -281,3 +281,208 @@ GMZ_EXPORT int gmz_head_conv1x1_backward(int dtype, const void *x, long P, int C
   }
   return fail("gmz_head_conv1x1_backward: dtype must be 0 (f32), 1 (f16) or 2 (bf16)");
 }
+
+namespace gmz {
+namespace {
+
+// ------------------------------------------------------------------ segmented BatchNorm of the batched heads
+// trainer._bn_seg_grad on the GPU: the heads' BatchNorms (policy_bn C = 2, value_bn C = 1, projection bn1 C = 512,
+// network.py:62,65,95) over nseg stacked unroll steps (trainer.BATCHED_HEADS), each step normalised over its own
+// live rows — what ~20 PyTorch launches per call forward and ~25 backward did, as ONE kernel each way.  x
+// [nseg*B][S][C] (channels-last 4-D, or [N][C] with S = 1) in the activation dtype; y f32 in the same layout.
+// One workgroup per channel, the segments in order: per segment a masked f64 sum, then a masked f64 sum of
+// squared deviations (two passes, as _bn), then y for EVERY row of the segment.  Running statistics (optional)
+// updated segment after segment in the workgroup — the reference's call order — optionally interleaved with a
+// previous call's segments (the projection: dynamics step s, then target s).
+constexpr int SB_THREADS = 256;
+
+__device__ __forceinline__ double sb_block_sum(double v, double *red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();  // red reused
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  double s = 0.0;
+#pragma unroll
+  for (int i = 0; i < SB_THREADS / 64; ++i) s += red[i];
+  return s;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(SB_THREADS) k_seg_bn_fwd(const T *__restrict__ x, const uint8_t *__restrict__ rmask,
+                                                          int nseg, int B, int S, int C, const float *__restrict__ gamma,
+                                                          const float *__restrict__ beta, float eps, float *__restrict__ y,
+                                                          float *__restrict__ st, int update, float momentum,
+                                                          float *__restrict__ rmean, float *__restrict__ rvar,
+                                                          int64_t *__restrict__ nbt, const float *__restrict__ pre) {
+  __shared__ double red[SB_THREADS / 64];
+  const int c = blockIdx.x;
+  const long rowlen = (long)S;  // elements of one row per channel
+  const long segn = (long)B * rowlen;
+  float *mean_o = st, *invstd_o = st + (size_t)nseg * C, *varu_o = st + 2 * (size_t)nseg * C;
+  float *cnt_o = st + 3 * (size_t)nseg * C;  // [nseg] live rows (written by channel 0)
+  const float g = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+  unsigned live_bits = 0;  // segment sg has live rows (nseg <= 32)
+  for (int sg = 0; sg < nseg; ++sg) {
+    const long r0 = (long)sg * B;
+    double a = 0.0, nl = 0.0;
+    for (long i = threadIdx.x; i < segn; i += SB_THREADS) {
+      const long r = r0 + i / rowlen;
+      if (rmask && !rmask[r]) continue;
+      a += (double)hld(x, (size_t)(r0 * rowlen + i) * C + c);
+      nl += 1.0;
+    }
+    a = sb_block_sum(a, red);
+    nl = sb_block_sum(nl, red);
+    const double n = nl, ns = n > 1.0 ? n : 1.0;
+    if (n > 0.0) live_bits |= 1u << sg;
+    const double mean = a / ns;
+    double q = 0.0;
+    for (long i = threadIdx.x; i < segn; i += SB_THREADS) {
+      const long r = r0 + i / rowlen;
+      if (rmask && !rmask[r]) continue;
+      const double d = (double)hld(x, (size_t)(r0 * rowlen + i) * C + c) - mean;
+      q += d * d;
+    }
+    q = sb_block_sum(q, red);
+    const double var = q / ns;
+    const float meanf = (float)mean, invstd = (float)(1.0 / sqrt(var + (double)eps));
+    for (long i = threadIdx.x; i < segn; i += SB_THREADS) {
+      const size_t k = (size_t)(r0 * rowlen + i) * C + c;
+      y[k] = (hld(x, k) - meanf) * invstd * g + bt;
+    }
+    if (threadIdx.x == 0) {
+      mean_o[(size_t)sg * C + c] = meanf;
+      invstd_o[(size_t)sg * C + c] = invstd;
+      varu_o[(size_t)sg * C + c] = (float)(n > 1.0 ? var * n / (n - 1.0) : var);
+      if (c == 0) cnt_o[sg] = (float)(n / (double)rowlen);
+    }
+  }
+  if (!update || threadIdx.x != 0) return;
+  // running statistics, segment after segment (a segment without live rows is skipped, as the reference skips the
+  // step); pre = an earlier call's [mean | invstd | varu | cnt] of the same nseg segments, applied first per segment
+  float rm = rmean[c], rv = rvar[c];
+  int64_t done = 0;
+  for (int sg = 0; sg < nseg; ++sg) {
+    if (pre) {
+      const float *pm = pre, *pv = pre + 2 * (size_t)nseg * C, *pc = pre + 3 * (size_t)nseg * C;
+      if (pc[sg] > 0.f) {
+        rm = rm * (1.f - momentum) + momentum * pm[(size_t)sg * C + c];
+        rv = rv * (1.f - momentum) + momentum * pv[(size_t)sg * C + c];
+        ++done;
+      }
+    }
+    if ((live_bits >> sg) & 1u) {
+      rm = rm * (1.f - momentum) + momentum * mean_o[(size_t)sg * C + c];
+      rv = rv * (1.f - momentum) + momentum * varu_o[(size_t)sg * C + c];
+      ++done;
+    }
+  }
+  rmean[c] = rm;
+  rvar[c] = rv;
+  if (c == 0 && nbt) nbt[0] += done;
+}
+
+// backward: per segment G1 = sum dy, G2 = sum dy * xhat over EVERY row (the forward's y of a row outside the mask
+// still depends on the segment's statistics), dx = gamma * invstd * (dy - w (G1 + xhat G2) / n) with w = the row's
+// mask; dgamma += sum_s G2, dbeta += sum_s G1 (f32 .grad, written or added: accumulate)
+template <typename T>
+__global__ void __launch_bounds__(SB_THREADS) k_seg_bn_bwd(const T *__restrict__ x, const float *__restrict__ dy,
+                                                          const uint8_t *__restrict__ rmask, int nseg, int B, int S,
+                                                          int C, const float *__restrict__ gamma,
+                                                          const float *__restrict__ st, T *__restrict__ dx,
+                                                          float *__restrict__ dgamma, float *__restrict__ dbeta,
+                                                          int accumulate) {
+  __shared__ double red[SB_THREADS / 64];
+  const int c = blockIdx.x;
+  const long rowlen = (long)S, segn = (long)B * rowlen;
+  const float *mean_i = st, *invstd_i = st + (size_t)nseg * C, *cnt_i = st + 3 * (size_t)nseg * C;
+  const float g = gamma ? gamma[c] : 1.f;
+  double tg1 = 0.0, tg2 = 0.0;
+  for (int sg = 0; sg < nseg; ++sg) {
+    const long r0 = (long)sg * B;
+    const float mean = mean_i[(size_t)sg * C + c], invstd = invstd_i[(size_t)sg * C + c];
+    double a1 = 0.0, a2 = 0.0;
+    for (long i = threadIdx.x; i < segn; i += SB_THREADS) {
+      const size_t k = (size_t)(r0 * rowlen + i) * C + c;
+      const double d = (double)dy[k];
+      a1 += d;
+      a2 += d * (double)((hld(x, k) - mean) * invstd);
+    }
+    a1 = sb_block_sum(a1, red);
+    a2 = sb_block_sum(a2, red);
+    tg1 += a1;
+    tg2 += a2;
+    const double n = (double)cnt_i[sg] * (double)rowlen;
+    const float c1 = n > 0.0 ? (float)(a1 / n) : 0.f, c2 = n > 0.0 ? (float)(a2 / n) : 0.f, k1 = g * invstd;
+    for (long i = threadIdx.x; i < segn; i += SB_THREADS) {
+      const long r = r0 + i / rowlen;
+      const size_t k = (size_t)(r0 * rowlen + i) * C + c;
+      const float w = (!rmask || rmask[r]) ? 1.f : 0.f;
+      const float xh = (hld(x, k) - mean) * invstd;
+      hst(dx, k, k1 * (dy[k] - w * (c1 + xh * c2)));
+    }
+  }
+  if (threadIdx.x == 0) {
+    if (dgamma) dgamma[c] = accumulate ? dgamma[c] + (float)tg2 : (float)tg2;
+    if (dbeta) dbeta[c] = accumulate ? dbeta[c] + (float)tg1 : (float)tg1;
+  }
+}
+
+template <typename T>
+int seg_bn_fwd(const void *x, const uint8_t *m, int nseg, int B, int S, int C, const float *gamma, const float *beta,
+               float eps, float *y, float *st, int update, float momentum, float *rmean, float *rvar, int64_t *nbt,
+               const float *pre, hipStream_t s) {
+  hipLaunchKernelGGL(k_seg_bn_fwd<T>, dim3(C), dim3(SB_THREADS), 0, s, (const T *)x, m, nseg, B, S, C, gamma, beta, eps,
+                     y, st, update, momentum, rmean, rvar, nbt, pre);
+  GMZ_LAUNCH_CHECK();
+  return 0;
+}
+
+template <typename T>
+int seg_bn_bwd(const void *x, const float *dy, const uint8_t *m, int nseg, int B, int S, int C, const float *gamma,
+               const float *st, void *dx, float *dgamma, float *dbeta, int acc, hipStream_t s) {
+  hipLaunchKernelGGL(k_seg_bn_bwd<T>, dim3(C), dim3(SB_THREADS), 0, s, (const T *)x, dy, m, nseg, B, S, C, gamma, st,
+                     (T *)dx, dgamma, dbeta, acc);
+  GMZ_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // namespace
+}  // namespace gmz
+
+GMZ_EXPORT int gmz_seg_bn_forward(int dtype, const void *x, const uint8_t *row_mask, int nseg, int B, int S, int C,
+                                  const float *gamma, const float *beta, float eps, float *y, float *stats, int update,
+                                  float momentum, float *running_mean, float *running_var, int64_t *num_batches,
+                                  const float *pre_stats, void *stream) {
+  if (!x || !y || !stats || nseg <= 0 || nseg > 32 || B <= 0 || S <= 0 || C <= 0 ||
+      (size_t)nseg * B * S * C >= (1ull << 31))
+    return fail("gmz_seg_bn_forward: bad arguments (1 <= nseg <= 32)");
+  if (update && (!running_mean || !running_var)) return fail("gmz_seg_bn_forward: update needs running statistics");
+  hipStream_t s = (hipStream_t)stream;
+  switch (dtype) {
+    case 0: return seg_bn_fwd<float>(x, row_mask, nseg, B, S, C, gamma, beta, eps, y, stats, update, momentum, running_mean,
+                                     running_var, num_batches, pre_stats, s);
+    case 1: return seg_bn_fwd<__half>(x, row_mask, nseg, B, S, C, gamma, beta, eps, y, stats, update, momentum, running_mean,
+                                      running_var, num_batches, pre_stats, s);
+    case 2: return seg_bn_fwd<__hip_bfloat16>(x, row_mask, nseg, B, S, C, gamma, beta, eps, y, stats, update, momentum,
+                                              running_mean, running_var, num_batches, pre_stats, s);
+  }
+  return fail("gmz_seg_bn_forward: dtype must be 0 (f32), 1 (f16) or 2 (bf16)");
+}
+
+GMZ_EXPORT int gmz_seg_bn_backward(int dtype, const void *x, const float *dy, const uint8_t *row_mask, int nseg, int B,
+                                   int S, int C, const float *gamma, const float *stats, void *dx, float *dgamma,
+                                   float *dbeta, int accumulate, void *stream) {
+  if (!x || !dy || !stats || !dx || nseg <= 0 || B <= 0 || S <= 0 || C <= 0 || (size_t)nseg * B * S * C >= (1ull << 31))
+    return fail("gmz_seg_bn_backward: bad arguments");
+  hipStream_t s = (hipStream_t)stream;
+  switch (dtype) {
+    case 0: return seg_bn_bwd<float>(x, dy, row_mask, nseg, B, S, C, gamma, stats, dx, dgamma, dbeta, accumulate, s);
+    case 1: return seg_bn_bwd<__half>(x, dy, row_mask, nseg, B, S, C, gamma, stats, dx, dgamma, dbeta, accumulate, s);
+    case 2:
+      return seg_bn_bwd<__hip_bfloat16>(x, dy, row_mask, nseg, B, S, C, gamma, stats, dx, dgamma, dbeta, accumulate, s);
+  }
+  return fail("gmz_seg_bn_backward: dtype must be 0 (f32), 1 (f16) or 2 (bf16)");
+}

@@ -1445,6 +1445,81 @@ def _bn_seg_grad(mod, x, ms):
     return y, st
 
 
+# the batched heads' segmented BatchNorms on one HIP kernel each way (gmz_seg_bn_forward / _backward, running
+# statistics inside the forward) instead of ~20 PyTorch launches forward and ~25 backward per call (False: PyTorch)
+SEG_BN_HIP = True
+
+
+class _SegBN(torch.autograd.Function):
+    """_bn_seg_grad's values and gradients for x [nseg*B, C(, H, W)] (channels-last 4-D or contiguous 2-D) on the
+    GPU: y float32 like x's layout, and the stats [3*nseg*C + nseg] (mean, invstd, unbiased var, live rows)."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, m, nseg, eps, update, momentum, rmean, rvar, nbt, pre):
+        from . import _lib
+        N, C = x.shape[0], x.shape[1]
+        S = x[0, 0].numel() if x.dim() > 2 else 1
+        if x.dim() == 4:
+            y = torch.empty((N, x.shape[2], x.shape[3], C), dtype=torch.float32, device=x.device).permute(0, 3, 1, 2)
+        else:
+            y = torch.empty((N, C), dtype=torch.float32, device=x.device)
+        st = torch.empty(3 * nseg * C + nseg, dtype=torch.float32, device=x.device)
+        _lib.check(_lib.load().gmz_seg_bn_forward(_BN_DTYPES[x.dtype], _lib.ptr(x), _lib.ptr(m), nseg, N // nseg, S, C,
+                                                  _lib.ptr(gamma), _lib.ptr(beta), float(eps), _lib.ptr(y), _lib.ptr(st),
+                                                  int(update), float(momentum), _lib.ptr(rmean), _lib.ptr(rvar),
+                                                  _lib.ptr(nbt), _lib.ptr(pre), _lib.stream_ptr()))
+        ctx.save_for_backward(x, gamma, beta, st, m)
+        ctx.nseg = nseg
+        ctx.mark_non_differentiable(st)
+        return y, st
+
+    @staticmethod
+    def backward(ctx, gy, _gst):
+        from . import _lib
+        x, gamma, beta, st, m = ctx.saved_tensors
+        N, C = x.shape[0], x.shape[1]
+        S = x[0, 0].numel() if x.dim() > 2 else 1
+        dy = gy.float()
+        dy = dy.permute(0, 2, 3, 1).contiguous() if x.dim() == 4 else dy.contiguous()  # [N][S][C] rows
+        dx = torch.empty_like(x)
+        direct = (_DIRECT_GRAD[0] and gamma.grad is not None and beta.grad is not None
+                  and gamma.grad.dtype == torch.float32 and beta.grad.dtype == torch.float32
+                  and gamma.grad.is_contiguous() and beta.grad.is_contiguous())
+        dg = gamma.grad if direct else torch.empty(C, dtype=torch.float32, device=x.device)
+        db = beta.grad if direct else torch.empty(C, dtype=torch.float32, device=x.device)
+        _lib.check(_lib.load().gmz_seg_bn_backward(_BN_DTYPES[x.dtype], _lib.ptr(x), _lib.ptr(dy), _lib.ptr(m), ctx.nseg,
+                                                   N // ctx.nseg, S, C, _lib.ptr(gamma), _lib.ptr(st), _lib.ptr(dx),
+                                                   _lib.ptr(dg), _lib.ptr(db), int(direct), _lib.stream_ptr()))
+        if direct:
+            return dx, None, None, None, None, None, None, None, None, None, None, None
+        return dx, dg, db, None, None, None, None, None, None, None, None, None
+
+
+def _bn_seg(mod, x, ms, update=True, pre=None):
+    """Training-mode BatchNorm of the ms.shape[0] stacked steps of x (each over its own live rows), the running
+    statistics updated (update) in step order — after ``pre``'s step by step when given (a previous call's handle:
+    the projection's dynamics steps before its targets').  Returns (y float32, handle).  GPU: _SegBN (HIP); CPU
+    and other layouts: _bn_seg_grad + _bn_running_update."""
+    nseg = ms.shape[0]
+    hip = (SEG_BN_HIP and FUSED_BN and x.is_cuda and x.dtype in _BN_DTYPES and mod.momentum is not None
+           and nseg <= 32 and x.shape[0] % nseg == 0
+           and ((x.dim() == 2 and x.is_contiguous()) or (x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last)))
+           and (pre is None or pre[0] == "hip"))
+    if hip:
+        m = ms.reshape(-1).contiguous().view(torch.uint8)
+        y, st = _SegBN.apply(x, mod.weight, mod.bias, m, nseg, mod.eps, bool(update), mod.momentum, mod.running_mean,
+                             mod.running_var, mod.num_batches_tracked, None if pre is None else pre[1])
+        return y, ("hip", st)
+    y, st = _bn_seg_grad(mod, x, ms)
+    if update:
+        if pre is None:
+            _bn_running_update(mod, [st])
+        else:  # interleaved: pre's step s, then this call's step s
+            _bn_running_update(mod, [tuple(torch.stack((a, b), 1).reshape(2 * nseg, *a.shape[1:])
+                                           for a, b in zip(pre[1], st))])
+    return y, ("torch", st)
+
+
 def _bn_running_update(mod, stats):
     """The running-statistics updates of a sequence of training-mode BatchNorm calls (``stats``: a list of
     _bn_seg_grad results, applied in list order, segment by segment; a segment with no live row is skipped, as the
@@ -1493,11 +1568,11 @@ def _prediction_seg(pred, h, ms, convs=None):
                                     pred.value_conv.bias)
     else:
         yp, yv = _conv1x1(pred.policy_conv, h), _conv1x1(pred.value_conv, h)
-    bp, sp = _bn_seg_grad(pred.policy_bn, yp, ms)
-    bv, sv = _bn_seg_grad(pred.value_bn, yv, ms)
+    bp, _ = _bn_seg(pred.policy_bn, yp, ms)  # running statistics updated in step order
+    bv, _ = _bn_seg(pred.value_bn, yv, ms)
     pol = pred.policy_fc(F.relu(bp).reshape(n, -1))
     v = F.relu(pred.value_fc1(F.relu(bv).reshape(n, -1)))
-    return pol, pred.value_fc2(v), (sp, sv)
+    return pol, pred.value_fc2(v)
 
 
 def _reward_projection_seg(model, h, ms, first=None):
@@ -1508,14 +1583,15 @@ def _reward_projection_seg(model, h, ms, first=None):
     proj = model.projection_net
     fc0, act, fc2 = model.dynamics_net.reward_fc
     a, r = first if first is not None else _linear_flat_pair(proj.fc1, fc0, h)
-    b, st = _bn_seg_grad(proj.bn1, a, ms)
+    b, st = _bn_seg(proj.bn1, a, ms, update=False)  # its running statistics go with the targets' (interleaved)
     return fc2(act(r)), proj.fc2(F.relu(b)), st
 
 
-def _projection_seg(proj, h, ms):
-    """projection (loss.py:104: with_grad=False) of U stacked steps, BatchNorm per step; returns (z, bn1 stats)."""
-    b, st = _bn_seg_grad(proj.bn1, _linear_flat(proj.fc1, h), ms)
-    return proj.fc2(F.relu(b)), st
+def _projection_seg(proj, h, ms, pre):
+    """projection (loss.py:104: with_grad=False) of U stacked steps, BatchNorm per step, its running statistics
+    updated after ``pre``'s (the dynamics projections') step by step — the reference's order."""
+    b, _ = _bn_seg(proj.bn1, _linear_flat(proj.fc1, h), ms, update=True, pre=pre)
+    return proj.fc2(F.relu(b))
 
 
 def _side_streams(device):
@@ -1620,9 +1696,7 @@ def muzero_loss(model, target_model, batch, is_weights, cfg, k=None, flip=None, 
             pred = model.prediction_net
             msp = torch.cat((torch.ones_like(ms[:1]), ms))
             first = _heads_input(model, hp, B)  # the heads' first layers in one node (None: no fused path)
-            pls_all, vls_all, (sp, sv) = _prediction_seg(pred, hp, msp, None if first is None else first[:2])
-            _bn_running_update(pred.policy_bn, [sp])
-            _bn_running_update(pred.value_bn, [sv])
+            pls_all, vls_all = _prediction_seg(pred, hp, msp, None if first is None else first[:2])
             rl_all, dyn_all, sdyn = _reward_projection_seg(model, hp[B:], ms, None if first is None else first[2:])
             with torch.no_grad():
                 if tru_h is None:
@@ -1634,10 +1708,8 @@ def muzero_loss(model, target_model, batch, is_weights, cfg, k=None, flip=None, 
                     th = tru_h[0] if len(tru_h) == 1 else torch.cat(tru_h)
                 if side is not None:
                     th.record_stream(main)
-                tru_all, stru = _projection_seg(model.projection_net, th, ms)
-            # the projection BatchNorm's running statistics in the reference's order: dynamics s, then target s
-            _bn_running_update(model.projection_net.bn1,
-                               [tuple(torch.stack((a, b), 1).reshape(2 * U, *a.shape[1:]) for a, b in zip(sdyn, stru))])
+                # the projection BatchNorm's running statistics in the reference's order: dynamics s, then target s
+                tru_all = _projection_seg(model.projection_net, th, ms, sdyn)
             pl, vl = pls_all[:B], vls_all[:B]
             lp = F.cross_entropy(pl.float(), pi[:, 0], reduction="none")
             lv = F.cross_entropy(vl.float(), zsup[0], reduction="none")

@@ -433,6 +433,24 @@ int gmz_grad_add_t_cols(int dtype, const void *src_dev, int P, int C, int O, int
 int gmz_head_conv1x1_forward(int dtype, const void *x_dev, long P, int C, const float *w0_dev, const float *b0_dev,
                              int O0, const float *w1_dev, const float *b1_dev, int O1, void *y0_dev, void *y1_dev,
                              void *stream);
+/* Training-mode BatchNorm of nseg stacked equal row segments (the batched heads' BatchNorms, network.py:62,65,95 over
+ * the unroll steps, trainer.BATCHED_HEADS): x_dev [nseg*B][S][C] (channels-last rows, or [N][C] with S = 1; dtype
+ * 0 = f32, 1 = f16, 2 = bf16), row_mask_dev uint8 [nseg*B] (NULL: every row) — segment s normalised over its own
+ * live rows (f64 sums, biased variance, eps), y_dev f32 [nseg*B][S][C] for every row.  stats_dev f32
+ * [3*nseg*C + nseg]: per segment and channel mean, invstd, unbiased variance, then per segment the live-row count.
+ * update != 0: running_mean/var_dev (f32 [C]) and num_batches_dev (int64) updated segment after segment, a segment
+ * without live rows skipped; pre_stats_dev (or NULL): an earlier call's stats of the same nseg segments whose update
+ * goes first in each segment (the projection's dynamics step s, then target s).  1 <= nseg <= 32.  (ABI 9) */
+int gmz_seg_bn_forward(int dtype, const void *x_dev, const uint8_t *row_mask_dev, int nseg, int B, int S, int C,
+                       const float *gamma_dev, const float *beta_dev, float eps, float *y_dev, float *stats_dev, int update,
+                       float momentum, float *running_mean_dev, float *running_var_dev, int64_t *num_batches_dev,
+                       const float *pre_stats_dev, void *stream);
+/* Its backward: dy_dev f32 like y; dx_dev like x (its dtype); dgamma/dbeta f32 [C] written or added (accumulate),
+ * NULL: skipped.  Every row's dy enters its segment's sums (a row outside the mask still depends on the segment's
+ * statistics through y); the mean/variance terms apply to the live rows. */
+int gmz_seg_bn_backward(int dtype, const void *x_dev, const float *dy_dev, const uint8_t *row_mask_dev, int nseg, int B,
+                        int S, int C, const float *gamma_dev, const float *stats_dev, void *dx_dev, float *dgamma_dev,
+                        float *dbeta_dev, int accumulate, void *stream);
 /* bytes of the backward's workspace for P positions and O = O0 + O1 outputs */
 int gmz_head_conv1x1_workspace_bytes(long P, int O, size_t *out);
 /* The backward of gmz_head_conv1x1_forward: dx_dev [P][128] = round(sum_o dy[p][o] W[o][c]) over BOTH heads
