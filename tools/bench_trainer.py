@@ -45,6 +45,8 @@ ap.add_argument("--per-step-heads", action="store_true",
                 help="prediction / reward / projection heads once per unroll step (trainer.BATCHED_HEADS off)")
 ap.add_argument("--torch-head-convs", action="store_true",
                 help="the prediction heads' 1x1 convs on PyTorch GEMMs (trainer.FUSED_HEADS off)")
+ap.add_argument("--torch-seg-bn", action="store_true",
+                help="the batched heads' segmented BatchNorms in PyTorch ops (trainer.SEG_BN_HIP off)")
 ap.add_argument("--no-benchmark", action="store_true", help="no torch.backends.cudnn.benchmark (MIOpen Find per shape)")
 a = ap.parse_args()
 a.channels_last, a.benchmark = not a.nchw, not a.no_benchmark
@@ -68,6 +70,7 @@ T.BATCHED_LOSS = T.BATCHED_LOSS and not a.per_step_loss
 T.BATCHED_CONSISTENCY = T.BATCHED_CONSISTENCY and not a.per_step_consistency
 T.BATCHED_HEADS = T.BATCHED_HEADS and not a.per_step_heads
 T.FUSED_HEADS = T.FUSED_HEADS and not a.torch_head_convs
+T.SEG_BN_HIP = T.SEG_BN_HIP and not a.torch_seg_bn
 T.DYN_STEM_HIP = T.DYN_STEM_HIP or a.hip_stem
 T.RELU_MASK = T.RELU_MASK or a.relu_mask
 T.TARGET_F16 = T.TARGET_F16 and not a.target_f32
@@ -140,6 +143,7 @@ if rank == 0:
                       "per": a.per, "sync_logs": a.sync_logs, "last_loss": logs[0], "data": "synthetic slices in a device ReplayBuffer",
                       "max_memory_allocated_gb": torch.cuda.max_memory_allocated() / 2 ** 30,
                       "defer_wgrad": T.DEFER_WGRAD, "batched_heads": T.BATCHED_HEADS, "fused_heads": T.FUSED_HEADS,
-                      "dyn_stem_hip": T.DYN_STEM_HIP, "relu_mask": T.RELU_MASK}))
+                      "dyn_stem_hip": T.DYN_STEM_HIP, "relu_mask": T.RELU_MASK,
+                      "seg_bn_hip": T.SEG_BN_HIP}))
 if dist:
     dist.destroy_process_group()
