@@ -1495,7 +1495,7 @@ class _SegBN(torch.autograd.Function):
         return dx, dg, db, None, None, None, None, None, None, None, None, None
 
 
-def _bn_seg(mod, x, ms, update=True, pre=None):
+def _bn_steps(mod, x, ms, update=True, pre=None):
     """Training-mode BatchNorm of the ms.shape[0] stacked steps of x (each over its own live rows), the running
     statistics updated (update) in step order — after ``pre``'s step by step when given (a previous call's handle:
     the projection's dynamics steps before its targets').  Returns (y float32, handle).  GPU: _SegBN (HIP); CPU
@@ -1568,8 +1568,8 @@ def _prediction_seg(pred, h, ms, convs=None):
                                     pred.value_conv.bias)
     else:
         yp, yv = _conv1x1(pred.policy_conv, h), _conv1x1(pred.value_conv, h)
-    bp, _ = _bn_seg(pred.policy_bn, yp, ms)  # running statistics updated in step order
-    bv, _ = _bn_seg(pred.value_bn, yv, ms)
+    bp, _ = _bn_steps(pred.policy_bn, yp, ms)  # running statistics updated in step order
+    bv, _ = _bn_steps(pred.value_bn, yv, ms)
     pol = pred.policy_fc(F.relu(bp).reshape(n, -1))
     v = F.relu(pred.value_fc1(F.relu(bv).reshape(n, -1)))
     return pol, pred.value_fc2(v)
@@ -1583,14 +1583,14 @@ def _reward_projection_seg(model, h, ms, first=None):
     proj = model.projection_net
     fc0, act, fc2 = model.dynamics_net.reward_fc
     a, r = first if first is not None else _linear_flat_pair(proj.fc1, fc0, h)
-    b, st = _bn_seg(proj.bn1, a, ms, update=False)  # its running statistics go with the targets' (interleaved)
+    b, st = _bn_steps(proj.bn1, a, ms, update=False)  # its running statistics go with the targets' (interleaved)
     return fc2(act(r)), proj.fc2(F.relu(b)), st
 
 
 def _projection_seg(proj, h, ms, pre):
     """projection (loss.py:104: with_grad=False) of U stacked steps, BatchNorm per step, its running statistics
     updated after ``pre``'s (the dynamics projections') step by step — the reference's order."""
-    b, _ = _bn_seg(proj.bn1, _linear_flat(proj.fc1, h), ms, update=True, pre=pre)
+    b, _ = _bn_steps(proj.bn1, _linear_flat(proj.fc1, h), ms, update=True, pre=pre)
     return proj.fc2(F.relu(b))
 
 
