@@ -1446,8 +1446,10 @@ def _bn_seg_grad(mod, x, ms):
 
 
 # the batched heads' segmented BatchNorms on one HIP kernel each way (gmz_seg_bn_forward / _backward, running
-# statistics inside the forward) instead of ~20 PyTorch launches forward and ~25 backward per call (False: PyTorch)
-SEG_BN_HIP = True
+# statistics inside the forward) instead of the PyTorch ops of _bn_seg_grad.  Equal to them (GPU test), 40 launches
+# fewer per step, but one workgroup per channel serialises the 1- and 2-channel heads (486 K elements each): 33.2 /
+# 34.0 vs 40.1 / 40.6 steps/s (profiles/r05_seg_bn_ab.txt).  Off; kept as an A/B path with its test
+SEG_BN_HIP = False
 
 
 class _SegBN(torch.autograd.Function):
