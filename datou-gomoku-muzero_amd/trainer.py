@@ -1348,16 +1348,17 @@ def augment(obs, pi, act, k, flip):
 def value_targets(rew, mcts_val, last_value, cfg):
     """loss.py:53-65: z_i = sum_{j<n, i+j<U} g^j r_{i+j} + g^n (v_{i+n} if i+n <= U else V_target(obs_U))."""
     U, n, g = cfg.NUM_UNROLL_STEPS, cfg.N_STEPS, cfg.DISCOUNT
-    out = torch.zeros_like(mcts_val)
-    for i in range(U + 1):
-        z = 0.0
-        for j in range(n):
-            if i + j >= U:
-                break
-            z = z + (g ** j) * rew[:, i + j]
-        boot = mcts_val[:, i + n] if i + n <= U else last_value
-        out[:, i] = z + (g ** n) * boot
-    return out
+    # every i at once, the same operations per element in the same order as the per-i loop of the reference
+    # (z_i = 0 + g^0 r_i + g^1 r_{i+1} + ..., then + g^n boot_i): bit-identical, ~13 launches instead of ~48
+    z = torch.zeros_like(mcts_val)
+    for j in range(min(n, U)):
+        z[:, :U - j] += (g ** j) * rew[:, j:U]
+    B = mcts_val.shape[0]
+    if n > U:
+        boot = last_value[:, None]
+    else:
+        boot = torch.cat((mcts_val[:, n:U + 1], last_value[:, None].expand(B, n)), 1)
+    return z + (g ** n) * boot
 
 
 class _HalveGrad(torch.autograd.Function):
