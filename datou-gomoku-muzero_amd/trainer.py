@@ -1447,10 +1447,12 @@ def _bn_seg_grad(mod, x, ms):
 
 
 # the batched heads' segmented BatchNorms on one HIP kernel each way (gmz_seg_bn_forward / _backward, running
-# statistics inside the forward) instead of the PyTorch ops of _bn_seg_grad.  Equal to them (GPU test), 40 launches
-# fewer per step, but one workgroup per channel serialises the 1- and 2-channel heads (486 K elements each): 33.2 /
-# 34.0 vs 40.1 / 40.6 steps/s (profiles/r05_seg_bn_ab.txt).  Off; kept as an A/B path with its test
-SEG_BN_HIP = False
+# statistics inside the forward) instead of the PyTorch ops of _bn_seg_grad — for the BatchNorms with at least
+# SEG_BN_HIP_MIN_C channels (the projection's bn1, C = 512: one workgroup per channel over 5 x 360 rows).  The 1- and
+# 2-channel heads stay on PyTorch: one workgroup per channel serialises their 486 K elements (all four on HIP: 33.2 /
+# 34.0 vs 40.1 / 40.6 steps/s, profiles/r05_seg_bn_ab.txt).  False: every call on PyTorch (A/B)
+SEG_BN_HIP = True
+SEG_BN_HIP_MIN_C = 64
 
 
 class _SegBN(torch.autograd.Function):
@@ -1505,7 +1507,7 @@ def _bn_steps(mod, x, ms, update=True, pre=None):
     and other layouts: _bn_seg_grad + _bn_running_update."""
     nseg = ms.shape[0]
     hip = (SEG_BN_HIP and FUSED_BN and x.is_cuda and x.dtype in _BN_DTYPES and mod.momentum is not None
-           and nseg <= 32 and x.shape[0] % nseg == 0
+           and x.shape[1] >= SEG_BN_HIP_MIN_C and nseg <= 32 and x.shape[0] % nseg == 0
            and ((x.dim() == 2 and x.is_contiguous()) or (x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last)))
            and (pre is None or pre[0] == "hip"))
     if hip:
