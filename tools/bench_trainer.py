@@ -47,6 +47,8 @@ ap.add_argument("--torch-head-convs", action="store_true",
                 help="the prediction heads' 1x1 convs on PyTorch GEMMs (trainer.FUSED_HEADS off)")
 ap.add_argument("--torch-seg-bn", action="store_true",
                 help="the batched heads' segmented BatchNorms in PyTorch ops (trainer.SEG_BN_HIP off)")
+ap.add_argument("--op-sources", type=int, default=0, metavar="N",
+                help="with --eager: profile one more step and print the N trainer.py lines launching the most PyTorch kernels")
 ap.add_argument("--no-benchmark", action="store_true", help="no torch.backends.cudnn.benchmark (MIOpen Find per shape)")
 a = ap.parse_args()
 a.channels_last, a.benchmark = not a.nchw, not a.no_benchmark
@@ -145,5 +147,71 @@ if rank == 0:
                       "defer_wgrad": T.DEFER_WGRAD, "batched_heads": T.BATCHED_HEADS, "fused_heads": T.FUSED_HEADS,
                       "dyn_stem_hip": T.DYN_STEM_HIP, "relu_mask": T.RELU_MASK,
                       "seg_bn_hip": T.SEG_BN_HIP}))
+if a.op_sources and rank == 0:
+    # which trainer.py lines launch PyTorch's kernels (the libgmz launches have no aten op and are not counted)
+    from collections import Counter
+    from torch.profiler import ProfilerActivity, profile
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
+        step()
+        torch.cuda.synchronize()
+    per_line, per_kernel = Counter(), Counter()
+    for ev in prof.events():
+        ks = getattr(ev, "kernels", None) or []
+        if not ks:
+            continue
+        # the kernels hang on the innermost aten op; the Python stack is on its outermost ancestor, and the
+        # backward's ops sit under the autograd node that ran them
+        fr, up = None, ev
+        while up is not None:
+            if up.name.startswith("autograd::engine::evaluate_function"):
+                fr = up.name.split(": ", 1)[-1]
+                break
+            if up.stack:
+                fr = next((f for f in up.stack if "trainer.py" in f), up.stack[0])
+                break
+            up = up.cpu_parent
+        per_line[(fr or "?", ev.name)] += len(ks)
+        for k in ks:
+            per_kernel[k.name[:60]] += 1
+    print("op-sources: %d PyTorch kernels in one eager step" % sum(per_line.values()))
+    # the same step under a dispatch mode: every aten op by the trainer.py line that issued it (forward, and the
+    # custom Functions' backward bodies; built-in backward nodes show as "<autograd>")
+    import traceback
+    from torch.utils._python_dispatch import TorchDispatchMode
+
+    class _Lines(TorchDispatchMode):
+        def __init__(self):
+            super().__init__()
+            self.n = Counter()
+
+        def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+            out = func(*args, **(kwargs or {}))
+            dev = any(isinstance(t, torch.Tensor) and t.is_cuda for t in torch.utils._pytree.tree_leaves((args, kwargs, out)))
+            if dev and func.__name__ not in ("view.default", "_unsafe_view.default", "t.default", "detach.default",
+                                             "as_strided.default", "permute.default", "expand.default",
+                                             "slice.Tensor", "select.int", "unsqueeze.default", "squeeze.dim",
+                                             "transpose.int", "reshape.default", "empty.memory_format",
+                                             "empty_strided.default", "alias.default", "unbind.int", "split.Tensor",
+                                             "split_with_sizes.default", "chunk.default", "narrow.default",
+                                             "_reshape_alias.default", "view_as.default", "empty_like.default",
+                                             "new_empty.default", "new_empty_strided.default", "is_same_size.default",
+                                             "set_.source_Storage_storage_offset", "_local_scalar_dense.default",
+                                             "squeeze.default", "diagonal.default", "view.dtype", "unflatten.int", "flatten.using_ints"):
+                fr = [f for f in traceback.extract_stack() if os.path.basename(f.filename) == "trainer.py"]
+                key = "%s:%d %s" % ("trainer.py", fr[-1].lineno, fr[-1].name) if fr else "<autograd>"
+                self.n[(key, func.__name__)] += 1
+            return out
+
+    m = _Lines()
+    with m:
+        step()
+        torch.cuda.synchronize()
+    print("dispatch: %d device aten ops (not view-like) in one eager step" % sum(m.n.values()))
+    for (fr, name), n in m.n.most_common(a.op_sources):
+        print("%5d  %-40s %s" % (n, name, fr))
+    for (fr, name), n in per_line.most_common(a.op_sources):
+        print("%5d  %-28s %s" % (n, name, fr))
+    for k, n in per_kernel.most_common(20):
+        print("%5d  %s" % (n, k))
 if dist:
     dist.destroy_process_group()
