@@ -809,11 +809,23 @@ int splits_for(int B, int C, int S, int nhwc) {
 
 size_t ws_doubles(int B, int C, int S, int nhwc) { return (size_t)C * splits_for(B, C, S, nhwc) * 3; }
 
-// NHWC elementwise grid: ~4 position steps per thread, at most 4096 workgroups
+// NHWC elementwise grid: ~2 position steps per thread, at most 16,384 workgroups (GMZ_BN_EW_STEPS: 1, 2, 4 or 8,
+// an A/B; trainer 40.59 / 40.64 steps/s at 2 vs 39.84 / 40.09 at 4 and 39.70 / 39.99 at 1,
+// profiles/r05_bn_ew_steps_ab.txt — the 1,800-board consistency BatchNorms gain from the larger grid)
+static int ew_steps() {
+  static int k = 0;
+  if (!k) {
+    const char *e = getenv("GMZ_BN_EW_STEPS");
+    const int v = e ? atoi(e) : 2;
+    k = (v == 1 || v == 2 || v == 4 || v == 8) ? v : 2;
+  }
+  return k;
+}
+
 int elementwise_blocks(long P, int C, int V) {
-  const long pl = BN_THREADS / (C / V);
-  long nb = (P + 4 * pl - 1) / (4 * pl);
-  return (int)(nb < 4096 ? (nb < 1 ? 1 : nb) : 4096);
+  const long pl = BN_THREADS / (C / V), k = ew_steps();
+  long nb = (P + k * pl - 1) / (k * pl);
+  return (int)(nb < 16384 ? (nb < 1 ? 1 : nb) : 16384);
 }
 
 // channel vector width of the NHWC kernels: 8 when C allows it and every operand is 16-B aligned

@@ -1,0 +1,17 @@
+#!/bin/bash
+# A/B of the NHWC BatchNorm elementwise passes' position steps per thread (GMZ_BN_EW_STEPS)
+set -o pipefail
+OUT=gpurun_out/bnew
+mkdir -p $OUT
+for i in 1 2; do
+  for n in 4 2 1 8; do
+    GMZ_BN_EW_STEPS=$n timeout -k 10 120 python3 tools/bn_bench.py 300 > $OUT/bn_${n}_$i.json 2> $OUT/bn_${n}_$i.err || { echo "bn $n failed"; tail -3 $OUT/bn_${n}_$i.err; exit 1; }
+    echo "steps $n: $(cat $OUT/bn_${n}_$i.json)" | tee -a $OUT/summary.txt
+  done
+done
+for i in 1 2; do
+  for n in 4 2 1; do
+    GMZ_BN_EW_STEPS=$n timeout -k 10 240 python3 -u tools/bench_trainer.py --steps 40 --warmup 8 --per > $OUT/tr_${n}_$i.json 2> $OUT/tr_${n}_$i.err || { echo "trainer $n failed"; tail -3 $OUT/tr_${n}_$i.err; exit 1; }
+    echo "trainer steps $n: $(python3 -c "import json; print(json.loads(open('$OUT/tr_${n}_$i.json').read().strip().splitlines()[-1])['value'])")" | tee -a $OUT/summary.txt
+  done
+done
