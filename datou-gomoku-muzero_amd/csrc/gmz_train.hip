@@ -321,6 +321,9 @@ __device__ __forceinline__ void stv(T *p, size_t k, const float *a) {
   *reinterpret_cast<VecT<T, V> *>(p + k) = r;
 }
 
+#ifndef GMZ_BN_APPLY_PAIR
+#define GMZ_BN_APPLY_PAIR 1
+#endif
 constexpr int BNL_MAX_SPLITS = 1024;  // 1,024 vs 512: backward 37.0 vs 38.6 us, forward 25.7 vs 25.1 (profiles/r05_bn_splits_ab.txt)
 
 // stats (BWD = 0) or dz sums (BWD = 1) of the masked pixels of workgroup t's pixel range.  nseg > 1: the B rows
@@ -454,27 +457,42 @@ __global__ void __launch_bounds__(BN_THREADS) k_bnl_apply(const T *__restrict__ 
   float mean[V];
 #pragma unroll
   for (int j = 0; j < V; ++j) mean[j] = save[c + j];
-  for (long p = pbeg + (long)blockIdx.x * pl + grp; p < P; p += (long)gridDim.x * pl) {
-    const size_t k = (size_t)p * C + c;
-    float v[V], r[V];
-    ldv<T, V>(x, k, v);
-    if (res) ldv<T, V>(res, k, r);
+  // two positions per trip, both loads issued before either is used (GMZ_BN_APPLY_PAIR, default on)
+  const long gs = (long)gridDim.x * pl;
+  for (long p = pbeg + (long)blockIdx.x * pl + grp; p < P; p += (GMZ_BN_APPLY_PAIR ? 2 : 1) * gs) {
+    constexpr int U = GMZ_BN_APPLY_PAIR ? 2 : 1;
+    float v[U][V], r[U][V];
+    bool ok[U];
 #pragma unroll
-    for (int j = 0; j < V; ++j) {
-      v[j] = (v[j] - mean[j]) * sc[j] + sh[j];
-      if (res) v[j] += r[j];
-      if (relu) v[j] = fmaxf(v[j], 0.f);
+    for (int u = 0; u < U; ++u) {
+      ok[u] = p + u * gs < P;
+      if (!ok[u]) continue;
+      const size_t k = (size_t)(p + u * gs) * C + c;
+      ldv<T, V>(x, k, v[u]);
+      if (res) ldv<T, V>(res, k, r[u]);
     }
-    stv<T, V>(y, k, v);
-    if (V == 8 && relu && rmask) {  // the ReLU's mask of the STORED (rounded) values: bit j = y > 0
-      uint8_t bits = 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (!ok[u]) continue;
+      const long pp = p + u * gs;
+      const size_t k = (size_t)pp * C + c;
 #pragma unroll
       for (int j = 0; j < V; ++j) {
-        T t[1];
-        st(t, 0, v[j]);
-        bits |= (ld(t, 0) > 0.f ? 1 : 0) << j;
+        v[u][j] = (v[u][j] - mean[j]) * sc[j] + sh[j];
+        if (res) v[u][j] += r[u][j];
+        if (relu) v[u][j] = fmaxf(v[u][j], 0.f);
       }
-      rmask[(size_t)p * (C / 8) + cp] = bits;
+      stv<T, V>(y, k, v[u]);
+      if (V == 8 && relu && rmask) {  // the ReLU's mask of the STORED (rounded) values: bit j = y > 0
+        uint8_t bits = 0;
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          T t[1];
+          st(t, 0, v[u][j]);
+          bits |= (ld(t, 0) > 0.f ? 1 : 0) << j;
+        }
+        rmask[(size_t)pp * (C / 8) + cp] = bits;
+      }
     }
   }
 }
