@@ -321,6 +321,9 @@ __device__ __forceinline__ void stv(T *p, size_t k, const float *a) {
   *reinterpret_cast<VecT<T, V> *>(p + k) = r;
 }
 
+#ifndef GMZ_BN_BWD_PAIR  // measured slower (backward 40.0-40.3 vs 37.4 us per call, profiles/r05_bn_bwd_pair_ab.txt)
+#define GMZ_BN_BWD_PAIR 0
+#endif
 #ifndef GMZ_BN_APPLY_PAIR
 #define GMZ_BN_APPLY_PAIR 1
 #endif
@@ -520,36 +523,51 @@ __global__ void __launch_bounds__(BN_THREADS) k_bnl_bwd_apply(const T *__restric
     mgx[j] = coef[C + c + j];
     k1[j] = gamma[c + j] * is[j];
   }
-  for (long p = (long)blockIdx.x * pl + grp; p < P; p += (long)gridDim.x * pl) {
-    const size_t k = (size_t)p * C + c;
-    const bool in = !mask || mask[p / S];
-    float g[V], d[V];
-    ldv<T, V>(dy, k, g);
-    if (use_mask) {
-      const uint8_t mb = rmask[(size_t)p * (C / 8) + cp];
+  // GMZ_BN_BWD_PAIR = 1: two positions per trip, every load of both issued before either is used (A/B; off)
+  constexpr int U = GMZ_BN_BWD_PAIR ? 2 : 1;
+  const long gs = (long)gridDim.x * pl;
+  for (long p = (long)blockIdx.x * pl + grp; p < P; p += U * gs) {
+    float g[U][V], yv[U][V], xv[U][V];
+    uint8_t mb[U];
+    bool ok[U], in[U];
 #pragma unroll
-      for (int j = 0; j < V; ++j)
-        if (!((mb >> j) & 1)) g[j] = 0.f;
-    } else if (relu) {
-      float yv[V];
-      ldv<T, V>(y, k, yv);
-#pragma unroll
-      for (int j = 0; j < V; ++j)
-        if (!(yv[j] > 0.f)) g[j] = 0.f;
-    }
-    if (dres) stv<T, V>(dres, k, g);
-    if (in) {
-      float xv[V];
-      ldv<T, V>(x, k, xv);
-#pragma unroll
-      for (int j = 0; j < V; ++j) d[j] = g[j] - mg[j] - (xv[j] - mean[j]) * is[j] * mgx[j];
-    } else {
-#pragma unroll
-      for (int j = 0; j < V; ++j) d[j] = g[j];
+    for (int u = 0; u < U; ++u) {
+      const long pp = p + u * gs;
+      ok[u] = pp < P;
+      if (!ok[u]) continue;
+      const size_t k = (size_t)pp * C + c;
+      in[u] = !mask || mask[pp / S];
+      ldv<T, V>(dy, k, g[u]);
+      if (use_mask) mb[u] = rmask[(size_t)pp * (C / 8) + cp];
+      else if (relu) ldv<T, V>(y, k, yv[u]);
+      if (in[u]) ldv<T, V>(x, k, xv[u]);
     }
 #pragma unroll
-    for (int j = 0; j < V; ++j) d[j] *= k1[j];
-    stv<T, V>(dx, k, d);
+    for (int u = 0; u < U; ++u) {
+      if (!ok[u]) continue;
+      const size_t k = (size_t)(p + u * gs) * C + c;
+      float d[V];
+      if (use_mask) {
+#pragma unroll
+        for (int j = 0; j < V; ++j)
+          if (!((mb[u] >> j) & 1)) g[u][j] = 0.f;
+      } else if (relu) {
+#pragma unroll
+        for (int j = 0; j < V; ++j)
+          if (!(yv[u][j] > 0.f)) g[u][j] = 0.f;
+      }
+      if (dres) stv<T, V>(dres, k, g[u]);
+      if (in[u]) {
+#pragma unroll
+        for (int j = 0; j < V; ++j) d[j] = g[u][j] - mg[j] - (xv[u][j] - mean[j]) * is[j] * mgx[j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < V; ++j) d[j] = g[u][j];
+      }
+#pragma unroll
+      for (int j = 0; j < V; ++j) d[j] *= k1[j];
+      stv<T, V>(dx, k, d);
+    }
   }
 }
 
