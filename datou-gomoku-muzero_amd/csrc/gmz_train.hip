@@ -321,6 +321,9 @@ __device__ __forceinline__ void stv(T *p, size_t k, const float *a) {
   *reinterpret_cast<VecT<T, V> *>(p + k) = r;
 }
 
+#ifndef GMZ_BNL_BWD_U  // positions per trip of the backward reduction (A/B)
+#define GMZ_BNL_BWD_U 2
+#endif
 #ifndef GMZ_BN_BWD_PAIR  // measured slower (backward 40.0-40.3 vs 37.4 us per call, profiles/r05_bn_bwd_pair_ab.txt)
 #define GMZ_BN_BWD_PAIR 0
 #endif
@@ -365,7 +368,7 @@ __global__ void __launch_bounds__(BN_THREADS) k_bnl_red(const T *__restrict__ x,
   if (grp < pl) {
     // U positions per thread per trip, every load of a trip issued before any arithmetic (the
     // loop is latency-bound otherwise: one HBM round trip per position)
-    constexpr int U = BWD ? 2 : 8;  // measured (tools/ab_bn.sh): backward 34.4 vs 35.7 us at U = 4, 36.8 at 8
+    constexpr int U = BWD ? GMZ_BNL_BWD_U : 8;  // measured (tools/ab_bn.sh): backward 34.4 vs 35.7 us at U = 4, 36.8 at 8
     using VT = VecT<T, V>;
     for (long p = p0 + grp; p < p1; p += (long)U * pl) {
       VT rx[U], rd[U], ry[U];
