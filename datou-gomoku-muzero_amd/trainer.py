@@ -2116,8 +2116,12 @@ class Trainer:
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        # with a process group, RCCL's watchdog thread queries its work events at any time; in the default global
+        # capture mode such a query from another thread during the capture fails the process ("operation not
+        # permitted when stream is capturing"), so the capture only restricts this thread
+        mode = "thread_local" if self.dist is not None else "global"
         with torch.cuda.stream(s):
-            with torch.cuda.graph(g1, stream=s):
+            with torch.cuda.graph(g1, stream=s, capture_error_mode=mode):
                 self._out = self._forward_backward(st[:6], st[6], augmented=True, flush=self.dist is None)
                 if self.dist is None:
                     self._update()
@@ -2126,9 +2130,9 @@ class Trainer:
                 # the deferred weight gradients (bucket B) as a graph of their own, replayed while bucket A's
                 # all-reduce runs; then the update
                 gf = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(gf, stream=s, pool=g1.pool()):
+                with torch.cuda.graph(gf, stream=s, pool=g1.pool(), capture_error_mode=mode):
                     self._flush()
-                with torch.cuda.graph(g2, stream=s, pool=g1.pool()):
+                with torch.cuda.graph(g2, stream=s, pool=g1.pool(), capture_error_mode=mode):
                     self._update()
         torch.cuda.current_stream(self.device).wait_stream(s)
         self._graphs = (g1, g2 if self.dist is not None else None, gf)
