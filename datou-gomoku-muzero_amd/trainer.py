@@ -2119,7 +2119,9 @@ class Trainer:
         # with a process group, RCCL's watchdog thread queries its work events at any time; in the default global
         # capture mode such a query from another thread during the capture fails the process ("operation not
         # permitted when stream is capturing"), so the capture only restricts this thread
-        mode = "thread_local" if self.dist is not None else "global"
+        import torch.distributed as tdist
+        pg = self.dist is not None or (tdist.is_available() and tdist.is_initialized())
+        mode = "thread_local" if pg else "global"
         with torch.cuda.stream(s):
             with torch.cuda.graph(g1, stream=s, capture_error_mode=mode):
                 self._out = self._forward_backward(st[:6], st[6], augmented=True, flush=self.dist is None)
