@@ -172,6 +172,9 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--trainer-steps", type=int, default=20, help="timed trainer steps (0: no trainer leg)")
     ap.add_argument("--trainer-warmup", type=int, default=6)
+    ap.add_argument("--trainer-f32-steps", type=int, default=10,
+                    help="timed steps of the same trainer with the reference's float32 target network (value_target_f32; "
+                         "0: skip)")
     ap.add_argument("--trainer-batch", type=int, default=360)
     ap.add_argument("--trainer-buffer", type=int, default=4096, help="synthetic slices per rank's PER shard")
     ap.add_argument("--loop-iters", type=int, default=20, help="timed iterations of the C4 loop (0: no loop leg)")
@@ -451,37 +454,52 @@ def trainer_leg(args, world, rank, dist, backend):
     torch.backends.cudnn.benchmark = True  # MIOpen Find for the convolutions left on MIOpen
     cfg = T.TrainConfig(BOARD_SIZE=args.size, NUM_RES_BLOCKS=args.blocks, PHYSICAL_BATCH_SIZE=args.trainer_batch,
                         TRAIN_BUFFER_SIZE=args.trainer_buffer, ENABLE_PER=True)
-    tr = T.Trainer(cfg, device="cuda")
     rb = T.ReplayBuffer(cfg, device="cuda")
     rs = np.random.RandomState(args.seed + 31 * rank)
     rb.add_arrays(*W.synthetic_slices(args.trainer_buffer, args.size, cfg.NUM_UNROLL_STEPS, rs))
     group = dist if dist is not None else None
-    pending = [None]
 
-    def step():
-        batch, idx, w = rb.sample(args.trainer_batch, rs, dist=group)
-        logs, td = tr.step(batch, w, sync=False)
-        rb.update_priorities(idx, td, dist=group)
-        prev, pending[0] = pending[0], logs
-        return prev
+    def timed_run(steps, target_f16):
+        """A fresh trainer with trainer.TARGET_F16 = target_f16: warm-up, then `steps` timed steps -> (seconds, last
+        loss, allreduce_ms)."""
+        saved = T.TARGET_F16
+        T.TARGET_F16 = target_f16
+        try:
+            tr = T.Trainer(cfg, device="cuda")
+            pending = [None]
 
-    t_w = time.perf_counter()
-    for _ in range(args.trainer_warmup):
-        step()
-    torch.cuda.synchronize()
-    log("rank %d: trainer warm-up %.1f s (MIOpen Find, graph capture)" % (rank, time.perf_counter() - t_w))
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.trainer_steps):
-        step()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    dt = collective_max(time.perf_counter() - t0, dist, backend)
-    loss = float(pending[0][0]) if pending[0] is not None else None
-    ar_ms = tr.allreduce_ms()
+            def step():
+                batch, idx, w = rb.sample(args.trainer_batch, rs, dist=group)
+                logs, td = tr.step(batch, w, sync=False)
+                rb.update_priorities(idx, td, dist=group)
+                pending[0] = logs
+
+            t_w = time.perf_counter()
+            for _ in range(args.trainer_warmup):
+                step()
+            torch.cuda.synchronize()
+            log("rank %d: trainer warm-up %.1f s (MIOpen Find, graph capture; target trunk %s)"
+                % (rank, time.perf_counter() - t_w, "f16" if target_f16 else "f32"))
+            if dist:
+                dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                step()
+            torch.cuda.synchronize()
+            if dist:
+                dist.barrier()
+            dt = collective_max(time.perf_counter() - t0, dist, backend)
+            return dt, float(pending[0][0]) if pending[0] is not None else None, tr.allreduce_ms()
+        finally:
+            T.TARGET_F16 = saved
+
+    dt, loss, ar_ms = timed_run(args.trainer_steps, True)
+    # the reference's precision for the target network's value (loss.py:54-55: a float32 forward outside autocast):
+    # the same step with trainer.TARGET_F16 = False, beside the line's f16-trunk rate (VERDICT r5 next #3)
+    f32_steps = args.trainer_f32_steps
+    dt32 = timed_run(f32_steps, False)[0] if f32_steps > 0 else None
+    torch.cuda.empty_cache()
     step_flop = trainer_flop_per_step(args.size, args.blocks, args.trainer_batch, cfg.NUM_UNROLL_STEPS)
     step_ach = step_flop * args.trainer_steps / dt / 1e12
     # the dominant HIP kernel of the step: the 128->128 residual-block conv (forward and input gradient),
@@ -507,7 +525,11 @@ def trainer_leg(args, world, rank, dist, backend):
             "value": args.trainer_steps / dt, "unit": "steps/s", "n_gpus": world, "steps": args.trainer_steps,
             "warmup": args.trainer_warmup, "ms_per_step": dt / args.trainer_steps * 1e3,
             "samples_per_s": args.trainer_steps * B * world / dt, "higher_is_better": True, "scaling": "weak",
-            "dtype": "fp16 autocast (f32 master weights; f32 target network, as the reference)",
+            "dtype": ("fp16 autocast (f32 master weights); the target network's value on an f16 trunk (f16 operands, f32 "
+                      "accumulation, f16 activations: trainer.TARGET_F16, a stated parity exception, DESIGN.md 8) — "
+                      "value_target_f32 is the same step with the reference's float32 target"),
+            "value_target_f32": f32_steps / dt32 if dt32 else None,
+            "steps_target_f32": f32_steps,
             "data": "synthetic slices in a device PER shard per rank (%d each)" % args.trainer_buffer,
             "parallelism": "ddp%d: one flat-bucket gradient all-reduce + sharded-PER syncs per step" % world
             if world > 1 else "single GPU",

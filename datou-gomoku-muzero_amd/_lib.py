@@ -11,12 +11,13 @@ import torch  # noqa: F401  (must precede the CDLL load: shared HIP runtime)
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GMZ_LIB") or os.path.join(PKG_DIR, "libgmz.so")  # GMZ_LIB: A/B builds (tools)
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 P = ctypes.c_void_p
 I = ctypes.c_int
 L = ctypes.c_long
 U64 = ctypes.c_uint64
+SZ = ctypes.c_size_t  # capacity arguments (ABI 10): a buffer's size in bytes
 
 
 class EngineCfg(ctypes.Structure):
@@ -59,36 +60,39 @@ _SIGS = {
     "gmz_hashnet_initial": ([P, I, I, P, P, P, P, P], I),
     "gmz_hashnet_recurrent": ([P, P, P, P, I, I, P, P, P, P], I),
     "gmz_bn_workspace_bytes": ([I, I, I, I, ctypes.POINTER(ctypes.c_size_t)], I),
-    "gmz_bn_forward": ([I, I, P, P, P, I, I, I, P, P, ctypes.c_float, ctypes.c_float, P, P, P, I, P, P, P, P], I),
-    "gmz_bn_backward": ([I, I, P, P, P, P, I, I, I, P, P, I, P, P, P, P, P, P], I),
-    "gmz_bn_backward_acc": ([I, I, P, P, P, P, I, I, I, P, P, I, P, P, P, P, P, P, I], I),
-    "gmz_bn_eval": ([I, I, P, P, I, I, I, P, P, P, P, ctypes.c_float, I, P, P, P], I),
+    "gmz_bn_forward": ([I, I, P, P, P, I, I, I, P, P, ctypes.c_float, ctypes.c_float, P, P, P, I, P, P, P, SZ, P], I),
+    "gmz_bn_backward": ([I, I, P, P, P, P, I, I, I, P, P, I, P, P, P, P, P, SZ, P], I),
+    "gmz_bn_backward_acc": ([I, I, P, P, P, P, I, I, I, P, P, I, P, P, P, P, P, SZ, P, I], I),
+    "gmz_bn_eval": ([I, I, P, P, I, I, I, P, P, P, P, ctypes.c_float, I, P, P, SZ, P], I),
     "gmz_conv3x3_pack": ([I, P, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, I, P, P], I),
     "gmz_conv3x3_forward": ([I, I, P, P, P, I, P], I),
     "gmz_conv3x3_forward_add": ([I, I, P, P, P, P, I, P], I),
     "gmz_conv3x3_stats_slots": ([I, ctypes.POINTER(ctypes.c_int)], I),
     "gmz_conv3x3_wgrad_workspace_bytes": ([I, ctypes.POINTER(ctypes.c_size_t)], I),
-    "gmz_conv3x3_wgrad": ([I, I, P, P, I, P, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, I, P, P], I),
+    "gmz_conv3x3_wgrad": ([I, I, P, P, I, P, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, I, P, SZ, P],
+                          I),
     "gmz_conv3x3_wgrad_segments": ([I, I, P, P, I, I, P, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
-                                    I, P, P], I),
-    "gmz_conv3x3_forward_stats": ([I, I, P, P, P, I, P, P, P], I),
-    "gmz_conv3x3_forward_bwdstats": ([I, I, P, P, P, P, I, P, P, P, P, I, P, P], I),
-    "gmz_bn_backward_stats": ([I, P, P, P, P, I, I, I, P, P, I, P, P, P, P, P, I, P, P, I], I),
+                                    I, P, SZ, P], I),
+    "gmz_conv3x3_forward_stats": ([I, I, P, P, P, I, P, P, I, P], I),
+    "gmz_conv3x3_forward_bwdstats": ([I, I, P, P, P, P, I, P, P, P, P, I, P, I, P], I),
+    "gmz_bn_backward_stats": ([I, P, P, P, P, I, I, I, P, P, I, P, P, P, P, P, I, SZ, P, SZ, P, I], I),
     "gmz_grad_add_t": ([I, P, I, I, I, P, P], I),
     "gmz_grad_add_t_cols": ([I, P, I, I, I, I, I, P, P], I),
     "gmz_head_conv1x1_forward": ([I, P, L, I, P, P, I, P, P, I, P, P, P], I),
     "gmz_head_conv1x1_workspace_bytes": ([L, I, P], I),
-    "gmz_seg_bn_forward": ([I, P, P, I, I, I, I, P, P, ctypes.c_float, P, P, I, ctypes.c_float, P, P, P, P, P], I),
-    "gmz_seg_bn_backward": ([I, P, P, P, I, I, I, I, P, P, P, P, P, I, P], I),
-    "gmz_head_conv1x1_backward": ([I, P, L, I, P, I, P, I, P, P, P, P, P, P, P, I, P, P], I),
-    "gmz_bn_forward_stats": ([I, P, P, I, I, I, P, P, ctypes.c_float, ctypes.c_float, P, P, P, I, P, P, P, I, P], I),
-    "gmz_bn_forward_seg": ([I, P, P, P, I, I, I, I, P, P, ctypes.c_float, ctypes.c_float, P, P, P, I, P, P, P, P, P], I),
-    "gmz_conv3x3_forward_board_stats": ([I, I, P, P, P, I, P, P, P], I),
+    "gmz_seg_bn_forward": ([I, P, P, I, I, I, I, P, P, ctypes.c_float, P, P, SZ, I, ctypes.c_float, P, P, P, P, P], I),
+    "gmz_seg_bn_backward": ([I, P, P, P, I, I, I, I, P, P, SZ, P, P, P, I, P], I),
+    "gmz_head_conv1x1_backward": ([I, P, L, I, P, I, P, I, P, P, P, P, P, P, P, I, P, SZ, P], I),
+    "gmz_bn_forward_stats": ([I, P, P, I, I, I, P, P, ctypes.c_float, ctypes.c_float, P, P, P, I, P, P, P, I, SZ, P], I),
+    "gmz_bn_forward_seg": ([I, P, P, P, I, I, I, I, P, P, ctypes.c_float, ctypes.c_float, P, P, P, I, P, P, P, SZ, P, SZ,
+                            P], I),
+    "gmz_conv3x3_forward_board_stats": ([I, I, P, P, P, I, P, P, I, P], I),
     "gmz_bn_sync_errors": ([ctypes.POINTER(ctypes.c_uint32), I], I),
-    "gmz_conv3x3_forward_stamp": ([I, I, P, P, P, I, P, P, P, P, P], I),
-    "gmz_bn_forward_m": ([I, I, P, P, P, I, I, I, P, P, ctypes.c_float, ctypes.c_float, P, P, P, I, P, P, P, P, P], I),
-    "gmz_bn_forward_stats_m": ([I, P, P, I, I, I, P, P, ctypes.c_float, ctypes.c_float, P, P, P, I, P, P, P, I, P, P], I),
-    "gmz_bn_backward_acc_m": ([I, I, P, P, P, P, I, I, I, P, P, I, P, P, P, P, P, P, P, I], I),
+    "gmz_conv3x3_forward_stamp": ([I, I, P, P, P, I, P, P, I, P, P, I, SZ, P], I),
+    "gmz_bn_forward_m": ([I, I, P, P, P, I, I, I, P, P, ctypes.c_float, ctypes.c_float, P, P, P, I, P, P, P, SZ, P, P], I),
+    "gmz_bn_forward_stats_m": ([I, P, P, I, I, I, P, P, ctypes.c_float, ctypes.c_float, P, P, P, I, P, P, P, I, SZ, P, P],
+                               I),
+    "gmz_bn_backward_acc_m": ([I, I, P, P, P, P, I, I, I, P, P, I, P, P, P, P, P, SZ, P, P, I], I),
 }
 
 # symbols added by the network kernels (declared in include/gmz.h too)
@@ -137,6 +141,11 @@ def check(rc):
 def ptr(t):
     """Device/host pointer of a torch tensor (or None → NULL)."""
     return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def nbytes(t):
+    """Size in bytes of a torch tensor's elements (None → 0): the capacity arguments of ABI 10."""
+    return 0 if t is None else t.numel() * t.element_size()
 
 
 def stream_ptr(stream=None):

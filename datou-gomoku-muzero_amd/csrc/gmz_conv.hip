@@ -39,7 +39,7 @@ typedef uint16_t u16x4_t __attribute__((ext_vector_type(4)));
 // timing ablations of k_conv3 (A/B builds only, results wrong): 1 = each workgroup DMAs only its first board,
 // 2 = no epilogue stores (kept behind a never-true runtime test), 4 = no MFMAs in the k-loop (operand loads kept),
 // 8 = no weight-fragment loads in the k-loop (the ring keeps its first fragments), 16 = no B-fragment LDS reads in
-// the k-loop (the first step's fragments reused)
+// the k-loop (the first step's fragments reused), 32 = no board DMA at all (the image stays zero)
 #ifndef GMZ_CONV_ABL
 #define GMZ_CONV_ABL 0
 #endif
@@ -167,7 +167,19 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
   const int bstride = HALVES == 2 ? (int)gridDim.x : (int)(gridDim.x >> 1);
   int ntile0 = half0 * 4 + nq * NTW;  // this wave's first n-tile (of 8)
 
-  for (int i = tid; i < I::BYTES / 16; i += NTHR) *(uint4 *)(img + i * 16) = make_uint4(0, 0, 0, 0);
+  // zero the image's border cells (2 HP + 2 H cells; every board's DMA rewrites the whole interior).  Indexed
+  // uint4 stores compile to ds_write_b128 (8 lanes = one contiguous 128 B: conflict-free); the round-5 fill of the
+  // whole 78 KB image as *(uint4 *)(img + 16 i) compiled to four ds_write_b32 per 16 B at a 16-B lane stride,
+  // 4-way bank conflicted: 1.26 M of the kernel's 1.47 M conflict cycles (profiles/r06_conv_lds_ab.txt)
+  {
+    constexpr int HP = I::HP, NBORDER = 2 * HP + 2 * H;
+    for (int i = tid; i < NBORDER * 16; i += NTHR) {
+      const int k = i >> 4, r = k - 2 * HP;
+      const int yy = k < HP ? 0 : k < 2 * HP ? HP - 1 : 1 + (r >> 1);
+      const int xx = k < HP ? k : k < 2 * HP ? k - HP : (r & 1) * (HP - 1);
+      ((uint4 *)(img + yy * RS + xx * PS))[i & 15] = make_uint4(0, 0, 0, 0);
+    }
+  }
 
   int pos[PTW];
 #pragma unroll
@@ -203,7 +215,7 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
   // ---- board bd -> image interior: 1 KB pieces of each board row's run of cells
   auto dma = [&](int bd) {
     const uint8_t *src = (const uint8_t *)(x + (size_t)bd * A * CC);
-    for (int j = w; j < (((GMZ_CONV_ABL & 1) && bd != b0) ? 0 : H * I::RUN_DMA); j += NW) {
+    for (int j = w; j < ((((GMZ_CONV_ABL & 1) && bd != b0) || (GMZ_CONV_ABL & 32)) ? 0 : H * I::RUN_DMA); j += NW) {
       const int yy = j / I::RUN_DMA, piece = j % I::RUN_DMA;
       const int o = piece * 1024 + lane * 16;
       const int xx = o / PS, ch = (o % PS) >> 4;
@@ -237,9 +249,13 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
         for (int k = 0; k < RD - 1; ++k) loadA(k, k);
     }
     f32x4_t acc[NTW][PTW];
+    // lanes past the board read the board's LAST position's cell (never stored): a 16-lane bank group of the
+    // last tile then holds that one address (a broadcast) and the valid positions' own slots, not a second
+    // address on the valid position's bank (tile 14 of 15x15 / tile 5 of 9x9 hold one valid position)
+    constexpr int LASTPOS = ((A - 1) / H) * RS + ((A - 1) % H) * PS;
     int bb[PTW];
 #pragma unroll
-    for (int i = 0; i < PTW; ++i) bb[i] = (pos[i] < 0 ? 0 : pos[i]) + cg * 16;
+    for (int i = 0; i < PTW; ++i) bb[i] = (pos[i] < 0 ? LASTPOS : pos[i]) + cg * 16;
     auto kloop = [&](auto ntl_c) {
       constexpr int NTL = decltype(ntl_c)::value;
       V bf[2][NTL];
@@ -507,7 +523,24 @@ __global__ void __launch_bounds__(512, 1) k_conv3_wgrad(WgSrc src, int N, int nc
   const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
   const int ocol = (wo * 32 + 4 * pp) * 2, ccol = (wc * 64 + 4 * pp) * 2;  // this lane's column bytes
 
-  for (int i = tid; i < L::BYTES / 16; i += 512) *(uint4 *)(smem + i * 16) = make_uint4(0, 0, 0, 0);
+  // zero what no board's DMA writes: the dy rows past the board (positions A..NPOS-1 of the last k-step) and the x
+  // image's border cells (ds_write_b128 stores, as in k_conv3)
+  {
+    constexpr int NTAIL = L::NPOS - A, NBORDER = 2 * HP + 2 * H;
+    for (int i = tid; i < (NTAIL + NBORDER) * 16; i += 512) {
+      const int k = i >> 4;
+      uint8_t *cellp;
+      if (k < NTAIL) {
+        cellp = smem + (A + k) * RB;
+      } else {
+        const int kb = k - NTAIL, r = kb - 2 * HP;
+        const int yy = kb < HP ? 0 : kb < 2 * HP ? HP - 1 : 1 + (r >> 1);
+        const int xx = kb < HP ? kb : kb < 2 * HP ? kb - HP : (r & 1) * (HP - 1);
+        cellp = xt + (yy * HP + xx) * RB;
+      }
+      ((uint4 *)cellp)[i & 15] = make_uint4(0, 0, 0, 0);
+    }
+  }
   __syncthreads();
 
   f32x4_t acc[3][2][4];
@@ -639,8 +672,21 @@ int conv3_grid(int N) {  // a multiple of 16 (whole XCD pairs; workgroups past t
   return (int)(items < cap ? items : cap);
 }
 
-// statistics slots (partials) of gmz_conv3x3_forward_stats: one per board pair of workgroups, or per workgroup
-int conv3_stats_slots(int N) { return conv_halves() == 2 ? conv3_grid(N) : conv3_grid(N) / 2; }
+// statistics slots (partials) a launch writes: one per board pair of workgroups, or per workgroup (HALVES = 2), or
+// per board (per_board, the segmented consistency trunk).  The same function answers gmz_conv3x3_stats_slots and
+// the capacity check before every launch, so the count asked for is the count the dispatch writes (ABI 10)
+int conv3_stats_slots(int N, bool per_board = false) {
+  if (per_board) return N;
+  return conv_halves() == 2 ? conv3_grid(N) : conv3_grid(N) / 2;
+}
+static int check_slots(const char *fn, const double *stats, int stats_slots, int N, bool per_board) {
+  if (!stats) return 0;
+  const int need = conv3_stats_slots(N, per_board);
+  if (stats_slots != need)
+    return fail(std::string(fn) + ": statistics buffer of " + std::to_string(stats_slots) + " slots, this launch writes " +
+                std::to_string(need) + (per_board ? " (one per board)" : " (gmz_conv3x3_stats_slots)"));
+  return 0;
+}
 
 template <int H, typename T, int HV, bool BWD, bool PB = false>
 void launch_conv3_k(const void *x, const void *wpk, void *y, int N, const uint8_t *mask, double *stats, const void *addend,
@@ -720,14 +766,15 @@ GMZ_EXPORT int gmz_conv3x3_pack(int dtype, const float *w, int64_t s0, int64_t s
 
 GMZ_EXPORT int gmz_conv3x3_stats_slots(int N, int *slots) {
   if (N <= 0 || !slots) return fail("gmz_conv3x3_stats_slots: bad arguments");
-  *slots = conv3_stats_slots(N);
+  *slots = conv3_stats_slots(N, false);
   return 0;
 }
 
 GMZ_EXPORT int gmz_conv3x3_forward_stats(int dtype, int H, const void *x, const void *packed, void *y, int N,
-                                         const uint8_t *mask, double *stats, void *stream) {
+                                         const uint8_t *mask, double *stats, int stats_slots, void *stream) {
   if (!x || !packed || !y) return fail("gmz_conv3x3_forward: null operand");
   if (N <= 0) return fail("gmz_conv3x3_forward: N must be positive");
+  if (check_slots("gmz_conv3x3_forward_stats", stats, stats_slots, N, false)) return -1;
   if (((uintptr_t)x | (uintptr_t)packed | (uintptr_t)y) & 15) return fail("gmz_conv3x3_forward: operands must be 16-B aligned");
   hipStream_t st = (hipStream_t)stream;
   if (dtype == 1) return conv3_dispatch<__half>(H, x, packed, y, N, mask, stats, nullptr, st);
@@ -736,9 +783,10 @@ GMZ_EXPORT int gmz_conv3x3_forward_stats(int dtype, int H, const void *x, const 
 }
 
 GMZ_EXPORT int gmz_conv3x3_forward_board_stats(int dtype, int H, const void *x, const void *packed, void *y, int N,
-                                               const uint8_t *mask, double *stats, void *stream) {
+                                               const uint8_t *mask, double *stats, int stats_slots, void *stream) {
   if (!x || !packed || !y || !stats) return fail("gmz_conv3x3_forward_board_stats: null operand");
   if (N <= 0) return fail("gmz_conv3x3_forward_board_stats: N must be positive");
+  if (check_slots("gmz_conv3x3_forward_board_stats", stats, stats_slots, N, true)) return -1;
   if (((uintptr_t)x | (uintptr_t)packed | (uintptr_t)y) & 15)
     return fail("gmz_conv3x3_forward_board_stats: operands must be 16-B aligned");
   hipStream_t st = (hipStream_t)stream;
@@ -748,21 +796,27 @@ GMZ_EXPORT int gmz_conv3x3_forward_board_stats(int dtype, int H, const void *x, 
 }
 
 GMZ_EXPORT int gmz_conv3x3_forward_stamp(int dtype, int H, const void *x, const void *packed, void *y, int N,
-                                         const uint8_t *mask, double *stats, const int32_t *action, const float *table,
-                                         void *stream) {
+                                         const uint8_t *mask, double *stats, int stats_slots, const int32_t *action,
+                                         const void *table, int table_dtype, size_t table_bytes, void *stream) {
   if (!x || !packed || !y || !action || !table) return fail("gmz_conv3x3_forward_stamp: null operand");
   if (N <= 0) return fail("gmz_conv3x3_forward_stamp: N must be positive");
+  // the kernel reads the table as f32 [9][128]: any other dtype or size fails here, before the launch (ABI 10; the
+  // round-5 faults were an f16 table built inside autocast, read past its 2,304 bytes)
+  if (table_dtype != 0) return fail("gmz_conv3x3_forward_stamp: table_dtype must be 0 (f32)");
+  if (table_bytes != (size_t)9 * CC * sizeof(float))
+    return fail("gmz_conv3x3_forward_stamp: table of " + std::to_string(table_bytes) + " bytes, must be f32 [9][128] = 4608");
+  if (check_slots("gmz_conv3x3_forward_stamp", stats, stats_slots, N, false)) return -1;
   if (((uintptr_t)x | (uintptr_t)packed | (uintptr_t)y) & 15)
     return fail("gmz_conv3x3_forward_stamp: operands must be 16-B aligned");
   hipStream_t st = (hipStream_t)stream;
-  const ActStamp as = {action, table};
+  const ActStamp as = {action, (const float *)table};
   if (dtype == 1) return conv3_dispatch<__half>(H, x, packed, y, N, mask, stats, nullptr, st, BnBwd{}, false, as);
   if (dtype == 2) return conv3_dispatch<__hip_bfloat16>(H, x, packed, y, N, mask, stats, nullptr, st, BnBwd{}, false, as);
   return fail("gmz_conv3x3_forward_stamp: dtype must be 1 (f16) or 2 (bf16)");
 }
 
 GMZ_EXPORT int gmz_conv3x3_forward(int dtype, int H, const void *x, const void *packed, void *y, int N, void *stream) {
-  return gmz_conv3x3_forward_stats(dtype, H, x, packed, y, N, nullptr, nullptr, stream);
+  return gmz_conv3x3_forward_stats(dtype, H, x, packed, y, N, nullptr, nullptr, 0, stream);
 }
 
 GMZ_EXPORT int gmz_conv3x3_forward_add(int dtype, int H, const void *x, const void *packed, const void *addend, void *y,
@@ -779,9 +833,11 @@ GMZ_EXPORT int gmz_conv3x3_forward_add(int dtype, int H, const void *x, const vo
 
 GMZ_EXPORT int gmz_conv3x3_forward_bwdstats(int dtype, int H, const void *x, const void *packed, const void *addend,
                                             void *y, int N, const uint8_t *mask, const void *bn_x, const void *bn_y,
-                                            const float *bn_save, int relu, double *stats, void *stream) {
+                                            const float *bn_save, int relu, double *stats, int stats_slots,
+                                            void *stream) {
   if (!x || !packed || !y || !bn_x || !bn_y || !bn_save || !stats) return fail("gmz_conv3x3_forward_bwdstats: null operand");
   if (N <= 0) return fail("gmz_conv3x3_forward_bwdstats: N must be positive");
+  if (check_slots("gmz_conv3x3_forward_bwdstats", stats, stats_slots, N, false)) return -1;
   if (((uintptr_t)x | (uintptr_t)packed | (uintptr_t)y | (uintptr_t)addend) & 15)
     return fail("gmz_conv3x3_forward_bwdstats: operands must be 16-B aligned");
   if (((uintptr_t)bn_x | (uintptr_t)bn_y) & 7) return fail("gmz_conv3x3_forward_bwdstats: BN operands must be 8-B aligned");
@@ -799,7 +855,11 @@ GMZ_EXPORT int gmz_conv3x3_wgrad_workspace_bytes(int N, size_t *out) {
 }
 
 static int wgrad_launch(int dtype, int H, const WgSrc &src, int N, float *dw, int64_t s0, int64_t s1, int64_t s2,
-                        int64_t s3, int accumulate, void *workspace, hipStream_t st) {
+                        int64_t s3, int accumulate, void *workspace, size_t workspace_bytes, hipStream_t st) {
+  const size_t need = (size_t)wgrad_chunks(N) * 9 * CC * CC * sizeof(float);  // the partials k_conv3_wgrad writes
+  if (workspace_bytes < need)
+    return fail("gmz_conv3x3_wgrad: workspace of " + std::to_string(workspace_bytes) + " bytes, " + std::to_string(N) +
+                " boards need " + std::to_string(need) + " (gmz_conv3x3_wgrad_workspace_bytes)");
   float *part = (float *)workspace;
   int rc;
   if (dtype == 1)
@@ -817,7 +877,8 @@ static int wgrad_launch(int dtype, int H, const WgSrc &src, int N, float *dw, in
 }
 
 GMZ_EXPORT int gmz_conv3x3_wgrad(int dtype, int H, const void *x, const void *dy, int N, float *dw, int64_t s0,
-                                 int64_t s1, int64_t s2, int64_t s3, int accumulate, void *workspace, void *stream) {
+                                 int64_t s1, int64_t s2, int64_t s3, int accumulate, void *workspace,
+                                 size_t workspace_bytes, void *stream) {
   if (!x || !dy || !dw || !workspace) return fail("gmz_conv3x3_wgrad: null operand");
   if (N <= 0) return fail("gmz_conv3x3_wgrad: N must be positive");
   if (((uintptr_t)x | (uintptr_t)dy) & 15) return fail("gmz_conv3x3_wgrad: operands must be 16-B aligned");
@@ -825,12 +886,13 @@ GMZ_EXPORT int gmz_conv3x3_wgrad(int dtype, int H, const void *x, const void *dy
   src.x[0] = (const uint16_t *)x;
   src.dy[0] = (const uint16_t *)dy;
   src.nps = N;
-  return wgrad_launch(dtype, H, src, N, dw, s0, s1, s2, s3, accumulate, workspace, (hipStream_t)stream);
+  return wgrad_launch(dtype, H, src, N, dw, s0, s1, s2, s3, accumulate, workspace, workspace_bytes, (hipStream_t)stream);
 }
 
 GMZ_EXPORT int gmz_conv3x3_wgrad_segments(int dtype, int H, const void *const *x_segs, const void *const *dy_segs,
                                           int nseg, int n_per_seg, float *dw, int64_t s0, int64_t s1, int64_t s2,
-                                          int64_t s3, int accumulate, void *workspace, void *stream) {
+                                          int64_t s3, int accumulate, void *workspace, size_t workspace_bytes,
+                                          void *stream) {
   if (!x_segs || !dy_segs || !dw || !workspace) return fail("gmz_conv3x3_wgrad_segments: null operand");
   if (nseg < 1 || nseg > WG_MAX_SEGS || n_per_seg <= 0)
     return fail("gmz_conv3x3_wgrad_segments: need 1 <= nseg <= 8 segments of n_per_seg > 0 boards");
@@ -843,5 +905,6 @@ GMZ_EXPORT int gmz_conv3x3_wgrad_segments(int dtype, int H, const void *const *x
     src.dy[i] = (const uint16_t *)dy_segs[i];
   }
   src.nps = n_per_seg;
-  return wgrad_launch(dtype, H, src, nseg * n_per_seg, dw, s0, s1, s2, s3, accumulate, workspace, (hipStream_t)stream);
+  return wgrad_launch(dtype, H, src, nseg * n_per_seg, dw, s0, s1, s2, s3, accumulate, workspace, workspace_bytes,
+                      (hipStream_t)stream);
 }

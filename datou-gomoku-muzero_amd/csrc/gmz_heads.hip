@@ -267,10 +267,16 @@ GMZ_EXPORT int gmz_head_conv1x1_workspace_bytes(long P, int O, size_t *out) {
 
 GMZ_EXPORT int gmz_head_conv1x1_backward(int dtype, const void *x, long P, int C, const float *w0, int O0,
                                          const float *w1, int O1, const void *dy0, const void *dy1, void *dx, float *dw0, float *db0, float *dw1,
-                                         float *db1, int accumulate, void *ws, void *stream) {
+                                         float *db1, int accumulate, void *ws, size_t ws_bytes, void *stream) {
   if (head_check("gmz_head_conv1x1_backward", C, P, O0, O1, x, w0, w1)) return -1;
   const HeadW hw{w0, nullptr, w1, nullptr};
   if (!dy0 || (O1 > 0 && !dy1) || !dx || !ws) return fail("gmz_head_conv1x1_backward: null operand");
+  {  // the per-workgroup partials the kernel writes (ABI 10)
+    const size_t need = (size_t)head_blocks(P) * (O0 + O1) * (HC + 1) * sizeof(float);
+    if (ws_bytes < need)
+      return fail("gmz_head_conv1x1_backward: workspace of " + std::to_string(ws_bytes) + " bytes, needs " +
+                  std::to_string(need) + " (gmz_head_conv1x1_workspace_bytes)");
+  }
   if (((uintptr_t)dx) % 16) return fail("gmz_head_conv1x1_backward: dx must be 16-B aligned");
   hipStream_t st = (hipStream_t)stream;
   switch (dtype) {
@@ -453,12 +459,14 @@ int seg_bn_bwd(const void *x, const float *dy, const uint8_t *m, int nseg, int B
 }  // namespace gmz
 
 GMZ_EXPORT int gmz_seg_bn_forward(int dtype, const void *x, const uint8_t *row_mask, int nseg, int B, int S, int C,
-                                  const float *gamma, const float *beta, float eps, float *y, float *stats, int update,
-                                  float momentum, float *running_mean, float *running_var, int64_t *num_batches,
-                                  const float *pre_stats, void *stream) {
+                                  const float *gamma, const float *beta, float eps, float *y, float *stats,
+                                  size_t stats_bytes, int update, float momentum, float *running_mean,
+                                  float *running_var, int64_t *num_batches, const float *pre_stats, void *stream) {
   if (!x || !y || !stats || nseg <= 0 || nseg > 32 || B <= 0 || S <= 0 || C <= 0 ||
       (size_t)nseg * B * S * C >= (1ull << 31))
     return fail("gmz_seg_bn_forward: bad arguments (1 <= nseg <= 32)");
+  if (stats_bytes < ((size_t)3 * nseg * C + nseg) * sizeof(float))  // what the kernel writes (ABI 10)
+    return fail("gmz_seg_bn_forward: stats of " + std::to_string(stats_bytes) + " bytes, needs (3 nseg C + nseg) f32");
   if (update && (!running_mean || !running_var)) return fail("gmz_seg_bn_forward: update needs running statistics");
   hipStream_t s = (hipStream_t)stream;
   switch (dtype) {
@@ -473,10 +481,12 @@ GMZ_EXPORT int gmz_seg_bn_forward(int dtype, const void *x, const uint8_t *row_m
 }
 
 GMZ_EXPORT int gmz_seg_bn_backward(int dtype, const void *x, const float *dy, const uint8_t *row_mask, int nseg, int B,
-                                   int S, int C, const float *gamma, const float *stats, void *dx, float *dgamma,
-                                   float *dbeta, int accumulate, void *stream) {
+                                   int S, int C, const float *gamma, const float *stats, size_t stats_bytes, void *dx,
+                                   float *dgamma, float *dbeta, int accumulate, void *stream) {
   if (!x || !dy || !stats || !dx || nseg <= 0 || B <= 0 || S <= 0 || C <= 0 || (size_t)nseg * B * S * C >= (1ull << 31))
     return fail("gmz_seg_bn_backward: bad arguments");
+  if (stats_bytes < ((size_t)3 * nseg * C + nseg) * sizeof(float))
+    return fail("gmz_seg_bn_backward: stats of " + std::to_string(stats_bytes) + " bytes, needs (3 nseg C + nseg) f32");
   hipStream_t s = (hipStream_t)stream;
   switch (dtype) {
     case 0: return seg_bn_bwd<float>(x, dy, row_mask, nseg, B, S, C, gamma, stats, dx, dgamma, dbeta, accumulate, s);

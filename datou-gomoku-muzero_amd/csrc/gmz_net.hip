@@ -326,7 +326,9 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
   };
 
   // ---- zero both images (borders and pads), biases of layer 0, action term
-  for (int i = tid; i < IMGS / 16; i += NTHR) *(uint4 *)(smem + i * 16) = make_uint4(0, 0, 0, 0);
+  // (indexed uint4 stores: ds_write_b128; the *(uint4 *)(smem + 16 i) form compiled to four 4-way bank-conflicted
+  // ds_write_b32 per 16 B)
+  for (int i = tid; i < IMGS / 16; i += NTHR) ((uint4 *)smem)[i] = make_uint4(0, 0, 0, 0);
   if (tid < C) sbias[tid] = t.bias[tid];
   if (tid < 2) s_cnt[tid] = 0;
   if (DYN)
@@ -345,6 +347,11 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
     tile_pos(pg + PG * i, lane, bsl, p);
     pos[i] = p < A ? bbase(bsl) + (p / H) * RS + (p % H) * PS : -1;
   }
+  // lanes past the boards read the tile space's LAST position's cell (never stored): within a 16-lane bank group
+  // of the last tile that is one broadcast address beside the valid positions' own slots, where image offset 0
+  // was a second address on a valid position's bank (a 2-way conflict on every read of that tile)
+  static_assert(NB == 1 || PACKED, "several boards per workgroup run as one packed position run");
+  const int lastpos = bbase(NB - 1) + ((A - 1) / H) * RS + ((A - 1) % H) * PS;
   f32x4 acc[NTW][PTW];
   // ONE: this lane's residual tile values, [NTW][PTW][64 lanes] x 4 16-bit values per wave (same lane writes
   // and reads back: program order suffices)
@@ -483,7 +490,7 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
       int bb[PTW];
 #pragma unroll
       for (int i = 0; i < PTW; ++i) {
-        bb[i] = (pos[i] < 0 ? 0 : pos[i] + cg * 16) + (int)(size_t)(img - smem) + (PP ? 64 * hh : 0);
+        bb[i] = (pos[i] < 0 ? lastpos : pos[i]) + cg * 16 + (int)(size_t)(img - smem) + (PP ? 64 * hh : 0);
         asm volatile("" : "+v"(bb[i]));  // one base VGPR per tile and layer; all else immediates
       }
       // k-loop over the NTL tiles this wave owns (NTL = PTW, or PTW - 1 for a short last position
@@ -568,7 +575,7 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
           for (int u = 0; u < NTW / 2; ++u)
 #pragma unroll
             for (int i = 0; i < PTW; ++i) {
-              const uint4 v = *(const uint4 *)(nimg + (pos[i] < 0 ? 0 : pos[i]) + RS + PS + chan0(2 * u) * 2);
+              const uint4 v = *(const uint4 *)(nimg + (pos[i] < 0 ? lastpos : pos[i]) + RS + PS + chan0(2 * u) * 2);
               xr[2 * u][i] = __builtin_bit_cast(u16x4, make_uint2(v.x, v.y));
               xr[2 * u + 1][i] = __builtin_bit_cast(u16x4, make_uint2(v.z, v.w));
             }
@@ -994,6 +1001,15 @@ GMZ_EXPORT int gmz_net_workspace_bytes(const gmz_net_weights *w, int rows, size_
   return 0;
 }
 
+// the caller's workspace holds what `rows` rows need (ABI 10): checked before any launch
+static int check_ws(const gmz_net_weights *w, int rows, size_t bytes, const char *fn) {
+  const size_t need = ws_bytes(w->board_size * w->board_size, rows);
+  if (bytes < need)
+    return fail(std::string(fn) + ": workspace of " + std::to_string(bytes) + " bytes, " + std::to_string(rows) +
+                " rows need " + std::to_string(need) + " (gmz_net_workspace_bytes)");
+  return 0;
+}
+
 // the heads of `rows` rows whose tower output (pv rows, hidden slots) is in place; reward != nullptr
 // adds the reward head (recurrent rows)
 static int heads(const gmz_net_weights *w, const uint16_t *pool, const int32_t *out_slot, int rows, void *workspace,
@@ -1017,9 +1033,10 @@ static int heads(const gmz_net_weights *w, const uint16_t *pool, const int32_t *
 }
 
 GMZ_EXPORT int gmz_net_initial_tower(const gmz_net_weights *w, const float *obs, int rows, const int32_t *out_slot,
-                                     uint16_t *pool, void *workspace, void *stream) {
+                                     uint16_t *pool, void *workspace, size_t workspace_bytes, void *stream) {
   if (check_w(w)) return -1;
   if (rows <= 0 || !obs || !out_slot || !pool || !workspace) return fail("gmz_net_initial_tower: bad argument");
+  if (check_ws(w, rows, workspace_bytes, "gmz_net_initial_tower")) return -1;
   const int H = w->board_size, A = H * H;
   TowerArgs a{w->repr_convs, w->repr_bias, 2 * w->blocks, w->repr_stem_w, w->repr_stem_b, nullptr, obs, pool,
               nullptr, nullptr, out_slot, w->head_conv_w, w->head_conv_b, ws_pv(workspace), rows,
@@ -1028,23 +1045,26 @@ GMZ_EXPORT int gmz_net_initial_tower(const gmz_net_weights *w, const float *obs,
 }
 
 GMZ_EXPORT int gmz_net_initial_heads(const gmz_net_weights *w, const uint16_t *pool, const int32_t *out_slot, int rows,
-                                     float *logits, float *value, void *workspace, void *stream) {
+                                     float *logits, float *value, void *workspace, size_t workspace_bytes, void *stream) {
   if (check_w(w)) return -1;
   if (rows <= 0 || !pool || !out_slot || !logits || !value || !workspace) return fail("gmz_net_initial_heads: bad argument");
+  if (check_ws(w, rows, workspace_bytes, "gmz_net_initial_heads")) return -1;
   return heads(w, pool, out_slot, rows, workspace, logits, value, nullptr, (hipStream_t)stream);
 }
 
 GMZ_EXPORT int gmz_net_initial(const gmz_net_weights *w, const float *obs, int rows, const int32_t *out_slot,
-                               uint16_t *pool, float *logits, float *value, void *workspace, void *stream) {
-  if (gmz_net_initial_tower(w, obs, rows, out_slot, pool, workspace, stream)) return -1;
-  return gmz_net_initial_heads(w, pool, out_slot, rows, logits, value, workspace, stream);
+                               uint16_t *pool, float *logits, float *value, void *workspace, size_t workspace_bytes,
+                               void *stream) {
+  if (gmz_net_initial_tower(w, obs, rows, out_slot, pool, workspace, workspace_bytes, stream)) return -1;
+  return gmz_net_initial_heads(w, pool, out_slot, rows, logits, value, workspace, workspace_bytes, stream);
 }
 
 GMZ_EXPORT int gmz_net_recurrent_tower(const gmz_net_weights *w, uint16_t *pool, const int32_t *in_slot,
                                        const int32_t *action, const int32_t *out_slot, int rows, void *workspace,
-                                       void *stream) {
+                                       size_t workspace_bytes, void *stream) {
   if (check_w(w)) return -1;
   if (rows <= 0 || !pool || !in_slot || !action || !out_slot || !workspace) return fail("gmz_net_recurrent_tower: bad argument");
+  if (check_ws(w, rows, workspace_bytes, "gmz_net_recurrent_tower")) return -1;
   const int A = w->board_size * w->board_size;
   TowerArgs a{w->dyn_convs, w->dyn_bias, 1 + 2 * w->blocks, nullptr, nullptr, w->dyn_action, nullptr, pool,
               in_slot, action, out_slot, w->head_conv_w, w->head_conv_b, ws_pv(workspace), rows,
@@ -1053,16 +1073,18 @@ GMZ_EXPORT int gmz_net_recurrent_tower(const gmz_net_weights *w, uint16_t *pool,
 }
 
 GMZ_EXPORT int gmz_net_recurrent_heads(const gmz_net_weights *w, const uint16_t *pool, const int32_t *out_slot, int rows,
-                                       float *logits, float *value, float *reward, void *workspace, void *stream) {
+                                       float *logits, float *value, float *reward, void *workspace,
+                                       size_t workspace_bytes, void *stream) {
   if (check_w(w)) return -1;
   if (rows <= 0 || !pool || !out_slot || !logits || !value || !reward || !workspace)
     return fail("gmz_net_recurrent_heads: bad argument");
+  if (check_ws(w, rows, workspace_bytes, "gmz_net_recurrent_heads")) return -1;
   return heads(w, pool, out_slot, rows, workspace, logits, value, reward, (hipStream_t)stream);
 }
 
 GMZ_EXPORT int gmz_net_recurrent(const gmz_net_weights *w, uint16_t *pool, const int32_t *in_slot, const int32_t *action,
                                  const int32_t *out_slot, int rows, float *logits, float *value, float *reward,
-                                 void *workspace, void *stream) {
-  if (gmz_net_recurrent_tower(w, pool, in_slot, action, out_slot, rows, workspace, stream)) return -1;
-  return gmz_net_recurrent_heads(w, pool, out_slot, rows, logits, value, reward, workspace, stream);
+                                 void *workspace, size_t workspace_bytes, void *stream) {
+  if (gmz_net_recurrent_tower(w, pool, in_slot, action, out_slot, rows, workspace, workspace_bytes, stream)) return -1;
+  return gmz_net_recurrent_heads(w, pool, out_slot, rows, logits, value, reward, workspace, workspace_bytes, stream);
 }

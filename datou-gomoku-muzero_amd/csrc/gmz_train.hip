@@ -1176,20 +1176,43 @@ static int check_layout(int layout, int C) {
   return fail("gmz_bn: layout must be 0 (NCHW) or 1 (NHWC with even C <= 512)");
 }
 
+static size_t bn_ws_need(int layout, int B, int C, int S) {
+  return (ws_doubles(B, C, S, layout) + (size_t)C) * sizeof(double);  // partials + f32 [2][C] coefficients
+}
+
 GMZ_EXPORT int gmz_bn_workspace_bytes(int layout, int B, int C, int S, size_t *out) {
   if (B <= 0 || C <= 0 || S <= 0 || !out) return fail("gmz_bn_workspace_bytes: bad shape");
   if (check_layout(layout, C)) return -1;
-  *out = (ws_doubles(B, C, S, layout) + (size_t)C) * sizeof(double);  // partials + f32 [2][C] coefficients
+  *out = bn_ws_need(layout, B, C, S);
+  return 0;
+}
+
+// capacity checks (ABI 10): every caller-allocated buffer the kernels write (workspace partials) or read at a
+// size the call implies (statistics partials) comes with its byte size; a short buffer fails here, before any
+// launch, instead of being written or read past its end
+static int check_bn_ws(const char *fn, int layout, int B, int C, int S, size_t bytes) {
+  const size_t need = bn_ws_need(layout, B, C, S);
+  if (bytes < need)
+    return fail(std::string(fn) + ": workspace of " + std::to_string(bytes) + " bytes, needs " + std::to_string(need) +
+                " (gmz_bn_workspace_bytes)");
+  return 0;
+}
+static int check_parts(const char *fn, int C, long ns, size_t bytes) {
+  const size_t need = (size_t)C * ns * 3 * sizeof(double);
+  if (bytes < need)
+    return fail(std::string(fn) + ": statistics partials of " + std::to_string(bytes) + " bytes, " + std::to_string(C) +
+                " channels x " + std::to_string(ns) + " slots need " + std::to_string(need));
   return 0;
 }
 
 GMZ_EXPORT int gmz_bn_forward(int dtype, int layout, const void *x, const void *res, const uint8_t *mask, int B, int C,
                               int S, const float *gamma, const float *beta, float eps, float momentum,
                               float *running_mean, float *running_var, int64_t *num_batches, int relu, void *y,
-                              float *save, void *ws, void *stream) {
+                              float *save, void *ws, size_t ws_bytes, void *stream) {
   if (B <= 0 || C <= 0 || S <= 0 || (size_t)B * C * S >= (1ull << 31)) return fail("gmz_bn_forward: bad shape");
   if (check_layout(layout, C)) return -1;
   if (!x || !y || !gamma || !beta || !save || !ws) return fail("gmz_bn_forward: null operand");
+  if (check_bn_ws("gmz_bn_forward", layout, B, C, S, ws_bytes)) return -1;
   if ((running_mean == nullptr) != (running_var == nullptr)) return fail("gmz_bn_forward: running stats pair");
   hipStream_t st = (hipStream_t)stream;
   switch (dtype) {
@@ -1205,12 +1228,13 @@ GMZ_EXPORT int gmz_bn_forward(int dtype, int layout, const void *x, const void *
 
 GMZ_EXPORT int gmz_bn_backward_acc(int dtype, int layout, const void *x, const void *y, const void *dy,
                                    const uint8_t *mask, int B, int C, int S, const float *gamma, const float *save,
-                                   int relu, void *dx, void *dres, float *dgamma, float *dbeta, void *ws, void *stream,
-                                   int accumulate) {
+                                   int relu, void *dx, void *dres, float *dgamma, float *dbeta, void *ws,
+                                   size_t ws_bytes, void *stream, int accumulate) {
   if (B <= 0 || C <= 0 || S <= 0 || (size_t)B * C * S >= (1ull << 31)) return fail("gmz_bn_backward: bad shape");
   if (check_layout(layout, C)) return -1;
   if (!x || !dy || !dx || !gamma || !save || !dgamma || !dbeta || !ws || (relu && !y))
     return fail("gmz_bn_backward: null operand");
+  if (check_bn_ws("gmz_bn_backward", layout, B, C, S, ws_bytes)) return -1;
   hipStream_t st = (hipStream_t)stream;
   switch (dtype) {
     case 0: return bn_backward<float>(layout, x, y, dy, mask, B, C, S, gamma, save, relu, dx, dres, dgamma, dbeta, ws,
@@ -1228,10 +1252,11 @@ GMZ_EXPORT int gmz_bn_backward_acc(int dtype, int layout, const void *x, const v
 GMZ_EXPORT int gmz_bn_forward_m(int dtype, int layout, const void *x, const void *res, const uint8_t *mask, int B, int C,
                                 int S, const float *gamma, const float *beta, float eps, float momentum,
                                 float *running_mean, float *running_var, int64_t *num_batches, int relu, void *y,
-                                float *save, void *ws, uint8_t *relu_mask, void *stream) {
+                                float *save, void *ws, size_t ws_bytes, uint8_t *relu_mask, void *stream) {
   if (B <= 0 || C <= 0 || S <= 0 || (size_t)B * C * S >= (1ull << 31)) return fail("gmz_bn_forward: bad shape");
   if (check_layout(layout, C)) return -1;
   if (!x || !y || !gamma || !beta || !save || !ws) return fail("gmz_bn_forward: null operand");
+  if (check_bn_ws("gmz_bn_forward_m", layout, B, C, S, ws_bytes)) return -1;
   if ((running_mean == nullptr) != (running_var == nullptr)) return fail("gmz_bn_forward: running stats pair");
   if (relu_mask && (!relu || layout != 1)) return fail("gmz_bn_forward_m: relu_mask needs relu and channels-last");
   hipStream_t st = (hipStream_t)stream;
@@ -1249,11 +1274,12 @@ GMZ_EXPORT int gmz_bn_forward_m(int dtype, int layout, const void *x, const void
 GMZ_EXPORT int gmz_bn_backward_acc_m(int dtype, int layout, const void *x, const void *y, const void *dy,
                                      const uint8_t *mask, int B, int C, int S, const float *gamma, const float *save,
                                      int relu, void *dx, void *dres, float *dgamma, float *dbeta, void *ws,
-                                     const uint8_t *relu_mask, void *stream, int accumulate) {
+                                     size_t ws_bytes, const uint8_t *relu_mask, void *stream, int accumulate) {
   if (B <= 0 || C <= 0 || S <= 0 || (size_t)B * C * S >= (1ull << 31)) return fail("gmz_bn_backward: bad shape");
   if (check_layout(layout, C)) return -1;
   if (!x || !dy || !dx || !gamma || !save || !dgamma || !dbeta || !ws || (relu && !y))
     return fail("gmz_bn_backward: null operand");
+  if (check_bn_ws("gmz_bn_backward_acc_m", layout, B, C, S, ws_bytes)) return -1;
   if (relu_mask && (!relu || layout != 1)) return fail("gmz_bn_backward_acc_m: relu_mask needs relu and channels-last");
   hipStream_t st = (hipStream_t)stream;
   switch (dtype) {
@@ -1270,10 +1296,12 @@ GMZ_EXPORT int gmz_bn_backward_acc_m(int dtype, int layout, const void *x, const
 GMZ_EXPORT int gmz_bn_forward_stats_m(int dtype, const void *x, const void *res, int B, int C, int S, const float *gamma,
                                       const float *beta, float eps, float momentum, float *running_mean,
                                       float *running_var, int64_t *num_batches, int relu, void *y, float *save,
-                                      const double *stats, int ns, uint8_t *relu_mask, void *stream) {
+                                      const double *stats, int ns, size_t stats_bytes, uint8_t *relu_mask,
+                                      void *stream) {
   if (B <= 0 || C <= 0 || S <= 0 || ns <= 0 || (size_t)B * C * S >= (1ull << 31)) return fail("gmz_bn_forward_stats: bad shape");
   if (check_layout(1, C)) return -1;
   if (!x || !y || !gamma || !beta || !save || !stats) return fail("gmz_bn_forward_stats: null operand");
+  if (check_parts("gmz_bn_forward_stats_m", C, ns, stats_bytes)) return -1;
   if ((running_mean == nullptr) != (running_var == nullptr)) return fail("gmz_bn_forward_stats: running stats pair");
   if (relu_mask && !relu) return fail("gmz_bn_forward_stats_m: relu_mask needs relu");
   hipStream_t st = (hipStream_t)stream;
@@ -1290,9 +1318,10 @@ GMZ_EXPORT int gmz_bn_forward_stats_m(int dtype, const void *x, const void *res,
 
 GMZ_EXPORT int gmz_bn_backward(int dtype, int layout, const void *x, const void *y, const void *dy,
                                const uint8_t *mask, int B, int C, int S, const float *gamma, const float *save,
-                               int relu, void *dx, void *dres, float *dgamma, float *dbeta, void *ws, void *stream) {
+                               int relu, void *dx, void *dres, float *dgamma, float *dbeta, void *ws, size_t ws_bytes,
+                               void *stream) {
   return gmz_bn_backward_acc(dtype, layout, x, y, dy, mask, B, C, S, gamma, save, relu, dx, dres, dgamma, dbeta, ws,
-                             stream, 0);
+                             ws_bytes, stream, 0);
 }
 
 GMZ_EXPORT int gmz_bn_sync_errors(uint32_t *out, int reset) {
@@ -1308,11 +1337,14 @@ GMZ_EXPORT int gmz_bn_sync_errors(uint32_t *out, int reset) {
 GMZ_EXPORT int gmz_bn_forward_seg(int dtype, const void *x, const void *res, const uint8_t *mask, int B, int nseg, int C,
                                   int S, const float *gamma, const float *beta, float eps, float momentum,
                                   float *running_mean, float *running_var, int64_t *num_batches, int relu, void *y,
-                                  float *save, void *ws, const double *board_stats, void *stream) {
+                                  float *save, void *ws, size_t ws_bytes, const double *board_stats,
+                                  size_t board_stats_bytes, void *stream) {
   if (B <= 0 || C <= 0 || S <= 0 || nseg <= 0 || B % nseg || (size_t)B * C * S >= (1ull << 31))
     return fail("gmz_bn_forward_seg: bad shape (B must be a multiple of nseg)");
   if (check_layout(1, C)) return -1;
   if (!x || !y || !gamma || !beta || !save || !ws) return fail("gmz_bn_forward_seg: null operand");
+  if (check_bn_ws("gmz_bn_forward_seg", 1, B, C, S, ws_bytes)) return -1;
+  if (board_stats && check_parts("gmz_bn_forward_seg", C, B, board_stats_bytes)) return -1;
   if ((running_mean == nullptr) != (running_var == nullptr)) return fail("gmz_bn_forward_seg: running stats pair");
   hipStream_t st = (hipStream_t)stream;
   switch (dtype) {
@@ -1328,10 +1360,12 @@ GMZ_EXPORT int gmz_bn_forward_seg(int dtype, const void *x, const void *res, con
 
 GMZ_EXPORT int gmz_bn_eval(int dtype, int layout, const void *x, const void *res, int B, int C, int S,
                            const float *gamma, const float *beta, const float *running_mean,
-                           const float *running_var, float eps, int relu, void *y, void *ws, void *stream) {
+                           const float *running_var, float eps, int relu, void *y, void *ws, size_t ws_bytes,
+                           void *stream) {
   if (B <= 0 || C <= 0 || S <= 0 || (size_t)B * C * S >= (1ull << 31)) return fail("gmz_bn_eval: bad shape");
   if (check_layout(layout, C)) return -1;
   if (!x || !y || !gamma || !beta || !running_mean || !running_var || !ws) return fail("gmz_bn_eval: null operand");
+  if (check_bn_ws("gmz_bn_eval", layout, B, C, S, ws_bytes)) return -1;
   hipStream_t st = (hipStream_t)stream;
   switch (dtype) {
     case 0: return bn_eval<float>(layout, x, res, B, C, S, gamma, beta, running_mean, running_var, eps, relu, y, ws, st);
@@ -1345,12 +1379,14 @@ GMZ_EXPORT int gmz_bn_eval(int dtype, int layout, const void *x, const void *res
 
 GMZ_EXPORT int gmz_bn_backward_stats(int dtype, const void *x, const void *y, const void *dy, const uint8_t *mask,
                                      int B, int C, int S, const float *gamma, const float *save, int relu, void *dx,
-                                     void *dres, float *dgamma, float *dbeta, const double *stats, int ns, void *ws,
-                                     void *stream, int accumulate) {
+                                     void *dres, float *dgamma, float *dbeta, const double *stats, int ns,
+                                     size_t stats_bytes, void *ws, size_t ws_bytes, void *stream, int accumulate) {
   if (B <= 0 || C <= 0 || S <= 0 || ns <= 0 || (size_t)B * C * S >= (1ull << 31)) return fail("gmz_bn_backward_stats: bad shape");
   if (check_layout(1, C)) return -1;
   if (!x || !dy || !dx || !gamma || !save || !dgamma || !dbeta || !stats || !ws || (relu && !y))
     return fail("gmz_bn_backward_stats: null operand");
+  if (check_parts("gmz_bn_backward_stats", C, ns, stats_bytes) || check_bn_ws("gmz_bn_backward_stats", 1, B, C, S, ws_bytes))
+    return -1;
   hipStream_t st = (hipStream_t)stream;
   float *coef = (float *)((double *)ws + ws_doubles(B, C, S, 1));  // where gmz_bn_backward keeps them
   switch (dtype) {
@@ -1367,10 +1403,11 @@ GMZ_EXPORT int gmz_bn_backward_stats(int dtype, const void *x, const void *y, co
 GMZ_EXPORT int gmz_bn_forward_stats(int dtype, const void *x, const void *res, int B, int C, int S, const float *gamma,
                                     const float *beta, float eps, float momentum, float *running_mean,
                                     float *running_var, int64_t *num_batches, int relu, void *y, float *save,
-                                    const double *stats, int ns, void *stream) {
+                                    const double *stats, int ns, size_t stats_bytes, void *stream) {
   if (B <= 0 || C <= 0 || S <= 0 || ns <= 0 || (size_t)B * C * S >= (1ull << 31)) return fail("gmz_bn_forward_stats: bad shape");
   if (check_layout(1, C)) return -1;
   if (!x || !y || !gamma || !beta || !save || !stats) return fail("gmz_bn_forward_stats: null operand");
+  if (check_parts("gmz_bn_forward_stats", C, ns, stats_bytes)) return -1;
   if ((running_mean == nullptr) != (running_var == nullptr)) return fail("gmz_bn_forward_stats: running stats pair");
   hipStream_t st = (hipStream_t)stream;
   switch (dtype) {

@@ -26,7 +26,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import P, I, check, ptr
+from ._lib import P, I, SZ, check, ptr
 from .config import from_any
 
 EPS = 1e-4
@@ -48,12 +48,12 @@ _TORCH16 = {"fp16": torch.float16, "bf16": torch.bfloat16}
 
 _lib.register({
     "gmz_net_workspace_bytes": ([ctypes.POINTER(NetWeights), I, ctypes.POINTER(ctypes.c_size_t)], I),
-    "gmz_net_initial": ([ctypes.POINTER(NetWeights), P, I, P, P, P, P, P, P], I),
-    "gmz_net_initial_tower": ([ctypes.POINTER(NetWeights), P, I, P, P, P, P], I),
-    "gmz_net_initial_heads": ([ctypes.POINTER(NetWeights), P, P, I, P, P, P, P], I),
-    "gmz_net_recurrent": ([ctypes.POINTER(NetWeights), P, P, P, P, I, P, P, P, P, P], I),
-    "gmz_net_recurrent_tower": ([ctypes.POINTER(NetWeights), P, P, P, P, I, P, P], I),
-    "gmz_net_recurrent_heads": ([ctypes.POINTER(NetWeights), P, P, I, P, P, P, P, P], I),
+    "gmz_net_initial": ([ctypes.POINTER(NetWeights), P, I, P, P, P, P, P, SZ, P], I),
+    "gmz_net_initial_tower": ([ctypes.POINTER(NetWeights), P, I, P, P, P, SZ, P], I),
+    "gmz_net_initial_heads": ([ctypes.POINTER(NetWeights), P, P, I, P, P, P, SZ, P], I),
+    "gmz_net_recurrent": ([ctypes.POINTER(NetWeights), P, P, P, P, I, P, P, P, P, SZ, P], I),
+    "gmz_net_recurrent_tower": ([ctypes.POINTER(NetWeights), P, P, P, P, I, P, SZ, P], I),
+    "gmz_net_recurrent_heads": ([ctypes.POINTER(NetWeights), P, P, I, P, P, P, P, SZ, P], I),
 })
 
 
@@ -320,12 +320,13 @@ class GomokuNetHip:
         t = self.repr_timer
         if t is not None:
             t.start()
+        wsb = self.workspace.numel()
         check(self.lib.gmz_net_initial_tower(ctypes.byref(self.w), ptr(obs), rows, ptr(out_slot), ptr(self.pool), ws,
-                                             stream))
+                                             wsb, stream))
         if t is not None:
             t.stop(rows)
         check(self.lib.gmz_net_initial_heads(ctypes.byref(self.w), ptr(self.pool), ptr(out_slot), rows, ptr(logits),
-                                             ptr(value), ws, stream))
+                                             ptr(value), ws, wsb, stream))
 
     def recurrent(self, in_slot, action, out_slot, logits, value, reward, stream):
         rows = in_slot.shape[0]
@@ -333,12 +334,13 @@ class GomokuNetHip:
         t = self.tower_timer
         if t is not None:
             t.start()
+        wsb = self.workspace.numel()
         check(self.lib.gmz_net_recurrent_tower(ctypes.byref(self.w), ptr(self.pool), ptr(in_slot), ptr(action),
-                                               ptr(out_slot), rows, ws, stream))
+                                               ptr(out_slot), rows, ws, wsb, stream))
         if t is not None:
             t.stop(rows)
         check(self.lib.gmz_net_recurrent_heads(ctypes.byref(self.w), ptr(self.pool), ptr(out_slot), rows,
-                                               ptr(logits), ptr(value), ptr(reward), ws, stream))
+                                               ptr(logits), ptr(value), ptr(reward), ws, wsb, stream))
 
     # ---- convenience (tests / single-game adapters): slots 0..rows-1 are used as scratch
     def hidden(self, slots):

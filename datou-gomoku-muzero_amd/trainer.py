@@ -24,6 +24,7 @@ The 128->128 residual-block convolutions (forward, input and weight gradients) a
 training-mode BatchNorm run on the HIP kernels of csrc/gmz_conv.hip / csrc/gmz_train.hip; the
 trunks' first convolutions, 1x1 convolutions and Linears run on MIOpen / hipBLASLt.
 """
+import collections
 import math
 from dataclasses import dataclass, field, asdict
 
@@ -226,27 +227,28 @@ class _FusedMaskedBN(torch.autograd.Function):
                                                     _lib.ptr(gamma), _lib.ptr(beta), float(eps), float(momentum),
                                                     _lib.ptr(running_mean), _lib.ptr(running_var),
                                                     _lib.ptr(num_batches), int(relu), _lib.ptr(y), _lib.ptr(save),
-                                                    _lib.ptr(stats[0]), int(stats[1]), _lib.ptr(rmask),
-                                                    _lib.stream_ptr()))
+                                                    _lib.ptr(stats[0]), int(stats[1]), _lib.nbytes(stats[0]),
+                                                    _lib.ptr(rmask), _lib.stream_ptr()))
             else:
                 _lib.check(L.gmz_bn_forward_stats(_BN_DTYPES[x.dtype], _lib.ptr(x), _lib.ptr(res), B, C, S,
                                                   _lib.ptr(gamma), _lib.ptr(beta), float(eps), float(momentum),
                                                   _lib.ptr(running_mean), _lib.ptr(running_var), _lib.ptr(num_batches),
                                                   int(relu), _lib.ptr(y), _lib.ptr(save), _lib.ptr(stats[0]),
-                                                  int(stats[1]), _lib.stream_ptr()))
+                                                  int(stats[1]), _lib.nbytes(stats[0]), _lib.stream_ptr()))
         else:
             ws = _bn_workspace(layout, B, C, S, x.device)
             if rmask is not None:
                 _lib.check(L.gmz_bn_forward_m(_BN_DTYPES[x.dtype], layout, _lib.ptr(x), _lib.ptr(res), _lib.ptr(mask),
                                               B, C, S, _lib.ptr(gamma), _lib.ptr(beta), float(eps), float(momentum),
                                               _lib.ptr(running_mean), _lib.ptr(running_var), _lib.ptr(num_batches),
-                                              int(relu), _lib.ptr(y), _lib.ptr(save), _lib.ptr(ws), _lib.ptr(rmask),
-                                              _lib.stream_ptr()))
+                                              int(relu), _lib.ptr(y), _lib.ptr(save), _lib.ptr(ws), _lib.nbytes(ws),
+                                              _lib.ptr(rmask), _lib.stream_ptr()))
             else:
                 _lib.check(L.gmz_bn_forward(_BN_DTYPES[x.dtype], layout, _lib.ptr(x), _lib.ptr(res), _lib.ptr(mask), B,
                                             C, S, _lib.ptr(gamma), _lib.ptr(beta), float(eps), float(momentum),
                                             _lib.ptr(running_mean), _lib.ptr(running_var), _lib.ptr(num_batches),
-                                            int(relu), _lib.ptr(y), _lib.ptr(save), _lib.ptr(ws), _lib.stream_ptr()))
+                                            int(relu), _lib.ptr(y), _lib.ptr(save), _lib.ptr(ws), _lib.nbytes(ws),
+                                            _lib.stream_ptr()))
         ctx.save_for_backward(x, y, mask, gamma, save)
         ctx.relu, ctx.has_res, ctx.layout = relu, res is not None, layout
         ctx.rmask = rmask
@@ -290,17 +292,19 @@ class _FusedMaskedBN(torch.autograd.Function):
             _lib.check(L.gmz_bn_backward_stats(_BN_DTYPES[x.dtype], _lib.ptr(x), _lib.ptr(y), _lib.ptr(dy),
                                                _lib.ptr(mask), B, C, S, _lib.ptr(gamma), _lib.ptr(save), int(ctx.relu),
                                                _lib.ptr(dx), _lib.ptr(dres), _lib.ptr(dgamma), _lib.ptr(dbeta),
-                                               _lib.ptr(pre[0]), int(pre[1]), _lib.ptr(ws), _lib.stream_ptr(), int(acc)))
+                                               _lib.ptr(pre[0]), int(pre[1]), _lib.nbytes(pre[0]), _lib.ptr(ws),
+                                               _lib.nbytes(ws), _lib.stream_ptr(), int(acc)))
         elif ctx.rmask is not None and _aligned16(x, y, dy, dx, dres):
             _lib.check(L.gmz_bn_backward_acc_m(_BN_DTYPES[x.dtype], layout, _lib.ptr(x), _lib.ptr(y), _lib.ptr(dy),
                                                _lib.ptr(mask), B, C, S, _lib.ptr(gamma), _lib.ptr(save), int(ctx.relu),
                                                _lib.ptr(dx), _lib.ptr(dres), _lib.ptr(dgamma), _lib.ptr(dbeta),
-                                               _lib.ptr(ws), _lib.ptr(ctx.rmask), _lib.stream_ptr(), int(acc)))
+                                               _lib.ptr(ws), _lib.nbytes(ws), _lib.ptr(ctx.rmask), _lib.stream_ptr(),
+                                               int(acc)))
         else:
             _lib.check(L.gmz_bn_backward_acc(_BN_DTYPES[x.dtype], layout, _lib.ptr(x), _lib.ptr(y), _lib.ptr(dy),
                                              _lib.ptr(mask), B, C, S, _lib.ptr(gamma), _lib.ptr(save), int(ctx.relu),
                                              _lib.ptr(dx), _lib.ptr(dres), _lib.ptr(dgamma), _lib.ptr(dbeta),
-                                             _lib.ptr(ws), _lib.stream_ptr(), int(acc)))
+                                             _lib.ptr(ws), _lib.nbytes(ws), _lib.stream_ptr(), int(acc)))
         ctx.rmask = None
         if ctx.link is not None and dres is not None:
             # the residual's gradient goes to the block's first conv, whose input-gradient epilogue adds it
@@ -374,7 +378,8 @@ def _bn_seg(mod, x, mask, res, relu, nseg):
                                               S, _lib.ptr(mod.weight), _lib.ptr(mod.bias), float(mod.eps),
                                               float(mod.momentum), _lib.ptr(mod.running_mean), _lib.ptr(mod.running_var),
                                               _lib.ptr(mod.num_batches_tracked), int(relu), _lib.ptr(y), _lib.ptr(save),
-                                              _lib.ptr(ws), _lib.ptr(board), _lib.stream_ptr()))
+                                              _lib.ptr(ws), _lib.nbytes(ws), _lib.ptr(board), _lib.nbytes(board),
+                                              _lib.stream_ptr()))
     return y
 
 
@@ -392,7 +397,7 @@ def _bn_eval(mod, x, res, relu):
     _lib.check(_lib.load().gmz_bn_eval(_BN_DTYPES[x.dtype], layout, _lib.ptr(x), _lib.ptr(res), B, C, S,
                                        _lib.ptr(mod.weight), _lib.ptr(mod.bias), _lib.ptr(mod.running_mean),
                                        _lib.ptr(mod.running_var), float(mod.eps), int(relu), _lib.ptr(y),
-                                       _lib.ptr(ws), _lib.stream_ptr()))
+                                       _lib.ptr(ws), _lib.nbytes(ws), _lib.stream_ptr()))
     return y
 
 
@@ -499,7 +504,7 @@ def _conv3x3_hip(x, packed, mask=None, stats=None, addend=None, bnb=None, bn_y=N
         _lib.check(_lib.load().gmz_conv3x3_forward_bwdstats(
             _CONV_DTYPES[x.dtype], x.shape[2], _lib.ptr(x), _lib.ptr(packed), _lib.ptr(addend), _lib.ptr(y), x.shape[0],
             _lib.ptr(bnb.mask), _lib.ptr(bnb.x), _lib.ptr(bn_y), _lib.ptr(bnb.save), int(bnb.relu), _lib.ptr(st),
-            _lib.stream_ptr()))
+            _stats_slots_of(st), _lib.stream_ptr()))
         bnb.bwd = (st, ns, y)
         return y
     if addend is not None:  # y = round(conv + addend) (the residual gradient folded into the input gradient)
@@ -509,8 +514,14 @@ def _conv3x3_hip(x, packed, mask=None, stats=None, addend=None, bnb=None, bn_y=N
         return y
     _lib.check(_lib.load().gmz_conv3x3_forward_stats(_CONV_DTYPES[x.dtype], x.shape[2], _lib.ptr(x), _lib.ptr(packed),
                                                      _lib.ptr(y), x.shape[0], _lib.ptr(mask), _lib.ptr(stats),
-                                                     _lib.stream_ptr()))
+                                                     _stats_slots_of(stats), _lib.stream_ptr()))
     return y
+
+
+def _stats_slots_of(stats):
+    """The slot capacity of an f64 [128][slots][3] statistics-partials buffer (0 for None): the library checks it
+    against the slot count of the launch before writing (ABI 10)."""
+    return 0 if stats is None else stats.numel() // (128 * 3)
 
 
 # the residual blocks' identity-path gradient folded into conv1's input-gradient epilogue (_ResLink):
@@ -572,7 +583,7 @@ def flush_wgrads():
                 _lib.check(L.gmz_conv3x3_wgrad_segments(_CONV_DTYPES[dt], H, ctypes.cast(xs, ctypes.c_void_p),
                                                         ctypes.cast(gs, ctypes.c_void_p), len(seg), N,
                                                         _lib.ptr(w.grad), st[0], st[1], st[2], st[3], 1, _lib.ptr(ws),
-                                                        _lib.stream_ptr()))
+                                                        _lib.nbytes(ws), _lib.stream_ptr()))
     _PENDING_WGRAD.clear()
 
 
@@ -589,7 +600,7 @@ def _conv3x3_wgrad_hip(x, gy, grad):
     ws = torch.empty(_WGRAD_WS[N] // 4, dtype=torch.float32, device=x.device)
     s = grad.stride()
     _lib.check(L.gmz_conv3x3_wgrad(_CONV_DTYPES[x.dtype], x.shape[2], _lib.ptr(x), _lib.ptr(gy), N, _lib.ptr(grad),
-                                   s[0], s[1], s[2], s[3], 1, _lib.ptr(ws), _lib.stream_ptr()))
+                                   s[0], s[1], s[2], s[3], 1, _lib.ptr(ws), _lib.nbytes(ws), _lib.stream_ptr()))
 
 
 def _conv_stats_buffer(N, device):
@@ -656,6 +667,10 @@ class _Conv3x3NHWC(torch.autograd.Function):
         return gx, gw, None, None, None, None
 
 
+# the stamp table's dtype code for gmz_conv3x3_forward_stamp: the library takes f32 only and rejects anything else
+# (or a table of the wrong size) before the launch (ABI 10); -1 = a dtype with no code
+_TABLE_DTYPES = collections.defaultdict(lambda: -1, {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2})
+
 # the dynamics trunk's first conv (144 -> 128) on the HIP conv: its 128 hidden planes as a 128 -> 128 conv, its 16
 # action-embedding planes (one one-hot cell per board) as a 3x3 stamp added in the conv's epilogue
 # (gmz_conv3x3_forward_stamp), instead of MIOpen's three 144-channel kernels and the concatenation (A/B switch;
@@ -690,15 +705,14 @@ class _DynStemHIP(torch.autograd.Function):
             w2 = W.detach()[:, 128:].to(dt).float().reshape(128, 16, 9)
             e = w_emb.detach().reshape(16).to(dt).float()
             table = torch.einsum("oct,c->to", w2, e).contiguous()
-        if table.dtype != torch.float32 or table.numel() != 9 * 128:
-            raise RuntimeError("_DynStemHIP: stamp table must be f32 [9][128]")
         a32 = a.to(torch.int32).contiguous()
         if a32.numel() != h.shape[0]:
             raise RuntimeError("_DynStemHIP: one action per board")
         y = torch.empty_like(h, memory_format=torch.channels_last)
         _lib.check(_lib.load().gmz_conv3x3_forward_stamp(
             _CONV_DTYPES[dt], H, _lib.ptr(h), _lib.ptr(_packed_conv_weight(W[:, :128], dt, 0, parent=W)), _lib.ptr(y), n,
-            _lib.ptr(mask), _lib.ptr(stats), _lib.ptr(a32), _lib.ptr(table), _lib.stream_ptr()))
+            _lib.ptr(mask), _lib.ptr(stats), _stats_slots_of(stats), _lib.ptr(a32), _lib.ptr(table),
+            _TABLE_DTYPES[table.dtype], _lib.nbytes(table), _lib.stream_ptr()))
         ctx.save_for_backward(h, W, w_emb, a32)
         return y
 
@@ -781,7 +795,7 @@ def _conv3_apply(conv, x, bn=None, mask=None, link=None, segments=1):
                 m = None if mask is None else mask.contiguous().view(torch.uint8)
                 _lib.check(_lib.load().gmz_conv3x3_forward_board_stats(_CONV_DTYPES[dt], xin.shape[2], _lib.ptr(xin),
                                                                        _lib.ptr(packed), _lib.ptr(y), N, _lib.ptr(m),
-                                                                       _lib.ptr(st), _lib.stream_ptr()))
+                                                                       _lib.ptr(st), N, _lib.stream_ptr()))
                 y._gmz_bnstats = (st, "board")
             else:
                 _lib.check(_lib.load().gmz_conv3x3_forward(_CONV_DTYPES[dt], xin.shape[2], _lib.ptr(xin), _lib.ptr(packed),
@@ -886,7 +900,7 @@ def _headconv_backward(x, saved, params, g0, g1):
     outs = [p.grad if direct else torch.empty(p.shape, dtype=torch.float32, device=x.device) for p in params]
     _lib.check(L.gmz_head_conv1x1_backward(_BN_DTYPES[x.dtype], _lib.ptr(x), P, C, _lib.ptr(w0m), O0, _lib.ptr(w1m), O1,
                                            _lib.ptr(g0), _lib.ptr(g1), _lib.ptr(dx), *[_lib.ptr(t) for t in outs],
-                                           int(direct), _lib.ptr(ws), _lib.stream_ptr()))
+                                           int(direct), _lib.ptr(ws), _lib.nbytes(ws), _lib.stream_ptr()))
     if direct:
         return dx, [None] * 4
     return dx, [t.to(p.dtype) for t, p in zip(outs, params)]
@@ -1471,7 +1485,7 @@ class _SegBN(torch.autograd.Function):
         st = torch.empty(3 * nseg * C + nseg, dtype=torch.float32, device=x.device)
         _lib.check(_lib.load().gmz_seg_bn_forward(_BN_DTYPES[x.dtype], _lib.ptr(x), _lib.ptr(m), nseg, N // nseg, S, C,
                                                   _lib.ptr(gamma), _lib.ptr(beta), float(eps), _lib.ptr(y), _lib.ptr(st),
-                                                  int(update), float(momentum), _lib.ptr(rmean), _lib.ptr(rvar),
+                                                  _lib.nbytes(st), int(update), float(momentum), _lib.ptr(rmean), _lib.ptr(rvar),
                                                   _lib.ptr(nbt), _lib.ptr(pre), _lib.stream_ptr()))
         ctx.save_for_backward(x, gamma, beta, st, m)
         ctx.nseg = nseg
@@ -1493,7 +1507,8 @@ class _SegBN(torch.autograd.Function):
         dg = gamma.grad if direct else torch.empty(C, dtype=torch.float32, device=x.device)
         db = beta.grad if direct else torch.empty(C, dtype=torch.float32, device=x.device)
         _lib.check(_lib.load().gmz_seg_bn_backward(_BN_DTYPES[x.dtype], _lib.ptr(x), _lib.ptr(dy), _lib.ptr(m), ctx.nseg,
-                                                   N // ctx.nseg, S, C, _lib.ptr(gamma), _lib.ptr(st), _lib.ptr(dx),
+                                                   N // ctx.nseg, S, C, _lib.ptr(gamma), _lib.ptr(st), _lib.nbytes(st),
+                                                   _lib.ptr(dx),
                                                    _lib.ptr(dg), _lib.ptr(db), int(direct), _lib.stream_ptr()))
         if direct:
             return dx, None, None, None, None, None, None, None, None, None, None, None

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define GMZ_ABI_VERSION 9
+#define GMZ_ABI_VERSION 10
 
 /* ------------------------------------------------------------------ misc */
 const char *gmz_last_error(void);
@@ -246,31 +246,35 @@ typedef struct gmz_net_weights {
  * be captured into a HIP graph: every replay would reuse one generation and, from the second replay
  * on, compute no boards. */
 int gmz_net_workspace_bytes(const gmz_net_weights *w, int rows, size_t *out);
+/* Capacity arguments (ABI 10): every entry point below that writes caller-allocated scratch or partials, or reads
+ * partials at a size its arguments imply, takes that buffer's size in bytes (workspace_bytes, ws_bytes, stats_bytes)
+ * or slots (stats_slots) and fails with gmz_last_error() — before any launch — when the buffer is short (slots: when
+ * they differ from what the launch writes, since the slot count is the partials' row stride). */
 /* network.py:137-143 initial_inference: obs_dev f32[rows][3][A] -> logits f32[rows][A],
  * value f32[rows] (support_to_scalar), hidden state -> hid_pool_dev[out_slot[r]] (dtype [A][C]).
  * Rows with out_slot[r] < 0 are skipped. */
 int gmz_net_initial(const gmz_net_weights *w, const float *obs_dev, int rows, const int32_t *out_slot_dev,
                     uint16_t *hid_pool_dev, float *logits_dev, float *value_dev, void *workspace_dev,
-                    void *stream);
+                    size_t workspace_bytes, void *stream);
 /* gmz_net_initial in two stream-ordered halves (representation tower, then the heads), like the
  * recurrent pair below. */
 int gmz_net_initial_tower(const gmz_net_weights *w, const float *obs_dev, int rows, const int32_t *out_slot_dev,
-                          uint16_t *hid_pool_dev, void *workspace_dev, void *stream);
+                          uint16_t *hid_pool_dev, void *workspace_dev, size_t workspace_bytes, void *stream);
 int gmz_net_initial_heads(const gmz_net_weights *w, const uint16_t *hid_pool_dev, const int32_t *out_slot_dev, int rows,
-                          float *logits_dev, float *value_dev, void *workspace_dev, void *stream);
+                          float *logits_dev, float *value_dev, void *workspace_dev, size_t workspace_bytes, void *stream);
 /* network.py:145-152 recurrent_inference: hid_pool[in_slot[r]], action[r] -> logits, value,
  * reward f32[rows], next hidden state -> hid_pool[out_slot[r]]. */
 int gmz_net_recurrent(const gmz_net_weights *w, uint16_t *hid_pool_dev, const int32_t *in_slot_dev,
                       const int32_t *action_dev, const int32_t *out_slot_dev, int rows, float *logits_dev,
-                      float *value_dev, float *reward_dev, void *workspace_dev, void *stream);
+                      float *value_dev, float *reward_dev, void *workspace_dev, size_t workspace_bytes, void *stream);
 /* gmz_net_recurrent in two stream-ordered halves (lets a caller time the dynamics tower alone):
  * the tower writes the next hidden state + head features into the workspace; the heads read them. */
 int gmz_net_recurrent_tower(const gmz_net_weights *w, uint16_t *hid_pool_dev, const int32_t *in_slot_dev,
                             const int32_t *action_dev, const int32_t *out_slot_dev, int rows, void *workspace_dev,
-                            void *stream);
+                            size_t workspace_bytes, void *stream);
 int gmz_net_recurrent_heads(const gmz_net_weights *w, const uint16_t *hid_pool_dev, const int32_t *out_slot_dev,
                             int rows, float *logits_dev, float *value_dev, float *reward_dev, void *workspace_dev,
-                            void *stream);
+                            size_t workspace_bytes, void *stream);
 
 /* ------------------------------------------------------------------ trainer kernels (trainer.py) */
 /* Row-masked BatchNorm with the residual add and ReLU fused (training mode), replacing the
@@ -290,29 +294,30 @@ int gmz_bn_workspace_bytes(int layout, int B, int C, int S, size_t *out);
 int gmz_bn_forward(int dtype, int layout, const void *x_dev, const void *res_dev, const uint8_t *mask_dev, int B, int C, int S,
                    const float *gamma_dev, const float *beta_dev, float eps, float momentum, float *running_mean_dev,
                    float *running_var_dev, int64_t *num_batches_dev, int relu, void *y_dev, float *save_dev,
-                   void *workspace_dev, void *stream);
+                   void *workspace_dev, size_t ws_bytes, void *stream);
 int gmz_bn_backward(int dtype, int layout, const void *x_dev, const void *y_dev, const void *dy_dev, const uint8_t *mask_dev, int B,
                     int C, int S, const float *gamma_dev, const float *save_dev, int relu, void *dx_dev, void *dres_dev,
-                    float *dgamma_dev, float *dbeta_dev, void *workspace_dev, void *stream);
+                    float *dgamma_dev, float *dbeta_dev, void *workspace_dev, size_t ws_bytes, void *stream);
 /* gmz_bn_backward with accumulate = 1: dgamma_dev/dbeta_dev += the gradients (the parameters' f32 .grad,
  * no separate gradient tensors or adds); accumulate = 0 is gmz_bn_backward. */
 int gmz_bn_backward_acc(int dtype, int layout, const void *x_dev, const void *y_dev, const void *dy_dev,
                         const uint8_t *mask_dev, int B, int C, int S, const float *gamma_dev, const float *save_dev,
                         int relu, void *dx_dev, void *dres_dev, float *dgamma_dev, float *dbeta_dev,
-                        void *workspace_dev, void *stream, int accumulate);
+                        void *workspace_dev, size_t ws_bytes, void *stream, int accumulate);
 /* gmz_bn_forward with the statistics already reduced to partials (e.g. by gmz_conv3x3_forward_stats):
- * stats_dev f64 [C][ns][3] (sum, sum of squares, counted elements); channels-last (layout 1) only. */
+ * stats_dev f64 [C][ns][3] (sum, sum of squares, counted elements), stats_bytes >= C * ns * 24; channels-last
+ * (layout 1) only. */
 int gmz_bn_forward_stats(int dtype, const void *x_dev, const void *res_dev, int B, int C, int S, const float *gamma_dev,
                          const float *beta_dev, float eps, float momentum, float *running_mean_dev,
                          float *running_var_dev, int64_t *num_batches_dev, int relu, void *y_dev, float *save_dev,
-                         const double *stats_dev, int ns, void *stream);
+                         const double *stats_dev, int ns, size_t stats_bytes, void *stream);
 /* gmz_bn_backward_acc (channels-last) with its dz sums already reduced to partials stats_dev f64 [C][ns][3]
  * (sum dz, sum dz * xhat, counted elements) by the producer of dy_dev (gmz_conv3x3_forward_bwdstats): the
  * finalisation and the elementwise pass only.  workspace_dev: gmz_bn_workspace_bytes(1, B, C, S).  (ABI 7) */
 int gmz_bn_backward_stats(int dtype, const void *x_dev, const void *y_dev, const void *dy_dev, const uint8_t *mask_dev,
                           int B, int C, int S, const float *gamma_dev, const float *save_dev, int relu, void *dx_dev,
                           void *dres_dev, float *dgamma_dev, float *dbeta_dev, const double *stats_dev, int ns,
-                          void *workspace_dev, void *stream, int accumulate);
+                          size_t stats_bytes, void *workspace_dev, size_t ws_bytes, void *stream, int accumulate);
 /* Eval-mode BatchNorm (running statistics) + residual + ReLU, same layouts/dtypes as gmz_bn_forward:
  * y = relu?(gamma*(x-running_mean)/sqrt(running_var+eps) + beta (+ res)) — nn.BatchNorm2d/1d in eval()
  * (the target network's value of loss.py:54-55).  workspace_dev: gmz_bn_workspace_bytes bytes. */
@@ -323,15 +328,15 @@ int gmz_bn_backward_stats(int dtype, const void *x_dev, const void *y_dev, const
 int gmz_bn_forward_m(int dtype, int layout, const void *x_dev, const void *res_dev, const uint8_t *mask_dev, int B,
                      int C, int S, const float *gamma_dev, const float *beta_dev, float eps, float momentum,
                      float *running_mean_dev, float *running_var_dev, int64_t *num_batches_dev, int relu, void *y_dev,
-                     float *save_dev, void *workspace_dev, uint8_t *relu_mask_dev, void *stream);
+                     float *save_dev, void *workspace_dev, size_t ws_bytes, uint8_t *relu_mask_dev, void *stream);
 int gmz_bn_forward_stats_m(int dtype, const void *x_dev, const void *res_dev, int B, int C, int S, const float *gamma_dev,
                            const float *beta_dev, float eps, float momentum, float *running_mean_dev,
                            float *running_var_dev, int64_t *num_batches_dev, int relu, void *y_dev, float *save_dev,
-                           const double *stats_dev, int slots, uint8_t *relu_mask_dev, void *stream);
+                           const double *stats_dev, int slots, size_t stats_bytes, uint8_t *relu_mask_dev, void *stream);
 int gmz_bn_backward_acc_m(int dtype, int layout, const void *x_dev, const void *y_dev, const void *dy_dev,
                           const uint8_t *mask_dev, int B, int C, int S, const float *gamma_dev, const float *save_dev,
                           int relu, void *dx_dev, void *dres_dev, float *dgamma_dev, float *dbeta_dev,
-                          void *workspace_dev, const uint8_t *relu_mask_dev, void *stream, int accumulate);
+                          void *workspace_dev, size_t ws_bytes, const uint8_t *relu_mask_dev, void *stream, int accumulate);
 /* Launches of the fused BatchNorm finalisation (the channels-last apply passes with GMZ_BN_FUSED_FIN=1; default: the
  * separate finalisation launch, measured faster) whose bounded wait for every channel's published constants ran
  * out: must stay 0.
@@ -341,15 +346,16 @@ int gmz_bn_sync_errors(uint32_t *out, int reset);
  * consistency representations, loss.py:102-104): segment g = rows [g B/nseg, (g+1) B/nseg), its statistics over
  * its own masked rows, save_dev f32 [nseg][2][C] = per segment (mean, invstd), the running statistics updated by
  * the segments in order (= nseg gmz_bn_forward calls).  board_stats_dev: per-board partials from
- * gmz_conv3x3_forward_board_stats (f64 [C][B][3]) or NULL (a reduction pass).  workspace_dev:
- * gmz_bn_workspace_bytes(1, B, C, S).  (ABI 8) */
+ * gmz_conv3x3_forward_board_stats (f64 [C][B][3], board_stats_bytes >= C * B * 24) or NULL (a reduction pass).
+ * workspace_dev: gmz_bn_workspace_bytes(1, B, C, S).  (ABI 8) */
 int gmz_bn_forward_seg(int dtype, const void *x_dev, const void *res_dev, const uint8_t *mask_dev, int B, int nseg,
                        int C, int S, const float *gamma_dev, const float *beta_dev, float eps, float momentum,
                        float *running_mean_dev, float *running_var_dev, int64_t *num_batches_dev, int relu, void *y_dev,
-                       float *save_dev, void *workspace_dev, const double *board_stats_dev, void *stream);
+                       float *save_dev, void *workspace_dev, size_t ws_bytes, const double *board_stats_dev,
+                       size_t board_stats_bytes, void *stream);
 int gmz_bn_eval(int dtype, int layout, const void *x_dev, const void *res_dev, int B, int C, int S, const float *gamma_dev,
                 const float *beta_dev, const float *running_mean_dev, const float *running_var_dev, float eps, int relu,
-                void *y_dev, void *workspace_dev, void *stream);
+                void *y_dev, void *workspace_dev, size_t ws_bytes, void *stream);
 /* 3x3 convolution, 128 -> 128 channels, stride 1, padding 1, no bias (the residual-block convs of
  * network.py:30-48), on channels-last activations x[N][H*H][128] -> y[N][H*H][128]; dtype 1 = f16,
  * 2 = bf16 (activations and packed weights; f32 accumulation); H = 9 or 15.  The training step's
@@ -361,18 +367,20 @@ int gmz_bn_eval(int dtype, int layout, const void *x_dev, const void *res_dev, i
 int gmz_conv3x3_pack(int dtype, const float *w_dev, int64_t s0, int64_t s1, int64_t s2, int64_t s3, int transpose,
                      void *packed_dev, void *stream);
 /* gmz_conv3x3_forward_stats with the BatchNorm statistics partials per BOARD: stats_dev f64 [128][N][3] (sum,
- * sum of squares, valid pixels of board n; 0 for a masked-out board), for gmz_bn_forward_seg.  (ABI 8) */
+ * sum of squares, valid pixels of board n; 0 for a masked-out board), for gmz_bn_forward_seg; stats_slots must be
+ * N.  (ABI 8; stats_slots ABI 10) */
 int gmz_conv3x3_forward_board_stats(int dtype, int H, const void *x_dev, const void *packed_dev, void *y_dev, int N,
-                                    const uint8_t *mask_dev, double *stats_dev, void *stream);
+                                    const uint8_t *mask_dev, double *stats_dev, int stats_slots, void *stream);
 /* The dynamics trunk's first conv (144 -> 128: 128 hidden planes + the 16-plane embedding of one action cell per
  * board, network.py:79-96) as the 128 -> 128 conv of the hidden planes (packed_dev from gmz_conv3x3_pack of
  * W[:, :128]) plus a 3x3 stamp around each board's action cell: out[n][q][o] += table_dev[tap][o] for q in the
  * cell's 3x3 window (tap = (a - q) + (1, 1)), table_dev f32 [9][128] = sum_c W[o][128 + c][tap] * embed[c],
- * added in f32 before the output's one rounding.  action_dev int32 [N]; stats_dev / mask_dev as
- * gmz_conv3x3_forward_stats (either may be NULL).  (ABI 8) */
+ * added in f32 before the output's one rounding: table_dtype must be 0 (f32) and table_bytes 4608.  action_dev
+ * int32 [N]; stats_dev / stats_slots / mask_dev as gmz_conv3x3_forward_stats (stats_dev and mask_dev may be
+ * NULL).  (ABI 8; stats_slots, table_dtype, table_bytes ABI 10) */
 int gmz_conv3x3_forward_stamp(int dtype, int H, const void *x_dev, const void *packed_dev, void *y_dev, int N,
-                              const uint8_t *mask_dev, double *stats_dev, const int32_t *action_dev,
-                              const float *table_dev, void *stream);
+                              const uint8_t *mask_dev, double *stats_dev, int stats_slots, const int32_t *action_dev,
+                              const void *table_dev, int table_dtype, size_t table_bytes, void *stream);
 int gmz_conv3x3_forward(int dtype, int H, const void *x_dev, const void *packed_dev, void *y_dev, int N, void *stream);
 /* The same convolution plus an addend of the output's shape and dtype, rounded once:
  * y = round(conv(x, W) + addend).  The residual blocks' input gradient with the identity path's
@@ -383,34 +391,35 @@ int gmz_conv3x3_forward_add(int dtype, int H, const void *x_dev, const void *pac
 /* The same convolution, also writing the BatchNorm statistics of the (rounded) output over the boards
  * whose mask_dev byte is nonzero (NULL: all): stats_dev f64 [128][slots][3] = (sum, sum of squares,
  * counted positions) per slot, slots from gmz_conv3x3_stats_slots(N) — the partials layout
- * gmz_bn_forward_stats consumes (channels-last, ns = slots). */
+ * gmz_bn_forward_stats consumes (channels-last, ns = slots).  stats_slots must equal that count (ABI 10). */
 int gmz_conv3x3_stats_slots(int N, int *slots);
 /* Weight gradient of the same convolution (the reference's autocast backward of the residual-block
  * convs): dw_dev f32 W[o][c][ky][kx] at element strides (s0..s3) = (accumulate ? dw + : ) sum over the
  * N boards of dy x^T per tap; x_dev, dy_dev channels-last [N][H*H][128] f16/bf16, 16-B aligned.
- * workspace_dev: gmz_conv3x3_wgrad_workspace_bytes(N) bytes (per-chunk partials). */
+ * workspace_dev: workspace_bytes >= gmz_conv3x3_wgrad_workspace_bytes(N) bytes (per-chunk partials). */
 int gmz_conv3x3_wgrad_workspace_bytes(int N, size_t *out);
 int gmz_conv3x3_wgrad(int dtype, int H, const void *x_dev, const void *dy_dev, int N, float *dw_dev, int64_t s0,
-                      int64_t s1, int64_t s2, int64_t s3, int accumulate, void *workspace_dev, void *stream);
+                      int64_t s1, int64_t s2, int64_t s3, int accumulate, void *workspace_dev, size_t workspace_bytes,
+                      void *stream);
 /* gmz_conv3x3_wgrad over the boards of nseg (<= 8) segments of n_per_seg boards each (host arrays of device
  * pointers x_segs[i], dy_segs[i]): the summed weight gradient of one convolution's several uses (the
  * dynamics trunk in every unroll step, loss.py:86-107) in one launch and one partial-sum reduction;
  * workspace: gmz_conv3x3_wgrad_workspace_bytes(nseg * n_per_seg). */
 int gmz_conv3x3_wgrad_segments(int dtype, int H, const void *const *x_segs, const void *const *dy_segs, int nseg,
                                int n_per_seg, float *dw_dev, int64_t s0, int64_t s1, int64_t s2, int64_t s3,
-                               int accumulate, void *workspace_dev, void *stream);
+                               int accumulate, void *workspace_dev, size_t workspace_bytes, void *stream);
 int gmz_conv3x3_forward_stats(int dtype, int H, const void *x_dev, const void *packed_dev, void *y_dev, int N,
-                              const uint8_t *mask_dev, double *stats_dev, void *stream);
+                              const uint8_t *mask_dev, double *stats_dev, int stats_slots, void *stream);
 /* The convolution as an input gradient (transposed packing; addend_dev optional, as gmz_conv3x3_forward_add)
  * whose output y is the output gradient dy of a channels-last BatchNorm (+ReLU) below it — bn_x_dev its input,
  * bn_y_dev its output, bn_save_dev its saved (mean, invstd) f32 [2][128], same [N][H*H][128] layout and dtype —
  * also writing that BatchNorm's BACKWARD sums over the boards whose mask_dev byte is nonzero: stats_dev f64
  * [128][slots][3] = (sum dz, sum dz * xhat, counted positions), dz = y * [bn_y > 0] (relu) or y,
  * xhat = (bn_x - mean) * invstd — the partials gmz_bn_backward_stats consumes instead of its reduction pass.
- * bn_x_dev / bn_y_dev 8-B aligned.  (ABI 7) */
+ * bn_x_dev / bn_y_dev 8-B aligned; stats_slots = gmz_conv3x3_stats_slots(N).  (ABI 7; stats_slots ABI 10) */
 int gmz_conv3x3_forward_bwdstats(int dtype, int H, const void *x_dev, const void *packed_dev, const void *addend_dev,
                                  void *y_dev, int N, const uint8_t *mask_dev, const void *bn_x_dev, const void *bn_y_dev,
-                                 const float *bn_save_dev, int relu, double *stats_dev, void *stream);
+                                 const float *bn_save_dev, int relu, double *stats_dev, int stats_slots, void *stream);
 /* dst_dev[o][c][p] += src_dev[(p*C + c)*O + o] (f32 accumulate; src dtype 0 = f32, 1 = f16, 2 = bf16):
  * the weight gradient x^T dy of a K = C*P Linear whose input was a channels-last [N][P][C] hidden state
  * flattened in (p, c) order, added into the f32 .grad of W [O][C*P] (the reference's NCHW flatten,
@@ -442,15 +451,15 @@ int gmz_head_conv1x1_forward(int dtype, const void *x_dev, long P, int C, const 
  * without live rows skipped; pre_stats_dev (or NULL): an earlier call's stats of the same nseg segments whose update
  * goes first in each segment (the projection's dynamics step s, then target s).  1 <= nseg <= 32.  (ABI 9) */
 int gmz_seg_bn_forward(int dtype, const void *x_dev, const uint8_t *row_mask_dev, int nseg, int B, int S, int C,
-                       const float *gamma_dev, const float *beta_dev, float eps, float *y_dev, float *stats_dev, int update,
-                       float momentum, float *running_mean_dev, float *running_var_dev, int64_t *num_batches_dev,
-                       const float *pre_stats_dev, void *stream);
+                       const float *gamma_dev, const float *beta_dev, float eps, float *y_dev, float *stats_dev,
+                       size_t stats_bytes, int update, float momentum, float *running_mean_dev, float *running_var_dev,
+                       int64_t *num_batches_dev, const float *pre_stats_dev, void *stream);
 /* Its backward: dy_dev f32 like y; dx_dev like x (its dtype); dgamma/dbeta f32 [C] written or added (accumulate),
  * NULL: skipped.  Every row's dy enters its segment's sums (a row outside the mask still depends on the segment's
  * statistics through y); the mean/variance terms apply to the live rows. */
 int gmz_seg_bn_backward(int dtype, const void *x_dev, const float *dy_dev, const uint8_t *row_mask_dev, int nseg, int B,
-                        int S, int C, const float *gamma_dev, const float *stats_dev, void *dx_dev, float *dgamma_dev,
-                        float *dbeta_dev, int accumulate, void *stream);
+                        int S, int C, const float *gamma_dev, const float *stats_dev, size_t stats_bytes, void *dx_dev,
+                        float *dgamma_dev, float *dbeta_dev, int accumulate, void *stream);
 /* bytes of the backward's workspace for P positions and O = O0 + O1 outputs */
 int gmz_head_conv1x1_workspace_bytes(long P, int O, size_t *out);
 /* The backward of gmz_head_conv1x1_forward: dx_dev [P][128] = round(sum_o dy[p][o] W[o][c]) over BOTH heads
@@ -460,7 +469,7 @@ int gmz_head_conv1x1_workspace_bytes(long P, int O, size_t *out);
 int gmz_head_conv1x1_backward(int dtype, const void *x_dev, long P, int C, const float *w0_dev, int O0,
                               const float *w1_dev, int O1,
                               const void *dy0_dev, const void *dy1_dev, void *dx_dev, float *dw0_dev, float *db0_dev,
-                              float *dw1_dev, float *db1_dev, int accumulate, void *ws_dev, void *stream);
+                              float *dw1_dev, float *db1_dev, int accumulate, void *ws_dev, size_t ws_bytes, void *stream);
 
 #ifdef __cplusplus
 }

@@ -37,12 +37,12 @@ P = _lib.ptr
 
 def fwd():
     _lib.check(L.gmz_bn_forward(1, 1, P(x), P(res), P(mask), B, C, S, P(gamma), P(beta), 1e-4, 0.1, P(rm), P(rv), P(nb),
-                                1, P(y), P(save), P(ws), _lib.stream_ptr()))
+                                1, P(y), P(save), P(ws), _lib.nbytes(ws), _lib.stream_ptr()))
 
 
 def bwd():
     _lib.check(L.gmz_bn_backward_acc(1, 1, P(x), P(y), P(dy), P(mask), B, C, S, P(gamma), P(save), 1, P(dx), P(dres),
-                                     P(dg), P(db), P(ws), _lib.stream_ptr(), 1))
+                                     P(dg), P(db), P(ws), _lib.nbytes(ws), _lib.stream_ptr(), 1))
 
 
 def timed(fn):
@@ -65,6 +65,7 @@ if hasattr(L, "gmz_bn_backward_stats"):  # ABI 7: the dz sums already reduced (b
 
     def bwd_stats():
         _lib.check(L.gmz_bn_backward_stats(1, P(x), P(y), P(dy), P(mask), B, C, S, P(gamma), P(save), 1, P(dx), P(dres),
-                                           P(dg), P(db), P(stats), ns, P(ws), _lib.stream_ptr(), 1))
+                                           P(dg), P(db), P(stats), ns, _lib.nbytes(stats), P(ws),
+                                           _lib.nbytes(ws), _lib.stream_ptr(), 1))
     out["backward_given_sums_us"] = timed(bwd_stats)
 print(json.dumps(out))
