@@ -490,11 +490,12 @@ def trainer_leg(args, world, rank, dist, backend):
             if dist:
                 dist.barrier()
             dt = collective_max(time.perf_counter() - t0, dist, backend)
-            return dt, float(pending[0][0]) if pending[0] is not None else None, tr.allreduce_ms()
+            return dt, float(pending[0][0]) if pending[0] is not None else None, tr.allreduce_times()
         finally:
             T.TARGET_F16 = saved
 
-    dt, loss, ar_ms = timed_run(args.trainer_steps, True)
+    dt, loss, ar = timed_run(args.trainer_steps, True)
+    ar_ms = None if ar is None else ar["wait_ms"]
     # the reference's precision for the target network's value (loss.py:54-55: a float32 forward outside autocast):
     # the same step with trainer.TARGET_F16 = False, beside the line's f16-trunk rate
     f32_steps = args.trainer_f32_steps
@@ -535,9 +536,12 @@ def trainer_leg(args, world, rank, dist, backend):
             if world > 1 else "single GPU",
             "last_loss": loss,
             "allreduce_ms": ar_ms,
-            "allreduce_note": ("per step on the compute stream, from bucket A's all-reduce issue (backward done) to both "
-                               "buckets averaged; bucket B's weight gradients run inside it" if ar_ms is not None else
-                               "single GPU: no all-reduce"),
+            "wgrad_flush_ms": None if ar is None else ar["flush_ms"],
+            "allreduce_window_ms": None if ar is None else ar["window_ms"],
+            "allreduce_note": ("per step on the compute stream: allreduce_ms = the exposed communication, from bucket B's "
+                               "weight gradients enqueued to both buckets averaged (B's all-reduce + what of A's did not "
+                               "hide); wgrad_flush_ms = bucket B's weight gradients, which A's all-reduce overlaps "
+                               "(trainer.allreduce_times)" if ar_ms is not None else "single GPU: no all-reduce"),
             "roofline_step": {"bound": "mfma", "achieved": step_ach, "peak": PEAK_MFMA_TFLOPS, "unit": "TFLOP/s",
                               "frac": step_ach / PEAK_MFMA_TFLOPS, "flop_per_step": step_flop,
                               "count": "bench.trainer_flop_per_step (DESIGN.md 8): convs + Linears, x3 with gradients"},

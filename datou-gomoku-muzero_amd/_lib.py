@@ -57,6 +57,7 @@ _SIGS = {
     "gmz_engine_set_hidden_bases": ([P, P, P], I),
     "gmz_engine_set_hidden_budget": ([P, P, P], I),
     "gmz_engine_errors": ([P, ctypes.POINTER(ctypes.c_int32), I], I),
+    "gmz_engine_errors_async": ([P, P, P], I),
     "gmz_hashnet_initial": ([P, I, I, P, P, P, P, P], I),
     "gmz_hashnet_recurrent": ([P, P, P, P, I, I, P, P, P, P], I),
     "gmz_bn_workspace_bytes": ([I, I, I, I, ctypes.POINTER(ctypes.c_size_t)], I),
@@ -87,7 +88,6 @@ _SIGS = {
     "gmz_bn_forward_seg": ([I, P, P, P, I, I, I, I, P, P, ctypes.c_float, ctypes.c_float, P, P, P, I, P, P, P, SZ, P, SZ,
                             P], I),
     "gmz_conv3x3_forward_board_stats": ([I, I, P, P, P, I, P, P, I, P], I),
-    "gmz_bn_sync_errors": ([ctypes.POINTER(ctypes.c_uint32), I], I),
     "gmz_conv3x3_forward_stamp": ([I, I, P, P, P, I, P, P, I, P, P, I, SZ, P], I),
     "gmz_bn_forward_m": ([I, I, P, P, P, I, I, I, P, P, ctypes.c_float, ctypes.c_float, P, P, P, I, P, P, P, SZ, P, P], I),
     "gmz_bn_forward_stats_m": ([I, P, P, I, I, I, P, P, ctypes.c_float, ctypes.c_float, P, P, P, I, P, P, P, I, SZ, P, P],

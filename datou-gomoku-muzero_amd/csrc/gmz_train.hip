@@ -324,9 +324,6 @@ __device__ __forceinline__ void stv(T *p, size_t k, const float *a) {
 #ifndef GMZ_BNL_BWD_U  // positions per trip of the backward reduction (A/B)
 #define GMZ_BNL_BWD_U 2
 #endif
-#ifndef GMZ_BN_BWD_PAIR  // measured slower (backward 40.0-40.3 vs 37.4 us per call, profiles/r05_bn_bwd_pair_ab.txt)
-#define GMZ_BN_BWD_PAIR 0
-#endif
 #ifndef GMZ_BN_APPLY_PAIR
 #define GMZ_BN_APPLY_PAIR 1
 #endif
@@ -526,8 +523,9 @@ __global__ void __launch_bounds__(BN_THREADS) k_bnl_bwd_apply(const T *__restric
     mgx[j] = coef[C + c + j];
     k1[j] = gamma[c + j] * is[j];
   }
-  // GMZ_BN_BWD_PAIR = 1: two positions per trip, every load of both issued before either is used (A/B; off)
-  constexpr int U = GMZ_BN_BWD_PAIR ? 2 : 1;
+  // one position per trip (two per trip, every load of both issued first, measured slower: 40.0-40.3 vs 37.4 us per
+  // call, profiles/r05_bn_bwd_pair_ab.txt)
+  constexpr int U = 1;
   const long gs = (long)gridDim.x * pl;
   for (long p = (long)blockIdx.x * pl + grp; p < P; p += U * gs) {
     float g[U][V], yv[U][V], xv[U][V];
@@ -574,262 +572,11 @@ __global__ void __launch_bounds__(BN_THREADS) k_bnl_bwd_apply(const T *__restric
   }
 }
 
-// ---------------------------------------------------------------- finalisation folded into the elementwise pass
-// k_bnl_apply_fin / k_bnl_bwd_apply_fin: one launch instead of k_bn_finalize + k_bnl_(bwd_)apply.  The first C
-// workgroups to arrive (an atomic ticket, so they are running) each finalise one channel from the partials and
-// publish its constants with write-through (sc1) stores, a drained vmcnt and an agent-scope atomic add on a
-// ready counter; every workgroup's thread 0 polls that counter with sc1 loads, the workgroup meets at a barrier,
-// and reads the constants with sc1 loads (MI355X_MICROARCH.md, visibility table: counter row); the last workgroup
-// to leave zeroes the counters for the next launch on that slot.  Each call site uses its own counter slot
-// (host-assigned, so concurrent streams never share one).  The poll is bounded: a launch that never sees every
-// channel published (cannot happen while the grid >= C) counts an error (gmz_bn_sync_errors) and proceeds.
-constexpr int BN_SYNC_SLOTS = 4096;
-__device__ unsigned g_bn_sync[BN_SYNC_SLOTS][4];  // {ticket, ready, done, -}; zero at load, zero after every launch
-__device__ unsigned g_bn_sync_err;
+// threads per channel of k_bn_finalize: 4 waves (one wave: noise-level slower, round 4)
+static int fin_threads() { return WAVE * FIN_MAX_WAVES; }
 
-__device__ __forceinline__ void st_sc1(float *p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-__device__ __forceinline__ float ld_sc1(const float *p) {
-  return __hip_atomic_load(const_cast<float *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// this workgroup's ticket; tk < C: finalise channel tk from parts [C][ns][3] -> (a, b, n) in thread 0
-__device__ __forceinline__ int fin_ticket(unsigned *sync) {
-  __shared__ int s_tk;
-  if (threadIdx.x == 0) s_tk = (int)atomicAdd(&sync[0], 1u);
-  __syncthreads();
-  return s_tk;
-}
-__device__ __forceinline__ void fin_sums(const double *__restrict__ parts, int c, int ns, double &a, double &b,
-                                         double &n) {
-  __shared__ double red[BN_THREADS / WAVE][3];
-  a = b = n = 0.0;
-#pragma unroll 2
-  for (int t = threadIdx.x; t < ns; t += BN_THREADS) {
-    const double *p = parts + ((size_t)c * ns + t) * 3;
-    a += p[0];
-    b += p[1];
-    n += p[2];
-  }
-  a = wave_sum_d(a);
-  b = wave_sum_d(b);
-  n = wave_sum_d(n);
-  const int w = threadIdx.x / WAVE;
-  if ((threadIdx.x & (WAVE - 1)) == 0) {
-    red[w][0] = a;
-    red[w][1] = b;
-    red[w][2] = n;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0)
-    for (int i = 1; i < BN_THREADS / WAVE; ++i) {
-      a += red[i][0];
-      b += red[i][1];
-      n += red[i][2];
-    }
-}
-// thread 0, after its sc1 stores: publish; then every workgroup waits for C published channels
-__device__ __forceinline__ void fin_publish(unsigned *sync) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  atomicAdd(&sync[1], 1u);
-}
-__device__ __forceinline__ void fin_wait(unsigned *sync, int C) {
-  if (threadIdx.x == 0) {
-    int spins = 0;
-    while (__hip_atomic_load(&sync[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)C) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins > (1 << 22)) {  // ~0.3 s: never while the grid >= C; no hang either way
-        atomicAdd(&g_bn_sync_err, 1u);
-        break;
-      }
-    }
-  }
-  __syncthreads();
-}
-__device__ __forceinline__ void fin_leave(unsigned *sync) {
-  if (threadIdx.x == 0 && atomicAdd(&sync[2], 1u) == gridDim.x - 1) {
-    atomicExch(&sync[0], 0u);
-    atomicExch(&sync[1], 0u);
-    atomicExch(&sync[2], 0u);
-  }
-}
-
-template <typename T, int V>
-__global__ void __launch_bounds__(BN_THREADS) k_bnl_apply_fin(const T *__restrict__ x, const T *__restrict__ res, long P,
-                                                              int C, const float *__restrict__ gamma,
-                                                              const float *__restrict__ beta, int relu,
-                                                              T *__restrict__ y, float *save,
-                                                              const double *__restrict__ parts, int ns, float eps,
-                                                              float momentum, float *running_mean, float *running_var,
-                                                              int64_t *num_batches, unsigned *sync) {
-  const int tk = fin_ticket(sync);
-  if (tk < C) {  // k_bn_finalize's forward branch for channel tk
-    double a, b, n;
-    fin_sums(parts, tk, ns, a, b, n);
-    if (threadIdx.x == 0) {
-      const double nn = n > 0.0 ? n : 1.0;
-      const double m = a / nn;
-      double v = b / nn - m * m;
-      v = v > 0.0 ? v : 0.0;
-      const float mean = (float)m, var_b = (float)v;
-      st_sc1(save + tk, mean);
-      st_sc1(save + C + tk, 1.0f / sqrtf(var_b + eps));
-      if (n > 0.0 && running_mean) {
-        const float unb = (float)(v * n / (n > 1.0 ? n - 1.0 : 1.0));
-        running_mean[tk] = (1.0f - momentum) * running_mean[tk] + momentum * mean;
-        running_var[tk] = (1.0f - momentum) * running_var[tk] + momentum * unb;
-        if (tk == 0 && num_batches) num_batches[0] += 1;
-      }
-      fin_publish(sync);
-    }
-  }
-  fin_wait(sync, C);
-  const int tpp = C / V, pl = BN_THREADS / tpp;
-  const int cp = threadIdx.x % tpp, grp = threadIdx.x / tpp;
-  if (grp < pl) {
-    const int c = V * cp;
-    float sc[V], sh[V], mean[V];
-#pragma unroll
-    for (int j = 0; j < V; ++j) {
-      mean[j] = ld_sc1(save + c + j);
-      sc[j] = gamma[c + j] * ld_sc1(save + C + c + j);
-      sh[j] = beta[c + j];
-    }
-    for (long p = (long)blockIdx.x * pl + grp; p < P; p += (long)gridDim.x * pl) {
-      const size_t k = (size_t)p * C + c;
-      float v[V], r[V];
-      ldv<T, V>(x, k, v);
-      if (res) ldv<T, V>(res, k, r);
-#pragma unroll
-      for (int j = 0; j < V; ++j) {
-        v[j] = (v[j] - mean[j]) * sc[j] + sh[j];
-        if (res) v[j] += r[j];
-        if (relu) v[j] = fmaxf(v[j], 0.f);
-      }
-      stv<T, V>(y, k, v);
-    }
-  }
-  fin_leave(sync);
-}
-
-template <typename T, int V>
-__global__ void __launch_bounds__(BN_THREADS) k_bnl_bwd_apply_fin(const T *__restrict__ x, const T *__restrict__ y,
-                                                                  const T *__restrict__ dy,
-                                                                  const uint8_t *__restrict__ mask, long P, int C, int S,
-                                                                  const float *__restrict__ gamma,
-                                                                  const float *__restrict__ save, int relu,
-                                                                  T *__restrict__ dx, T *__restrict__ dres, float *coef,
-                                                                  const double *__restrict__ parts, int ns, int backward,
-                                                                  float *dgamma, float *dbeta, unsigned *sync) {
-  const int tk = fin_ticket(sync);
-  if (tk < C) {  // k_bn_finalize's backward branch for channel tk
-    double a, b, n;
-    fin_sums(parts, tk, ns, a, b, n);
-    if (threadIdx.x == 0) {
-      if (backward == 2) {
-        dgamma[tk] += (float)b;
-        dbeta[tk] += (float)a;
-      } else {
-        dgamma[tk] = (float)b;
-        dbeta[tk] = (float)a;
-      }
-      st_sc1(coef + tk, n > 0.0 ? (float)(a / n) : 0.0f);
-      st_sc1(coef + C + tk, n > 0.0 ? (float)(b / n) : 0.0f);
-      fin_publish(sync);
-    }
-  }
-  fin_wait(sync, C);
-  const int tpp = C / V, pl = BN_THREADS / tpp;
-  const int cp = threadIdx.x % tpp, grp = threadIdx.x / tpp;
-  if (grp < pl) {
-    const int c = V * cp;
-    float mean[V], is[V], mg[V], mgx[V], k1[V];
-#pragma unroll
-    for (int j = 0; j < V; ++j) {
-      mean[j] = save[c + j];
-      is[j] = save[C + c + j];
-      mg[j] = ld_sc1(coef + c + j);
-      mgx[j] = ld_sc1(coef + C + c + j);
-      k1[j] = gamma[c + j] * is[j];
-    }
-    for (long p = (long)blockIdx.x * pl + grp; p < P; p += (long)gridDim.x * pl) {
-      const size_t k = (size_t)p * C + c;
-      const bool in = !mask || mask[p / S];
-      float g[V], d[V];
-      ldv<T, V>(dy, k, g);
-      if (relu) {
-        float yv[V];
-        ldv<T, V>(y, k, yv);
-#pragma unroll
-        for (int j = 0; j < V; ++j)
-          if (!(yv[j] > 0.f)) g[j] = 0.f;
-      }
-      if (dres) stv<T, V>(dres, k, g);
-      if (in) {
-        float xv[V];
-        ldv<T, V>(x, k, xv);
-#pragma unroll
-        for (int j = 0; j < V; ++j) d[j] = g[j] - mg[j] - (xv[j] - mean[j]) * is[j] * mgx[j];
-      } else {
-#pragma unroll
-        for (int j = 0; j < V; ++j) d[j] = g[j];
-      }
-#pragma unroll
-      for (int j = 0; j < V; ++j) d[j] *= k1[j];
-      stv<T, V>(dx, k, d);
-    }
-  }
-  fin_leave(sync);
-}
-
-// the fused finalisation: OFF by default (GMZ_BN_FUSED_FIN=1 turns it on, for A/B).  Measured (round 5, eager op
-// census, 15x15, B = 360): the fused forward pass 57 us and the fused backward pass 62 us per launch against
-// 9.5 + 4.8 us and 14.6 + 4.8 us as two launches — the ~1,100 workgroups that wait poll one ready counter with
-// write-through loads while the 128 finalisers' atomic adds hit the same line; the saved launch costs far less
-static bool fused_fin() {
-  static int v = -1;
-  if (v < 0) {
-    const char *e = getenv("GMZ_BN_FUSED_FIN");
-    v = (e && atoi(e) == 1) ? 1 : 0;
-  }
-  return v == 1;
-}
-static unsigned *next_sync_slot() {
-  static unsigned next = 0;
-  static unsigned *base = nullptr;  // looked up once (the first BatchNorm runs eagerly, before any graph capture)
-  if (!base && (hipGetSymbolAddress((void **)&base, HIP_SYMBOL(g_bn_sync)) != hipSuccess || !base)) {
-    base = nullptr;
-    return nullptr;
-  }
-  return base + (size_t)(next++ % BN_SYNC_SLOTS) * 4;
-}
-int elementwise_blocks(long P, int C, int V);
-// the fused launch's grid: the elementwise pass's, and at least C workgroups (one finaliser per channel)
-static int fin_blocks(long P, int C, int V) {
-  const int nb = elementwise_blocks(P, C, V);
-  return nb < C ? C : nb;
-}
-
-// threads per channel of k_bn_finalize: 256 (GMZ_BN_FIN_THREADS=64: the one-wave version, for A/B)
-static int fin_threads() {
-  static int t = 0;
-  if (!t) {
-    const char *e = getenv("GMZ_BN_FIN_THREADS");
-    const int v = e ? atoi(e) : WAVE * FIN_MAX_WAVES;
-    t = (v == WAVE || v == 2 * WAVE || v == 4 * WAVE) ? v : WAVE * FIN_MAX_WAVES;
-  }
-  return t;
-}
-
-// NHWC reduction splits cap (GMZ_BNL_SPLITS: an A/B of 256 .. 4096; default BNL_MAX_SPLITS)
-static int bnl_split_cap() {
-  static int c = 0;
-  if (!c) {
-    const char *e = getenv("GMZ_BNL_SPLITS");
-    const int v = e ? atoi(e) : BNL_MAX_SPLITS;
-    c = (v >= 64 && v <= 4096) ? v : BNL_MAX_SPLITS;
-  }
-  return c;
-}
+// NHWC reduction splits cap (256 .. 4096 measured, profiles/r05_bn_splits_ab.txt)
+static int bnl_split_cap() { return BNL_MAX_SPLITS; }
 
 int splits_for(int B, int C, int S, int nhwc) {
   // NCHW: (C x ns) workgroups, enough to cover the 256 CUs (>= ~2048), never more splits than rows;
@@ -848,18 +595,10 @@ int splits_for(int B, int C, int S, int nhwc) {
 
 size_t ws_doubles(int B, int C, int S, int nhwc) { return (size_t)C * splits_for(B, C, S, nhwc) * 3; }
 
-// NHWC elementwise grid: ~2 position steps per thread, at most 16,384 workgroups (GMZ_BN_EW_STEPS: 1, 2, 4 or 8,
-// an A/B; trainer 40.59 / 40.64 steps/s at 2 vs 39.84 / 40.09 at 4 and 39.70 / 39.99 at 1,
-// profiles/r05_bn_ew_steps_ab.txt — the 1,800-board consistency BatchNorms gain from the larger grid)
-static int ew_steps() {
-  static int k = 0;
-  if (!k) {
-    const char *e = getenv("GMZ_BN_EW_STEPS");
-    const int v = e ? atoi(e) : 2;
-    k = (v == 1 || v == 2 || v == 4 || v == 8) ? v : 2;
-  }
-  return k;
-}
+// NHWC elementwise grid: ~2 position steps per thread, at most 16,384 workgroups (trainer 40.59 / 40.64 steps/s at 2
+// vs 39.84 / 40.09 at 4 and 39.70 / 39.99 at 1, profiles/r05_bn_ew_steps_ab.txt — the 1,800-board consistency
+// BatchNorms gain from the larger grid)
+static int ew_steps() { return 2; }
 
 int elementwise_blocks(long P, int C, int V) {
   const long pl = BN_THREADS / (C / V), k = ew_steps();
@@ -894,22 +633,6 @@ int bn_forward(int nhwc, const void *x, const void *res, const uint8_t *mask, in
                        (double *)ws);
   }
   GMZ_LAUNCH_CHECK();
-  if (nhwc) {
-    unsigned *sync = (fused_fin() && !rmask) ? next_sync_slot() : nullptr;
-    if (sync) {
-      const long P = (long)B * S;
-      if (V == 8)
-        hipLaunchKernelGGL((k_bnl_apply_fin<T, 8>), dim3(fin_blocks(P, C, 8)), dim3(BN_THREADS), 0, st, (const T *)x,
-                           (const T *)res, P, C, gamma, beta, relu, (T *)y, save, (const double *)ws, ns, eps, momentum,
-                           rm, rv, nb, sync);
-      else
-        hipLaunchKernelGGL((k_bnl_apply_fin<T, 2>), dim3(fin_blocks(P, C, 2)), dim3(BN_THREADS), 0, st, (const T *)x,
-                           (const T *)res, P, C, gamma, beta, relu, (T *)y, save, (const double *)ws, ns, eps, momentum,
-                           rm, rv, nb, sync);
-      GMZ_LAUNCH_CHECK();
-      return 0;
-    }
-  }
   hipLaunchKernelGGL(k_bn_finalize, dim3(C), dim3(fin_threads()), 0, st, (const double *)ws, C, ns, ns, 1, 0, eps,
                      momentum, save, rm, rv, nb, (float *)nullptr, (float *)nullptr, (float *)nullptr);
   GMZ_LAUNCH_CHECK();
@@ -949,22 +672,6 @@ int bn_backward(int nhwc, const void *x, const void *y, const void *dy, const ui
                        (const T *)dy, mask, B, C, S, save, relu, (double *)ws);
   }
   GMZ_LAUNCH_CHECK();
-  if (nhwc) {
-    unsigned *sync = (fused_fin() && !rmask) ? next_sync_slot() : nullptr;
-    if (sync) {
-      const long P = (long)B * S;
-      if (V == 8)
-        hipLaunchKernelGGL((k_bnl_bwd_apply_fin<T, 8>), dim3(fin_blocks(P, C, 8)), dim3(BN_THREADS), 0, st,
-                           (const T *)x, (const T *)y, (const T *)dy, mask, P, C, S, gamma, save, relu, (T *)dx,
-                           (T *)dres, coef, (const double *)ws, ns, accumulate ? 2 : 1, dgamma, dbeta, sync);
-      else
-        hipLaunchKernelGGL((k_bnl_bwd_apply_fin<T, 2>), dim3(fin_blocks(P, C, 2)), dim3(BN_THREADS), 0, st,
-                           (const T *)x, (const T *)y, (const T *)dy, mask, P, C, S, gamma, save, relu, (T *)dx,
-                           (T *)dres, coef, (const double *)ws, ns, accumulate ? 2 : 1, dgamma, dbeta, sync);
-      GMZ_LAUNCH_CHECK();
-      return 0;
-    }
-  }
   hipLaunchKernelGGL(k_bn_finalize, dim3(C), dim3(fin_threads()), 0, st, (const double *)ws, C, ns, ns, 1,
                      accumulate ? 2 : 1, 0.f, 0.f, (float *)nullptr, (float *)nullptr, (float *)nullptr,
                      (int64_t *)nullptr, dgamma, dbeta, coef);
@@ -1017,20 +724,6 @@ int bn_forward_stats(const void *x, const void *res, int B, int C, int S, const 
                      const double *stats, int ns, hipStream_t st, uint8_t *rmask = nullptr) {
   if (rmask && nhwc_vec(C, sizeof(T), {x, res, y}) != 8)
     return fail("gmz_bn: relu_mask needs channels-last 16-B aligned operands with C % 8 == 0");
-  if (unsigned *sync = (fused_fin() && !rmask) ? next_sync_slot() : nullptr) {
-    const int V = nhwc_vec(C, sizeof(T), {x, res, y});
-    const long P = (long)B * S;
-    if (V == 8)
-      hipLaunchKernelGGL((k_bnl_apply_fin<T, 8>), dim3(fin_blocks(P, C, 8)), dim3(BN_THREADS), 0, st, (const T *)x,
-                         (const T *)res, P, C, gamma, beta, relu, (T *)y, save, stats, ns, eps, momentum, rm, rv, nb,
-                         sync);
-    else
-      hipLaunchKernelGGL((k_bnl_apply_fin<T, 2>), dim3(fin_blocks(P, C, 2)), dim3(BN_THREADS), 0, st, (const T *)x,
-                         (const T *)res, P, C, gamma, beta, relu, (T *)y, save, stats, ns, eps, momentum, rm, rv, nb,
-                         sync);
-    GMZ_LAUNCH_CHECK();
-    return 0;
-  }
   hipLaunchKernelGGL(k_bn_finalize, dim3(C), dim3(fin_threads()), 0, st, stats, C, ns, ns, 1, 0, eps, momentum, save, rm,
                      rv, nb, (float *)nullptr, (float *)nullptr, (float *)nullptr);
   GMZ_LAUNCH_CHECK();
@@ -1322,16 +1015,6 @@ GMZ_EXPORT int gmz_bn_backward(int dtype, int layout, const void *x, const void 
                                void *stream) {
   return gmz_bn_backward_acc(dtype, layout, x, y, dy, mask, B, C, S, gamma, save, relu, dx, dres, dgamma, dbeta, ws,
                              ws_bytes, stream, 0);
-}
-
-GMZ_EXPORT int gmz_bn_sync_errors(uint32_t *out, int reset) {
-  if (!out) return fail("gmz_bn_sync_errors: null argument");
-  unsigned *d = nullptr;
-  GMZ_HIP(hipGetSymbolAddress((void **)&d, HIP_SYMBOL(g_bn_sync_err)));
-  GMZ_HIP(hipDeviceSynchronize());
-  GMZ_HIP(hipMemcpy(out, d, sizeof(unsigned), hipMemcpyDeviceToHost));
-  if (reset) GMZ_HIP(hipMemset(d, 0, sizeof(unsigned)));
-  return 0;
 }
 
 GMZ_EXPORT int gmz_bn_forward_seg(int dtype, const void *x, const void *res, const uint8_t *mask, int B, int nseg, int C,

@@ -2234,6 +2234,12 @@ GMZ_EXPORT int gmz_engine_set_hidden_budget(gmz_engine *e, const int32_t *budget
   return 0;
 }
 
+GMZ_EXPORT int gmz_engine_errors_async(gmz_engine *e, int32_t *dst, void *stream) {
+  if (!e || !dst) return fail("gmz_engine_errors_async: null argument");
+  GMZ_HIP(hipMemcpyAsync(dst, e->D.err, sizeof(int32_t), hipMemcpyDefault, (hipStream_t)stream));
+  return 0;
+}
+
 GMZ_EXPORT int gmz_engine_errors(gmz_engine *e, int32_t *out, int reset) {
   if (!e || !out) return fail("gmz_engine_errors: null argument");
   GMZ_HIP(hipDeviceSynchronize());

@@ -21,7 +21,7 @@ import torch
 
 from . import _lib
 from .config import from_any
-from ._lib import check, ptr
+from ._lib import GmzError, check, ptr
 
 
 class HashNetBackend:
@@ -132,6 +132,7 @@ class BatchedSelfPlayEngine:
         self.action = torch.zeros(G, dtype=i32, device=dev)
         self.status = torch.zeros(G, dtype=torch.int8, device=dev)
         self._status_host = torch.zeros(G, dtype=torch.int8).pin_memory()
+        self._err_host = torch.zeros(1, dtype=i32).pin_memory()  # the engine's error word, copied with each status
         self._status_event = None
         self._n_legal = np.full(G, A, dtype=np.int32)
         self._last_reset = True
@@ -195,6 +196,10 @@ class BatchedSelfPlayEngine:
     def _sync_status(self):
         if self._status_event is not None:
             self._status_event.synchronize()
+            err = int(self._err_host[0])
+            if err:  # a void search must not reach self-play records or the replay buffer
+                raise GmzError("engine error bits 0x%x after the last move: a search passed its game's hidden-state "
+                               "slot budget, so that game's search result is void (gmz_engine_errors)" % err)
             st = self._status_host.numpy()
             ended = st != 2
             played = st != 3
@@ -313,6 +318,7 @@ class BatchedSelfPlayEngine:
         a = self.action if action is None else torch.as_tensor(action, dtype=torch.int32).to(self.device)
         check(self.lib.gmz_engine_play(self.handle, ptr(a), ptr(self.status), 1 if reset_finished else 0, s))
         self._status_host.copy_(self.status, non_blocking=True)
+        check(self.lib.gmz_engine_errors_async(self.handle, ptr(self._err_host), s))
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream() if stream is None else stream)
         self._status_event = ev

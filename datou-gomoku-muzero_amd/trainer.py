@@ -1535,9 +1535,20 @@ def _bn_steps(mod, x, ms, update=True, pre=None):
         if pre is None:
             _bn_running_update(mod, [st])
         else:  # interleaved: pre's step s, then this call's step s
+            ps = pre[1] if pre[0] == "torch" else _seg_stats_as_torch(pre[1], nseg, x.shape[1])
             _bn_running_update(mod, [tuple(torch.stack((a, b), 1).reshape(2 * nseg, *a.shape[1:])
-                                           for a, b in zip(pre[1], st))])
+                                           for a, b in zip(ps, st))])
     return y, ("torch", st)
+
+
+def _seg_stats_as_torch(flat, nseg, C):
+    """A _SegBN handle's flat statistics [mean | invstd | unbiased var | live count] (gmz_seg_bn_forward) as the
+    (mean [nseg, C], unbiased var [nseg, C], ok [nseg]) tuple of _bn_seg_grad: when the dynamics projection's call
+    took the HIP kernel and the targets' call cannot, the interleaved running-statistics update still gets
+    (mean, var, ok) per step."""
+    f = flat.reshape(-1)
+    n = nseg * C
+    return f[:n].view(nseg, C), f[2 * n:3 * n].view(nseg, C), f[3 * n:3 * n + nseg] > 0
 
 
 def _bn_running_update(mod, stats):
@@ -1724,6 +1735,11 @@ def muzero_loss(model, target_model, batch, is_weights, cfg, k=None, flip=None, 
                 elif side is not None:
                     main.wait_event(tru_ev[-1])
                 th = getattr(tru_h, "stacked", None)
+                if side is not None:
+                    # every per-step state made on side[1] is consumed on main (by the cat, or as th itself): each
+                    # is recorded on main so none returns to side[1]'s pool while main's use is still queued
+                    for t in tru_h:
+                        t.record_stream(main)
                 if th is None:
                     th = tru_h[0] if len(tru_h) == 1 else torch.cat(tru_h)
                 if side is not None:
@@ -2018,7 +2034,7 @@ class Trainer:
         for p in layout:
             p.grad = self.flat_grad[off:off + p.numel()].as_strided(p.shape, p.stride())  # same layout as p
             off += p.numel()
-        self.comm_events = []  # (start, end) CUDA events around each step's all-reduce window (N > 1)
+        self.comm_events = []  # [A issued, B's weight gradients done, both averaged] CUDA events per step (N > 1)
         cuda = self.device.type == "cuda"
         lr = torch.tensor(c.LEARNING_RATE, device=self.device) if cuda else c.LEARNING_RATE
         self.opt = torch.optim.Adam(self.params, lr=lr, weight_decay=c.WEIGHT_DECAY,
@@ -2067,8 +2083,15 @@ class Trainer:
         if self.device.type == "cuda":
             ev = torch.cuda.Event(enable_timing=True)
             ev.record()
-            self.comm_events.append([ev, None])
+            self.comm_events.append([ev, None, None])
         return self.dist.all_reduce(self.flat_grad[:self._bucket_a], async_op=True)
+
+    def _mark_flushed(self):
+        """Bucket B's weight gradients are enqueued (the compute stream's work between A's issue and B's)."""
+        if self.dist is not None and self.device.type == "cuda" and self.comm_events:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            self.comm_events[-1][1] = ev
 
     def _allreduce_finish(self, work):
         """Bucket B's all-reduce (its gradients are final once flush_wgrads ran), then both buckets averaged."""
@@ -2081,21 +2104,32 @@ class Trainer:
         if self.device.type == "cuda" and self.comm_events:
             ev = torch.cuda.Event(enable_timing=True)
             ev.record()
-            self.comm_events[-1][1] = ev
+            self.comm_events[-1][2] = ev
             del self.comm_events[:-64]
 
     def _allreduce(self):
         if self.dist is not None:  # data parallel: the two buckets' all-reduces (RCCL), A's issued first
-            self._allreduce_finish(self._allreduce_start())
+            work = self._allreduce_start()
+            self._mark_flushed()
+            self._allreduce_finish(work)
 
-    def allreduce_ms(self):
-        """Mean time (ms) of the recent steps' all-reduce windows on the compute stream: from bucket A's issue (the
-        backward done) to both buckets averaged — with bucket B's weight gradients computed inside it (N > 1)."""
-        done = [(a, b) for a, b in self.comm_events if b is not None]
+    def allreduce_times(self):
+        """Mean per-step times (ms) on the compute stream over the recent steps (N > 1; None before any):
+        ``flush_ms`` from bucket A's all-reduce issue (the backward done) to bucket B's weight gradients enqueued — the
+        work A's communication overlaps; ``wait_ms`` from there to both buckets averaged — bucket B's all-reduce and
+        whatever of A's did not hide under the flush: the exposed communication; ``window_ms`` the sum."""
+        done = [e for e in self.comm_events if e[2] is not None and e[1] is not None]
         if not done:
             return None
-        done[-1][1].synchronize()
-        return sum(a.elapsed_time(b) for a, b in done) / len(done)
+        done[-1][2].synchronize()
+        flush = sum(a.elapsed_time(b) for a, b, _ in done) / len(done)
+        wait = sum(b.elapsed_time(c) for _, b, c in done) / len(done)
+        return {"flush_ms": flush, "wait_ms": wait, "window_ms": flush + wait}
+
+    def allreduce_ms(self):
+        """The exposed communication per step (``allreduce_times()['wait_ms']``), None without a process group."""
+        t = self.allreduce_times()
+        return None if t is None else t["wait_ms"]
 
     def _update(self):
         c = self.cfg
@@ -2169,6 +2203,7 @@ class Trainer:
             if g2 is not None:
                 work = self._allreduce_start()
                 gf.replay()
+                self._mark_flushed()
                 self._allreduce_finish(work)
                 g2.replay()
             logs, td = self._out
@@ -2181,6 +2216,7 @@ class Trainer:
             if overlap:  # bucket A's all-reduce beside bucket B's weight gradients
                 work = self._allreduce_start()
                 self._flush()
+                self._mark_flushed()
                 self._allreduce_finish(work)
             if last:
                 self._update()

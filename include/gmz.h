@@ -130,6 +130,9 @@ int gmz_engine_set_hidden_budget(gmz_engine *e, const int32_t *budget_dev, void 
 /* Sticky error bits of the engine's kernels into *out (synchronises the device); reset != 0 clears them.
  * Bit 0: a hidden-state slot past a game's budget (gmz_engine_set_hidden_budget).  (ABI 8) */
 int gmz_engine_errors(gmz_engine *e, int32_t *out, int reset);
+/* The same error word copied stream-ordered (no synchronisation) to dst (host-pinned or device int32): the engine
+ * checks it once per move, where it already waits for the previous move's status (engine.py).  (ABI 10) */
+int gmz_engine_errors_async(gmz_engine *e, int32_t *dst, void *stream);
 /* Step 3 (mcts.py:326-336 / 233-253): one wave.  For each game with an unfinished search:
  * descend to the leaf, allocate its node, and emit the network request
  *   MuZero:    in_slot_dev[g] = hbase[g] + parent node, action_dev[g] = leaf action,
@@ -337,11 +340,6 @@ int gmz_bn_backward_acc_m(int dtype, int layout, const void *x_dev, const void *
                           const uint8_t *mask_dev, int B, int C, int S, const float *gamma_dev, const float *save_dev,
                           int relu, void *dx_dev, void *dres_dev, float *dgamma_dev, float *dbeta_dev,
                           void *workspace_dev, size_t ws_bytes, const uint8_t *relu_mask_dev, void *stream, int accumulate);
-/* Launches of the fused BatchNorm finalisation (the channels-last apply passes with GMZ_BN_FUSED_FIN=1; default: the
- * separate finalisation launch, measured faster) whose bounded wait for every channel's published constants ran
- * out: must stay 0.
- * Synchronises the device; reset != 0 clears the count.  (ABI 8) */
-int gmz_bn_sync_errors(uint32_t *out, int reset);
 /* Training-mode channels-last BatchNorm (+ res, ReLU) of nseg equal row segments at once (the trainer's batched
  * consistency representations, loss.py:102-104): segment g = rows [g B/nseg, (g+1) B/nseg), its statistics over
  * its own masked rows, save_dev f32 [nseg][2][C] = per segment (mean, invstd), the running statistics updated by
