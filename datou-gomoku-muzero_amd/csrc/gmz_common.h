@@ -24,6 +24,24 @@ int fail(const std::string &msg);  // set_error + return -1
 #define GMZ_LAUNCH_CHECK() GMZ_HIP(hipGetLastError())
 
 constexpr int WAVE = 64;
+
+// The 3x3 taps (bit t = tap (t / 3, t % 3), offsets (t / 3 - 1, t % 3 - 1)) that reach at least one in-board cell
+// from some position of the global range [g0, g1) of a run of H x H boards (global index g -> position g % (H*H)).
+// A conv tile holding only such positions multiplies the zero border at every other tap: the towers and the
+// trainer's conv skip those k-steps (their MFMAs and B-fragment reads) for the boards' last tile, which holds only
+// the bottom-right corner cell at 15x15 (taps 0, 1, 3, 4: 16 of 36 k-steps) and two bottom-row cells in the packed
+// 9x9 run (taps 0-5: 24 of 36).
+__host__ __device__ constexpr unsigned live_taps(int H, int g0, int g1) {
+  unsigned m = 0;
+  for (int g = g0; g < g1; ++g) {
+    const int p = g % (H * H), y = p / H, x = p % H;
+    for (int t = 0; t < 9; ++t) {
+      const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
+      if (yy >= 0 && yy < H && xx >= 0 && xx < H) m |= 1u << t;
+    }
+  }
+  return m;
+}
 constexpr int MAX_A = 512;              // board_size <= 22
 constexpr int NJ = MAX_A / WAVE;        // actions per lane
 constexpr int MAX_TOP = 64;             // num_top_actions <= 64

@@ -149,6 +149,11 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
   constexpr int NTW = 2, PTW = (NPT + PG - 1) / PG, RD = GMZ_CONV_RD, NW = 2 * PG, NTHR = 64 * NW;
   constexpr int PS = I::PS, RS = I::RS;
   static_assert(CKSTEPS % RD == 0, "ring slots repeat per item");
+  // the board's last tile (15x15: the corner cell alone) skips the k-steps whose tap reaches only the zero border
+  // (gmz_common.h live_taps); only the PTW-tile k-loop holds it when NPT = PG (PTW - 1) + 1
+  constexpr bool LAST_ONE = NPT == PG * (PTW - 1) + 1;
+  constexpr unsigned LAST_TAPS = LAST_ONE ? live_taps(H, (NPT - 1) * 16, A) : 0x1ffu;
+  static_assert(LAST_TAPS & 1u, "tap 0 of the last tile starts its accumulation");
   __shared__ __attribute__((aligned(16))) uint8_t img[I::BYTES];
   static_assert(I::BYTES >= PG * 64 * 2 * 4, "stats scratch fits in the image");
   static_assert(!PB || (HALVES == 1 && !BWD), "per-board statistics: forward sums, one half per workgroup");
@@ -259,11 +264,13 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
     auto kloop = [&](auto ntl_c) {
       constexpr int NTL = decltype(ntl_c)::value;
       V bf[2][NTL];
+      auto live = [&](int i, int st) { return !(LAST_ONE && NTL == PTW && i == NTL - 1) || ((LAST_TAPS >> (st >> 2)) & 1u); };
       auto readB = [&](int buf, int st) {
         const int tap = st >> 2, ks = st & 3;
         const int off = (tap / 3) * RS + (tap % 3) * PS + ks * 32;
 #pragma unroll
-        for (int i = 0; i < NTL; ++i) bf[buf][i] = *(const V *)(img + bb[i] + off);
+        for (int i = 0; i < NTL; ++i)
+          if (live(i, st)) bf[buf][i] = *(const V *)(img + bb[i] + off);
       };
       readB(0, 0);
 #pragma unroll
@@ -277,6 +284,7 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int i = 0; i < NTL; ++i)
+          if (live(i, st))
 #pragma unroll
           for (int nt = 0; nt < NTW; ++nt) {
             if constexpr ((GMZ_CONV_ABL & 4) != 0) {  // ablation: operands consumed by one VALU op, no MFMA

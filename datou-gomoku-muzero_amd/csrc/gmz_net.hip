@@ -188,6 +188,12 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
   constexpr int NW = NQ * PG, NTHR = 64 * NW;       // waves: NQ channel groups x PG position groups
   constexpr int NTW = 8 / NQ, PTW = (NPTB + PG - 1) / PG;  // n-tiles / position tiles per wave
   static_assert(8 % NQ == 0, "channel groups");
+  // LAST_ONE: only the k-loop instantiated for PTW tiles (NTL == PTW) holds the tile space's last tile, as its tile
+  // PTW - 1 (one wave group's short slot: NPTB = PG (PTW - 1) + 1; 15x15: tile 14 = the corner cell alone, packed
+  // 9x9: tile 10 = two bottom-row cells).  That tile skips the k-steps of the taps that reach only the zero border.
+  constexpr bool LAST_ONE = !PIPE && NPTB == PG * (PTW - 1) + 1;
+  constexpr unsigned LAST_TAPS = LAST_ONE ? live_taps(H, (NPTB - 1) * 16, NB * A < NPTB * 16 ? NB * A : NPTB * 16) : 0x1ffu;
+  static_assert(LAST_TAPS & 1u, "tap 0 of the last tile starts its accumulation");
   constexpr int PS = I::PS, RS = I::RS, IMG = I::BYTES;
   constexpr int KSTEPS = 36;  // 9 taps x 4 k-steps of 32 input channels
   // two images when they fit (15x15: 2 x 78 KB); otherwise (19x19: 119 KB) ONE image, an extra
@@ -502,11 +508,16 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
 #pragma unroll
           for (int nt = 0; nt < NTW; ++nt) acc[nt][i] = bv[nt];  // the empty slot (never stored)
         V8 b[2][NTL];
+        // tile i's k-step st multiplies in-board cells (LAST_TAPS; compile-time once the loops are unrolled)
+        auto live = [&](int i, int st) {
+          return !(LAST_ONE && NTL == PTW && i == NTL - 1) || ((LAST_TAPS >> (st >> 2)) & 1u);
+        };
         auto readB = [&](int buf, int st) {
           const int tap = PP ? (st < 18 ? st : st - 18) >> 1 : st >> 2, ks = PP ? (st & 1) : st & 3;
           const int off = (tap / 3) * RS + (tap % 3) * PS + ks * 32;
 #pragma unroll
-          for (int i = 0; i < NTL; ++i) b[buf][i] = *(const V8 *)(smem + bb[i] + off);
+          for (int i = 0; i < NTL; ++i)
+            if (PP || live(i, st)) b[buf][i] = *(const V8 *)(smem + bb[i] + off);
         };
         readB(0, 0);
         if constexpr (PP) {
@@ -548,9 +559,10 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
           for (int i = 0; i < NTL; ++i)
+            if (live(i, st))
 #pragma unroll
-            for (int nt = 0; nt < NTW; ++nt)
-              acc[nt][i] = E::mfma(ar[st % RD][nt], b[st & 1][i], st == 0 ? bv[nt] : acc[nt][i]);
+              for (int nt = 0; nt < NTW; ++nt)
+                acc[nt][i] = E::mfma(ar[st % RD][nt], b[st & 1][i], st == 0 ? bv[nt] : acc[nt][i]);
           // the last k-step stays open: the scheduler may start the epilogue of the tiles whose final
           // MFMA has issued while the remaining ones run (ABL & 256 pins it, for comparison)
           if ((ABL & 256) || st + 1 < KSTEPS) __builtin_amdgcn_sched_barrier(0);
