@@ -89,6 +89,35 @@ def tree_bytes(ctr, A):
             + 20 * A * (ctr["select_levels"] - ctr["selects"]) + 8 * ctr["select_levels"])
 
 
+def backup_bytes(ctr, A):
+    """The backup phase's share of tree_bytes: the leaf's expansion (24A + 16 per game-wave) and 24 B per level backed
+    up (mcts.py:119-138, the north-star 'backup kernel')."""
+    return ctr["backups"] * (24 * A + 16) + 24 * ctr["backup_levels"]
+
+
+BACKUP_SPLIT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r06_tree_backup_split.json")
+
+
+def backup_roofline(ctr, A, n_launch, busy_ms, G):
+    """roofline_tree.backup: the north-star backup kernel inside the fused launch.  k_expand_select runs the backup
+    of wave i and the selection of wave i+1 in one launch, so the backup's time is its measured share of the launch's
+    cycles (s_memtime phase stamps per game-wave, tools/tree_backup_split.py with a -DGMZ_TREE_PROF build, committed
+    as profiles/r06_tree_backup_split.json; builder-measured) times this run's busy time."""
+    try:
+        sp = json.load(open(BACKUP_SPLIT)).get("G%d" % G)
+    except Exception:
+        sp = None
+    if not sp or n_launch <= 0 or busy_ms <= 0 or A != 225:
+        return None
+    b = backup_bytes(ctr, A)
+    t = sp["backup_share"] * busy_ms * 1e-3
+    gbs = b / t / 1e9
+    return {"bound": "hbm", "achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS,
+            "bytes_per_launch": b / n_launch, "share_of_launch": sp["backup_share"],
+            "share_source": "builder-measured phase cycles, %s (G=%d, layout %s)" % (
+                os.path.relpath(BACKUP_SPLIT, os.path.dirname(os.path.abspath(__file__))), G, sp.get("layout"))}
+
+
 PEAK_MFMA_TFLOPS = 2500.0   # MI355X dense f16 / bf16 MFMA (MI355X_MICROARCH.md, no sparsity)
 PEAK_HBM_GBS = 8000.0
 
@@ -708,6 +737,7 @@ def selfplay_leg(args, rank, world, dist, backend, size, sims, mode, blocks, G, 
             "games_per_launch": ctr["backups"] / n_tree, "streams": streams, "busy_ms": busy_tree,
             "layout": parts[0].layout, "descent_hint": parts[0].descent_hint, "waves_per_game": 2 if parts[0].pair else 1,
             "achieved_per_launch": bpl / (ms_tree * 1e-3) / 1e9,
+            "backup": backup_roofline(ctr, A, n_tree, busy_tree, G),
             "note": ("two streams: each launch runs on the CUs the other stream's capped tower leaves free (about "
                      "a quarter of them), so this is the kernel inside the step, not its own rate; "
                      "single_stream_kernels.tree has the kernel alone on every CU" if streams > 1 else
@@ -747,7 +777,8 @@ def selfplay_leg(args, rank, world, dist, backend, size, sims, mode, blocks, G, 
         n2, m2, _ = timer_stats([tt1], b1)
         if n2:
             g2 = tree_bytes(c1, size * size) / n2 / (m2 * 1e-3) / 1e9
-            ss["tree"] = {"mean_launch_ms": m2, "achieved_gbs": g2, "frac": g2 / PEAK_HBM_GBS}
+            ss["tree"] = {"mean_launch_ms": m2, "achieved_gbs": g2, "frac": g2 / PEAK_HBM_GBS,
+                          "backup": backup_roofline(c1, size * size, n2, m2 * n2, G)}
         res["single_stream_kernels"] = ss
         net.tower_timer = net.repr_timer = None
         e1.close()
