@@ -31,6 +31,32 @@ constexpr int WAVE = 64;
 // trainer's conv skip those k-steps (their MFMAs and B-fragment reads) for the boards' last tile, which holds only
 // the bottom-right corner cell at 15x15 (taps 0, 1, 3, 4: 16 of 36 k-steps) and two bottom-row cells in the packed
 // 9x9 run (taps 0-5: 24 of 36).
+// ---- 15x15 border tiles (round 6).  The 225 positions go to 15 tiles of 16 slots so that four tiles hold board-edge
+// cells only: tile 0 the left column (15 cells), tile 1 the right column (15), tile 2 the top row's 13 inner cells,
+// tile 3 the bottom row's cells 8..13; tiles 4..14 the remaining 176 cells (rows 1..13, x = 1..13, then row 14, x =
+// 1..7) in raster order.  A tile of edge cells never reads three of the nine taps (they reach only the zero border):
+// those k-steps are skipped (remap15_taps), 48 of the 15 x 36 tile k-steps per layer (8.9 % of the MFMAs; the raster
+// order's one corner-cell tile skipped 20).  Bank keys: a cell's read base (y RS + x PS) has key (13 y + x) mod 16
+// (Img3<15>::RS in gmz_net.hip, CImg<15>::RS in gmz_conv.hip), so each tile's 16 slots carry 16 consecutive keys — the columns by slot order y = 5 s mod 16, the
+// rows and the raster runs by construction — and a pad slot reads a border address with its slot's key: every
+// ds_read_b128 lane group stays conflict-free (modelled for every tile, tap and k-step).
+__host__ __device__ constexpr int remap15(int t, int s) {  // tile t, slot s -> position (y * 15 + x), -1 = pad
+  if (t == 0 || t == 1) {
+    const int y = (5 * s) & 15;
+    return y >= 15 ? -1 : y * 15 + (t == 0 ? 0 : 14);
+  }
+  if (t == 2) return s <= 12 ? s + 1 : -1;
+  if (t == 3) return s <= 5 ? 14 * 15 + 8 + s : -1;
+  const int m = (t - 4) * 16 + s;
+  return m < 169 ? (1 + m / 13) * 15 + 1 + m % 13 : 14 * 15 + 1 + (m - 169);
+}
+__host__ __device__ constexpr int remap15_key0(int t) {  // key of slot 0's read base (slot s: key0 + s)
+  return t == 0 ? 0 : t == 1 ? 14 : t == 2 ? 1 : t == 3 ? 14 : ((13 * (remap15(t, 0) / 15) + remap15(t, 0) % 15) & 15);
+}
+__host__ __device__ constexpr unsigned remap15_taps(int t) {  // taps that reach in-board cells from tile t
+  return t == 0 ? 0x1b6u : t == 1 ? 0x0dbu : t == 2 ? 0x1f8u : t == 3 ? 0x03fu : 0x1ffu;
+}
+
 __host__ __device__ constexpr unsigned live_taps(int H, int g0, int g1) {
   unsigned m = 0;
   for (int g = g0; g < g1; ++g) {

@@ -151,7 +151,11 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
   static_assert(CKSTEPS % RD == 0, "ring slots repeat per item");
   // the board's last tile (15x15: the corner cell alone) skips the k-steps whose tap reaches only the zero border
   // (gmz_common.h live_taps); only the PTW-tile k-loop holds it when NPT = PG (PTW - 1) + 1
-  constexpr bool LAST_ONE = NPT == PG * (PTW - 1) + 1;
+  // REMAP would be the towers' 15x15 border-tile order (remap15, gmz_common.h): measured slower here (forward 29.0 vs
+  // 27.5 us at 360 boards, trainer 40.4 vs 41.0 steps/s, profiles/r06_conv_remap_ab.txt) — this kernel's epilogue
+  // stores straight to HBM, 8 B per lane, and a column tile's positions are 15 cells apart: scattered stores.  Off.
+  constexpr bool REMAP = false;
+  constexpr bool LAST_ONE = !REMAP && NPT == PG * (PTW - 1) + 1;
   constexpr unsigned LAST_TAPS = LAST_ONE ? live_taps(H, (NPT - 1) * 16, A) : 0x1ffu;
   static_assert(LAST_TAPS & 1u, "tap 0 of the last tile starts its accumulation");
   __shared__ __attribute__((aligned(16))) uint8_t img[I::BYTES];
@@ -186,12 +190,22 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
     }
   }
 
-  int pos[PTW];
+  // tile pt, lane -> board position (A: a pad), in raster order or (15x15) the border-tile order
+  auto tile_p = [&](int pt) {
+    if constexpr (REMAP) {
+      const int p = pt < NPT ? remap15(pt, csigma16(lane & 15)) : -1;
+      return p < 0 ? A : p;
+    }
+    const int p = pt * 16 + csigma16(lane & 15);
+    return (pt < NPT && p < A) ? p : A;
+  };
+  int pos[PTW];  // read base of each tile's cell; ~base for a pad (REMAP: a top-border address with the slot's key)
 #pragma unroll
   for (int i = 0; i < PTW; ++i) {
-    const int pt = pg + PG * i;
-    const int p = pt * 16 + csigma16(lane & 15);
-    pos[i] = (pt < NPT && p < A) ? (p / H) * RS + (p % H) * PS : -1;
+    const int pt = pg + PG * i, p = tile_p(pt);
+    const int pad = REMAP ? 16 * ((remap15_key0(pt) + csigma16(lane & 15)) & 15)
+                          : ((A - 1) / H) * RS + ((A - 1) % H) * PS;  // the last cell: one broadcast address
+    pos[i] = p < A ? (p / H) * RS + (p % H) * PS : ~pad;
   }
   const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc((void *)wpk, (short)0, FRAG_BYTES, 0x00020000);
   int wvoff = ntile0 * 1024 + lane * 16;
@@ -254,17 +268,22 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
         for (int k = 0; k < RD - 1; ++k) loadA(k, k);
     }
     f32x4_t acc[NTW][PTW];
-    // lanes past the board read the board's LAST position's cell (never stored): a 16-lane bank group of the
-    // last tile then holds that one address (a broadcast) and the valid positions' own slots, not a second
-    // address on the valid position's bank (tile 14 of 15x15 / tile 5 of 9x9 hold one valid position)
-    constexpr int LASTPOS = ((A - 1) / H) * RS + ((A - 1) % H) * PS;
+    // lanes past the board read their pad address (~pos): the board's LAST cell, one broadcast address in its bank
+    // group beside the valid positions' own slots (raster order), or a top-border address with the slot's key (15x15
+    // border tiles)
     int bb[PTW];
 #pragma unroll
-    for (int i = 0; i < PTW; ++i) bb[i] = (pos[i] < 0 ? LASTPOS : pos[i]) + cg * 16;
+    for (int i = 0; i < PTW; ++i) bb[i] = (pos[i] < 0 ? ~pos[i] : pos[i]) + cg * 16;
     auto kloop = [&](auto ntl_c) {
       constexpr int NTL = decltype(ntl_c)::value;
       V bf[2][NTL];
-      auto live = [&](int i, int st) { return !(LAST_ONE && NTL == PTW && i == NTL - 1) || ((LAST_TAPS >> (st >> 2)) & 1u); };
+      constexpr int PGK = NTL == PTW ? 0 : 1;  // REMAP: the position group of this instantiation
+      auto taps = [&](int i) -> unsigned {
+        if constexpr (REMAP) return remap15_taps(PGK + PG * i);
+        return (LAST_ONE && NTL == PTW && i == NTL - 1) ? LAST_TAPS : 0x1ffu;
+      };
+      auto live = [&](int i, int st) { return ((taps(i) >> (st >> 2)) & 1u) != 0; };
+      auto first = [&](int i) { return 4 * __builtin_ctz(taps(i)); };
       auto readB = [&](int buf, int st) {
         const int tap = st >> 2, ks = st & 3;
         const int off = (tap / 3) * RS + (tap % 3) * PS + ks * 32;
@@ -291,7 +310,7 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
               if (st == 0) acc[nt][i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
               acc[nt][i][0] += __builtin_bit_cast(f32x4_t, ar[st % RD][nt])[0] + __builtin_bit_cast(f32x4_t, bf[st & 1][i])[0];
             } else {
-              acc[nt][i] = M::run(ar[st % RD][nt], bf[st & 1][i], st == 0 ? f32x4_t{0.f, 0.f, 0.f, 0.f} : acc[nt][i]);
+              acc[nt][i] = M::run(ar[st % RD][nt], bf[st & 1][i], st == first(i) ? f32x4_t{0.f, 0.f, 0.f, 0.f} : acc[nt][i]);
             }
           }
         if (st + 1 < CKSTEPS) __builtin_amdgcn_sched_barrier(0);
@@ -331,9 +350,8 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
     }
 #pragma unroll
     for (int i = 0; i < PTW; ++i) {
-      const int pt = pg + PG * i;
-      const int p = pt * 16 + csigma16(lane & 15);
-      if (pt >= NPT || p >= A) continue;
+      const int p = tile_p(pg + PG * i);
+      if (p >= A) continue;
 #pragma unroll
       for (int nt = 0; nt < NTW; ++nt) {
         const int n0 = (ntile0 + nt) * 16 + g4 * 4;

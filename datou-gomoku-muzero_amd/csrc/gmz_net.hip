@@ -126,6 +126,7 @@ struct F16 {
 // touches 16 distinct slots: conflict-free B-operand reads.
 __device__ __forceinline__ int sigma16(int j) { return j < 8 ? (j ^ 4) : j; }
 
+
 // ------------------------------------------------------------------------------------------------
 // k_tower3: the tower kernel the library launches.  Persistent (one 512-thread workgroup per CU,
 //  boards strided over the grid) and barrier-light:
@@ -149,7 +150,10 @@ __device__ __forceinline__ int sigma16(int j) { return j < 8 ? (j ^ 4) : j; }
 //  (the skewed images leave no room for all 17 layers' biases).
 template <int H>
 struct Img3 {
-  static constexpr int HP = H + 2, PS = 272, RS = HP * PS - 32;
+  // RS / 16 = H (mod 16): 16 consecutive positions of the raster order have 16 consecutive bank keys.  15x15 runs the
+  // border-tile order (remap15 below) instead, whose runs are 13-cell rows: RS / 16 = 13 (mod 16) there (4,560 B:
+  // rows overlap by 64 B, all of it in the zero border cells at the row ends, which nothing writes)
+  static constexpr int HP = H + 2, PS = 272, RS = H == 15 ? 285 * 16 : HP * PS - 32;
   static constexpr int BYTES = ((HP - 1) * RS + HP * PS + 255) / 256 * 256;
   static constexpr int RUN = (H - 1) * PS + 256;     // bytes of one board row's interior cells
   static constexpr int RUN_DMA = (RUN + 1023) / 1024; // 1 KB LDS-DMA pieces per board row
@@ -191,7 +195,10 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
   // LAST_ONE: only the k-loop instantiated for PTW tiles (NTL == PTW) holds the tile space's last tile, as its tile
   // PTW - 1 (one wave group's short slot: NPTB = PG (PTW - 1) + 1; 15x15: tile 14 = the corner cell alone, packed
   // 9x9: tile 10 = two bottom-row cells).  That tile skips the k-steps of the taps that reach only the zero border.
-  constexpr bool LAST_ONE = !PIPE && NPTB == PG * (PTW - 1) + 1;
+  // REMAP (15x15, one board per workgroup, two images): the border-tile order (remap15); each of the two wave groups
+  // has its own k-loop instantiation (8 and 7 tiles), so a tile's skipped taps are known at compile time
+  constexpr bool REMAP = H == 15 && NB == 1 && PG == 2 && NPTB == 15;
+  constexpr bool LAST_ONE = !PIPE && !REMAP && NPTB == PG * (PTW - 1) + 1;
   constexpr unsigned LAST_TAPS = LAST_ONE ? live_taps(H, (NPTB - 1) * 16, NB * A < NPTB * 16 ? NB * A : NPTB * 16) : 0x1ffu;
   static_assert(LAST_TAPS & 1u, "tap 0 of the last tile starts its accumulation");
   constexpr int PS = I::PS, RS = I::RS, IMG = I::BYTES;
@@ -209,7 +216,11 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
   auto bbase = [](int b) { return b * BB + (PACKED ? ((b * A) & 15) * 16 : 0); };
   // position tile pt, lane column l -> (board slot bsl, position p); p = A: past the boards
   auto tile_pos = [](int pt, int l, int &bsl, int &p) {
-    if constexpr (PACKED) {
+    if constexpr (REMAP) {
+      bsl = 0;
+      p = pt < NPTB ? remap15(pt, sigma16(l & 15)) : -1;
+      if (p < 0) p = A;
+    } else if constexpr (PACKED) {
       const int gp = pt * 16 + sigma16(l & 15);
       bsl = gp / A;
       p = gp - bsl * A;
@@ -346,18 +357,20 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
 
   // per tile: LDS byte offset of the top-left neighbour of this lane's column position (+ its
   // k-chunk for B reads); -1 marks positions past the board
+  // lanes past the boards (pads) read the tile space's LAST position's cell (never stored): within a 16-lane bank
+  // group of the last tile that is one broadcast address beside the valid positions' own slots, where image offset 0
+  // was a second address on a valid position's bank (a 2-way conflict on every read of that tile).  REMAP: a pad reads
+  // the top border address with its slot's bank key.  pos[i] < 0 marks a pad, ~pos[i] its read base.
+  static_assert(NB == 1 || PACKED, "several boards per workgroup run as one packed position run");
+  const int lastpos = bbase(NB - 1) + ((A - 1) / H) * RS + ((A - 1) % H) * PS;
   int pos[PTW];
 #pragma unroll
   for (int i = 0; i < PTW; ++i) {
     int bsl, p;
     tile_pos(pg + PG * i, lane, bsl, p);
-    pos[i] = p < A ? bbase(bsl) + (p / H) * RS + (p % H) * PS : -1;
+    const int pad = REMAP ? 16 * ((remap15_key0(pg + PG * i) + sigma16(lane & 15)) & 15) : lastpos;
+    pos[i] = p < A ? bbase(bsl) + (p / H) * RS + (p % H) * PS : ~pad;
   }
-  // lanes past the boards read the tile space's LAST position's cell (never stored): within a 16-lane bank group
-  // of the last tile that is one broadcast address beside the valid positions' own slots, where image offset 0
-  // was a second address on a valid position's bank (a 2-way conflict on every read of that tile)
-  static_assert(NB == 1 || PACKED, "several boards per workgroup run as one packed position run");
-  const int lastpos = bbase(NB - 1) + ((A - 1) / H) * RS + ((A - 1) % H) * PS;
   f32x4 acc[NTW][PTW];
   // ONE: this lane's residual tile values, [NTW][PTW][64 lanes] x 4 16-bit values per wave (same lane writes
   // and reads back: program order suffices)
@@ -496,7 +509,7 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
       int bb[PTW];
 #pragma unroll
       for (int i = 0; i < PTW; ++i) {
-        bb[i] = (pos[i] < 0 ? lastpos : pos[i]) + cg * 16 + (int)(size_t)(img - smem) + (PP ? 64 * hh : 0);
+        bb[i] = (pos[i] < 0 ? ~pos[i] : pos[i]) + cg * 16 + (int)(size_t)(img - smem) + (PP ? 64 * hh : 0);
         asm volatile("" : "+v"(bb[i]));  // one base VGPR per tile and layer; all else immediates
       }
       // k-loop over the NTL tiles this wave owns (NTL = PTW, or PTW - 1 for a short last position
@@ -508,10 +521,15 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
 #pragma unroll
           for (int nt = 0; nt < NTW; ++nt) acc[nt][i] = bv[nt];  // the empty slot (never stored)
         V8 b[2][NTL];
-        // tile i's k-step st multiplies in-board cells (LAST_TAPS; compile-time once the loops are unrolled)
-        auto live = [&](int i, int st) {
-          return !(LAST_ONE && NTL == PTW && i == NTL - 1) || ((LAST_TAPS >> (st >> 2)) & 1u);
+        // tile i's k-step st multiplies in-board cells (LAST_TAPS / remap15_taps; compile-time once the loops are
+        // unrolled); first(i): its first live k-step, which starts the accumulation from the bias
+        constexpr int PGK = NTL == PTW ? 0 : 1;  // REMAP: the wave group of this instantiation
+        auto taps = [&](int i) -> unsigned {
+          if constexpr (REMAP) return remap15_taps(PGK + PG * i);
+          return (LAST_ONE && NTL == PTW && i == NTL - 1) ? LAST_TAPS : 0x1ffu;
         };
+        auto live = [&](int i, int st) { return ((taps(i) >> (st >> 2)) & 1u) != 0; };
+        auto first = [&](int i) { return 4 * __builtin_ctz(taps(i)); };
         auto readB = [&](int buf, int st) {
           const int tap = PP ? (st < 18 ? st : st - 18) >> 1 : st >> 2, ks = PP ? (st & 1) : st & 3;
           const int off = (tap / 3) * RS + (tap % 3) * PS + ks * 32;
@@ -562,7 +580,7 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
             if (live(i, st))
 #pragma unroll
               for (int nt = 0; nt < NTW; ++nt)
-                acc[nt][i] = E::mfma(ar[st % RD][nt], b[st & 1][i], st == 0 ? bv[nt] : acc[nt][i]);
+                acc[nt][i] = E::mfma(ar[st % RD][nt], b[st & 1][i], st == first(i) ? bv[nt] : acc[nt][i]);
           // the last k-step stays open: the scheduler may start the epilogue of the tiles whose final
           // MFMA has issued while the remaining ones run (ABL & 256 pins it, for comparison)
           if ((ABL & 256) || st + 1 < KSTEPS) __builtin_amdgcn_sched_barrier(0);
@@ -587,7 +605,7 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
           for (int u = 0; u < NTW / 2; ++u)
 #pragma unroll
             for (int i = 0; i < PTW; ++i) {
-              const uint4 v = *(const uint4 *)(nimg + (pos[i] < 0 ? lastpos : pos[i]) + RS + PS + chan0(2 * u) * 2);
+              const uint4 v = *(const uint4 *)(nimg + (pos[i] < 0 ? ~pos[i] : pos[i]) + RS + PS + chan0(2 * u) * 2);
               xr[2 * u][i] = __builtin_bit_cast(u16x4, make_uint2(v.x, v.y));
               xr[2 * u + 1][i] = __builtin_bit_cast(u16x4, make_uint2(v.z, v.w));
             }
@@ -626,7 +644,10 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
             }
             const u16x4 o = __builtin_bit_cast(u16x4, make_uint2(E::relu2(v[0], v[1]), E::relu2(v[2], v[3])));
             if (nt & 1) {
-              if ((NB == 1 && (PG * i + PG) * 16 <= A) || pos[i] >= 0) store_pair(nimg, nt >> 1, i, olo[i], o);
+              // tiles known to hold no pad skip the test (REMAP: the raster tiles 4..13 of either wave group; slot
+              // PTW - 1 is tile 14 for group 0 but the empty slot for group 1)
+              if ((REMAP ? (i >= 2 && i < PTW - 1) : (NB == 1 && (PG * i + PG) * 16 <= A)) || pos[i] >= 0)
+                store_pair(nimg, nt >> 1, i, olo[i], o);
             } else {
               olo[i] = o;
             }
