@@ -52,7 +52,7 @@ PY
     ;;
   pmc)  # one counter group per rocprofv3 run (MI355X_MICROARCH.md: separate passes) on the self-play step
     cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-    for CTR in FETCH_SIZE WRITE_SIZE "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_MFMA" "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES"; do
+    for CTR in FETCH_SIZE WRITE_SIZE "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_MFMA" "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES" "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAIT_INST_LDS"; do
       NAME=$(echo $CTR | tr ' ' '_' | cut -c1-40)
       timeout -s KILL 240 rocprofv3 --pmc $CTR --kernel-include-regex "k_tower3|k_expand_select" --output-format csv -d $OUT/$NAME -o pmc -- \
         python3 bench.py --steps 1 --warmup 0 --single-stream-moves 0 $SP "$@" > $OUT/$NAME.json 2> $OUT/$NAME.err || { echo "pmc $CTR failed"; tail -3 $OUT/$NAME.err; exit 1; }
