@@ -36,18 +36,6 @@ typedef uint16_t u16x4_t __attribute__((ext_vector_type(4)));
 #ifndef GMZ_CONV_RD
 #define GMZ_CONV_RD 3
 #endif
-// timing ablations of k_conv3 (A/B builds only, results wrong): 1 = each workgroup DMAs only its first board,
-// 2 = no epilogue stores (kept behind a never-true runtime test), 4 = no MFMAs in the k-loop (operand loads kept),
-// 8 = no weight-fragment loads in the k-loop (the ring keeps its first fragments), 16 = no B-fragment LDS reads in
-// the k-loop (the first step's fragments reused), 32 = no board DMA at all (the image stays zero)
-#ifndef GMZ_CONV_ABL
-#define GMZ_CONV_ABL 0
-#endif
-// EARLY (one half per workgroup): the next board's DMA is issued as soon as every wave has left the k-loop, and
-// completes under this board's epilogue, instead of after it (A/B build switch)
-#ifndef GMZ_CONV_EARLY
-#define GMZ_CONV_EARLY 0
-#endif
 constexpr int CC = 128;         // channels in and out
 constexpr int CKSTEPS = 36;     // 9 taps x 4 k-steps of 32 input channels
 constexpr int FRAG_BYTES = 294912;  // 36 k-steps x 8 n-tiles x 64 lanes x 16 B
@@ -128,16 +116,16 @@ struct ActStamp {
   const float *table;     // [9][128]
 };
 
-// HALVES = 2: one workgroup per board computes both halves of the output channels from ONE DMA of the
-// board image (the k-loop twice, the weight ring reloaded for the second half's n-tiles): N workgroups
-// instead of 2N, one board DMA instead of two (gmz_conv3x3 A/B: GMZ_CONV_HALVES).
+// (Measured and removed: one workgroup per board computing both channel halves from one DMA — forward 33.9 vs 28.7 us,
+// profiles/r04_trainer_ab_defer_target.txt; the next board's DMA issued before the epilogue; the timing ablations of
+// profiles/r05_conv_ablations.txt and r06_conv_lds_ab.txt, built from commit 3a54982's gmz_conv.hip with GMZ_CONV_ABL.)
 // BWD: the epilogue's statistics are the BatchNorm BACKWARD sums of the output taken as that BN's output
 // gradient dy — sum dz and sum dz * xhat, dz = dy * [y > 0], xhat = (x - mean) * invstd (what k_bnl_red<.., 1, ..>
 // reduces in a pass of its own) — instead of the forward sums of the output.
 // PB: the statistics partials per BOARD (stats [C][N][3], slot = board) instead of per workgroup, so a
 // consumer can take them over any board ranges: the trainer's batched consistency trunk (five unroll steps'
 // observations as one launch, each step's BatchNorm statistics over its own boards; gmz_bn_forward_seg).
-template <int H, typename T, int PG, int HALVES = 1, bool BWD = false, bool PB = false>
+template <int H, typename T, int PG, bool BWD = false, bool PB = false>
 __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restrict__ x, const uint16_t *__restrict__ wpk,
                                                   uint16_t *__restrict__ y, int N, const uint8_t *__restrict__ mask,
                                                   double *__restrict__ stats, const uint16_t *__restrict__ addend,
@@ -160,7 +148,7 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
   static_assert(LAST_TAPS & 1u, "tap 0 of the last tile starts its accumulation");
   __shared__ __attribute__((aligned(16))) uint8_t img[I::BYTES];
   static_assert(I::BYTES >= PG * 64 * 2 * 4, "stats scratch fits in the image");
-  static_assert(!PB || (HALVES == 1 && !BWD), "per-board statistics: forward sums, one half per workgroup");
+  static_assert(!PB || !BWD, "per-board statistics: forward sums");
   __shared__ float pbred[PB ? PG * 64 * 2 : 1];  // PB: [PG][64 channels of this half][2], per board
 
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
@@ -170,11 +158,11 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
   // XCD-aware items: workgroups are dealt to the 8 XCDs round-robin by index, so workgroup i runs on
   // XCD i % 8; the two halves of a board are workgroups i and i ^ 8 (same XCD, dispatched together),
   // and the second one's board DMA is served by that XCD's L2 instead of HBM
-  const int half0 = HALVES == 2 ? 0 : (blockIdx.x >> 3) & 1;
+  const int half0 = (blockIdx.x >> 3) & 1;
   // first board; also the statistics slot
-  const int b0 = HALVES == 2 ? (int)blockIdx.x : (int)((blockIdx.x >> 4) * 8 + (blockIdx.x & 7));
-  const int bstride = HALVES == 2 ? (int)gridDim.x : (int)(gridDim.x >> 1);
-  int ntile0 = half0 * 4 + nq * NTW;  // this wave's first n-tile (of 8)
+  const int b0 = (int)((blockIdx.x >> 4) * 8 + (blockIdx.x & 7));
+  const int bstride = (int)(gridDim.x >> 1);
+  const int ntile0 = half0 * 4 + nq * NTW;  // this wave's first n-tile (of 8)
 
   // zero the image's border cells (2 HP + 2 H cells; every board's DMA rewrites the whole interior).  Indexed
   // uint4 stores compile to ds_write_b128 (8 lanes = one contiguous 128 B: conflict-free); the round-5 fill of the
@@ -208,7 +196,7 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
     pos[i] = p < A ? (p / H) * RS + (p % H) * PS : ~pad;
   }
   const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc((void *)wpk, (short)0, FRAG_BYTES, 0x00020000);
-  int wvoff = ntile0 * 1024 + lane * 16;
+  const int wvoff = ntile0 * 1024 + lane * 16;
   V ar[RD][NTW];
   auto loadA = [&](int slot, int st) {
     const int soff = (st < CKSTEPS ? st : st - CKSTEPS) * 8192;
@@ -221,20 +209,17 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
   __syncthreads();  // zeroed image before the first DMA
   // BatchNorm statistics of the (rounded) output over the boards in the mask: per lane, its 4
   // channels of each n-tile summed over its positions and boards
-  float s1[HALVES][NTW][4], s2[HALVES][NTW][4];
+  float s1[NTW][4], s2[NTW][4];
 #pragma unroll
-  for (int hh = 0; hh < HALVES; ++hh)
+  for (int nt = 0; nt < NTW; ++nt)
 #pragma unroll
-    for (int nt = 0; nt < NTW; ++nt)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) s1[hh][nt][e] = s2[hh][nt][e] = 0.f;
+    for (int e = 0; e < 4; ++e) s1[nt][e] = s2[nt][e] = 0.f;
   int nvalid = 0;
 
-  constexpr bool EARLY = GMZ_CONV_EARLY && HALVES == 1;
   // ---- board bd -> image interior: 1 KB pieces of each board row's run of cells
   auto dma = [&](int bd) {
     const uint8_t *src = (const uint8_t *)(x + (size_t)bd * A * CC);
-    for (int j = w; j < ((((GMZ_CONV_ABL & 1) && bd != b0) || (GMZ_CONV_ABL & 32)) ? 0 : H * I::RUN_DMA); j += NW) {
+    for (int j = w; j < H * I::RUN_DMA; j += NW) {
       const int yy = j / I::RUN_DMA, piece = j % I::RUN_DMA;
       const int o = piece * 1024 + lane * 16;
       const int xx = o / PS, ch = (o % PS) >> 4;
@@ -244,29 +229,13 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
                                          16, 0, 0);
     }
   };
-  if (EARLY && b0 < N) {
-    dma(b0);
+  for (int b = b0; b < N; b += bstride) {
+    dma(b);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-  }
-  for (int b = b0; b < N; b += bstride) {
-    if (!EARLY) {
-      dma(b);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
     const bool counted = stats && (!mask || mask[b]);
     nvalid += counted;
 
-#pragma unroll
-    for (int hh = 0; hh < HALVES; ++hh) {
-    if (HALVES == 2) {  // this half's n-tiles: the weight ring restarts on them
-      ntile0 = hh * 4 + nq * NTW;
-      wvoff = ntile0 * 1024 + lane * 16;
-      if (hh == 1)
-#pragma unroll
-        for (int k = 0; k < RD - 1; ++k) loadA(k, k);
-    }
     f32x4_t acc[NTW][PTW];
     // lanes past the board read their pad address (~pos): the board's LAST cell, one broadcast address in its bank
     // group beside the valid positions' own slots (raster order), or a top-border address with the slot's key (15x15
@@ -294,25 +263,15 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
       readB(0, 0);
 #pragma unroll
       for (int st = 0; st < CKSTEPS; ++st) {
-        if constexpr ((GMZ_CONV_ABL & 8) == 0) loadA((st + RD - 1) % RD, st + RD - 1);
-        if constexpr ((GMZ_CONV_ABL & 16) == 0) {
-          if (st + 1 < CKSTEPS) readB((st + 1) & 1, st + 1);
-        } else if (st == 0) {
-          readB(1, 1);
-        }
+        loadA((st + RD - 1) % RD, st + RD - 1);
+        if (st + 1 < CKSTEPS) readB((st + 1) & 1, st + 1);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int i = 0; i < NTL; ++i)
           if (live(i, st))
 #pragma unroll
-          for (int nt = 0; nt < NTW; ++nt) {
-            if constexpr ((GMZ_CONV_ABL & 4) != 0) {  // ablation: operands consumed by one VALU op, no MFMA
-              if (st == 0) acc[nt][i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-              acc[nt][i][0] += __builtin_bit_cast(f32x4_t, ar[st % RD][nt])[0] + __builtin_bit_cast(f32x4_t, bf[st & 1][i])[0];
-            } else {
+            for (int nt = 0; nt < NTW; ++nt)
               acc[nt][i] = M::run(ar[st % RD][nt], bf[st & 1][i], st == first(i) ? f32x4_t{0.f, 0.f, 0.f, 0.f} : acc[nt][i]);
-            }
-          }
         if (st + 1 < CKSTEPS) __builtin_amdgcn_sched_barrier(0);
       }
 #pragma unroll
@@ -323,10 +282,6 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
     if constexpr (PTW * PG == NPT) kloop(std::integral_constant<int, PTW>{});
     else if (pg + PG * (PTW - 1) < NPT) kloop(std::integral_constant<int, PTW>{});
     else kloop(std::integral_constant<int, PTW - 1>{});
-    if constexpr (EARLY) {  // every wave has read its last B fragments: the image is free for the next board
-      __syncthreads();
-      if (b + bstride < N) dma(b + bstride);
-    }
 
     // ---- epilogue: 4 consecutive output channels of one position per lane -> 8-byte store
     uint16_t *dst = y + (size_t)b * A * CC;
@@ -372,7 +327,7 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
 #pragma unroll
           for (int e = 0; e < 4; ++e) o[e] = M::bits(acc[nt][i][e]);
         }
-        if ((GMZ_CONV_ABL & 2) == 0 || o[0] == 0x7c01) *(u16x4_t *)(dst + (size_t)p * CC + n0) = o;
+        *(u16x4_t *)(dst + (size_t)p * CC + n0) = o;
         if (counted) {
           if constexpr (BWD) {  // the rounded output is the BatchNorm's dy
             const size_t k = ((size_t)b * A + p) * CC + n0;
@@ -381,21 +336,20 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
             for (int e = 0; e < 4; ++e) {
               float g = M::value(o[e]);
               if (bn.relu && !(M::value(yv[e]) > 0.f)) g = 0.f;
-              s1[hh][nt][e] += g;
-              s2[hh][nt][e] = fmaf(g, (M::value(xv[e]) - mu[nt][e]) * isd[nt][e], s2[hh][nt][e]);
+              s1[nt][e] += g;
+              s2[nt][e] = fmaf(g, (M::value(xv[e]) - mu[nt][e]) * isd[nt][e], s2[nt][e]);
             }
           } else {
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
               const float v = M::value(o[e]);
-              s1[hh][nt][e] += v;
-              s2[hh][nt][e] = fmaf(v, v, s2[hh][nt][e]);
+              s1[nt][e] += v;
+              s2[nt][e] = fmaf(v, v, s2[nt][e]);
             }
           }
         }
       }
     }
-    }  // halves
     if constexpr (PB) {  // this board's partials -> slot b, then the accumulators restart
       if (stats) {
 #pragma unroll
@@ -404,8 +358,8 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
           for (int e = 0; e < 4; ++e)
 #pragma unroll
             for (int o = 1; o < 16; o <<= 1) {
-              s1[0][nt][e] += __shfl_xor(s1[0][nt][e], o, 64);
-              s2[0][nt][e] += __shfl_xor(s2[0][nt][e], o, 64);
+              s1[nt][e] += __shfl_xor(s1[nt][e], o, 64);
+              s2[nt][e] += __shfl_xor(s2[nt][e], o, 64);
             }
         if ((lane & 15) == 0) {
 #pragma unroll
@@ -413,14 +367,14 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
               const int cl = (nq * NTW + nt) * 16 + g4 * 4 + e;
-              pbred[(pg * 64 + cl) * 2] = s1[0][nt][e];
-              pbred[(pg * 64 + cl) * 2 + 1] = s2[0][nt][e];
+              pbred[(pg * 64 + cl) * 2] = s1[nt][e];
+              pbred[(pg * 64 + cl) * 2 + 1] = s2[nt][e];
             }
         }
 #pragma unroll
         for (int nt = 0; nt < NTW; ++nt)  // every lane: its accumulators now hold the group's reduced sums
 #pragma unroll
-          for (int e = 0; e < 4; ++e) s1[0][nt][e] = s2[0][nt][e] = 0.f;
+          for (int e = 0; e < 4; ++e) s1[nt][e] = s2[nt][e] = 0.f;
         __syncthreads();
         if (tid < 64) {
           double a = 0.0, q = 0.0;
@@ -436,20 +390,9 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
         }
       }
     }
-    if (HALVES == 2)  // the next board's first k-steps for half 0 (the ring holds half 1's)
-#pragma unroll
-      for (int k = 0; k < RD - 1; ++k) {
-        wvoff = nq * NTW * 1024 + lane * 16;
-        loadA(k, k);
-      }
-    if constexpr (EARLY) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next board has landed
-    __syncthreads();  // every wave is done reading the image before the next board's DMA (EARLY: it is in)
+    __syncthreads();  // every wave is done reading the image before the next board's DMA
   }
   if (!stats || PB) return;
-#pragma unroll
-  for (int hh = 0; hh < HALVES; ++hh) {
-  const int half = HALVES == 2 ? hh : half0;
-  if (hh > 0) __syncthreads();  // the previous half's partials have left the LDS scratch
   // ---- per-workgroup partials: the 16 lanes of a lane group hold the same 4 channels at different
   // positions; then the PG position-group waves of a channel group meet in LDS (the image is free)
 #pragma unroll
@@ -458,8 +401,8 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
     for (int e = 0; e < 4; ++e)
 #pragma unroll
       for (int o = 1; o < 16; o <<= 1) {
-        s1[hh][nt][e] += __shfl_xor(s1[hh][nt][e], o, 64);
-        s2[hh][nt][e] += __shfl_xor(s2[hh][nt][e], o, 64);
+        s1[nt][e] += __shfl_xor(s1[nt][e], o, 64);
+        s2[nt][e] += __shfl_xor(s2[nt][e], o, 64);
       }
   float *red = (float *)img;  // [PG][64 channels of this half][2]
   if ((lane & 15) == 0) {
@@ -468,8 +411,8 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int cl = (nq * NTW + nt) * 16 + g4 * 4 + e;  // channel within this half
-        red[(pg * 64 + cl) * 2] = s1[hh][nt][e];
-        red[(pg * 64 + cl) * 2 + 1] = s2[hh][nt][e];
+        red[(pg * 64 + cl) * 2] = s1[nt][e];
+        red[(pg * 64 + cl) * 2 + 1] = s2[nt][e];
       }
   }
   __syncthreads();
@@ -480,12 +423,11 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
       a += (double)red[(g * 64 + tid) * 2];
       q += (double)red[(g * 64 + tid) * 2 + 1];
     }
-    double *out = stats + ((size_t)(half * 64 + tid) * bstride + b0) * 3;  // channel-major [C][slots][3]
+    double *out = stats + ((size_t)(half0 * 64 + tid) * bstride + b0) * 3;  // channel-major [C][slots][3]
     out[0] = a;
     out[1] = q;
     out[2] = (double)nvalid * A;
   }
-  }  // halves
 }
 
 // ---- weight gradient: dW[o][c][t] = sum over boards n and positions p of dy[n][p][o] * x[n][p + d(t)][c]
@@ -517,9 +459,6 @@ __device__ __forceinline__ s16x4_t tr_read(const uint8_t *lds_base, int off) {
       (__attribute__((address_space(3))) uint8_t *)lds_base + off));
 }
 
-#ifndef WGRAD_ABL
-#define WGRAD_ABL 0  // timing ablations (tools only): 1 = no DMA, 2 = k-loop twice per board
-#endif
 // the boards of one weight-gradient launch: up to 8 segments of nps boards each (board b of the launch is
 // board b % nps of segment b / nps), so the gradient contributions of one weight over several uses (the
 // dynamics trunk's convs in every unroll step) are one launch and one partial-sum reduction
@@ -582,7 +521,7 @@ __global__ void __launch_bounds__(512, 1) k_conv3_wgrad(WgSrc src, int N, int nc
     const int sg = b / src.nps, lb = b - sg * src.nps;
     const uint8_t *sd = (const uint8_t *)(src.dy[sg] + (size_t)lb * A * CC);
     const uint8_t *sx = (const uint8_t *)(src.x[sg] + (size_t)lb * A * CC);
-    for (int j = w; j < ((WGRAD_ABL & 1) ? 0 : L::NPD + H * L::RUN_DMA); j += 8) {
+    for (int j = w; j < L::NPD + H * L::RUN_DMA; j += 8) {
       if (j < L::NPD) {
         const int o = j * 1024 + lane * 16;
         const int row = o / RB, ch = (o % RB) >> 4;
@@ -603,8 +542,7 @@ __global__ void __launch_bounds__(512, 1) k_conv3_wgrad(WgSrc src, int N, int nc
     __syncthreads();
 
 #pragma unroll 2
-    for (int kk = 0; kk < ((WGRAD_ABL & 2) ? 2 * KS : KS); ++kk) {
-      const int ks = kk % KS;
+    for (int ks = 0; ks < KS; ++ks) {
       const int p0 = ks * 32 + 4 * g + q, p1 = p0 + 16;
       // x rows: cell (y + ty, x) of the padded image for tap column 0; columns 1, 2 are +RB, +2 RB.
       // Positions past the board (zero dy rows) read the last position's cells
@@ -678,33 +616,17 @@ static int cu_count_conv() {
 
 constexpr int CONV_PG = 2;  // position groups per workgroup: 2 -> 4 waves, 8|7 tiles per wave
 
-// halves of the output channels per workgroup: 1 (two workgroups per board, the product since round 3) or
-// 2 (one per board, one DMA); GMZ_CONV_HALVES=2 selects the second (A/B)
-static int conv_halves() {
-  static int h = 0;
-  if (!h) {
-    const char *e = getenv("GMZ_CONV_HALVES");
-    h = (e && atoi(e) == 2) ? 2 : 1;
-  }
-  return h;
-}
-
-int conv3_grid(int N) {  // a multiple of 16 (whole XCD pairs; workgroups past the boards do nothing)
-  if (conv_halves() == 2) {  // one workgroup per board, at most two per CU
-    const long cap = 2L * cu_count_conv();
-    return (int)(N < cap ? N : cap);
-  }
+// two workgroups per board (one per half of the output channels), at most two per CU: a multiple of 16 (whole XCD
+// pairs; workgroups past the boards do nothing)
+int conv3_grid(int N) {
   const long items = (2L * N + 15) / 16 * 16, cap = 2L * 2 * cu_count_conv() / 16 * 16;
   return (int)(items < cap ? items : cap);
 }
 
-// statistics slots (partials) a launch writes: one per board pair of workgroups, or per workgroup (HALVES = 2), or
-// per board (per_board, the segmented consistency trunk).  The same function answers gmz_conv3x3_stats_slots and
-// the capacity check before every launch, so the count asked for is the count the dispatch writes (ABI 10)
-int conv3_stats_slots(int N, bool per_board = false) {
-  if (per_board) return N;
-  return conv_halves() == 2 ? conv3_grid(N) : conv3_grid(N) / 2;
-}
+// statistics slots (partials) a launch writes: one per board pair of workgroups, or per board (per_board, the
+// segmented consistency trunk).  The same function answers gmz_conv3x3_stats_slots and the capacity check before
+// every launch, so the count asked for is the count the dispatch writes (ABI 10)
+int conv3_stats_slots(int N, bool per_board = false) { return per_board ? N : conv3_grid(N) / 2; }
 static int check_slots(const char *fn, const double *stats, int stats_slots, int N, bool per_board) {
   if (!stats) return 0;
   const int need = conv3_stats_slots(N, per_board);
@@ -714,14 +636,10 @@ static int check_slots(const char *fn, const double *stats, int stats_slots, int
   return 0;
 }
 
-template <int H, typename T, int HV, bool BWD, bool PB = false>
+template <int H, typename T, bool BWD, bool PB = false>
 void launch_conv3_k(const void *x, const void *wpk, void *y, int N, const uint8_t *mask, double *stats, const void *addend,
                     const BnBwd &bn, hipStream_t st, const ActStamp &as = ActStamp{}) {
-  // per-board statistics: two workgroups per board (one per half), never the one-workgroup-per-board A/B
-  const int grid = PB ? (int)((2L * N + 15) / 16 * 16 < 2L * 2 * cu_count_conv() / 16 * 16 ? (2L * N + 15) / 16 * 16
-                                                                                             : 2L * 2 * cu_count_conv() / 16 * 16)
-                      : conv3_grid(N);
-  hipLaunchKernelGGL((k_conv3<H, T, CONV_PG, HV, BWD, PB>), dim3(grid), dim3(128 * CONV_PG), 0, st,
+  hipLaunchKernelGGL((k_conv3<H, T, CONV_PG, BWD, PB>), dim3(conv3_grid(N)), dim3(128 * CONV_PG), 0, st,
                      (const uint16_t *)x, (const uint16_t *)wpk, (uint16_t *)y, N, mask, stats, (const uint16_t *)addend, bn,
                      as);
 }
@@ -730,15 +648,9 @@ template <int H, typename T>
 int launch_conv3(const void *x, const void *wpk, void *y, int N, const uint8_t *mask, double *stats, const void *addend,
                  const BnBwd &bn, hipStream_t st, bool per_board = false, const ActStamp &as = ActStamp{}) {
   const bool bwd = bn.x != nullptr;
-  if (per_board) {
-    launch_conv3_k<H, T, 1, false, true>(x, wpk, y, N, mask, stats, addend, bn, st, as);
-  } else if (conv_halves() == 2) {
-    if (bwd) launch_conv3_k<H, T, 2, true>(x, wpk, y, N, mask, stats, addend, bn, st, as);
-    else launch_conv3_k<H, T, 2, false>(x, wpk, y, N, mask, stats, addend, bn, st, as);
-  } else {
-    if (bwd) launch_conv3_k<H, T, 1, true>(x, wpk, y, N, mask, stats, addend, bn, st, as);
-    else launch_conv3_k<H, T, 1, false>(x, wpk, y, N, mask, stats, addend, bn, st, as);
-  }
+  if (per_board) launch_conv3_k<H, T, false, true>(x, wpk, y, N, mask, stats, addend, bn, st, as);
+  else if (bwd) launch_conv3_k<H, T, true>(x, wpk, y, N, mask, stats, addend, bn, st, as);
+  else launch_conv3_k<H, T, false>(x, wpk, y, N, mask, stats, addend, bn, st, as);
   GMZ_LAUNCH_CHECK();
   return 0;
 }

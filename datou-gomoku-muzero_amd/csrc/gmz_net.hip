@@ -159,22 +159,10 @@ struct Img3 {
   static constexpr int RUN_DMA = (RUN + 1023) / 1024; // 1 KB LDS-DMA pieces per board row
 };
 
-// k_tower3 ablation bits (0 in the product; timing-only variants in tools/tower_ablate.hip):
-// 1 = A fragments from one k-step (L1-resident), 2 = no weight loads, 32 = no per-board I/O,
-// 128 = s_memtime phase stamps -> pv_feat, 256 = pin the last k-step, 512 = no epilogue,
-// 1024 = no per-layer barrier, 2048 = weight k-steps past ABL_ALIAS_KS aliased back onto the first ones
-// (the streamed set <= 3.5 MB fits a 4 MB XCD L2), 4096 = k-steps past ABL_ALIAS_KS loaded non-temporal
-constexpr int ABL_ALIAS_KS = 12 * 36;
-// PIPE (15x15 two-image configuration, 8 waves = 4 channel quarters x 2 position groups): 0 = one workgroup barrier
-// per layer; 1 = the layer hand-off split into two channel halves that run as a pipeline: half h = the waves of
-// channel quarters h and h + 2, whose output chunks {0-3, 8-11} / {4-7, 12-15} are exactly the input chunks of
-// k-steps {0, 1} / {2, 3} (the LDS chunk pairing {2s, 2s+8, 2s+1, 2s+9}).  A half runs its own k-steps of every tap
-// first (they read only its own previous epilogue) and the other half's second, so it waits for its own half's
-// epilogue before a layer and for the other half's only half way through it: one half's epilogue runs under the
-// other half's MFMAs.  The two waves of a SIMD belong to different halves (and different position groups, so every
-// SIMD keeps 15 tiles).  Hand-offs are LDS counters (epilogues done per half); the board's last layer still ends in
-// a workgroup barrier.  2 = 1 with half 0 at a raised issue priority (it leads, half 1 fills its epilogues).
-template <int H, bool DYN, int ABL = 0, int RD = 4, int NQ = 2, int PG = 4, int NB = 1, typename E = F16, int PIPE = 0>
+// The timing ablations of this kernel and its PIPE variant (the layer hand-off as a two-half pipeline, measured 1 %
+// slower) live in a copy for the tools/ harnesses (tools/tower_ablation_kernel.inc, k_tower3_abl): the product kernel
+// keeps only code that gives correct results.
+template <int H, bool DYN, int RD = 4, int NQ = 2, int PG = 4, int NB = 1, typename E = F16>
 __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
   using G = Geo<H>;
   using I = Img3<H>;
@@ -198,7 +186,7 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
   // REMAP (15x15, one board per workgroup, two images): the border-tile order (remap15); each of the two wave groups
   // has its own k-loop instantiation (8 and 7 tiles), so a tile's skipped taps are known at compile time
   constexpr bool REMAP = H == 15 && NB == 1 && PG == 2 && NPTB == 15;
-  constexpr bool LAST_ONE = !PIPE && !REMAP && NPTB == PG * (PTW - 1) + 1;
+  constexpr bool LAST_ONE = !REMAP && NPTB == PG * (PTW - 1) + 1;
   constexpr unsigned LAST_TAPS = LAST_ONE ? live_taps(H, (NPTB - 1) * 16, NB * A < NPTB * 16 ? NB * A : NPTB * 16) : 0x1ffu;
   static_assert(LAST_TAPS & 1u, "tap 0 of the last tile starts its accumulation");
   constexpr int PS = I::PS, RS = I::RS, IMG = I::BYTES;
@@ -285,19 +273,13 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
     finish_launch();
     return;
   }
-  constexpr bool PP = PIPE != 0;
-  // PIPE branches per half on w: a scalar there.  Elsewhere w stays a VGPR value: a scalar w changed the product
-  // kernels' register allocation (19x19: 39 instead of 12 scratch reloads; 15x15: +3 % instructions)
-  const int tid = threadIdx.x, w = PP ? __builtin_amdgcn_readfirstlane(tid >> 6) : tid >> 6, lane = tid & 63;
-  static_assert(!PP || (NB == 1 && !ONE && NQ == 4 && PG == 2), "the half pipeline is the 15x15 8-wave two-image tower's");
+  // w stays a VGPR value (a scalar w, readfirstlane, changed the register allocation: 19x19 39 instead of 12 scratch
+  // reloads, 15x15 +3 % instructions)
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   // wave w -> (channel group nh, position group pg) = (w % NQ, w / NQ): the waves sharing a SIMD
   // (w, w+4, ...) get different position groups, so a short last group does not load one SIMD less.
-  // PIPE: w -> half hh = w / 4, quarter hh + 2 (w & 1), position group (w >> 1) & 1 (half 0) or its complement
-  // (half 1): SIMD j hosts one wave of each half and of each position group
-  const int hh = PP ? (w >> 2) : 0;
-  const int nh = PP ? hh + 2 * (w & 1) : w % NQ;
-  const int pg = PP ? (hh == 0 ? ((w >> 1) & 1) : 1 - ((w >> 1) & 1)) : w / NQ;
-  if constexpr (PIPE == 2) if (hh == 0) __builtin_amdgcn_s_setprio(1);
+  const int nh = w % NQ;
+  const int pg = w / NQ;
   const int g4 = lane >> 4;
   const int cg = (g4 & 1) * 8 + (g4 >> 1);  // {0, 8, 1, 9}
   auto cell = [&](int p) { return (p / H + 1) * RS + (p % H + 1) * PS; };
@@ -318,28 +300,12 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
                                          16, 0, 0);
     }
   };
-  // ---- bias of layer L -> sbias[slot]: one 512 B LDS-DMA by wave 0 (32 lanes); PIPE: each half's first wave
-  //      DMAs its own half's channels (quarters hh and hh + 2: 2 x 128 B), the only ones its half reads
+  // ---- bias of layer L -> sbias[slot]: one 512 B LDS-DMA by wave 0 (32 lanes)
   auto issue_bias = [&](int L, int slot) {
-    if constexpr (PP) {
-      if ((w & 3) == 0 && lane < 8) {
-#pragma unroll
-        for (int q = 0; q < 2; ++q)
-          __builtin_amdgcn_global_load_lds((const void *)(t.bias + L * C + (hh + 2 * q) * 32 + lane * 4),
-                                           (__attribute__((address_space(3))) void *)(sbias + slot * C + (hh + 2 * q) * 32),
-                                           16, 0, 0);
-      }
-    } else if (w == 0 && lane < 32) {
+    if (w == 0 && lane < 32) {
       __builtin_amdgcn_global_load_lds((const void *)(t.bias + L * C + lane * 4),
                                        (__attribute__((address_space(3))) void *)(sbias + slot * C), 16, 0, 0);
     }
-  };
-  // ---- PIPE hand-offs: s_cnt[h] = epilogues finished by half h's 4 waves (cumulative over this workgroup's layers)
-  __shared__ int s_cnt[2];
-  auto wait_cnt = [&](int h, int target) {
-    volatile int *c = s_cnt + h;
-    while (*c < target) __builtin_amdgcn_s_sleep(1);
-    asm volatile("" ::: "memory");
   };
 
   // ---- zero both images (borders and pads), biases of layer 0, action term
@@ -347,11 +313,10 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
   // ds_write_b32 per 16 B)
   for (int i = tid; i < IMGS / 16; i += NTHR) ((uint4 *)smem)[i] = make_uint4(0, 0, 0, 0);
   if (tid < C) sbias[tid] = t.bias[tid];
-  if (tid < 2) s_cnt[tid] = 0;
   if (DYN)
     for (int i = tid; i < 9 * C; i += NTHR) saction[i] = t.action_term[i];
   __syncthreads();  // zeroing done before the DMA writes the interior
-  if constexpr (DYN && !(ABL & 32))
+  if constexpr (DYN)
 #pragma unroll
     for (int b = 0; b < NB; ++b) issue_input(rr[b], b);
 
@@ -397,41 +362,17 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
   static_assert(KSTEPS % RD == 0, "ring slots must repeat per layer");
   V8 ar[RD][NTW];
   auto loadA = [&](int slot, int gs) {
-    if constexpr ((ABL & 2) != 0) if (gs >= 2) return;  // ablation: no weight stream in the loop
-    int g = gs < total_ks ? gs : gs - total_ks;
-    if constexpr ((ABL & 2048) != 0) if (g >= ABL_ALIAS_KS) g -= ABL_ALIAS_KS;  // ablation: weight set <= 3.5 MB
-    const int soff = (ABL & 1) ? 0 : g * 8192;  // ablation 1: L1-resident
-    if ((ABL & 4096) != 0 && g >= ABL_ALIAS_KS) {  // ablation: the tail past 3.5 MB streamed non-temporal
-#pragma unroll
-      for (int nt = 0; nt < NTW; ++nt)
-        ar[slot][nt] = __builtin_bit_cast(V8, __builtin_amdgcn_raw_buffer_load_b128(wrsrc, wvoff + nt * 1024, soff, 2));
-      return;
-    }
+    const int g = gs < total_ks ? gs : gs - total_ks;
+    const int soff = g * 8192;
 #pragma unroll
     for (int nt = 0; nt < NTW; ++nt) {
       const auto v = __builtin_amdgcn_raw_buffer_load_b128(wrsrc, wvoff + nt * 1024, soff, 0);
       ar[slot][nt] = __builtin_bit_cast(V8, v);
     }
   };
-  // PIPE: k-step s of layer Lk in the half's order: s < 18 -> tap s / 2, k-step 2 hh + (s & 1) (own half's input
-  // chunks), s >= 18 -> tap (s - 18) / 2, k-step 2 (1 - hh) + (s & 1); Lk = n_layers is the next board's layer 0
-  const int hown = hh * 16384, hoth = (1 - hh) * 16384;
-  auto loadAp = [&](int slot, int Lk, int s) {
-    const int Lw = Lk < t.n_layers ? Lk : Lk - t.n_layers;
-    const int tap = (s < 18 ? s : s - 18) >> 1;
-    const int soff = (Lw * KSTEPS + tap * 4 + (s & 1)) * 8192 + (s < 18 ? hown : hoth);
 #pragma unroll
-    for (int nt = 0; nt < NTW; ++nt)
-      ar[slot][nt] = __builtin_bit_cast(V8, __builtin_amdgcn_raw_buffer_load_b128(wrsrc, wvoff + nt * 1024, soff, 0));
-  };
-#pragma unroll
-  for (int k = 0; k < RD - 1; ++k) {
-    if constexpr (PP) loadAp(k, 0, k);
-    else loadA(k, k);
-  }
+  for (int k = 0; k < RD - 1; ++k) loadA(k, k);
   int gl = 0;  // layers run by this workgroup so far: bias slot = gl & 1
-  uint64_t st_loop = 0, st_epi = 0, st_bar = 0, st_t0 = 0, st_t1 = 0, st_t2 = 0;  // ABL & 128 stamps
-  const uint64_t st_start = (ABL & 128) ? __builtin_amdgcn_s_memtime() : 0;
 
   while (rr[0] < t.rows) {
     if constexpr (!DYN) {  // ---- REPR stem (one MFMA k-step on an im2col operand) -> img0
@@ -491,11 +432,6 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
     for (int L = 0; L < t.n_layers; ++L, ++gl) {
       const uint8_t *img = smem + (ONE ? 0 : (L & 1) * IMG);
       uint8_t *nimg = smem + (ONE ? 0 : ((L + 1) & 1) * IMG);
-      if constexpr (PP) {  // own half's epilogues of the previous layer (its bias DMA landed before them)
-        if (ABL & 128) st_t2 = __builtin_amdgcn_s_memtime();
-        wait_cnt(hh, 4 * gl);
-        if (ABL & 128) st_bar += __builtin_amdgcn_s_memtime() - st_t2;
-      }
       // the next layer's bias (for the last layer: the next board's layer 0) -> the other slot;
       // that slot was last read by the previous layer's epilogue, which the barrier has closed
       issue_bias(L + 1 < t.n_layers ? L + 1 : 0, (gl + 1) & 1);
@@ -509,7 +445,7 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
       int bb[PTW];
 #pragma unroll
       for (int i = 0; i < PTW; ++i) {
-        bb[i] = (pos[i] < 0 ? ~pos[i] : pos[i]) + cg * 16 + (int)(size_t)(img - smem) + (PP ? 64 * hh : 0);
+        bb[i] = (pos[i] < 0 ? ~pos[i] : pos[i]) + cg * 16 + (int)(size_t)(img - smem);
         asm volatile("" : "+v"(bb[i]));  // one base VGPR per tile and layer; all else immediates
       }
       // k-loop over the NTL tiles this wave owns (NTL = PTW, or PTW - 1 for a short last position
@@ -531,43 +467,13 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
         auto live = [&](int i, int st) { return ((taps(i) >> (st >> 2)) & 1u) != 0; };
         auto first = [&](int i) { return 4 * __builtin_ctz(taps(i)); };
         auto readB = [&](int buf, int st) {
-          const int tap = PP ? (st < 18 ? st : st - 18) >> 1 : st >> 2, ks = PP ? (st & 1) : st & 3;
+          const int tap = st >> 2, ks = st & 3;
           const int off = (tap / 3) * RS + (tap % 3) * PS + ks * 32;
 #pragma unroll
           for (int i = 0; i < NTL; ++i)
-            if (PP || live(i, st)) b[buf][i] = *(const V8 *)(smem + bb[i] + off);
+            if (live(i, st)) b[buf][i] = *(const V8 *)(smem + bb[i] + off);
         };
         readB(0, 0);
-        if constexpr (PP) {
-          if (ABL & 128) st_t0 = __builtin_amdgcn_s_memtime();
-#pragma unroll
-          for (int st = 0; st < KSTEPS; ++st) {
-            const int sn = st + RD - 1;
-            if (sn < KSTEPS) loadAp(sn % RD, L, sn);
-            else loadAp(sn % RD, L + 1, sn - KSTEPS);
-            if (st + 1 < KSTEPS && st + 1 != 18) readB((st + 1) & 1, st + 1);
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int i = 0; i < NTL; ++i)
-#pragma unroll
-              for (int nt = 0; nt < NTW; ++nt)
-                acc[nt][i] = E::mfma(ar[st % RD][nt], b[st & 1][i], st == 0 ? bv[nt] : acc[nt][i]);
-            if (st == 17) {  // half way: the other half's chunks, written by its epilogues of the previous layer
-              __builtin_amdgcn_sched_barrier(0);
-              uint64_t tw = 0;
-              if (ABL & 128) tw = __builtin_amdgcn_s_memtime();
-              wait_cnt(1 - hh, 4 * gl);
-              if (ABL & 128) st_bar += __builtin_amdgcn_s_memtime() - tw;
-              const int dsw = 64 - 128 * hh;
-#pragma unroll
-              for (int i = 0; i < NTL; ++i) bb[i] += dsw;
-              readB(0, 18);
-            }
-            if ((ABL & 256) || st + 1 < KSTEPS) __builtin_amdgcn_sched_barrier(0);
-          }
-          return;
-        }
-        if (ABL & 128) st_t0 = __builtin_amdgcn_s_memtime();
         const int gs0 = L * KSTEPS;
 #pragma unroll
         for (int st = 0; st < KSTEPS; ++st) {
@@ -582,14 +488,13 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
               for (int nt = 0; nt < NTW; ++nt)
                 acc[nt][i] = E::mfma(ar[st % RD][nt], b[st & 1][i], st == first(i) ? bv[nt] : acc[nt][i]);
           // the last k-step stays open: the scheduler may start the epilogue of the tiles whose final
-          // MFMA has issued while the remaining ones run (ABL & 256 pins it, for comparison)
-          if ((ABL & 256) || st + 1 < KSTEPS) __builtin_amdgcn_sched_barrier(0);
+          // MFMA has issued while the remaining ones run
+          if (st + 1 < KSTEPS) __builtin_amdgcn_sched_barrier(0);
         }
       };
       if constexpr (PTW * PG == NPTB) kloop(std::integral_constant<int, PTW>{});
       else if (pg + PG * (PTW - 1) < NPTB) kloop(std::integral_constant<int, PTW>{});
       else kloop(std::integral_constant<int, PTW - 1>{});
-      if (ABL & 128) { st_t1 = __builtin_amdgcn_s_memtime(); st_loop += st_t1 - st_t0; }
       // epilogue: (action term) (+ residual) + ReLU -> E -> the other image.  One straight-line
       // copy per layer kind; every LDS operand (residual) is read in one batch before any
       // arithmetic, so the epilogue pays one LDS latency, not one per tile.
@@ -656,30 +561,13 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
           if constexpr (ONE) __builtin_amdgcn_sched_barrier(0);
         }
       };
-      if constexpr ((ABL & 512) != 0) {  // ablation: no epilogue (timing only; acc kept live)
-#pragma unroll
-        for (int nt = 0; nt < NTW; ++nt)
-#pragma unroll
-          for (int i = 0; i < PTW; ++i) asm volatile("" ::"v"(acc[nt][i]));
-      } else if (DYN && kind == 0) epilogue(std::integral_constant<int, 0>{});
+      if (DYN && kind == 0) epilogue(std::integral_constant<int, 0>{});
       else if (kind == 1) epilogue(std::integral_constant<int, 1>{});
       else epilogue(std::integral_constant<int, 2>{});
       // the bias DMA (issued before this layer's 36 k-steps) is older than the (RD-1)*NTW ring loads
       // still in flight: this count retires it before the barrier publishes the slot
-      if (w == 0 || (PP && w == 4)) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((RD - 1) * NTW) : "memory");
-      if (ABL & 128) { st_t2 = __builtin_amdgcn_s_memtime(); st_epi += st_t2 - st_t1; }
-      if constexpr (PP) {
-        // this wave's epilogue stores (and, for the half's first wave, the bias DMA) are complete: count it
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (lane == 0) __hip_atomic_fetch_add(s_cnt + hh, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (L == t.n_layers - 1) {
-          __syncthreads();  // the board's output stage reads every channel
-          if (ABL & 128) st_bar += __builtin_amdgcn_s_memtime() - st_t2;
-        }
-      } else {
-        if constexpr (!(ABL & 1024)) __syncthreads();  // ablation 1024: no per-layer barrier (timing only)
-        if (ABL & 128) st_bar += __builtin_amdgcn_s_memtime() - st_t2;
-      }
+      if (w == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((RD - 1) * NTW) : "memory");
+      __syncthreads();
     }
 
     // ---- next boards' input -> the free images, overlapped with these boards' output stage
@@ -688,7 +576,7 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
     for (int b = 0; b < NB; ++b) nrr[b] = rr[b];
     if (dsched) rr[0] = s_row;
     else take_rows(rr[NB - 1] + gridDim.x);
-    if constexpr (DYN && !ONE && !(ABL & 32)) {
+    if constexpr (DYN && !ONE) {
       if (rr[0] < t.rows)  // DYN has 1 + 2*blocks (odd) layers: the result is in img[1]
 #pragma unroll
         for (int b = 0; b < NB; ++b) issue_input(rr[b], b);
@@ -698,7 +586,7 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
     if (b > 0 && nrr[b] == nrr[b - 1]) break;  // a repeated row: already stored
     const int r = nrr[b], os = t.out_slot[r];
     const uint8_t *fin = smem + bbase(b) + (ONE ? 0 : (t.n_layers & 1) * IMG);
-    if (!(ABL & 32)) {
+    {
       uint4 *dst = (uint4 *)(t.pool + (size_t)os * A * C);
       for (int i = tid; i < A * 16; i += NTHR) dst[i] = *(const uint4 *)(fin + cell(i >> 4) + (i & 15) * 16);
       for (int i = tid; i < pv_stride(A); i += NTHR) {  // head 1x1 convs -> pv row (zero pads)
@@ -723,16 +611,11 @@ __global__ void __launch_bounds__(64 * NQ * PG) k_tower3(TowerArgs t) {
     }
     }
     __syncthreads();  // the next board's layer 0 overwrites img[1]
-    if constexpr (DYN && ONE && !(ABL & 32)) {
+    if constexpr (DYN && ONE) {
       if (rr[0] < t.rows) issue_input(rr[0], 0);  // single image: only now is it free
     }
   }
   finish_launch();
-  if ((ABL & 128) && lane == 0) {  // diagnostic build only: per-wave phase cycles -> pv_feat
-    float *o = t.pv_feat + (blockIdx.x * NW + w) * 4;
-    o[0] = (float)st_loop; o[1] = (float)st_epi; o[2] = (float)st_bar;
-    o[3] = (float)(__builtin_amdgcn_s_memtime() - st_start);
-  }
 }
 
 // ---- prediction / reward heads (network.py:66-88): two launches per batch
@@ -971,7 +854,7 @@ static int launch_tower(const TowerArgs &a, hipStream_t s) {
   const int need = (a.rows + T::NB - 1) / T::NB;
   const int cus = (a.max_grid > 0 && a.max_grid < cu_count()) ? a.max_grid : cu_count();
   const int grid = need < cus ? need : cus;
-  hipLaunchKernelGGL((k_tower3<H, DYN, 0, T::RD, T::NQ, T::PG, T::NB, E>), dim3(grid), dim3(64 * T::NQ * T::PG), 0, s, a);
+  hipLaunchKernelGGL((k_tower3<H, DYN, T::RD, T::NQ, T::PG, T::NB, E>), dim3(grid), dim3(64 * T::NQ * T::PG), 0, s, a);
   GMZ_LAUNCH_CHECK();
   return 0;
 }

@@ -2,6 +2,7 @@
 // one process, same random data).  Build: hipcc -O3 --offload-arch=gfx950 -std=c++17
 //   -ffp-contract=off -Iinclude tools/tower_ablate.hip -o /tmp/tower_ablate
 #include "../datou-gomoku-muzero_amd/csrc/gmz_net.hip"
+#include "tower_ablation_kernel.inc"  // k_tower3_abl: the tower with its timing ablations (not in the product)
 #include "tower_k1.hip"  // the first tower kernel (bit-exact reference of the bf16 path)
 #include <cstdio>
 #include <vector>
@@ -26,7 +27,7 @@ float run(const TowerArgs &a, int reps) {
   (void)hipEventRecord(e0, 0);
   for (int i = 0; i < reps; ++i) {
     if (V == 1) hipLaunchKernelGGL((k_tower<15, true, ABL>), dim3(a.rows), dim3(512), 0, 0, a);
-    else hipLaunchKernelGGL((k_tower3<15, true, ABL, RD, NQ, PG, 1, Bf16>), dim3(256), dim3(64 * NQ * PG), 0, 0, a);
+    else hipLaunchKernelGGL((k_tower3_abl<15, true, ABL, RD, NQ, PG, 1, Bf16>), dim3(256), dim3(64 * NQ * PG), 0, 0, a);
   }
   (void)hipEventRecord(e1, 0);
   (void)hipEventSynchronize(e1);
@@ -85,7 +86,7 @@ int main(int argc, char **argv) {
     CK(hipMemcpy(p1.data(), dpv, p1.size() * 4, hipMemcpyDeviceToHost));
     CK(hipMemset(dpool + (size_t)rows * A * 128, 0, o1.size() * 2));
     CK(hipMemset(dpv, 0, p1.size() * 4));
-    hipLaunchKernelGGL((k_tower3<15, true, 0, 4, 2, 4, 1, Bf16>), dim3(256), dim3(512), 0, 0, a3);
+    hipLaunchKernelGGL((k_tower3_abl<15, true, 0, 4, 2, 4, 1, Bf16>), dim3(256), dim3(512), 0, 0, a3);
     CK(hipMemcpy(o2.data(), dpool + (size_t)rows * A * 128, o2.size() * 2, hipMemcpyDeviceToHost));
     CK(hipMemcpy(p2.data(), dpv, p2.size() * 4, hipMemcpyDeviceToHost));
     size_t dh = 0, dp = 0;
@@ -95,7 +96,7 @@ int main(int argc, char **argv) {
     printf("tower3 vs tower: hidden mismatches %zu / %zu (max |diff| %g), pv mismatches %zu / %zu\n", dh, o1.size(), mxd, dp, p1.size());
     CK(hipMemset(dpool + (size_t)rows * A * 128, 0, o1.size() * 2));
     CK(hipMemset(dpv, 0, p1.size() * 4));
-    hipLaunchKernelGGL((k_tower3<15, true, 0, 3, 4, 3, 1, Bf16>), dim3(256), dim3(768), 0, 0, a3);
+    hipLaunchKernelGGL((k_tower3_abl<15, true, 0, 3, 4, 3, 1, Bf16>), dim3(256), dim3(768), 0, 0, a3);
     CK(hipMemcpy(o2.data(), dpool + (size_t)rows * A * 128, o2.size() * 2, hipMemcpyDeviceToHost));
     CK(hipMemcpy(p2.data(), dpv, p2.size() * 4, hipMemcpyDeviceToHost));
     dh = dp = 0;
@@ -105,7 +106,7 @@ int main(int argc, char **argv) {
     printf("tower3 12w vs tower: hidden mismatches %zu / %zu (max |diff| %g), pv mismatches %zu / %zu\n", dh, o1.size(), mxd, dp, p1.size());
     CK(hipMemset(dpool + (size_t)rows * A * 128, 0, o1.size() * 2));
     CK(hipMemset(dpv, 0, p1.size() * 4));
-    hipLaunchKernelGGL((k_tower3<15, true, 0, 3, 4, 2, 1, Bf16>), dim3(256), dim3(512), 0, 0, a3);
+    hipLaunchKernelGGL((k_tower3_abl<15, true, 0, 3, 4, 2, 1, Bf16>), dim3(256), dim3(512), 0, 0, a3);
     CK(hipMemcpy(o2.data(), dpool + (size_t)rows * A * 128, o2.size() * 2, hipMemcpyDeviceToHost));
     CK(hipMemcpy(p2.data(), dpv, p2.size() * 4, hipMemcpyDeviceToHost));
     dh = dp = 0;

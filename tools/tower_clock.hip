@@ -6,6 +6,7 @@
 //   clock = the longest wave's lifetime in cycles / the launch's wall time (HIP events).
 // Build: hipcc -O3 --offload-arch=gfx950 -std=c++17 -ffp-contract=off -Iinclude tools/tower_clock.hip -o tools/tower_clock.bin
 #include "../datou-gomoku-muzero_amd/csrc/gmz_net.hip"
+#include "tower_ablation_kernel.inc"  // k_tower3_abl: the tower with its timing ablations (not in the product)
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -25,7 +26,7 @@ template <int ABL, int PIPE = 0>
 static void launch(TowerArgs a, int grid, unsigned long long gen) {
   using T = TowerCfg<15>;
   a.gen = gen;
-  hipLaunchKernelGGL((k_tower3<15, true, ABL, T::RD, T::NQ, T::PG, T::NB, F16, PIPE>), dim3(grid), dim3(64 * T::NQ * T::PG), 0,
+  hipLaunchKernelGGL((k_tower3_abl<15, true, ABL, T::RD, T::NQ, T::PG, T::NB, F16, PIPE>), dim3(grid), dim3(64 * T::NQ * T::PG), 0,
                      0, a);
 }
 
@@ -33,7 +34,7 @@ static void launch(TowerArgs a, int grid, unsigned long long gen) {
 template <int ABL, int NQ, int PG, int RD>
 static void launch_dec(TowerArgs a, int grid, unsigned long long gen) {
   a.gen = gen;
-  hipLaunchKernelGGL((k_tower3<15, true, ABL, RD, NQ, PG, 1, F16>), dim3(grid), dim3(64 * NQ * PG), 0, 0, a);
+  hipLaunchKernelGGL((k_tower3_abl<15, true, ABL, RD, NQ, PG, 1, F16>), dim3(grid), dim3(64 * NQ * PG), 0, 0, a);
 }
 
 static uint16_t half_bits(float f) {

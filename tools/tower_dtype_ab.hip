@@ -4,6 +4,7 @@
 // s_memtime phase stamps (ABL 128).  Build:
 //   hipcc -O3 --offload-arch=gfx950 -std=c++17 -ffp-contract=off -Iinclude tools/tower_dtype_ab.hip -o /tmp/tower_dtype_ab
 #include "../datou-gomoku-muzero_amd/csrc/gmz_net.hip"
+#include "tower_ablation_kernel.inc"  // k_tower3_abl: the tower with its timing ablations (not in the product)
 #include <cstdio>
 #include <cstring>
 #include <random>
@@ -33,7 +34,7 @@ static float run(const TowerArgs &a, int reps) {
   (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
   (void)hipEventRecord(e0, 0);
   for (int i = 0; i < reps; ++i)
-    hipLaunchKernelGGL((k_tower3<15, true, ABL, 3, 4, 2, 1, E>), dim3(256), dim3(512), 0, 0, a);
+    hipLaunchKernelGGL((k_tower3_abl<15, true, ABL, 3, 4, 2, 1, E>), dim3(256), dim3(512), 0, 0, a);
   (void)hipEventRecord(e1, 0);
   (void)hipEventSynchronize(e1);
   float ms; (void)hipEventElapsedTime(&ms, e0, e1);
@@ -98,8 +99,8 @@ int main(int argc, char **argv) {
     cyc /= 256 * 8;
     printf("%-10s stamps: kernel %.0f cycles (s_memtime) in %.3f ms\n", what, cyc, ms);
   };
-  clock("bf16", ab, [&] { hipLaunchKernelGGL((k_tower3<15, true, 128, 3, 4, 2, 1, Bf16>), dim3(256), dim3(512), 0, 0, ab); });
-  clock("f16", ah, [&] { hipLaunchKernelGGL((k_tower3<15, true, 128, 3, 4, 2, 1, F16>), dim3(256), dim3(512), 0, 0, ah); });
+  clock("bf16", ab, [&] { hipLaunchKernelGGL((k_tower3_abl<15, true, 128, 3, 4, 2, 1, Bf16>), dim3(256), dim3(512), 0, 0, ab); });
+  clock("f16", ah, [&] { hipLaunchKernelGGL((k_tower3_abl<15, true, 128, 3, 4, 2, 1, F16>), dim3(256), dim3(512), 0, 0, ah); });
   CK(hipDeviceSynchronize());
   return 0;
 }

@@ -5,6 +5,7 @@
 // at 1,024 rows on every CU and at 512 rows on 192 CUs (the two-stream step's launch).
 // Build: hipcc -O3 --offload-arch=gfx950 -std=c++17 -ffp-contract=off -Iinclude tools/tower_pair_ab.hip -o tools/tower_pair_ab.bin
 #include "../datou-gomoku-muzero_amd/csrc/gmz_net.hip"
+#include "tower_ablation_kernel.inc"  // k_tower3_abl: the tower with its timing ablations (not in the product)
 #include "tower_pair.hip"
 #include <cstdio>
 #include <vector>
@@ -22,7 +23,7 @@ template <bool DYN, int V>
 static void launch(const TowerArgs &a0, int grid) {
   TowerArgs a = a0;
   a.gen = next_gen();  // k_tower3's ticket generation (one per launch)
-  if (V == 0) hipLaunchKernelGGL((k_tower3<15, DYN, 0, 3, 4, 2, 1, F16>), dim3(grid), dim3(512), 0, 0, a);
+  if (V == 0) hipLaunchKernelGGL((k_tower3_abl<15, DYN, 0, 3, 4, 2, 1, F16>), dim3(grid), dim3(512), 0, 0, a);
   else {
     (void)hipMemsetAsync(a.tickets, 0, 8, 0);  // k_tower_pair counts from 0 (a k_tower3 launch leaves its generation)
     hipLaunchKernelGGL((k_tower_pair<15, DYN, 0, 4, F16>), dim3(grid), dim3(512), 0, 0, a);

@@ -15,11 +15,12 @@
 // fold of the GEMM result into the 2x2 output accumulators (A^T M A, in registers) - with NO input
 // transform, NO epilogue and NO board I/O.  Every piece it leaves out only adds time, so its time per
 // board-layer is a LOWER BOUND of any Winograd tower of this layout.  Beside it, on the same box and
-// data: the product tower (k_tower3<15, DYN>, everything included) and its core (ABL 512 + 32: no
+// data: the product tower (k_tower3_abl<15, DYN>, everything included) and its core (ABL 512 + 32: no
 // epilogue, no board I/O), 1,024 boards on every CU.
 //
 // Build: hipcc -O3 --offload-arch=gfx950 -std=c++17 -ffp-contract=off -Iinclude tools/winograd_core_ab.hip -o tools/winograd_core_ab.bin
 #include "../datou-gomoku-muzero_amd/csrc/gmz_net.hip"
+#include "tower_ablation_kernel.inc"  // k_tower3_abl: the tower with its timing ablations (not in the product)
 #include <cstdio>
 #include <cstring>
 #include <random>
@@ -129,7 +130,7 @@ template <int ABL>
 static void launch_tower(const TowerArgs &a0, int grid) {
   TowerArgs a = a0;
   a.gen = next_gen();
-  hipLaunchKernelGGL((k_tower3<15, true, ABL, 3, 4, 2, 1, F16>), dim3(grid), dim3(512), 0, 0, a);
+  hipLaunchKernelGGL((k_tower3_abl<15, true, ABL, 3, 4, 2, 1, F16>), dim3(grid), dim3(512), 0, 0, a);
 }
 
 template <typename F>
@@ -203,7 +204,7 @@ int main(int argc, char **argv) {
     best[3] = fminf(best[3], timed(wino_nf, 10));
   }
   CK(hipDeviceSynchronize());
-  const char *names[4] = {"direct tower k_tower3<15,DYN> (product, everything)",
+  const char *names[4] = {"direct tower k_tower3_abl<15,DYN> (product, everything)",
                           "direct core (ABL 512|32: no epilogue, no board I/O)",
                           "winograd core (GEMMs + fold into 2x2 outputs; no transforms, epilogue, I/O)",
                           "winograd GEMMs only (no fold)"};
