@@ -509,6 +509,7 @@ def trainer_leg(args, world, rank, dist, backend):
             torch.cuda.synchronize()
             log("rank %d: trainer warm-up %.1f s (MIOpen Find, graph capture; target trunk %s)"
                 % (rank, time.perf_counter() - t_w, "f16" if target_f16 else "f32"))
+            tr.reset_allreduce_times()
             if dist:
                 dist.barrier()
             torch.cuda.synchronize()

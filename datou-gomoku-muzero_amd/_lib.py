@@ -79,6 +79,7 @@ _SIGS = {
     "gmz_bn_backward_stats": ([I, P, P, P, P, I, I, I, P, P, I, P, P, P, P, P, I, SZ, P, SZ, P, I], I),
     "gmz_grad_add_t": ([I, P, I, I, I, P, P], I),
     "gmz_grad_add_t_cols": ([I, P, I, I, I, I, I, P, P], I),
+    "gmz_comm_stamp": ([P, I, P], I),
     "gmz_head_conv1x1_forward": ([I, P, L, I, P, P, I, P, P, I, P, P, P], I),
     "gmz_head_conv1x1_workspace_bytes": ([L, I, P], I),
     "gmz_seg_bn_forward": ([I, P, P, I, I, I, I, P, P, ctypes.c_float, P, P, SZ, I, ctypes.c_float, P, P, P, P, P], I),
@@ -89,6 +90,8 @@ _SIGS = {
                             P], I),
     "gmz_conv3x3_forward_board_stats": ([I, I, P, P, P, I, P, P, I, P], I),
     "gmz_conv3x3_forward_stamp": ([I, I, P, P, P, I, P, P, I, P, P, I, SZ, P], I),
+    "gmz_conv3x3_forward_bnapply": ([I, I, P, P, P, P, P, I, P, P, P, I, P, P, I, P], I),
+    "gmz_bn_forward_deferred": ([I, P, P, I, I, I, ctypes.c_float, ctypes.c_float, P, P, P, P, P, I, SZ, P, SZ, P], I),
     "gmz_bn_forward_m": ([I, I, P, P, P, I, I, I, P, P, ctypes.c_float, ctypes.c_float, P, P, P, I, P, P, P, SZ, P, P], I),
     "gmz_bn_forward_stats_m": ([I, P, P, I, I, I, P, P, ctypes.c_float, ctypes.c_float, P, P, P, I, P, P, P, I, SZ, P, P],
                                I),

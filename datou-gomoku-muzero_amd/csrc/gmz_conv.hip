@@ -116,6 +116,18 @@ struct ActStamp {
   const float *table;     // [9][128]
 };
 
+// The training-mode BatchNorm (+ residual, ReLU) whose output is this conv's input, applied in the board-staging
+// prologue instead of a pass of its own (gmz_conv3x3_forward_bnapply; VERDICT r5 next #4, loss.py:70-111's residual
+// blocks): the prologue reads the BatchNorm's input z (and the residual), stages relu?((z - mean) * gamma * invstd +
+// beta (+ res)) into the LDS image and writes it to out, the normalised activation the backward needs — each of a
+// board's two channel-half workgroups its own 64 channels.  Same arithmetic and rounding as k_bnl_apply (gmz_train.hip).
+struct BnApply {
+  const uint16_t *z, *res;  // [N][A][128] the BatchNorm's input, the residual (or nullptr)
+  const float *gamma, *beta, *save;  // save = (mean, invstd) f32 [2][128] (gmz_bn_forward_deferred)
+  uint16_t *out;  // [N][A][128] the BatchNorm's output = this conv's input
+  int relu;
+};
+
 // (Measured and removed: one workgroup per board computing both channel halves from one DMA — forward 33.9 vs 28.7 us,
 // profiles/r04_trainer_ab_defer_target.txt; the next board's DMA issued before the epilogue; the timing ablations of
 // profiles/r05_conv_ablations.txt and r06_conv_lds_ab.txt, built from commit 3a54982's gmz_conv.hip with GMZ_CONV_ABL.)
@@ -125,11 +137,12 @@ struct ActStamp {
 // PB: the statistics partials per BOARD (stats [C][N][3], slot = board) instead of per workgroup, so a
 // consumer can take them over any board ranges: the trainer's batched consistency trunk (five unroll steps'
 // observations as one launch, each step's BatchNorm statistics over its own boards; gmz_bn_forward_seg).
-template <int H, typename T, int PG, bool BWD = false, bool PB = false>
+// BNA: the input is staged by the BatchNorm-apply prologue (BnApply ba) instead of the DMA of x.
+template <int H, typename T, int PG, bool BWD = false, bool PB = false, bool BNA = false>
 __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restrict__ x, const uint16_t *__restrict__ wpk,
                                                   uint16_t *__restrict__ y, int N, const uint8_t *__restrict__ mask,
                                                   double *__restrict__ stats, const uint16_t *__restrict__ addend,
-                                                  BnBwd bn, ActStamp as) {
+                                                  BnBwd bn, ActStamp as, BnApply ba) {
   using I = CImg<H>;
   using M = Mfma<T>;
   typedef typename M::V V;
@@ -149,6 +162,8 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
   __shared__ __attribute__((aligned(16))) uint8_t img[I::BYTES];
   static_assert(I::BYTES >= PG * 64 * 2 * 4, "stats scratch fits in the image");
   static_assert(!PB || !BWD, "per-board statistics: forward sums");
+  static_assert(!BNA || (!BWD && !PB), "BatchNorm-apply prologue: the forward with per-workgroup statistics");
+  static_assert(NTHR % 16 == 0, "BNA: a thread's chunk of every cell it stages is tid & 15");
   __shared__ float pbred[PB ? PG * 64 * 2 : 1];  // PB: [PG][64 channels of this half][2], per board
 
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
@@ -229,9 +244,73 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
                                          16, 0, 0);
     }
   };
+  // ---- BNA: board bd's BatchNorm output -> image interior (and out).  Thread tid always takes 8-channel chunk
+  // tid & 15 of a cell (NTHR is a multiple of 16); its channels' constants are re-read per board (L1 hits: kept live
+  // across the k-loop they spilled it), loads of U cells issued before any arithmetic
+  auto bn_stage = [&](int bd) {
+    // an opaque copy of tid per board: the 15 cells' addresses are re-derived here, not hoisted out of the board loop
+    // and kept live across the k-loop (which spilled it)
+    int t = tid;
+    asm volatile("" : "+v"(t));
+    const int bch = t & 15;
+    float bmu[8], bsc[8], bsh[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = bch * 8 + j;
+      bmu[j] = ba.save[c];
+      bsc[j] = ba.gamma[c] * ba.save[CC + c];
+      bsh[j] = ba.beta[c];
+    }
+    constexpr int NCH = A * 16, NI = (NCH + NTHR - 1) / NTHR, U = 8;
+    const size_t base = (size_t)bd * NCH;
+    const uint4 *zs = (const uint4 *)ba.z + base;
+    const uint4 *rs = ba.res ? (const uint4 *)ba.res + base : nullptr;
+    uint4 *os = (uint4 *)ba.out + base;
+    const bool mine = (bch >> 3) == half0;  // this workgroup's channel half of the output
+#pragma unroll
+    for (int i0 = 0; i0 < NI; i0 += U) {
+      uint4 zv[U], rv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = t + (i0 + u) * NTHR;
+        if (i0 + u < NI && i < NCH) {
+          zv[u] = zs[i];
+          if (rs) rv[u] = rs[i];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = t + (i0 + u) * NTHR;
+        if (!(i0 + u < NI && i < NCH)) continue;
+        const uint32_t *zw = (const uint32_t *)&zv[u], *rw = (const uint32_t *)&rv[u];
+        uint32_t ow[4];
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          uint32_t packed = 0;
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const int j = 2 * h + e;
+            float v = (M::value((uint16_t)(zw[h] >> (16 * e))) - bmu[j]) * bsc[j] + bsh[j];
+            if (rs) v += M::value((uint16_t)(rw[h] >> (16 * e)));
+            if (ba.relu) v = fmaxf(v, 0.f);
+            packed |= (uint32_t)M::bits(v) << (16 * e);
+          }
+          ow[h] = packed;
+        }
+        const uint4 o = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+        const int p = i >> 4;
+        ((uint4 *)(img + (p / H + 1) * RS + (p % H + 1) * PS))[bch] = o;
+        if (mine) os[i] = o;
+      }
+    }
+  };
   for (int b = b0; b < N; b += bstride) {
-    dma(b);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (BNA) {
+      bn_stage(b);
+    } else {
+      dma(b);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __syncthreads();
     const bool counted = stats && (!mask || mask[b]);
     nvalid += counted;
@@ -636,19 +715,21 @@ static int check_slots(const char *fn, const double *stats, int stats_slots, int
   return 0;
 }
 
-template <int H, typename T, bool BWD, bool PB = false>
+template <int H, typename T, bool BWD, bool PB = false, bool BNA = false>
 void launch_conv3_k(const void *x, const void *wpk, void *y, int N, const uint8_t *mask, double *stats, const void *addend,
-                    const BnBwd &bn, hipStream_t st, const ActStamp &as = ActStamp{}) {
-  hipLaunchKernelGGL((k_conv3<H, T, CONV_PG, BWD, PB>), dim3(conv3_grid(N)), dim3(128 * CONV_PG), 0, st,
+                    const BnBwd &bn, hipStream_t st, const ActStamp &as = ActStamp{}, const BnApply &ba = BnApply{}) {
+  hipLaunchKernelGGL((k_conv3<H, T, CONV_PG, BWD, PB, BNA>), dim3(conv3_grid(N)), dim3(128 * CONV_PG), 0, st,
                      (const uint16_t *)x, (const uint16_t *)wpk, (uint16_t *)y, N, mask, stats, (const uint16_t *)addend, bn,
-                     as);
+                     as, ba);
 }
 
 template <int H, typename T>
 int launch_conv3(const void *x, const void *wpk, void *y, int N, const uint8_t *mask, double *stats, const void *addend,
-                 const BnBwd &bn, hipStream_t st, bool per_board = false, const ActStamp &as = ActStamp{}) {
+                 const BnBwd &bn, hipStream_t st, bool per_board = false, const ActStamp &as = ActStamp{},
+                 const BnApply &ba = BnApply{}) {
   const bool bwd = bn.x != nullptr;
-  if (per_board) launch_conv3_k<H, T, false, true>(x, wpk, y, N, mask, stats, addend, bn, st, as);
+  if (ba.z) launch_conv3_k<H, T, false, false, true>(x, wpk, y, N, mask, stats, addend, bn, st, as, ba);
+  else if (per_board) launch_conv3_k<H, T, false, true>(x, wpk, y, N, mask, stats, addend, bn, st, as);
   else if (bwd) launch_conv3_k<H, T, true>(x, wpk, y, N, mask, stats, addend, bn, st, as);
   else launch_conv3_k<H, T, false>(x, wpk, y, N, mask, stats, addend, bn, st, as);
   GMZ_LAUNCH_CHECK();
@@ -657,10 +738,11 @@ int launch_conv3(const void *x, const void *wpk, void *y, int N, const uint8_t *
 
 template <typename T>
 int conv3_dispatch(int H, const void *x, const void *wpk, void *y, int N, const uint8_t *mask, double *stats, const void *addend,
-                   hipStream_t st, const BnBwd &bn = BnBwd{}, bool per_board = false, const ActStamp &as = ActStamp{}) {
+                   hipStream_t st, const BnBwd &bn = BnBwd{}, bool per_board = false, const ActStamp &as = ActStamp{},
+                   const BnApply &ba = BnApply{}) {
   switch (H) {
-    case 9: return launch_conv3<9, T>(x, wpk, y, N, mask, stats, addend, bn, st, per_board, as);
-    case 15: return launch_conv3<15, T>(x, wpk, y, N, mask, stats, addend, bn, st, per_board, as);
+    case 9: return launch_conv3<9, T>(x, wpk, y, N, mask, stats, addend, bn, st, per_board, as, ba);
+    case 15: return launch_conv3<15, T>(x, wpk, y, N, mask, stats, addend, bn, st, per_board, as, ba);
   }
   return fail("gmz_conv3x3: board size must be 9 or 15");
 }
@@ -751,6 +833,26 @@ GMZ_EXPORT int gmz_conv3x3_forward_stamp(int dtype, int H, const void *x, const 
   if (dtype == 1) return conv3_dispatch<__half>(H, x, packed, y, N, mask, stats, nullptr, st, BnBwd{}, false, as);
   if (dtype == 2) return conv3_dispatch<__hip_bfloat16>(H, x, packed, y, N, mask, stats, nullptr, st, BnBwd{}, false, as);
   return fail("gmz_conv3x3_forward_stamp: dtype must be 1 (f16) or 2 (bf16)");
+}
+
+GMZ_EXPORT int gmz_conv3x3_forward_bnapply(int dtype, int H, const void *bn_x, const void *bn_res, const float *gamma,
+                                           const float *beta, const float *bn_save, int relu, void *bn_y,
+                                           const void *packed, void *y, int N, const uint8_t *mask, double *stats,
+                                           int stats_slots, void *stream) {
+  if (!bn_x || !gamma || !beta || !bn_save || !bn_y || !packed || !y)
+    return fail("gmz_conv3x3_forward_bnapply: null operand");
+  if (N <= 0) return fail("gmz_conv3x3_forward_bnapply: N must be positive");
+  if (check_slots("gmz_conv3x3_forward_bnapply", stats, stats_slots, N, false)) return -1;
+  if (((uintptr_t)bn_x | (uintptr_t)bn_res | (uintptr_t)bn_y | (uintptr_t)packed | (uintptr_t)y) & 15)
+    return fail("gmz_conv3x3_forward_bnapply: operands must be 16-B aligned");
+  if (bn_y == bn_x || bn_y == bn_res || bn_y == y || y == bn_x)
+    return fail("gmz_conv3x3_forward_bnapply: the BatchNorm output, its input and the conv output must not alias");
+  hipStream_t st = (hipStream_t)stream;
+  const BnApply ba = {(const uint16_t *)bn_x, (const uint16_t *)bn_res, gamma, beta, bn_save, (uint16_t *)bn_y, relu};
+  if (dtype == 1) return conv3_dispatch<__half>(H, bn_y, packed, y, N, mask, stats, nullptr, st, BnBwd{}, false, ActStamp{}, ba);
+  if (dtype == 2)
+    return conv3_dispatch<__hip_bfloat16>(H, bn_y, packed, y, N, mask, stats, nullptr, st, BnBwd{}, false, ActStamp{}, ba);
+  return fail("gmz_conv3x3_forward_bnapply: dtype must be 1 (f16) or 2 (bf16)");
 }
 
 GMZ_EXPORT int gmz_conv3x3_forward(int dtype, int H, const void *x, const void *packed, void *y, int N, void *stream) {

@@ -830,10 +830,33 @@ __global__ void __launch_bounds__(256) k_grad_add_t(const T *__restrict__ src, i
   }
 }
 
+// The data-parallel step's communication clock (one lane; a kernel, so that it is captured into the step's HIP
+// graph beside the RCCL all-reduces, where host event timing is not available): phase 0 stamps bucket A's issue,
+// phase 1 bucket B's weight gradients done, phase 2 both buckets averaged and adds the two intervals to running
+// sums.  acc: int64 [5] = t0, t1, sum(t1 - t0), sum(t2 - t1), count; the 100 MHz constant clock.
+__global__ void k_comm_stamp(long long *acc, int phase) {
+  if (threadIdx.x != 0) return;
+  const long long t = (long long)__builtin_amdgcn_s_memrealtime();
+  if (phase < 2) {
+    acc[phase] = t;
+    return;
+  }
+  acc[2] += acc[1] - acc[0];
+  acc[3] += t - acc[1];
+  acc[4] += 1;
+}
+
 }  // namespace
 }  // namespace gmz
 
 using namespace gmz;
+
+GMZ_EXPORT int gmz_comm_stamp(int64_t *acc, int phase, void *stream) {
+  if (!acc || phase < 0 || phase > 2) return fail("gmz_comm_stamp: acc must be int64 [5], phase 0, 1 or 2");
+  hipLaunchKernelGGL(k_comm_stamp, dim3(1), dim3(64), 0, (hipStream_t)stream, (long long *)acc, phase);
+  GMZ_LAUNCH_CHECK();
+  return 0;
+}
 
 GMZ_EXPORT int gmz_grad_add_t_cols(int dtype, const void *src, int P, int C, int O, int ldo, int col0, float *dst,
                                    void *stream) {
@@ -1081,6 +1104,52 @@ GMZ_EXPORT int gmz_bn_backward_stats(int dtype, const void *x, const void *y, co
                                                      stats, ns, coef, st, accumulate);
   }
   return fail("gmz_bn_backward_stats: dtype must be 0 (f32), 1 (f16) or 2 (bf16)");
+}
+
+template <typename T>
+int bn_forward_deferred(const void *x, const uint8_t *mask, int B, int C, int S, float eps, float momentum, float *rm,
+                        float *rv, int64_t *nb, float *save, const double *stats, int ns, void *ws, hipStream_t st) {
+  if (!stats) {  // no producer partials: one reduction pass (channels-last)
+    ns = splits_for(B, C, S, 1);
+    if (nhwc_vec(C, sizeof(T), {x}) == 8)
+      hipLaunchKernelGGL((k_bnl_red<T, 0, 8>), dim3(ns), dim3(BN_THREADS), 0, st, (const T *)x, (const T *)nullptr,
+                         (const T *)nullptr, mask, B, C, S, (const float *)nullptr, 0, (double *)ws);
+    else
+      hipLaunchKernelGGL((k_bnl_red<T, 0, 2>), dim3(ns), dim3(BN_THREADS), 0, st, (const T *)x, (const T *)nullptr,
+                         (const T *)nullptr, mask, B, C, S, (const float *)nullptr, 0, (double *)ws);
+    GMZ_LAUNCH_CHECK();
+    stats = (const double *)ws;
+  }
+  hipLaunchKernelGGL(k_bn_finalize, dim3(C), dim3(fin_threads()), 0, st, stats, C, ns, ns, 1, 0, eps, momentum, save, rm,
+                     rv, nb, (float *)nullptr, (float *)nullptr, (float *)nullptr);
+  GMZ_LAUNCH_CHECK();
+  return 0;
+}
+
+GMZ_EXPORT int gmz_bn_forward_deferred(int dtype, const void *x, const uint8_t *mask, int B, int C, int S, float eps,
+                                       float momentum, float *running_mean, float *running_var, int64_t *num_batches,
+                                       float *save, const double *stats, int ns, size_t stats_bytes, void *ws,
+                                       size_t ws_bytes, void *stream) {
+  if (B <= 0 || C <= 0 || S <= 0 || (size_t)B * C * S >= (1ull << 31)) return fail("gmz_bn_forward_deferred: bad shape");
+  if (check_layout(1, C)) return -1;
+  if (!save || (!stats && (!x || !ws))) return fail("gmz_bn_forward_deferred: null operand");
+  if (stats) {
+    if (ns <= 0) return fail("gmz_bn_forward_deferred: ns must be positive");
+    if (check_parts("gmz_bn_forward_deferred", C, ns, stats_bytes)) return -1;
+  } else if (check_bn_ws("gmz_bn_forward_deferred", 1, B, C, S, ws_bytes)) {
+    return -1;
+  }
+  if ((running_mean == nullptr) != (running_var == nullptr)) return fail("gmz_bn_forward_deferred: running stats pair");
+  hipStream_t st = (hipStream_t)stream;
+  switch (dtype) {
+    case 0: return bn_forward_deferred<float>(x, mask, B, C, S, eps, momentum, running_mean, running_var, num_batches,
+                                              save, stats, ns, ws, st);
+    case 1: return bn_forward_deferred<__half>(x, mask, B, C, S, eps, momentum, running_mean, running_var, num_batches,
+                                               save, stats, ns, ws, st);
+    case 2: return bn_forward_deferred<__hip_bfloat16>(x, mask, B, C, S, eps, momentum, running_mean, running_var,
+                                                       num_batches, save, stats, ns, ws, st);
+  }
+  return fail("gmz_bn_forward_deferred: dtype must be 0 (f32), 1 (f16) or 2 (bf16)");
 }
 
 GMZ_EXPORT int gmz_bn_forward_stats(int dtype, const void *x, const void *res, int B, int C, int S, const float *gamma,

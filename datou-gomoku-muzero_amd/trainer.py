@@ -196,6 +196,33 @@ def _like(t, layout):
     return t.contiguous(memory_format=torch.channels_last) if layout == 1 else t.contiguous()
 
 
+# a training-mode BatchNorm (+ residual, ReLU) whose output is the input of a HIP 3x3 conv: its elementwise pass runs
+# in that conv's board-staging prologue (gmz_conv3x3_forward_bnapply, which also writes the output for the backward)
+# instead of a pass of its own: one launch and one read of the BatchNorm's input fewer per use
+DEFER_BN_APPLY = True
+
+
+class _PendingBN:
+    """A deferred BatchNorm output's recipe, attached to the (not yet written) output tensor as ``_gmz_pending``:
+    its input z, residual, gamma, beta, saved (mean, invstd) and ReLU flag.  Only _conv3_apply consumes it."""
+    __slots__ = ("z", "res", "gamma", "beta", "save", "relu")
+
+    def __init__(self, z, res, gamma, beta, save, relu):
+        self.z, self.res, self.gamma, self.beta, self.save, self.relu = z, res, gamma, beta, save, relu
+
+
+def _conv_takes_pending(conv, z):
+    """True when ``_conv3_apply(conv, y)`` of a training-mode BatchNorm output y of z's shape, dtype and layout
+    runs the HIP conv that can apply the BatchNorm in its prologue (the conditions of its single-segment path)."""
+    if not (DEFER_BN_APPLY and FUSED_BN and FUSED_CONV and not RELU_MASK and not FUSED_BN_BWD_STATS and z.is_cuda
+            and z.dim() == 4 and z.shape[1] == 128 and z.shape[2] == z.shape[3] and z.shape[2] in (9, 15)):
+        return False
+    if conv.weight.shape != (128, 128, 3, 3) or conv.bias is not None:
+        return False
+    dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else z.dtype
+    return dt == z.dtype and dt in _CONV_DTYPES and z.is_contiguous(memory_format=torch.channels_last)
+
+
 class _FusedMaskedBN(torch.autograd.Function):
     """Row-masked training-mode BatchNorm + residual + ReLU as three HIP kernels forward and three
     backward (``gmz_bn_forward`` / ``gmz_bn_backward``, csrc/gmz_train.hip), on NCHW or channels-last
@@ -205,7 +232,7 @@ class _FusedMaskedBN(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, gamma, beta, res, mask, running_mean, running_var, num_batches, eps, momentum, relu,
-                stats=None, link=None, bwd_link=False):
+                stats=None, link=None, bwd_link=False, defer=False):
         from . import _lib
         L = _lib.load()
         layout = _bn_layout(x)
@@ -221,7 +248,19 @@ class _FusedMaskedBN(torch.autograd.Function):
         if (RELU_MASK and relu and layout == 1 and C % 8 == 0 and x.dtype != torch.float32 and torch.is_grad_enabled()
                 and _aligned16(x, res, y) and not (FUSED_BN_BWD_STATS and bwd_link)):
             rmask = torch.empty(B * S * (C // 8), dtype=torch.uint8, device=x.device)
-        if stats is not None and layout == 1:  # statistics reduced by the producing conv's epilogue
+        if defer and layout == 1 and rmask is None and _aligned16(x, res, y):
+            # DEFER_BN_APPLY: statistics and running stats now; y is written by the consuming conv's prologue
+            # (gmz_conv3x3_forward_bnapply, _conv3_apply), which the caller guarantees comes next
+            ws = None if stats is not None else _bn_workspace(1, B, C, S, x.device)
+            _lib.check(L.gmz_bn_forward_deferred(_BN_DTYPES[x.dtype], _lib.ptr(x), _lib.ptr(mask), B, C, S, float(eps),
+                                                 float(momentum), _lib.ptr(running_mean), _lib.ptr(running_var),
+                                                 _lib.ptr(num_batches), _lib.ptr(save),
+                                                 None if stats is None else _lib.ptr(stats[0]),
+                                                 0 if stats is None else int(stats[1]),
+                                                 0 if stats is None else _lib.nbytes(stats[0]), _lib.ptr(ws),
+                                                 _lib.nbytes(ws), _lib.stream_ptr()))
+            y._gmz_pending = _PendingBN(x, res, gamma, beta, save, relu)
+        elif stats is not None and layout == 1:  # statistics reduced by the producing conv's epilogue
             if rmask is not None:
                 _lib.check(L.gmz_bn_forward_stats_m(_BN_DTYPES[x.dtype], _lib.ptr(x), _lib.ptr(res), B, C, S,
                                                     _lib.ptr(gamma), _lib.ptr(beta), float(eps), float(momentum),
@@ -311,8 +350,8 @@ class _FusedMaskedBN(torch.autograd.Function):
             # (_ResLink): autograd then has one gradient for the block input, no accumulation pass
             ctx.link.dres, dres = dres, None
         if acc:
-            return dx, None, None, dres, None, None, None, None, None, None, None, None, None, None
-        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None, None
+            return dx, None, None, dres, None, None, None, None, None, None, None, None, None, None, None
+        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None, None, None
 
 
 _WS_BYTES = {}
@@ -329,11 +368,13 @@ def _bn_workspace(layout, B, C, S, device):
     return torch.empty((_WS_BYTES[key] + 7) // 8, dtype=torch.float64, device=device)
 
 
-def _bn_act(mod, x, mask=None, res=None, relu=True, link=None, segments=1):
+def _bn_act(mod, x, mask=None, res=None, relu=True, link=None, segments=1, consumer=None):
     """relu?(BatchNorm(x) (+ res)) with row-masked training statistics (see ``_bn``).  Training-mode
     BatchNorm on the GPU runs the fused HIP kernels; eval mode and the CPU use PyTorch ops.  ``link``:
     the block's _ResLink, used when ``res`` is the very tensor its first HIP conv consumed.  ``segments``:
-    see ``_bn`` (no autograd: the batched consistency representations run under no_grad)."""
+    see ``_bn`` (no autograd: the batched consistency representations run under no_grad).  ``consumer``: the
+    3x3 conv that consumes the output next — when it can (``_conv_takes_pending``), the output is deferred to its
+    prologue (DEFER_BN_APPLY)."""
     if segments > 1 and mod.training:
         if FUSED_BN and x.is_cuda and x.dtype in _BN_DTYPES and _bn_layout(x) == 1 and not torch.is_grad_enabled():
             return _bn_seg(mod, x, mask, res, relu, segments)
@@ -347,9 +388,10 @@ def _bn_act(mod, x, mask=None, res=None, relu=True, link=None, segments=1):
         m = None if mask is None else mask.contiguous().view(torch.uint8)
         use = link if (link is not None and res is not None and link.xin is res) else None
         want = FUSED_BN_BWD_STATS and torch.is_grad_enabled() and (x.requires_grad or mod.weight.requires_grad)
+        defer = consumer is not None and _conv_takes_pending(consumer, x)
         return _FusedMaskedBN.apply(x, mod.weight, mod.bias, res, m, mod.running_mean, mod.running_var,
                                     mod.num_batches_tracked, mod.eps, mod.momentum, relu,
-                                    getattr(x, "_gmz_bnstats", None), use, want)
+                                    getattr(x, "_gmz_bnstats", None), use, want, defer)
     if (FUSED_BN and not mod.training and x.is_cuda and x.dtype in _BN_DTYPES and _bn_layout(x) is not None
             and not (torch.is_grad_enabled() and (x.requires_grad or mod.weight.requires_grad))):
         return _bn_eval(mod, x, res, relu)
@@ -492,11 +534,18 @@ def _packed_conv_weight(w, dtype, transpose, parent=None):
 _STATS_SLOTS = {}
 
 
-def _conv3x3_hip(x, packed, mask=None, stats=None, addend=None, bnb=None, bn_y=None):
+def _conv3x3_hip(x, packed, mask=None, stats=None, addend=None, bnb=None, bn_y=None, pend=None):
     """``bnb``: a _BnBwdLink whose BatchNorm output ``bn_y`` fed the forward conv: the output (its dy) also
-    gets that BatchNorm's backward dz sums, returned as ``bnb.bwd``."""
+    gets that BatchNorm's backward dz sums, returned as ``bnb.bwd``.  ``pend``: x is a deferred BatchNorm output
+    (_PendingBN), applied and written by this conv's prologue."""
     from . import _lib
     y = torch.empty_like(x, memory_format=torch.channels_last)
+    if pend is not None:
+        _lib.check(_lib.load().gmz_conv3x3_forward_bnapply(
+            _CONV_DTYPES[x.dtype], x.shape[2], _lib.ptr(pend.z), _lib.ptr(pend.res), _lib.ptr(pend.gamma),
+            _lib.ptr(pend.beta), _lib.ptr(pend.save), int(pend.relu), _lib.ptr(x), _lib.ptr(packed), _lib.ptr(y),
+            x.shape[0], _lib.ptr(mask), _lib.ptr(stats), _stats_slots_of(stats), _lib.stream_ptr()))
+        return y
     if bnb is not None:
         if addend is not None:
             addend = addend.to(x.dtype).contiguous(memory_format=torch.channels_last)
@@ -623,11 +672,11 @@ class _Conv3x3NHWC(torch.autograd.Function):
     converts it (what autocast's cast would do)."""
 
     @staticmethod
-    def forward(ctx, x, w, mask=None, stats=None, link=None, bnsrc=None):
+    def forward(ctx, x, w, mask=None, stats=None, link=None, bnsrc=None, pend=None):
         ctx.save_for_backward(x, w)
         ctx.link = link
         ctx.bnsrc = bnsrc  # the _BnBwdLink of the BatchNorm whose output x is (FUSED_BN_BWD_STATS)
-        return _conv3x3_hip(x, _packed_conv_weight(w, x.dtype, 0), mask, stats)
+        return _conv3x3_hip(x, _packed_conv_weight(w, x.dtype, 0), mask, stats, pend=pend)
 
     @staticmethod
     def backward(ctx, gy):
@@ -664,7 +713,7 @@ class _Conv3x3NHWC(torch.autograd.Function):
                     gw = None
                 else:
                     gw = gw.to(w.dtype)
-        return gx, gw, None, None, None, None
+        return gx, gw, None, None, None, None, None
 
 
 # the stamp table's dtype code for gmz_conv3x3_forward_stamp: the library takes f32 only and rejects anything else
@@ -808,12 +857,19 @@ def _conv3_apply(conv, x, bn=None, mask=None, link=None, segments=1):
             m = None if mask is None else mask.contiguous().view(torch.uint8)
             xin = x.to(dt)
             bnsrc = getattr(xin, "_gmz_bnsrc", None) if xin is x else None  # x = a BatchNorm's output, as is
-            y = _Conv3x3NHWC.apply(xin, conv.weight, m, None if st is None else st[0], link, bnsrc)
+            pend = getattr(x, "_gmz_pending", None)
+            if pend is not None:  # x is written by this conv's prologue (once: later readers see it written)
+                if xin is not x:
+                    raise RuntimeError("_conv3_apply: a deferred BatchNorm output needs a conv of its own dtype")
+                x._gmz_pending = None
+            y = _Conv3x3NHWC.apply(xin, conv.weight, m, None if st is None else st[0], link, bnsrc, pend)
             if link is not None:
                 link.xin = xin
             if st is not None:
                 y._gmz_bnstats = st
             return y
+    if getattr(x, "_gmz_pending", None) is not None:
+        raise RuntimeError("_conv3_apply: a deferred BatchNorm output reached a conv that cannot apply it")
     return conv(x)
 
 
@@ -825,15 +881,18 @@ class _Block(nn.Module):
         self.conv1, self.bn1 = _conv3(c, c), nn.BatchNorm2d(c, eps=1e-4)
         self.conv2, self.bn2 = _conv3(c, c), nn.BatchNorm2d(c, eps=1e-4)
 
-    def forward(self, x, mask=None, segments=1):
+    def forward(self, x, mask=None, segments=1, consumer=None):
+        """``consumer``: the 3x3 conv that consumes the block's output next (the next block's conv1), which may
+        then apply bn2 in its prologue (DEFER_BN_APPLY); bn1's output always goes to conv2."""
         if segments > 1:  # the batched consistency representations (no_grad): per-segment statistics
             y = _bn_act(self.bn1, _conv3_apply(self.conv1, x, self.bn1, mask, segments=segments), mask,
                         segments=segments)
             return _bn_act(self.bn2, _conv3_apply(self.conv2, y, self.bn2, mask, segments=segments), mask, res=x,
                            segments=segments)
         link = _ResLink() if (FUSED_RES_GRAD and torch.is_grad_enabled() and x.requires_grad) else None
-        y = _bn_act(self.bn1, _conv3_apply(self.conv1, x, self.bn1, mask, link=link), mask)
-        return _bn_act(self.bn2, _conv3_apply(self.conv2, y, self.bn2, mask), mask, res=x, link=link)
+        y = _bn_act(self.bn1, _conv3_apply(self.conv1, x, self.bn1, mask, link=link), mask, consumer=self.conv2)
+        return _bn_act(self.bn2, _conv3_apply(self.conv2, y, self.bn2, mask), mask, res=x, link=link,
+                       consumer=consumer)
 
 
 class _Trunk(nn.Module):
@@ -848,9 +907,20 @@ class _Trunk(nn.Module):
         self.resblocks = nn.Sequential(*[_Block(c) for _ in range(blocks)])
 
     def forward(self, x, mask=None, segments=1):
-        h = _bn_act(self.bn, self.conv(x), mask, segments=segments)
-        for blk in self.resblocks:
-            h = blk(h, mask, segments) if segments > 1 else blk(h, mask)
+        if segments > 1:
+            h = _bn_act(self.bn, self.conv(x), mask, segments=segments)
+            for blk in self.resblocks:
+                h = blk(h, mask, segments)
+            return h
+        return self._blocks(self.conv(x), mask)
+
+    def _blocks(self, z, mask):
+        """The stem's BatchNorm + ReLU of z, then the residual blocks; every BatchNorm output that a next block's
+        conv1 consumes is deferred to that conv's prologue (DEFER_BN_APPLY); the trunk's output is written."""
+        blocks = list(self.resblocks)
+        h = _bn_act(self.bn, z, mask, consumer=blocks[0].conv1 if blocks else None)
+        for i, blk in enumerate(blocks):
+            h = blk(h, mask, consumer=blocks[i + 1].conv1 if i + 1 < len(blocks) else None)
         return h
 
 
@@ -996,9 +1066,7 @@ class _Dynamics(_Trunk):
                                   None if st is None else st[0])
             if st is not None:
                 y._gmz_bnstats = st
-            x = _bn_act(self.bn, y, mask)
-            for blk in self.resblocks:
-                x = blk(x, mask)
+            x = self._blocks(y, mask)
             if not reward:
                 return x, None
             fc0, act, fc2 = self.reward_fc
@@ -1983,9 +2051,8 @@ class Trainer:
     the learning rate as a device tensor and the AMP inf-check handed to it on the device; with
     ``graph=True`` (default on cuda, GRADIENT_ACCUMULATION_STEPS == 1) the whole step — target-net
     bootstrap, loss, backward, unscale, clip, Adam, scale update, soft target update — is captured
-    once into a HIP graph and replayed (two graphs around the eager RCCL all-reduce when
-    distributed).  The batch is augmented eagerly into static input buffers before each replay.
-    The first ``graph_warmup`` steps run eagerly (they are real steps)."""
+    once into a HIP graph and replayed (distributed: with the RCCL all-reduces inside it).  The
+    batch is augmented eagerly into static input buffers before each replay.  The first ``graph_warmup`` steps run eagerly (they are real steps)."""
 
     def __init__(self, cfg=None, device="cuda", state_dict=None, amp=None, amp_dtype=None, channels_last=None,
                  graph=None, graph_warmup=3):
@@ -2034,7 +2101,10 @@ class Trainer:
         for p in layout:
             p.grad = self.flat_grad[off:off + p.numel()].as_strided(p.shape, p.stride())  # same layout as p
             off += p.numel()
-        self.comm_events = []  # [A issued, B's weight gradients done, both averaged] CUDA events per step (N > 1)
+        # the communication clock of the data-parallel step (gmz_comm_stamp, int64 [5]: captured into the step's graph
+        # with the all-reduces, where host events cannot time): bucket A issued, B's weight gradients done, both averaged
+        self._comm_clock = (torch.zeros(5, dtype=torch.int64, device=self.device)
+                            if self.dist is not None and self.device.type == "cuda" else None)
         cuda = self.device.type == "cuda"
         lr = torch.tensor(c.LEARNING_RATE, device=self.device) if cuda else c.LEARNING_RATE
         self.opt = torch.optim.Adam(self.params, lr=lr, weight_decay=c.WEIGHT_DECAY,
@@ -2048,7 +2118,8 @@ class Trainer:
         self.step_count = 0
         self.graph = (cuda and acc == 1) if graph is None else (bool(graph) and cuda and acc == 1)
         self.graph_warmup = max(1, int(graph_warmup))  # eager steps first: lazy AMP/optimiser state
-        self._graphs = None
+        self._graphs = None  # the captured step (torch.cuda.CUDAGraph)
+        self.graph_allreduce = False  # True once the captured step holds the RCCL all-reduces
         self._static = None
 
     # ------------------------------------------------------------------ step pieces
@@ -2076,22 +2147,21 @@ class Trainer:
         finally:
             _PENDING_WGRAD.clear()
 
+    def _stamp(self, phase):
+        if self._comm_clock is not None:
+            from . import _lib
+            _lib.check(_lib.load().gmz_comm_stamp(_lib.ptr(self._comm_clock), phase, _lib.stream_ptr()))
+
     def _allreduce_start(self):
         """Bucket A's all-reduce, issued asynchronously (RCCL on its own stream, after the backward's kernels)."""
         if self.dist is None:
             return None
-        if self.device.type == "cuda":
-            ev = torch.cuda.Event(enable_timing=True)
-            ev.record()
-            self.comm_events.append([ev, None, None])
+        self._stamp(0)
         return self.dist.all_reduce(self.flat_grad[:self._bucket_a], async_op=True)
 
     def _mark_flushed(self):
         """Bucket B's weight gradients are enqueued (the compute stream's work between A's issue and B's)."""
-        if self.dist is not None and self.device.type == "cuda" and self.comm_events:
-            ev = torch.cuda.Event(enable_timing=True)
-            ev.record()
-            self.comm_events[-1][1] = ev
+        self._stamp(1)
 
     def _allreduce_finish(self, work):
         """Bucket B's all-reduce (its gradients are final once flush_wgrads ran), then both buckets averaged."""
@@ -2101,11 +2171,7 @@ class Trainer:
             self.dist.all_reduce(self.flat_grad[self._bucket_a:])
         work.wait()
         self.flat_grad.div_(self.dist.get_world_size())
-        if self.device.type == "cuda" and self.comm_events:
-            ev = torch.cuda.Event(enable_timing=True)
-            ev.record()
-            self.comm_events[-1][2] = ev
-            del self.comm_events[:-64]
+        self._stamp(2)
 
     def _allreduce(self):
         if self.dist is not None:  # data parallel: the two buckets' all-reduces (RCCL), A's issued first
@@ -2114,17 +2180,22 @@ class Trainer:
             self._allreduce_finish(work)
 
     def allreduce_times(self):
-        """Mean per-step times (ms) on the compute stream over the recent steps (N > 1; None before any):
-        ``flush_ms`` from bucket A's all-reduce issue (the backward done) to bucket B's weight gradients enqueued — the
-        work A's communication overlaps; ``wait_ms`` from there to both buckets averaged — bucket B's all-reduce and
-        whatever of A's did not hide under the flush: the exposed communication; ``window_ms`` the sum."""
-        done = [e for e in self.comm_events if e[2] is not None and e[1] is not None]
-        if not done:
+        """Mean per-step times (ms) on the compute stream since construction or ``reset_allreduce_times`` (GPU with a
+        process group; None otherwise or before any step): ``flush_ms`` from bucket A's all-reduce issue (the backward
+        done) to bucket B's weight gradients done — the work A's communication overlaps; ``wait_ms`` from there to
+        both buckets averaged — bucket B's all-reduce and whatever of A's did not hide under the flush: the exposed
+        communication; ``window_ms`` the sum.  Read from the device clock gmz_comm_stamp keeps (one host sync)."""
+        if self._comm_clock is None:
             return None
-        done[-1][2].synchronize()
-        flush = sum(a.elapsed_time(b) for a, b, _ in done) / len(done)
-        wait = sum(b.elapsed_time(c) for _, b, c in done) / len(done)
-        return {"flush_ms": flush, "wait_ms": wait, "window_ms": flush + wait}
+        t0, t1, flush, wait, n = self._comm_clock.tolist()
+        if n == 0:
+            return None
+        flush, wait = flush / n / 1e5, wait / n / 1e5  # 100 MHz ticks -> ms
+        return {"flush_ms": flush, "wait_ms": wait, "window_ms": flush + wait, "steps": n}
+
+    def reset_allreduce_times(self):
+        if self._comm_clock is not None:
+            self._comm_clock.zero_()
 
     def allreduce_ms(self):
         """The exposed communication per step (``allreduce_times()['wait_ms']``), None without a process group."""
@@ -2161,10 +2232,14 @@ class Trainer:
             dst.copy_(t)
 
     def _capture(self):
+        """The whole step as ONE HIP graph.  Data parallel (workers.py:571-580): the graph holds
+        the RCCL all-reduces too — bucket A's issued on the process group's stream right after the backward (a fork
+        in the graph), bucket B's weight gradients computed beside it on the capture stream, then B's all-reduce,
+        the join, the average and the update — so no host call sits between the backward and the update."""
         st = self._static
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
-        g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        g = torch.cuda.CUDAGraph()
         # with a process group, RCCL's watchdog thread queries its work events at any time; in the default global
         # capture mode such a query from another thread during the capture fails the process ("operation not
         # permitted when stream is capturing"), so the capture only restricts this thread
@@ -2172,21 +2247,18 @@ class Trainer:
         pg = self.dist is not None or (tdist.is_available() and tdist.is_initialized())
         mode = "thread_local" if pg else "global"
         with torch.cuda.stream(s):
-            with torch.cuda.graph(g1, stream=s, capture_error_mode=mode):
-                self._out = self._forward_backward(st[:6], st[6], augmented=True, flush=self.dist is None)
-                if self.dist is None:
-                    self._update()
-            gf = None
-            if self.dist is not None:
-                # the deferred weight gradients (bucket B) as a graph of their own, replayed while bucket A's
-                # all-reduce runs; then the update
-                gf = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(gf, stream=s, pool=g1.pool(), capture_error_mode=mode):
+            with torch.cuda.graph(g, stream=s, capture_error_mode=mode):
+                dp = self.dist is not None
+                self._out = self._forward_backward(st[:6], st[6], augmented=True, flush=not dp)
+                if dp:  # bucket A's all-reduce beside bucket B's weight gradients, inside the graph
+                    work = self._allreduce_start()
                     self._flush()
-                with torch.cuda.graph(g2, stream=s, pool=g1.pool(), capture_error_mode=mode):
-                    self._update()
+                    self._mark_flushed()
+                    self._allreduce_finish(work)
+                self._update()
         torch.cuda.current_stream(self.device).wait_stream(s)
-        self._graphs = (g1, g2 if self.dist is not None else None, gf)
+        self._graphs = g
+        self.graph_allreduce = self.dist is not None
 
     def step(self, batch, is_weights, k=None, flip=None, sync=True):
         """One training step -> ((total, policy, value, reward, consistency) floats, td errors [B]).
@@ -2198,14 +2270,7 @@ class Trainer:
             self._augment_into_static(batch, is_weights, k, flip)
             if self._graphs is None:
                 self._capture()
-            g1, g2, gf = self._graphs
-            g1.replay()
-            if g2 is not None:
-                work = self._allreduce_start()
-                gf.replay()
-                self._mark_flushed()
-                self._allreduce_finish(work)
-                g2.replay()
+            self._graphs.replay()
             logs, td = self._out
             td = td.clone()
             self.sched.step()

@@ -314,6 +314,15 @@ int gmz_bn_forward_stats(int dtype, const void *x_dev, const void *res_dev, int 
                          const float *beta_dev, float eps, float momentum, float *running_mean_dev,
                          float *running_var_dev, int64_t *num_batches_dev, int relu, void *y_dev, float *save_dev,
                          const double *stats_dev, int ns, size_t stats_bytes, void *stream);
+/* The training-mode channels-last BatchNorm forward WITHOUT its elementwise pass: save_dev = (mean, invstd) f32 [2][C]
+ * and the running statistics, from a producer's partials stats_dev f64 [C][ns][3] (stats_bytes >= C * ns * 24) or,
+ * stats_dev NULL, from one reduction pass over x_dev (workspace_dev: gmz_bn_workspace_bytes(1, B, C, S)).  The
+ * normalised output is then written by the consuming conv's prologue (gmz_conv3x3_forward_bnapply).  (Round 6,
+ * additive: ABI stays 10) */
+int gmz_bn_forward_deferred(int dtype, const void *x_dev, const uint8_t *mask_dev, int B, int C, int S, float eps,
+                            float momentum, float *running_mean_dev, float *running_var_dev, int64_t *num_batches_dev,
+                            float *save_dev, const double *stats_dev, int ns, size_t stats_bytes, void *workspace_dev,
+                            size_t ws_bytes, void *stream);
 /* gmz_bn_backward_acc (channels-last) with its dz sums already reduced to partials stats_dev f64 [C][ns][3]
  * (sum dz, sum dz * xhat, counted elements) by the producer of dy_dev (gmz_conv3x3_forward_bwdstats): the
  * finalisation and the elementwise pass only.  workspace_dev: gmz_bn_workspace_bytes(1, B, C, S).  (ABI 7) */
@@ -380,6 +389,17 @@ int gmz_conv3x3_forward_stamp(int dtype, int H, const void *x_dev, const void *p
                               const uint8_t *mask_dev, double *stats_dev, int stats_slots, const int32_t *action_dev,
                               const void *table_dev, int table_dtype, size_t table_bytes, void *stream);
 int gmz_conv3x3_forward(int dtype, int H, const void *x_dev, const void *packed_dev, void *y_dev, int N, void *stream);
+/* gmz_conv3x3_forward_stats whose input is the output of a training-mode BatchNorm (+ residual, ReLU) applied in the
+ * conv's board-staging prologue (the residual blocks' conv-BN-ReLU-conv chain, network.py:30-48 / loss.py:70-111):
+ * the conv's input bn_y_dev[n][p][c] = relu?((bn_x_dev - mean) * gamma * invstd + beta (+ bn_res_dev)) with
+ * (mean, invstd) = bn_save_dev f32 [2][128] (gmz_bn_forward_deferred), the same arithmetic and rounding as
+ * gmz_bn_forward_stats' elementwise pass, is WRITTEN to bn_y_dev (the activation the backward reads) and convolved;
+ * no separate pass.  bn_res_dev may be NULL; bn_y_dev must not alias bn_x_dev, bn_res_dev or y_dev.  stats_dev,
+ * stats_slots, mask_dev as gmz_conv3x3_forward_stats.  (Round 6, additive: ABI stays 10) */
+int gmz_conv3x3_forward_bnapply(int dtype, int H, const void *bn_x_dev, const void *bn_res_dev, const float *gamma_dev,
+                                const float *beta_dev, const float *bn_save_dev, int relu, void *bn_y_dev,
+                                const void *packed_dev, void *y_dev, int N, const uint8_t *mask_dev, double *stats_dev,
+                                int stats_slots, void *stream);
 /* The same convolution plus an addend of the output's shape and dtype, rounded once:
  * y = round(conv(x, W) + addend).  The residual blocks' input gradient with the identity path's
  * gradient folded in (network.py:40-47 backward: d(block input) = conv1'(d conv1 out) + d(residual)),
@@ -428,6 +448,11 @@ int gmz_grad_add_t(int dtype, const void *src_dev, int P, int C, int O, float *d
  * read the same flattened hidden state, network.py:95,105: one GEMM, [K][O1 + O2]).  (ABI 9) */
 int gmz_grad_add_t_cols(int dtype, const void *src_dev, int P, int C, int O, int ldo, int col0, float *dst_dev,
                         void *stream);
+/* The data-parallel trainer step's communication clock (workers.py:571-580's all-reduce): a one-lane
+ * kernel, so it is captured into the step's HIP graph with the RCCL all-reduces.  phase 0 = bucket A's all-reduce
+ * issued, 1 = bucket B's weight gradients done, 2 = both buckets averaged: stamps the 100 MHz constant clock and at
+ * phase 2 adds (t1 - t0) and (t2 - t1) to acc_dev int64 [5] = {t0, t1, sum flush, sum wait, count}. */
+int gmz_comm_stamp(int64_t *acc_dev, int phase, void *stream);
 
 /* ------------------------------------------------------------------ prediction heads' 1x1 convs (ABI 9)
  * The two 1x1 convolutions of the prediction net (network.py:61,64: policy_conv 128 -> 2, value_conv 128 -> 1,

@@ -73,7 +73,7 @@ SCRIPT = textwrap.dedent(r"""
         th.join(timeout=30)
     assert not errors, errors
     assert polls[0] > 1000, polls[0]
-    assert tr1._graphs is not None and tr1._graphs[1] is not None
+    assert tr1._graphs is not None and tr1.graph_allreduce
     assert np.array_equal(l0, l1), (l0, l1)
     assert np.array_equal(p0, p1)
     dist.barrier()

@@ -7,8 +7,8 @@ gloo (tests/test_loop.py, test_trainer.py, test_pipeline_gpu.py) and RCCL itself
   * the small SUM / MAX all-reduces of the sharded PER and of the bench's max-over-ranks timing
     (trainer._allreduce, bench.collective_max);
   * the DDP trainer (trainer.Trainer under an initialised process group: rank 0's weights broadcast at
-    construction, then per step the flat-bucket gradient all-reduce between the two captured HIP
-    graphs) — equal to the single-process trainer's steps (same kernels; an all-reduce over one rank
+    construction, then per step the two gradient buckets' all-reduces captured inside the step's HIP
+    graph, timed by the in-graph communication clock) — equal to the single-process trainer's steps (same kernels; an all-reduce over one rank
     leaves the bucket unchanged).
 It runs in a child process so that no process group outlives it."""
 import os
@@ -53,7 +53,10 @@ SCRIPT = textwrap.dedent(r"""
     dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, rank=0, world_size=1)
     assert dist.get_backend() == "nccl"
     tr1, l1, p1 = run()  # DDP path: init broadcast + flat-bucket all-reduce per step over RCCL
-    assert tr1.dist is not None and tr1._graphs[1] is not None
+    assert tr1.dist is not None and tr1.graph_allreduce  # the all-reduces are inside the captured step
+    t = tr1.allreduce_times()  # the in-graph communication clock (gmz_comm_stamp): every step stamped
+    assert t is not None and t["steps"] == 5 and t["flush_ms"] > 0 and t["wait_ms"] >= 0, t
+    print("allreduce_times", t)
     assert np.array_equal(l0, l1), (l0, l1)
     assert np.array_equal(p0, p1)
     # the weight push: one flat fp32 broadcast of the trainer's state_dict
@@ -82,3 +85,4 @@ def test_rccl_world_one_trainer_weight_push_and_allreduces():
                        cwd=REPO)
     assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
     assert "rccl ok" in r.stdout
+    print([ln for ln in r.stdout.splitlines() if ln.startswith("allreduce_times")])
