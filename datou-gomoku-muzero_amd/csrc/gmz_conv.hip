@@ -267,12 +267,17 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
     const uint4 *rs = ba.res ? (const uint4 *)ba.res + base : nullptr;
     uint4 *os = (uint4 *)ba.out + base;
     const bool mine = (bch >> 3) == half0;  // this workgroup's channel half of the output
+    // branch-free element math: no residual = adding -0.0 (the identity, signed zeros included), no ReLU = a max
+    // with -inf; the same values as k_bnl_apply's conditional forms
+    const uint32_t nz = M::bits(-0.f) * 0x10001u;
+    const float lo = ba.relu ? 0.f : -__builtin_inff();
 #pragma unroll
     for (int i0 = 0; i0 < NI; i0 += U) {
       uint4 zv[U], rv[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int i = t + (i0 + u) * NTHR;
+        rv[u] = make_uint4(nz, nz, nz, nz);
         if (i0 + u < NI && i < NCH) {
           zv[u] = zs[i];
           if (rs) rv[u] = rs[i];
@@ -291,8 +296,8 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
           for (int e = 0; e < 2; ++e) {
             const int j = 2 * h + e;
             float v = (M::value((uint16_t)(zw[h] >> (16 * e))) - bmu[j]) * bsc[j] + bsh[j];
-            if (rs) v += M::value((uint16_t)(rw[h] >> (16 * e)));
-            if (ba.relu) v = fmaxf(v, 0.f);
+            v += M::value((uint16_t)(rw[h] >> (16 * e)));
+            v = fmaxf(v, lo);
             packed |= (uint32_t)M::bits(v) << (16 * e);
           }
           ow[h] = packed;
