@@ -196,6 +196,10 @@ def _like(t, layout):
     return t.contiguous(memory_format=torch.channels_last) if layout == 1 else t.contiguous()
 
 
+# data parallel: the gradient all-reduces captured inside the step's HIP graph (Trainer._capture) when every rank can
+# capture a collective; False: three graphs with the all-reduces issued between their replays (A/B, fallback)
+GRAPH_ALLREDUCE = True
+
 # a training-mode BatchNorm (+ residual, ReLU) whose output is the input of a HIP 3x3 conv: its elementwise pass runs
 # in that conv's board-staging prologue (gmz_conv3x3_forward_bnapply, which also writes the output for the backward)
 # instead of a pass of its own: one launch and one read of the BatchNorm's input fewer per use
@@ -2118,7 +2122,7 @@ class Trainer:
         self.step_count = 0
         self.graph = (cuda and acc == 1) if graph is None else (bool(graph) and cuda and acc == 1)
         self.graph_warmup = max(1, int(graph_warmup))  # eager steps first: lazy AMP/optimiser state
-        self._graphs = None  # the captured step (torch.cuda.CUDAGraph)
+        self._graphs = None  # the captured step: a CUDAGraph, or (step, flush, update) graphs (see _capture)
         self.graph_allreduce = False  # True once the captured step holds the RCCL all-reduces
         self._static = None
 
@@ -2235,30 +2239,70 @@ class Trainer:
         """The whole step as ONE HIP graph.  Data parallel (workers.py:571-580): the graph holds
         the RCCL all-reduces too — bucket A's issued on the process group's stream right after the backward (a fork
         in the graph), bucket B's weight gradients computed beside it on the capture stream, then B's all-reduce,
-        the join, the average and the update — so no host call sits between the backward and the update."""
+        the join, the average and the update — so no host call sits between the backward and the update.  If any
+        rank cannot capture a collective (``_graph_collectives_ok``), every rank falls back to three graphs with the
+        all-reduces issued eagerly between their replays (the round-5 form)."""
         st = self._static
-        s = torch.cuda.Stream(self.device)
-        s.wait_stream(torch.cuda.current_stream(self.device))
-        g = torch.cuda.CUDAGraph()
         # with a process group, RCCL's watchdog thread queries its work events at any time; in the default global
         # capture mode such a query from another thread during the capture fails the process ("operation not
         # permitted when stream is capturing"), so the capture only restricts this thread
         import torch.distributed as tdist
         pg = self.dist is not None or (tdist.is_available() and tdist.is_initialized())
         mode = "thread_local" if pg else "global"
+        dp = self.dist is not None
+        in_graph = dp and GRAPH_ALLREDUCE and self._graph_collectives_ok(mode)
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        g = torch.cuda.CUDAGraph()
         with torch.cuda.stream(s):
             with torch.cuda.graph(g, stream=s, capture_error_mode=mode):
-                dp = self.dist is not None
                 self._out = self._forward_backward(st[:6], st[6], augmented=True, flush=not dp)
-                if dp:  # bucket A's all-reduce beside bucket B's weight gradients, inside the graph
+                if in_graph:  # bucket A's all-reduce beside bucket B's weight gradients, inside the graph
                     work = self._allreduce_start()
                     self._flush()
                     self._mark_flushed()
                     self._allreduce_finish(work)
-                self._update()
+                if not dp or in_graph:
+                    self._update()
+            if dp and not in_graph:  # bucket B's weight gradients and the update as graphs of their own
+                gf, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gf, stream=s, pool=g.pool(), capture_error_mode=mode):
+                    self._flush()
+                with torch.cuda.graph(g2, stream=s, pool=g.pool(), capture_error_mode=mode):
+                    self._update()
         torch.cuda.current_stream(self.device).wait_stream(s)
-        self._graphs = g
-        self.graph_allreduce = self.dist is not None
+        self._graphs = (g, gf, g2) if (dp and not in_graph) else g
+        self.graph_allreduce = in_graph
+
+    def _graph_collectives_ok(self, mode):
+        """Whether every rank can capture an RCCL all-reduce into a HIP graph and replay it correctly: each rank
+        captures a small one, the ranks agree (an eager MIN all-reduce) BEFORE any replays it — a rank replaying a
+        collective its peers never captured would wait forever — then replay and check the sum, and agree again."""
+        dist = self.dist
+        if dist.get_backend() != "nccl":  # gloo stages device tensors through the host: never capturable (all ranks)
+            return False
+        n, r = dist.get_world_size(), dist.get_rank()
+        t = torch.full((64,), float(r + 1), device=self.device)
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        ok = 1
+        try:
+            with torch.cuda.stream(s):
+                with torch.cuda.graph(g, stream=s, capture_error_mode=mode):
+                    dist.all_reduce(t)
+        except Exception:  # noqa: BLE001 - any capture failure means: not in the graph
+            ok = 0
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        flag = torch.tensor([ok], dtype=torch.int32, device=self.device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if int(flag.item()) == 0:
+            return False
+        t.fill_(float(r + 1))
+        g.replay()
+        flag.fill_(int(bool((t == n * (n + 1) / 2).all())))
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        return int(flag.item()) == 1
 
     def step(self, batch, is_weights, k=None, flip=None, sync=True):
         """One training step -> ((total, policy, value, reward, consistency) floats, td errors [B]).
@@ -2270,7 +2314,16 @@ class Trainer:
             self._augment_into_static(batch, is_weights, k, flip)
             if self._graphs is None:
                 self._capture()
-            self._graphs.replay()
+            if isinstance(self._graphs, tuple):  # collectives not capturable: the all-reduces between replays
+                g1, gf, g2 = self._graphs
+                g1.replay()
+                work = self._allreduce_start()
+                gf.replay()
+                self._mark_flushed()
+                self._allreduce_finish(work)
+                g2.replay()
+            else:
+                self._graphs.replay()
             logs, td = self._out
             td = td.clone()
             self.sched.step()

@@ -8,7 +8,8 @@ gloo (tests/test_loop.py, test_trainer.py, test_pipeline_gpu.py) and RCCL itself
     (trainer._allreduce, bench.collective_max);
   * the DDP trainer (trainer.Trainer under an initialised process group: rank 0's weights broadcast at
     construction, then per step the two gradient buckets' all-reduces captured inside the step's HIP
-    graph, timed by the in-graph communication clock) — equal to the single-process trainer's steps (same kernels; an all-reduce over one rank
+    graph, timed by the in-graph communication clock; and the fallback with the all-reduces between three
+    graphs) — equal to the single-process trainer's steps (same kernels; an all-reduce over one rank
     leaves the bucket unchanged).
 It runs in a child process so that no process group outlives it."""
 import os
@@ -57,6 +58,13 @@ SCRIPT = textwrap.dedent(r"""
     t = tr1.allreduce_times()  # the in-graph communication clock (gmz_comm_stamp): every step stamped
     assert t is not None and t["steps"] == 5 and t["flush_ms"] > 0 and t["wait_ms"] >= 0, t
     print("allreduce_times", t)
+    T.GRAPH_ALLREDUCE = False  # the fallback: three graphs, the all-reduces issued between their replays
+    tr2, l2, p2 = run()
+    T.GRAPH_ALLREDUCE = True
+    assert not tr2.graph_allreduce and isinstance(tr2._graphs, tuple)
+    assert np.array_equal(l0, l2) and np.array_equal(p0, p2)
+    t2 = tr2.allreduce_times()
+    assert t2 is not None and t2["steps"] == 5, t2
     assert np.array_equal(l0, l1), (l0, l1)
     assert np.array_equal(p0, p1)
     # the weight push: one flat fp32 broadcast of the trainer's state_dict
