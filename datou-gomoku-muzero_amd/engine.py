@@ -356,13 +356,21 @@ class BatchedSelfPlayEngine:
         return visits, rn, rw, mx, mn
 
 
+# the CUs a two-stream engine's tower leaves to the other part's latency-bound tree and head kernels: a 512-game tree
+# launch is 512 single-wave workgroups at 2 waves per SIMD (the hint kernel's 136 VGPRs), which 32 free CUs hold in
+# two rounds and 24 in three — the cliff below.  Sweep with the round-6 tower
+# (tools/cap_sweep.sh, profiles/r06_tower_cap_sweep.txt, 1,024 games, two rounds): cap 192 12,270-12,347 moves/s, 208
+# 12,279-12,285, 216 12,321-12,342, 224 = 256 - 32: 12,465-12,515, 232 10,364-10,381, 240 10,257-10,340, no cap 11,357
+TOWER_FREE_CUS = 32
+
+
 class SplitSelfPlayEngine:
     """G games as ``parts`` BatchedSelfPlayEngines of G/parts games, each on its own HIP stream, with
     their simulation waves interleaved on the host (same public interface as BatchedSelfPlayEngine).
 
     Why: one tower launch fills every CU (a persistent workgroup per CU), and the tree / head kernels
     between two towers are short and latency-bound.  With two halves on two streams and each half's
-    tower grid capped at 3/4 of the CUs (``max_grid``), one half's tree and head kernels run on the
+    tower grid capped at all CUs but TOWER_FREE_CUS (``max_grid``), one half's tree and head kernels run on the
     CUs the other half's tower leaves free, and each tower's ramp-up and tail overlap the other
     half's work (measured with tools/dual_stream_probe.py).  Every game's search is
     exactly the unsplit engine's: part i plays games [i*G/parts, (i+1)*G/parts) with ``game_offset``
@@ -386,8 +394,9 @@ class SplitSelfPlayEngine:
         g = self.g = G // parts
         # descent_hint / layout None: each part's defaults — the cached-exp softmax in every part, as one
         # engine with every game (the layout may differ per part: results are identical)
-        if max_grid is None:
-            max_grid = torch.cuda.get_device_properties(self.device).multi_processor_count * 3 // 4 if parts > 1 else 0
+        if max_grid is None:  # every CU but TOWER_FREE_CUS for the other part's tree and head kernels
+            cus = torch.cuda.get_device_properties(self.device).multi_processor_count
+            max_grid = max(cus // 2, cus - TOWER_FREE_CUS) if parts > 1 else 0
         if net is None:
             net = HashNetBackend(hidden_slots(c, G), self.A, device)
         self.net = net
