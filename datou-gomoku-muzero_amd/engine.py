@@ -357,8 +357,8 @@ class BatchedSelfPlayEngine:
 
 
 # the CUs a two-stream engine's tower leaves to the other part's latency-bound tree and head kernels: a 512-game tree
-# launch is 512 single-wave workgroups at 2 waves per SIMD (the hint kernel's 136 VGPRs), which 32 free CUs hold in
-# two rounds and 24 in three — the cliff below.  Sweep with the round-6 tower
+# launch is 512 waves at 4 waves per SIMD (the 15x15 hint kernel's 105 VGPRs), which 32 free CUs hold in one round
+# and 24 in two — the cliff below.  Sweep with the round-6 tower
 # (tools/cap_sweep.sh, profiles/r06_tower_cap_sweep.txt, 1,024 games, two rounds): cap 192 12,270-12,347 moves/s, 208
 # 12,279-12,285, 216 12,321-12,342, 224 = 256 - 32: 12,465-12,515, 232 10,364-10,381, 240 10,257-10,340, no cap 11,357
 TOWER_FREE_CUS = 32
