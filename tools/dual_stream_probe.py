@@ -18,13 +18,17 @@ ap.add_argument("--max-grid", type=int, default=None)
 ap.add_argument("--games", type=int, default=1024)
 ap.add_argument("--moves", type=int, default=6)
 ap.add_argument("--warmup", type=int, default=2)
+ap.add_argument("--size", type=int, default=15)
+ap.add_argument("--sims", type=int, default=400)
+ap.add_argument("--mode", default="MuZero")
+ap.add_argument("--blocks", type=int, default=8)
 a = ap.parse_args()
 from datou_gomoku_muzero_amd import engine as E, network as N, weights as W  # noqa: E402
 from datou_gomoku_muzero_amd.config import GmzConfig  # noqa: E402
 
-cfg = GmzConfig(BOARD_SIZE=15, NUM_SIMULATIONS=400)
+cfg = GmzConfig(BOARD_SIZE=a.size, NUM_SIMULATIONS=a.sims, MCTS_IMPLEMENTATION=a.mode, NUM_RES_BLOCKS=a.blocks)
 sd = W.synthetic_state_dict(cfg, seed=1234, with_projection=False)
-net = N.GomokuNetHip(sd, cfg, num_slots=a.games * 402, max_rows=a.games)
+net = N.GomokuNetHip(sd, cfg, num_slots=E.hidden_slots(cfg, a.games), max_rows=a.games)
 if a.parts == 1:
     eng = E.BatchedSelfPlayEngine(cfg, num_games=a.games, net=net, seed=7)
 else:
@@ -40,5 +44,5 @@ for _ in range(a.moves):
     eng.play(reset_finished=True)
 torch.cuda.synchronize()
 dt = time.perf_counter() - t0
-print(json.dumps({"parts": a.parts, "max_grid": a.max_grid, "games": a.games, "moves_per_s": a.games * a.moves / dt,
+print(json.dumps({"size": a.size, "mode": a.mode, "parts": a.parts, "max_grid": a.max_grid, "games": a.games, "moves_per_s": a.games * a.moves / dt,
                   "ms_per_move": dt / a.moves * 1e3}))
