@@ -2,7 +2,7 @@
 
 bench.py times ``engine.make_engine`` with its defaults at 15x15 / 400 simulations / 1,024 games: a
 SplitSelfPlayEngine of two 512-game halves on two HIP streams, each half's 8-block f16 dynamics tower on
-a grid capped at 3/4 of the CUs with ticket-scheduled boards, the dense tree rows with the descent hint,
+a grid capped at all CUs but engine.TOWER_FREE_CUS with ticket-scheduled boards, the dense tree rows with the descent hint,
 the halves' waves interleaved.  Its pieces are pinned separately at full size elsewhere (the network in
 test_net_gpu.py, the tree kernels with HashNet in test_tree_*_gpu.py); here the composition itself is
 checked, from the headline's own start positions (engine.seeded_openings, as bench.py --stagger 80):
@@ -61,7 +61,7 @@ def test_headline_composed_path_at_its_own_size(mods):
     two = E.make_engine(cfg, num_games=G, net=net2, seed=7)
     assert isinstance(two, E.SplitSelfPlayEngine) and two.parts == 2 and two.g == 512
     cus = torch.cuda.get_device_properties(0).multi_processor_count
-    assert all(e.net.w.max_grid == cus * 3 // 4 for e in two.engines)
+    assert all(e.net.w.max_grid == max(cus // 2, cus - E.TOWER_FREE_CUS) for e in two.engines)
     assert all(e.layout == "dense" and e.descent_hint for e in two.engines)
     two.reset_games()
     two.set_positions(*openings)
