@@ -835,7 +835,7 @@ def subline(args, key, rank, world, dist, backend):
             q = r[k]
             out[k] = {x: q[x] for x in ("kernel", "achieved", "unit", "frac", "mean_launch_ms", "bytes_per_launch",
                                         "layout", "games_per_launch", "mean_select_levels", "traffic",
-                                        "achieved_measured", "frac_measured", "traffic_source") if x in q}
+                                        "achieved_measured", "frac_measured", "traffic_source", "backup") if x in q}
     return out
 
 
