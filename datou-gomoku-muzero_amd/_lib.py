@@ -80,6 +80,9 @@ _SIGS = {
     "gmz_grad_add_t": ([I, P, I, I, I, P, P], I),
     "gmz_grad_add_t_cols": ([I, P, I, I, I, I, I, P, P], I),
     "gmz_comm_stamp": ([P, I, P], I),
+    "gmz_opt_layout": ([ctypes.POINTER(SZ), ctypes.POINTER(I), ctypes.POINTER(SZ)], I),
+    "gmz_opt_step": ([P, I, P, P, P, ctypes.c_longlong, P, I, ctypes.c_float, P, ctypes.c_float, ctypes.c_float,
+                      ctypes.c_float, ctypes.c_float, ctypes.c_float, P, P, P, SZ, P], I),
     "gmz_head_conv1x1_forward": ([I, P, L, I, P, P, I, P, P, I, P, P, P], I),
     "gmz_head_conv1x1_workspace_bytes": ([L, I, P], I),
     "gmz_seg_bn_forward": ([I, P, P, I, I, I, I, P, P, ctypes.c_float, P, P, SZ, I, ctypes.c_float, P, P, P, P, P], I),

@@ -830,6 +830,94 @@ __global__ void __launch_bounds__(256) k_grad_add_t(const T *__restrict__ src, i
   }
 }
 
+// ---- the optimiser step of Trainer._update on the GPU (workers.py:565-583: GradScaler.unscale_, clip_grad_norm_,
+// Adam with L2 weight decay, GradScaler.update, the soft target update of utils.py:28-31) in three launches over the
+// flat f32 gradient bucket, instead of PyTorch's unscale / per-tensor norm / fused-Adam / foreach-update kernels.
+// A parameter is a dense tensor whose gradient is the bucket range [off, off + n) in the SAME memory order (the
+// trainer makes every .grad a view of the bucket with its parameter's strides), so p[i], t[i], g[off + i],
+// m[off + i], v[off + i] are one element whatever the layout.  Work items = (segment, 4,096-element chunk) from a
+// host-built table, so no item crosses a parameter.
+constexpr int OPT_THREADS = 256, OPT_CHUNK = 4096, OPT_NORM_BLOCKS = 1024;  // OPT_CHUNK: gmz_opt_layout
+struct OptItem {
+  float *p, *t;  // parameter, its target-network twin (nullptr: updated elsewhere)
+  long long off;  // bucket offset of this chunk's first element
+  int n;          // elements in the chunk (<= OPT_CHUNK)
+  int pi;         // the chunk's first element within the parameter
+};
+
+// pass 1: per-block f64 sums of squares of the (still scaled) gradient, and a non-finite flag
+__global__ void __launch_bounds__(OPT_THREADS) k_opt_sumsq(const float *__restrict__ g, long long N,
+                                                            double *__restrict__ part, int *__restrict__ nonfinite) {
+  double s = 0.0, dummy = 0.0;
+  bool bad = false;
+  const long long n4 = N / 4;
+  for (long long i = (long long)blockIdx.x * OPT_THREADS + threadIdx.x; i < n4; i += (long long)gridDim.x * OPT_THREADS) {
+    const float4 v = ((const float4 *)g)[i];
+    bad |= !(isfinite(v.x) && isfinite(v.y) && isfinite(v.z) && isfinite(v.w));
+    s += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
+  }
+  for (long long i = n4 * 4 + (long long)blockIdx.x * OPT_THREADS + threadIdx.x; i < N; i += (long long)gridDim.x * OPT_THREADS) {
+    const float v = g[i];
+    bad |= !isfinite(v);
+    s += (double)v * v;
+  }
+  if (bad) *nonfinite = 1;  // benign race: every writer stores 1
+  block_sum2(s, dummy);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+// pass 2 (one wave): coef = {found_inf (0/1), gradient multiplier = inv_scale * clip}; the Adam step advanced when
+// the step is taken; nonfinite reset for the next step
+__global__ void k_opt_finalize(const double *__restrict__ part, int nb, int *__restrict__ nonfinite,
+                               const float *__restrict__ scale, float max_norm, int skip_on_inf, float *__restrict__ coef,
+                               float *__restrict__ step) {
+  double s = 0.0;
+  for (int i = threadIdx.x; i < nb; i += WAVE) s += part[i];
+  s = wave_sum_d(s);
+  if (threadIdx.x != 0) return;
+  const float inv = scale ? 1.0f / scale[0] : 1.0f;
+  const bool inf = *nonfinite != 0;
+  const float norm = (float)(sqrt(s) * (double)inv);  // the norm of the unscaled gradient
+  const float clip = fminf(max_norm / (norm + 1e-6f), 1.0f);
+  const bool skip = inf && skip_on_inf;
+  coef[0] = skip ? 1.0f : 0.0f;
+  coef[1] = inv * clip;
+  if (!skip) step[0] += 1.0f;
+  *nonfinite = 0;
+}
+
+// pass 3: Adam (torch.optim.Adam, weight_decay as L2) unless the step is skipped, the soft target update
+// t = (1 - tau) t + tau p, and the gradient zeroed for the next step
+__global__ void __launch_bounds__(OPT_THREADS) k_opt_adam(const OptItem *__restrict__ items, float *__restrict__ g,
+                                                           float *__restrict__ m, float *__restrict__ v,
+                                                           const float *__restrict__ coef, const float *__restrict__ step,
+                                                           const float *__restrict__ lr, float beta1, float beta2,
+                                                           float eps, float wd, float tau) {
+  const OptItem it = items[blockIdx.x];
+  const bool skip = coef[0] != 0.0f;
+  const float mult = coef[1];
+  const float st = step[0], lrv = lr[0];
+  const float bc1 = 1.0f - powf(beta1, st), bc2 = 1.0f - powf(beta2, st);
+  const float step_size = lrv / bc1, bc2_sqrt = sqrtf(bc2);
+  for (int i = threadIdx.x; i < it.n; i += OPT_THREADS) {
+    const long long k = it.off + i;
+    float pv = it.p[it.pi + i];
+    if (!skip) {
+      float gv = g[k] * mult;
+      gv += pv * wd;
+      const float mv = beta1 * m[k] + (1.0f - beta1) * gv;
+      const float vv = beta2 * v[k] + (1.0f - beta2) * gv * gv;
+      m[k] = mv;
+      v[k] = vv;
+      const float denom = sqrtf(vv) / bc2_sqrt + eps;
+      pv -= step_size * mv / denom;
+      it.p[it.pi + i] = pv;
+    }
+    if (it.t) it.t[it.pi + i] = it.t[it.pi + i] * (1.0f - tau) + pv * tau;
+    g[k] = 0.0f;
+  }
+}
+
 // The data-parallel step's communication clock (one lane; a kernel, so that it is captured into the step's HIP
 // graph beside the RCCL all-reduces, where host event timing is not available): phase 0 stamps bucket A's issue,
 // phase 1 bucket B's weight gradients done, phase 2 both buckets averaged and adds the two intervals to running
@@ -850,6 +938,38 @@ __global__ void k_comm_stamp(long long *acc, int phase) {
 }  // namespace gmz
 
 using namespace gmz;
+
+GMZ_EXPORT int gmz_opt_layout(size_t *item_bytes, int *chunk, size_t *workspace_bytes) {
+  if (!item_bytes || !chunk || !workspace_bytes) return fail("gmz_opt_layout: null");
+  *item_bytes = sizeof(OptItem);
+  *chunk = OPT_CHUNK;
+  *workspace_bytes = OPT_NORM_BLOCKS * sizeof(double) + sizeof(int) * 4;
+  return 0;
+}
+
+GMZ_EXPORT int gmz_opt_step(const void *items, int n_items, float *grad, float *exp_avg, float *exp_avg_sq,
+                            long long n, const float *scale, int skip_on_inf, float max_norm, const float *lr,
+                            float beta1, float beta2, float eps, float weight_decay, float tau, float *step, float *coef,
+                            void *workspace, size_t workspace_bytes, void *stream) {
+  if (!items || n_items <= 0 || !grad || !exp_avg || !exp_avg_sq || n <= 0 || !lr || !step || !coef || !workspace)
+    return fail("gmz_opt_step: bad arguments");
+  const size_t need = OPT_NORM_BLOCKS * sizeof(double) + sizeof(int) * 4;
+  if (workspace_bytes < need)
+    return fail("gmz_opt_step: workspace of " + std::to_string(workspace_bytes) + " bytes, needs " + std::to_string(need));
+  if (((uintptr_t)grad) & 15) return fail("gmz_opt_step: the gradient bucket must be 16-B aligned");
+  hipStream_t st = (hipStream_t)stream;
+  double *part = (double *)workspace;
+  int *nonfinite = (int *)(part + OPT_NORM_BLOCKS);  // zero-initialised by the caller once; reset by k_opt_finalize
+  hipLaunchKernelGGL(k_opt_sumsq, dim3(OPT_NORM_BLOCKS), dim3(OPT_THREADS), 0, st, (const float *)grad, n, part, nonfinite);
+  GMZ_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_opt_finalize, dim3(1), dim3(WAVE), 0, st, (const double *)part, OPT_NORM_BLOCKS, nonfinite, scale,
+                     max_norm, skip_on_inf, coef, step);
+  GMZ_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_opt_adam, dim3(n_items), dim3(OPT_THREADS), 0, st, (const OptItem *)items, grad, exp_avg,
+                     exp_avg_sq, (const float *)coef, (const float *)step, lr, beta1, beta2, eps, weight_decay, tau);
+  GMZ_LAUNCH_CHECK();
+  return 0;
+}
 
 GMZ_EXPORT int gmz_comm_stamp(int64_t *acc, int phase, void *stream) {
   if (!acc || phase < 0 || phase > 2) return fail("gmz_comm_stamp: acc must be int64 [5], phase 0, 1 or 2");

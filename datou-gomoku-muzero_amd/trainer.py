@@ -196,6 +196,11 @@ def _like(t, layout):
     return t.contiguous(memory_format=torch.channels_last) if layout == 1 else t.contiguous()
 
 
+# the optimiser step on the GPU as gmz_opt_step (unscale + clip + Adam + soft target update + zero_grad in three
+# launches over the flat gradient bucket) instead of PyTorch's unscale_ / clip_grad_norm_ / fused Adam / foreach
+# update (A/B: False)
+FUSED_OPT = True
+
 # data parallel: the gradient all-reduces captured inside the step's HIP graph (Trainer._capture) when every rank can
 # capture a collective; False: three graphs with the all-reduces issued between their replays (A/B, fallback)
 GRAPH_ALLREDUCE = True
@@ -2123,6 +2128,7 @@ class Trainer:
         self.graph = (cuda and acc == 1) if graph is None else (bool(graph) and cuda and acc == 1)
         self.graph_warmup = max(1, int(graph_warmup))  # eager steps first: lazy AMP/optimiser state
         self._graphs = None  # the captured step: a CUDAGraph, or (step, flush, update) graphs (see _capture)
+        self._fopt = None  # FUSED_OPT's buffers (built at the first update)
         self.graph_allreduce = False  # True once the captured step holds the RCCL all-reduces
         self._static = None
 
@@ -2206,8 +2212,85 @@ class Trainer:
         t = self.allreduce_times()
         return None if t is None else t["wait_ms"]
 
+    def _fused_opt_ok(self):
+        g = self.opt.param_groups[0]
+        return (FUSED_OPT and self.device.type == "cuda" and len(self.opt.param_groups) == 1
+                and torch.is_tensor(g["lr"]) and not g.get("amsgrad") and not g.get("maximize")
+                and all(p.dtype == torch.float32 for p in self.params))
+
+    def _fused_opt_setup(self):
+        """gmz_opt_step's work items over the gradient bucket, the Adam moments as bucket-shaped buffers (torch's
+        optimiser state becomes views of them, so state_dict / load_state_dict keep the reference's format) and the
+        target twins (a parameter whose twin has other strides gets its soft update from PyTorch)."""
+        import ctypes
+        from . import _lib
+        L = _lib.load()
+        ib, ch, wsb = ctypes.c_size_t(), ctypes.c_int(), ctypes.c_size_t()
+        _lib.check(L.gmz_opt_layout(ctypes.byref(ib), ctypes.byref(ch), ctypes.byref(wsb)))
+        dt = np.dtype([("p", "<u8"), ("t", "<u8"), ("off", "<i8"), ("n", "<i4"), ("pi", "<i4")])
+        if ib.value != dt.itemsize:
+            raise _lib.GmzError("gmz_opt_layout: item of %d bytes, expected %d" % (ib.value, dt.itemsize))
+        twin = {id(p): t for t, p in zip(self.target.parameters(), self.model.parameters())}
+        m, v = torch.zeros_like(self.flat_grad), torch.zeros_like(self.flat_grad)
+        step = torch.zeros((), dtype=torch.float32, device=self.device)
+        base, items, fallback = self.flat_grad.data_ptr(), [], []
+        for p in self.params:
+            n = p.numel()
+            off = (p.grad.data_ptr() - base) // 4
+            dense = p.is_contiguous() or p.is_contiguous(memory_format=torch.channels_last)
+            if not (dense and p.grad.stride() == p.stride() and 0 <= off and off + n <= self.flat_grad.numel()):
+                raise RuntimeError("Trainer: a parameter's gradient is not its bucket range in its own layout")
+            t = twin.get(id(p))
+            t_ok = t is not None and t.is_cuda and t.dtype == torch.float32 and t.stride() == p.stride()
+            if t is not None and not t_ok:
+                fallback.append((t, p))
+            for i0 in range(0, n, ch.value):
+                items.append((p.data_ptr(), t.data_ptr() if t_ok else 0, off + i0, min(ch.value, n - i0), i0))
+            mv = m[off:off + n].as_strided(p.shape, p.stride())
+            vv = v[off:off + n].as_strided(p.shape, p.stride())
+            st = self.opt.state.get(p)
+            if st:  # resumed or earlier PyTorch steps: the moments and the step carry over
+                mv.copy_(st["exp_avg"])
+                vv.copy_(st["exp_avg_sq"])
+                step.copy_(torch.as_tensor(st["step"], dtype=torch.float32))
+            self.opt.state[p] = {"step": step, "exp_avg": mv, "exp_avg_sq": vv}
+        arr = np.array(items, dtype=dt)
+        versioned = list(self.params) + [twin[id(p)] for p in self.params if id(p) in twin]
+        self._fopt = {"items": torch.from_numpy(arr.view(np.uint8)).to(self.device), "n_items": len(items),
+                      "m": m, "v": v, "step": step, "coef": torch.zeros(2, dtype=torch.float32, device=self.device),
+                      "ws": torch.zeros((wsb.value + 7) // 8, dtype=torch.float64, device=self.device),
+                      "fallback": fallback, "versioned": versioned}
+
     def _update(self):
         c = self.cfg
+        if self._fused_opt_ok():  # FUSED_OPT: unscale + clip + Adam + soft update + zero_grad in three launches
+            from . import _lib
+            if self._fopt is None:
+                self._fused_opt_setup()
+            f, g = self._fopt, self.opt.param_groups[0]
+            amp = self.scaler.is_enabled()
+            scale = self.scaler._scale if amp else None
+            b1, b2 = g["betas"]
+            _lib.check(_lib.load().gmz_opt_step(
+                _lib.ptr(f["items"]), f["n_items"], _lib.ptr(self.flat_grad), _lib.ptr(f["m"]), _lib.ptr(f["v"]),
+                self.flat_grad.numel(), _lib.ptr(scale), int(amp), float(c.GRAD_CLIP_NORM), _lib.ptr(g["lr"]),
+                float(b1), float(b2), float(g["eps"]), float(g["weight_decay"]), float(c.TARGET_MODEL_TAU),
+                _lib.ptr(f["step"]), _lib.ptr(f["coef"]), _lib.ptr(f["ws"]), _lib.nbytes(f["ws"]), _lib.stream_ptr()))
+            if amp:  # GradScaler.update with the step's found_inf
+                torch._amp_update_scale_(self.scaler._scale, self.scaler._growth_tracker, f["coef"][:1],
+                                         self.scaler._growth_factor, self.scaler._backoff_factor,
+                                         self.scaler._growth_interval)
+            # the kernel wrote the parameters through raw pointers: advance their version counters as PyTorch's
+            # in-place update would, so the packed-weight caches keyed on them (_packed_conv_weight, _bigk_weight)
+            # re-pack — and a graph capture after this step records the packs
+            from torch.autograd.graph import increment_version
+            increment_version(f["versioned"])
+            if f["fallback"]:
+                with torch.no_grad():
+                    tp, sp = [t for t, _ in f["fallback"]], [p for _, p in f["fallback"]]
+                    torch._foreach_mul_(tp, 1.0 - c.TARGET_MODEL_TAU)
+                    torch._foreach_add_(tp, sp, alpha=c.TARGET_MODEL_TAU)
+            return
         self.scaler.unscale_(self.opt)
         torch.nn.utils.clip_grad_norm_(self.params, c.GRAD_CLIP_NORM, foreach=self.device.type == "cuda")
         self.scaler.step(self.opt)
@@ -2365,6 +2448,7 @@ class Trainer:
         self.step_count = int(state.get("train_step_count", 0))
         self.games_completed = int(state.get("games_completed_count", 0))
         self._graphs, self._static = None, None  # re-captured on the next step
+        self._fopt = None  # FUSED_OPT adopts the loaded moments and step at the next update
 
     def trainer_state(self, games_completed_count=None):
         """The reference's checkpoint dict (workers.py:594-597), CPU tensors, optimiser state in the

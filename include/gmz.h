@@ -448,6 +448,21 @@ int gmz_grad_add_t(int dtype, const void *src_dev, int P, int C, int O, float *d
  * read the same flattened hidden state, network.py:95,105: one GEMM, [K][O1 + O2]).  (ABI 9) */
 int gmz_grad_add_t_cols(int dtype, const void *src_dev, int P, int C, int O, int ldo, int col0, float *dst_dev,
                         void *stream);
+/* The trainer's optimiser step on the GPU (workers.py:565-583: GradScaler.unscale_, clip_grad_norm_(max_norm), Adam with
+ * L2 weight decay as torch.optim.Adam, the soft target update t = (1 - tau) t + tau p of utils.py:28-31), in three
+ * launches over the flat f32 gradient bucket grad[n] (16-B aligned), its Adam moments exp_avg / exp_avg_sq laid out
+ * like it, and a table of work items (gmz_opt_layout: item_bytes each, device memory): per item {float *p, float *t,
+ * int64 off, int32 len, int32 p_index} = parameter elements [p_index, p_index + len) <-> bucket [off, off + len), t the
+ * target twin or NULL; every element of the bucket in exactly one item, items of at most `chunk` elements.
+ * scale: the GradScaler's scale (device f32, NULL = 1); skip_on_inf: a non-finite gradient skips Adam (the target
+ * update and the gradient zeroing still run).  lr, step: device f32 scalars (step advanced on the device when the
+ * step is taken); coef: device f32 [2] = {found_inf, inv_scale * clip} written for the GradScaler's update.
+ * workspace: gmz_opt_layout's bytes, zero-filled once.  The gradient is zeroed for the next step.  (Round 6, additive) */
+int gmz_opt_layout(size_t *item_bytes, int *chunk, size_t *workspace_bytes);
+int gmz_opt_step(const void *items_dev, int n_items, float *grad_dev, float *exp_avg_dev, float *exp_avg_sq_dev,
+                 long long n, const float *scale_dev, int skip_on_inf, float max_norm, const float *lr_dev, float beta1,
+                 float beta2, float eps, float weight_decay, float tau, float *step_dev, float *coef_dev,
+                 void *workspace_dev, size_t workspace_bytes, void *stream);
 /* The data-parallel trainer step's communication clock (workers.py:571-580's all-reduce): a one-lane
  * kernel, so it is captured into the step's HIP graph with the RCCL all-reduces.  phase 0 = bucket A's all-reduce
  * issued, 1 = bucket B's weight gradients done, 2 = both buckets averaged: stamps the 100 MHz constant clock and at
