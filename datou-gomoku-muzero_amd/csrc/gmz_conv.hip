@@ -309,7 +309,15 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
       }
     }
   };
-  for (int b = b0; b < N; b += bstride) {
+  // the row-mask bytes of this workgroup's boards, one per lane (lane j: board b0 + j * bstride), loaded once here:
+  // read per board, each byte was a vector load with a full round trip of its own between the board's barrier and
+  // its first LDS read (profiles/r06_conv_mask_ab.txt)
+  int mrow = 1;
+  if (mask) {
+    const int bj = b0 + lane * bstride;
+    mrow = bj < N ? (int)mask[bj] : 0;
+  }
+  for (int b = b0, j = 0; b < N; b += bstride, ++j) {
     if constexpr (BNA) {
       bn_stage(b);
     } else {
@@ -317,7 +325,7 @@ __global__ void __launch_bounds__(128 * PG, 2) k_conv3(const uint16_t *__restric
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
-    const bool counted = stats && (!mask || mask[b]);
+    const bool counted = stats && (!mask || (j < WAVE ? __builtin_amdgcn_readlane(mrow, j) != 0 : mask[b] != 0));
     nvalid += counted;
 
     f32x4_t acc[NTW][PTW];
