@@ -5,5 +5,5 @@ T=${1:-r06_final}
 bash tools/gpu.sh tests $T && \
 bash tools/gpu.sh smoke $T && \
 bash tools/gpu.sh bench $T && \
-bash tools/gpu.sh trace $T && \
+bash tools/gpu.sh trace $T --single-stream-moves 0 && \
 bash tools/gpu.sh pmc $T
