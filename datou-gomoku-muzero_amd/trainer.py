@@ -2291,6 +2291,11 @@ class Trainer:
                     torch._foreach_mul_(tp, 1.0 - c.TARGET_MODEL_TAU)
                     torch._foreach_add_(tp, sp, alpha=c.TARGET_MODEL_TAU)
             return
+        if self._fopt is not None:  # back on PyTorch's optimiser after fused steps: one step tensor per parameter again
+            for p in self.params:
+                st = self.opt.state[p]
+                st["step"] = st["step"].clone()
+            self._fopt = None
         self.scaler.unscale_(self.opt)
         torch.nn.utils.clip_grad_norm_(self.params, c.GRAD_CLIP_NORM, foreach=self.device.type == "cuda")
         self.scaler.step(self.opt)
