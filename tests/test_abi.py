@@ -84,3 +84,38 @@ def test_capacity_arguments_fail_before_any_launch():
     assert "gmz_net_workspace_bytes" in err()
     assert lib.gmz_net_initial_heads(ctypes.byref(w), fake, fake, 512, fake, fake, fake, need.value - 1, None) < 0
     assert "workspace" in err()
+
+
+def test_round6_entry_points_check_before_launching():
+    """The round-6 additions keep the same contract: the fused optimiser's workspace and gradient alignment, the
+    deferred BatchNorm's statistics partials, the BatchNorm-apply conv's slots and aliasing — all refused before
+    any launch (fake pointers, no GPU)."""
+    import ctypes
+    import datou_gomoku_muzero_amd._lib as L
+    lib = L.load()
+    fake = ctypes.c_void_p(1 << 20)
+    err = lambda: lib.gmz_last_error().decode()  # noqa: E731
+    ib, ch, wsb = ctypes.c_size_t(), ctypes.c_int(), ctypes.c_size_t()
+    assert lib.gmz_opt_layout(ctypes.byref(ib), ctypes.byref(ch), ctypes.byref(wsb)) == 0
+    assert ib.value == 32 and ch.value > 0 and wsb.value > 0
+    assert lib.gmz_opt_step(fake, 4, fake, fake, fake, 1000, None, 1, 5.0, fake, 0.9, 0.999, 1e-8, 1e-5, 0.995, fake,
+                            fake, fake, wsb.value - 1, None) < 0
+    assert "workspace" in err()
+    assert lib.gmz_opt_step(fake, 4, ctypes.c_void_p((1 << 20) + 4), fake, fake, 1000, None, 1, 5.0, fake, 0.9, 0.999,
+                            1e-8, 1e-5, 0.995, fake, fake, fake, wsb.value, None) < 0
+    assert "aligned" in err()
+    ns = ctypes.c_int()
+    assert lib.gmz_conv3x3_stats_slots(360, ctypes.byref(ns)) == 0
+    assert lib.gmz_bn_forward_deferred(1, fake, None, 360, 128, 225, 1e-4, 0.1, None, None, None, fake, fake, ns.value,
+                                       128 * ns.value * 24 - 8, None, 0, None) < 0
+    assert "partials" in err()
+    assert lib.gmz_bn_forward_deferred(1, fake, None, 360, 128, 225, 1e-4, 0.1, None, None, None, fake, None, 0, 0, fake,
+                                       8, None) < 0
+    assert "workspace" in err()
+    assert lib.gmz_conv3x3_forward_bnapply(1, 15, fake, None, fake, fake, fake, 1, fake, fake, fake, 360, None, fake,
+                                           ns.value - 1, None) < 0
+    assert "slots" in err()
+    assert lib.gmz_conv3x3_forward_bnapply(1, 15, fake, None, fake, fake, fake, 1, fake, fake,
+                                           ctypes.c_void_p((1 << 20) + 4096), 360, None, None, 0, None) < 0
+    assert "alias" in err()
+    assert lib.gmz_comm_stamp(fake, 3, None) < 0 and "phase" in err()
