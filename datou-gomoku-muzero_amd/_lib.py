@@ -87,6 +87,10 @@ _SIGS = {
     "gmz_head_conv1x1_workspace_bytes": ([L, I, P], I),
     "gmz_seg_bn_forward": ([I, P, P, I, I, I, I, P, P, ctypes.c_float, P, P, SZ, I, ctypes.c_float, P, P, P, P, P], I),
     "gmz_seg_bn_backward": ([I, P, P, P, I, I, I, I, P, P, SZ, P, P, P, I, P], I),
+    "gmz_seg_bn_small_workspace_bytes": ([I, I, ctypes.POINTER(SZ)], I),
+    "gmz_seg_bn_forward_small": ([I, P, P, I, I, I, I, P, P, ctypes.c_float, P, P, SZ, I, ctypes.c_float, P, P, P, P, P, SZ,
+                                  P], I),
+    "gmz_seg_bn_backward_small": ([I, P, P, P, I, I, I, I, P, P, SZ, P, P, P, I, P, SZ, P], I),
     "gmz_head_conv1x1_backward": ([I, P, L, I, P, I, P, I, P, P, P, P, P, P, P, I, P, SZ, P], I),
     "gmz_bn_forward_stats": ([I, P, P, I, I, I, P, P, ctypes.c_float, ctypes.c_float, P, P, P, I, P, P, P, I, SZ, P], I),
     "gmz_bn_forward_seg": ([I, P, P, P, I, I, I, I, P, P, ctypes.c_float, ctypes.c_float, P, P, P, I, P, P, P, SZ, P, SZ,

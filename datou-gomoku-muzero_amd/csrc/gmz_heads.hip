@@ -455,8 +455,296 @@ int seg_bn_bwd(const void *x, const float *dy, const uint8_t *m, int nseg, int B
   return 0;
 }
 
+// ---- the same segmented BatchNorm for a FEW channels (the 1- and 2-channel prediction heads, network.py:62,65): one
+// workgroup per channel would serialise 6 x 81,000 elements per channel on one CU, so the work is split into
+// (segment, chunk) workgroups for every channel at once: f64 partials (sum, sum of squares, live elements) per
+// (segment, chunk, channel), a one-workgroup finalisation (statistics, running statistics in segment order, the
+// backward's coefficients and dgamma / dbeta), and an elementwise pass.  Variance as E[x^2] - mean^2 in f64.
+constexpr int SBS_MAXC = 8, SBS_MAXK = 64;
+
+__device__ __forceinline__ double sbs_block_sum(double v, double *red) { return sb_block_sum(v, red); }
+
+template <typename T>
+__global__ void __launch_bounds__(SB_THREADS) k_sbs_fwd_part(const T *__restrict__ x, const uint8_t *__restrict__ rmask,
+                                                            int B, int S, int C, int K, double *__restrict__ part) {
+  __shared__ double red[SB_THREADS / 64];
+  const int k = blockIdx.x, sg = blockIdx.y;
+  const long segn = (long)B * S, i0 = segn * k / K, i1 = segn * (k + 1) / K, r0 = (long)sg * B;
+  double a[SBS_MAXC], q[SBS_MAXC], nl = 0.0;
+#pragma unroll
+  for (int c = 0; c < SBS_MAXC; ++c) a[c] = q[c] = 0.0;
+  for (long i = i0 + threadIdx.x; i < i1; i += SB_THREADS) {
+    if (rmask && !rmask[r0 + i / S]) continue;
+    nl += 1.0;
+    const size_t base = (size_t)(r0 * S + i) * C;
+#pragma unroll
+    for (int c = 0; c < SBS_MAXC; ++c)
+      if (c < C) {
+        const double v = (double)hld(x, base + c);
+        a[c] += v;
+        q[c] += v * v;
+      }
+  }
+  double *o = part + ((size_t)sg * K + k) * (2 * C + 1);
+  const double n = sbs_block_sum(nl, red);
+  if (threadIdx.x == 0) o[2 * C] = n;
+  for (int c = 0; c < C; ++c) {
+    const double sa = sbs_block_sum(a[c], red), sq = sbs_block_sum(q[c], red);
+    if (threadIdx.x == 0) {
+      o[2 * c] = sa;
+      o[2 * c + 1] = sq;
+    }
+  }
+}
+
+// one workgroup: thread t < nseg * C finalises (segment t / C, channel t % C); then thread c < C updates channel c's
+// running statistics segment after segment (pre: an earlier call's stats of the same segments, applied first)
+__global__ void __launch_bounds__(SB_THREADS) k_sbs_fwd_fin(const double *__restrict__ part, int nseg, int S, int C, int K,
+                                                           float eps, float *__restrict__ st, int update, float momentum,
+                                                           float *__restrict__ rmean, float *__restrict__ rvar,
+                                                           int64_t *__restrict__ nbt, const float *__restrict__ pre) {
+  float *mean_o = st, *invstd_o = st + (size_t)nseg * C, *varu_o = st + 2 * (size_t)nseg * C;
+  float *cnt_o = st + 3 * (size_t)nseg * C;
+  for (int t = threadIdx.x; t < nseg * C; t += SB_THREADS) {
+    const int sg = t / C, c = t % C;
+    double a = 0.0, q = 0.0, n = 0.0;
+    for (int k = 0; k < K; ++k) {
+      const double *o = part + ((size_t)sg * K + k) * (2 * C + 1);
+      a += o[2 * c];
+      q += o[2 * c + 1];
+      n += o[2 * C];
+    }
+    const double ns = n > 1.0 ? n : 1.0, mean = a / ns;
+    double var = q / ns - mean * mean;
+    var = var > 0.0 ? var : 0.0;
+    mean_o[(size_t)sg * C + c] = (float)mean;
+    invstd_o[(size_t)sg * C + c] = (float)(1.0 / sqrt(var + (double)eps));
+    varu_o[(size_t)sg * C + c] = (float)(n > 1.0 ? var * n / (n - 1.0) : var);
+    if (c == 0) cnt_o[sg] = (float)(n / (double)S);
+  }
+  __syncthreads();
+  if (!update || threadIdx.x >= C) return;
+  const int c = threadIdx.x;
+  float rm = rmean[c], rv = rvar[c];
+  int64_t done = 0;
+  for (int sg = 0; sg < nseg; ++sg) {
+    if (pre) {
+      const float *pm = pre, *pv = pre + 2 * (size_t)nseg * C, *pc = pre + 3 * (size_t)nseg * C;
+      if (pc[sg] > 0.f) {
+        rm = rm * (1.f - momentum) + momentum * pm[(size_t)sg * C + c];
+        rv = rv * (1.f - momentum) + momentum * pv[(size_t)sg * C + c];
+        ++done;
+      }
+    }
+    if (cnt_o[sg] > 0.f) {
+      rm = rm * (1.f - momentum) + momentum * mean_o[(size_t)sg * C + c];
+      rv = rv * (1.f - momentum) + momentum * varu_o[(size_t)sg * C + c];
+      ++done;
+    }
+  }
+  rmean[c] = rm;
+  rvar[c] = rv;
+  if (c == 0 && nbt) nbt[0] += done;
+}
+
+// y for every element: (x - mean) * invstd * gamma + beta with its segment's statistics
+template <typename T>
+__global__ void __launch_bounds__(SB_THREADS) k_sbs_apply(const T *__restrict__ x, long total, long segelems, int C,
+                                                         const float *__restrict__ gamma, const float *__restrict__ beta,
+                                                         const float *__restrict__ st, int nseg, float *__restrict__ y) {
+  const float *mean_i = st, *invstd_i = st + (size_t)nseg * C;
+  for (long k = (long)blockIdx.x * SB_THREADS + threadIdx.x; k < total; k += (long)gridDim.x * SB_THREADS) {
+    const int c = (int)(k % C), sg = (int)(k / segelems);
+    const float g = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+    y[k] = (hld(x, k) - mean_i[(size_t)sg * C + c]) * invstd_i[(size_t)sg * C + c] * g + bt;
+  }
+}
+
+// backward partials over EVERY row: G1 = sum dy, G2 = sum dy * xhat per (segment, chunk, channel)
+template <typename T>
+__global__ void __launch_bounds__(SB_THREADS) k_sbs_bwd_part(const T *__restrict__ x, const float *__restrict__ dy,
+                                                            int B, int S, int C, int K, const float *__restrict__ st,
+                                                            int nseg, double *__restrict__ part) {
+  __shared__ double red[SB_THREADS / 64];
+  const int k = blockIdx.x, sg = blockIdx.y;
+  const long segn = (long)B * S, i0 = segn * k / K, i1 = segn * (k + 1) / K, r0 = (long)sg * B;
+  const float *mean_i = st + (size_t)sg * C, *invstd_i = st + (size_t)nseg * C + (size_t)sg * C;
+  double a1[SBS_MAXC], a2[SBS_MAXC];
+#pragma unroll
+  for (int c = 0; c < SBS_MAXC; ++c) a1[c] = a2[c] = 0.0;
+  for (long i = i0 + threadIdx.x; i < i1; i += SB_THREADS) {
+    const size_t base = (size_t)(r0 * S + i) * C;
+#pragma unroll
+    for (int c = 0; c < SBS_MAXC; ++c)
+      if (c < C) {
+        const double d = (double)dy[base + c];
+        a1[c] += d;
+        a2[c] += d * (double)((hld(x, base + c) - mean_i[c]) * invstd_i[c]);
+      }
+  }
+  double *o = part + ((size_t)sg * K + k) * (2 * C);
+  for (int c = 0; c < C; ++c) {
+    const double s1 = sbs_block_sum(a1[c], red), s2 = sbs_block_sum(a2[c], red);
+    if (threadIdx.x == 0) {
+      o[2 * c] = s1;
+      o[2 * c + 1] = s2;
+    }
+  }
+}
+
+// coef [nseg][C][2] = (G1 / n, G2 / n); dgamma = sum_s G2, dbeta = sum_s G1 in segment order (written or added)
+__global__ void __launch_bounds__(SB_THREADS) k_sbs_bwd_fin(const double *__restrict__ part, int nseg, int S, int C, int K,
+                                                           const float *__restrict__ st, float *__restrict__ coef,
+                                                           float *__restrict__ dgamma, float *__restrict__ dbeta,
+                                                           int accumulate) {
+  const float *cnt_i = st + 3 * (size_t)nseg * C;
+  if (threadIdx.x >= C) return;
+  const int c = threadIdx.x;
+  double tg1 = 0.0, tg2 = 0.0;
+  for (int sg = 0; sg < nseg; ++sg) {
+    double g1 = 0.0, g2 = 0.0;
+    for (int k = 0; k < K; ++k) {
+      const double *o = part + ((size_t)sg * K + k) * (2 * C);
+      g1 += o[2 * c];
+      g2 += o[2 * c + 1];
+    }
+    tg1 += g1;
+    tg2 += g2;
+    const double n = (double)cnt_i[sg] * (double)S;
+    coef[((size_t)sg * C + c) * 2] = n > 0.0 ? (float)(g1 / n) : 0.f;
+    coef[((size_t)sg * C + c) * 2 + 1] = n > 0.0 ? (float)(g2 / n) : 0.f;
+  }
+  if (dgamma) dgamma[c] = accumulate ? dgamma[c] + (float)tg2 : (float)tg2;
+  if (dbeta) dbeta[c] = accumulate ? dbeta[c] + (float)tg1 : (float)tg1;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(SB_THREADS) k_sbs_bwd_apply(const T *__restrict__ x, const float *__restrict__ dy,
+                                                             const uint8_t *__restrict__ rmask, long total, int S,
+                                                             long segelems, int C, const float *__restrict__ gamma,
+                                                             const float *__restrict__ st, int nseg,
+                                                             const float *__restrict__ coef, T *__restrict__ dx) {
+  const float *mean_i = st, *invstd_i = st + (size_t)nseg * C;
+  for (long k = (long)blockIdx.x * SB_THREADS + threadIdx.x; k < total; k += (long)gridDim.x * SB_THREADS) {
+    const int c = (int)(k % C), sg = (int)(k / segelems);
+    const long row = k / ((long)S * C);
+    const float g = gamma ? gamma[c] : 1.f;
+    const float mean = mean_i[(size_t)sg * C + c], invstd = invstd_i[(size_t)sg * C + c];
+    const float c1 = coef[((size_t)sg * C + c) * 2], c2 = coef[((size_t)sg * C + c) * 2 + 1];
+    const float w = (!rmask || rmask[row]) ? 1.f : 0.f;
+    const float xh = (hld(x, k) - mean) * invstd;
+    hst(dx, k, g * invstd * (dy[k] - w * (c1 + xh * c2)));
+  }
+}
+
+int sbs_chunks(long segn) {
+  long k = segn / 2048;
+  return (int)(k < 1 ? 1 : k > SBS_MAXK ? SBS_MAXK : k);
+}
+
+int sbs_grid(long total) {
+  const long b = (total + SB_THREADS * 4 - 1) / (SB_THREADS * 4);
+  return (int)(b < 1 ? 1 : b > 4096 ? 4096 : b);
+}
+
+template <typename T>
+int sbs_fwd(const void *x, const uint8_t *m, int nseg, int B, int S, int C, const float *gamma, const float *beta,
+            float eps, float *y, float *st, int update, float momentum, float *rmean, float *rvar, int64_t *nbt,
+            const float *pre, double *ws, hipStream_t s) {
+  const int K = sbs_chunks((long)B * S);
+  const long total = (long)nseg * B * S * C;
+  hipLaunchKernelGGL(k_sbs_fwd_part<T>, dim3(K, nseg), dim3(SB_THREADS), 0, s, (const T *)x, m, B, S, C, K, ws);
+  GMZ_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_sbs_fwd_fin, dim3(1), dim3(SB_THREADS), 0, s, (const double *)ws, nseg, S, C, K, eps, st, update,
+                     momentum, rmean, rvar, nbt, pre);
+  GMZ_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_sbs_apply<T>, dim3(sbs_grid(total)), dim3(SB_THREADS), 0, s, (const T *)x, total,
+                     (long)B * S * C, C, gamma, beta, (const float *)st, nseg, y);
+  GMZ_LAUNCH_CHECK();
+  return 0;
+}
+
+template <typename T>
+int sbs_bwd(const void *x, const float *dy, const uint8_t *m, int nseg, int B, int S, int C, const float *gamma,
+            const float *st, void *dx, float *dgamma, float *dbeta, int acc, double *ws, hipStream_t s) {
+  const int K = sbs_chunks((long)B * S);
+  const long total = (long)nseg * B * S * C;
+  float *coef = (float *)(ws + (size_t)nseg * SBS_MAXK * 2 * SBS_MAXC);
+  hipLaunchKernelGGL(k_sbs_bwd_part<T>, dim3(K, nseg), dim3(SB_THREADS), 0, s, (const T *)x, dy, B, S, C, K, st, nseg, ws);
+  GMZ_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_sbs_bwd_fin, dim3(1), dim3(SB_THREADS), 0, s, (const double *)ws, nseg, S, C, K, st, coef, dgamma,
+                     dbeta, acc);
+  GMZ_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_sbs_bwd_apply<T>, dim3(sbs_grid(total)), dim3(SB_THREADS), 0, s, (const T *)x, dy, m, total, S,
+                     (long)B * S * C, C, gamma, st, nseg, (const float *)coef, (T *)dx);
+  GMZ_LAUNCH_CHECK();
+  return 0;
+}
+
+size_t sbs_ws_need(int nseg) {
+  // partials (forward: 2C + 1, backward: 2C doubles per segment and chunk) + the backward's f32 coefficients
+  return ((size_t)nseg * SBS_MAXK * (2 * SBS_MAXC + 1)) * sizeof(double) + (size_t)nseg * SBS_MAXC * 2 * sizeof(float);
+}
+
 }  // namespace
 }  // namespace gmz
+
+GMZ_EXPORT int gmz_seg_bn_small_workspace_bytes(int nseg, int C, size_t *out) {
+  if (!out || nseg <= 0 || nseg > 32 || C <= 0 || C > SBS_MAXC)
+    return fail("gmz_seg_bn_small_workspace_bytes: 1 <= nseg <= 32, 1 <= C <= 8");
+  *out = sbs_ws_need(nseg);
+  return 0;
+}
+
+GMZ_EXPORT int gmz_seg_bn_forward_small(int dtype, const void *x, const uint8_t *row_mask, int nseg, int B, int S, int C,
+                                        const float *gamma, const float *beta, float eps, float *y, float *stats,
+                                        size_t stats_bytes, int update, float momentum, float *running_mean,
+                                        float *running_var, int64_t *num_batches, const float *pre_stats, void *ws,
+                                        size_t ws_bytes, void *stream) {
+  if (!x || !y || !stats || !ws || nseg <= 0 || nseg > 32 || B <= 0 || S <= 0 || C <= 0 || C > SBS_MAXC ||
+      (size_t)nseg * B * S * C >= (1ull << 31))
+    return fail("gmz_seg_bn_forward_small: bad arguments (1 <= nseg <= 32, 1 <= C <= 8)");
+  if (stats_bytes < ((size_t)3 * nseg * C + nseg) * sizeof(float))
+    return fail("gmz_seg_bn_forward_small: stats of " + std::to_string(stats_bytes) + " bytes, needs (3 nseg C + nseg) f32");
+  if (ws_bytes < sbs_ws_need(nseg))
+    return fail("gmz_seg_bn_forward_small: workspace of " + std::to_string(ws_bytes) + " bytes, needs " +
+                std::to_string(sbs_ws_need(nseg)));
+  if (update && (!running_mean || !running_var)) return fail("gmz_seg_bn_forward_small: update needs running statistics");
+  hipStream_t s = (hipStream_t)stream;
+  double *w = (double *)ws;
+  switch (dtype) {
+    case 0: return sbs_fwd<float>(x, row_mask, nseg, B, S, C, gamma, beta, eps, y, stats, update, momentum, running_mean,
+                                  running_var, num_batches, pre_stats, w, s);
+    case 1: return sbs_fwd<__half>(x, row_mask, nseg, B, S, C, gamma, beta, eps, y, stats, update, momentum, running_mean,
+                                   running_var, num_batches, pre_stats, w, s);
+    case 2: return sbs_fwd<__hip_bfloat16>(x, row_mask, nseg, B, S, C, gamma, beta, eps, y, stats, update, momentum,
+                                           running_mean, running_var, num_batches, pre_stats, w, s);
+  }
+  return fail("gmz_seg_bn_forward_small: dtype must be 0 (f32), 1 (f16) or 2 (bf16)");
+}
+
+GMZ_EXPORT int gmz_seg_bn_backward_small(int dtype, const void *x, const float *dy, const uint8_t *row_mask, int nseg,
+                                         int B, int S, int C, const float *gamma, const float *stats, size_t stats_bytes,
+                                         void *dx, float *dgamma, float *dbeta, int accumulate, void *ws,
+                                         size_t ws_bytes, void *stream) {
+  if (!x || !dy || !stats || !dx || !ws || nseg <= 0 || nseg > 32 || B <= 0 || S <= 0 || C <= 0 || C > SBS_MAXC ||
+      (size_t)nseg * B * S * C >= (1ull << 31))
+    return fail("gmz_seg_bn_backward_small: bad arguments (1 <= nseg <= 32, 1 <= C <= 8)");
+  if (stats_bytes < ((size_t)3 * nseg * C + nseg) * sizeof(float))
+    return fail("gmz_seg_bn_backward_small: stats of " + std::to_string(stats_bytes) + " bytes, needs (3 nseg C + nseg) f32");
+  if (ws_bytes < sbs_ws_need(nseg))
+    return fail("gmz_seg_bn_backward_small: workspace of " + std::to_string(ws_bytes) + " bytes, needs " +
+                std::to_string(sbs_ws_need(nseg)));
+  hipStream_t s = (hipStream_t)stream;
+  double *w = (double *)ws;
+  switch (dtype) {
+    case 0: return sbs_bwd<float>(x, dy, row_mask, nseg, B, S, C, gamma, stats, dx, dgamma, dbeta, accumulate, w, s);
+    case 1: return sbs_bwd<__half>(x, dy, row_mask, nseg, B, S, C, gamma, stats, dx, dgamma, dbeta, accumulate, w, s);
+    case 2:
+      return sbs_bwd<__hip_bfloat16>(x, dy, row_mask, nseg, B, S, C, gamma, stats, dx, dgamma, dbeta, accumulate, w, s);
+  }
+  return fail("gmz_seg_bn_backward_small: dtype must be 0 (f32), 1 (f16) or 2 (bf16)");
+}
 
 GMZ_EXPORT int gmz_seg_bn_forward(int dtype, const void *x, const uint8_t *row_mask, int nseg, int B, int S, int C,
                                   const float *gamma, const float *beta, float eps, float *y, float *stats,

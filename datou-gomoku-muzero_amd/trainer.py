@@ -1546,6 +1546,23 @@ SEG_BN_HIP = True
 SEG_BN_HIP_MIN_C = 64
 
 
+# the 1- and 2-channel heads' segmented BatchNorms (C <= _SEG_BN_SMALL_C) on gmz_seg_bn_*_small: (segment, chunk)
+# workgroups over every channel instead of one workgroup per channel (SEG_BN_SMALL; False: PyTorch's _bn_seg_grad)
+SEG_BN_SMALL = True
+_SEG_BN_SMALL_C = 8
+_SBS_WS = {}
+
+
+def _seg_bn_small_ws(nseg, C, device):
+    import ctypes
+    from . import _lib
+    if nseg not in _SBS_WS:
+        n = ctypes.c_size_t()
+        _lib.check(_lib.load().gmz_seg_bn_small_workspace_bytes(nseg, C, ctypes.byref(n)))
+        _SBS_WS[nseg] = n.value
+    return torch.empty((_SBS_WS[nseg] + 7) // 8, dtype=torch.float64, device=device)
+
+
 class _SegBN(torch.autograd.Function):
     """_bn_seg_grad's values and gradients for x [nseg*B, C(, H, W)] (channels-last 4-D or contiguous 2-D) on the
     GPU: y float32 like x's layout, and the stats [3*nseg*C + nseg] (mean, invstd, unbiased var, live rows)."""
@@ -1560,10 +1577,18 @@ class _SegBN(torch.autograd.Function):
         else:
             y = torch.empty((N, C), dtype=torch.float32, device=x.device)
         st = torch.empty(3 * nseg * C + nseg, dtype=torch.float32, device=x.device)
-        _lib.check(_lib.load().gmz_seg_bn_forward(_BN_DTYPES[x.dtype], _lib.ptr(x), _lib.ptr(m), nseg, N // nseg, S, C,
-                                                  _lib.ptr(gamma), _lib.ptr(beta), float(eps), _lib.ptr(y), _lib.ptr(st),
-                                                  _lib.nbytes(st), int(update), float(momentum), _lib.ptr(rmean), _lib.ptr(rvar),
-                                                  _lib.ptr(nbt), _lib.ptr(pre), _lib.stream_ptr()))
+        if C <= _SEG_BN_SMALL_C:  # few channels: (segment, chunk) workgroups over every channel
+            ws = _seg_bn_small_ws(nseg, C, x.device)
+            _lib.check(_lib.load().gmz_seg_bn_forward_small(
+                _BN_DTYPES[x.dtype], _lib.ptr(x), _lib.ptr(m), nseg, N // nseg, S, C, _lib.ptr(gamma), _lib.ptr(beta),
+                float(eps), _lib.ptr(y), _lib.ptr(st), _lib.nbytes(st), int(update), float(momentum), _lib.ptr(rmean),
+                _lib.ptr(rvar), _lib.ptr(nbt), _lib.ptr(pre), _lib.ptr(ws), _lib.nbytes(ws), _lib.stream_ptr()))
+        else:
+            _lib.check(_lib.load().gmz_seg_bn_forward(_BN_DTYPES[x.dtype], _lib.ptr(x), _lib.ptr(m), nseg, N // nseg, S, C,
+                                                      _lib.ptr(gamma), _lib.ptr(beta), float(eps), _lib.ptr(y),
+                                                      _lib.ptr(st), _lib.nbytes(st), int(update), float(momentum),
+                                                      _lib.ptr(rmean), _lib.ptr(rvar), _lib.ptr(nbt), _lib.ptr(pre),
+                                                      _lib.stream_ptr()))
         ctx.save_for_backward(x, gamma, beta, st, m)
         ctx.nseg = nseg
         ctx.mark_non_differentiable(st)
@@ -1583,10 +1608,17 @@ class _SegBN(torch.autograd.Function):
                   and gamma.grad.is_contiguous() and beta.grad.is_contiguous())
         dg = gamma.grad if direct else torch.empty(C, dtype=torch.float32, device=x.device)
         db = beta.grad if direct else torch.empty(C, dtype=torch.float32, device=x.device)
-        _lib.check(_lib.load().gmz_seg_bn_backward(_BN_DTYPES[x.dtype], _lib.ptr(x), _lib.ptr(dy), _lib.ptr(m), ctx.nseg,
-                                                   N // ctx.nseg, S, C, _lib.ptr(gamma), _lib.ptr(st), _lib.nbytes(st),
-                                                   _lib.ptr(dx),
-                                                   _lib.ptr(dg), _lib.ptr(db), int(direct), _lib.stream_ptr()))
+        if C <= _SEG_BN_SMALL_C:
+            ws = _seg_bn_small_ws(ctx.nseg, C, x.device)
+            _lib.check(_lib.load().gmz_seg_bn_backward_small(
+                _BN_DTYPES[x.dtype], _lib.ptr(x), _lib.ptr(dy), _lib.ptr(m), ctx.nseg, N // ctx.nseg, S, C,
+                _lib.ptr(gamma), _lib.ptr(st), _lib.nbytes(st), _lib.ptr(dx), _lib.ptr(dg), _lib.ptr(db), int(direct),
+                _lib.ptr(ws), _lib.nbytes(ws), _lib.stream_ptr()))
+        else:
+            _lib.check(_lib.load().gmz_seg_bn_backward(_BN_DTYPES[x.dtype], _lib.ptr(x), _lib.ptr(dy), _lib.ptr(m),
+                                                       ctx.nseg, N // ctx.nseg, S, C, _lib.ptr(gamma), _lib.ptr(st),
+                                                       _lib.nbytes(st), _lib.ptr(dx), _lib.ptr(dg), _lib.ptr(db),
+                                                       int(direct), _lib.stream_ptr()))
         if direct:
             return dx, None, None, None, None, None, None, None, None, None, None, None
         return dx, dg, db, None, None, None, None, None, None, None, None, None
@@ -1599,7 +1631,8 @@ def _bn_steps(mod, x, ms, update=True, pre=None):
     and other layouts: _bn_seg_grad + _bn_running_update."""
     nseg = ms.shape[0]
     hip = (SEG_BN_HIP and FUSED_BN and x.is_cuda and x.dtype in _BN_DTYPES and mod.momentum is not None
-           and x.shape[1] >= SEG_BN_HIP_MIN_C and nseg <= 32 and x.shape[0] % nseg == 0
+           and (x.shape[1] >= SEG_BN_HIP_MIN_C or (SEG_BN_SMALL and x.shape[1] <= _SEG_BN_SMALL_C))
+           and nseg <= 32 and x.shape[0] % nseg == 0
            and ((x.dim() == 2 and x.is_contiguous()) or (x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last)))
            and (pre is None or pre[0] == "hip"))
     if hip:

@@ -498,6 +498,20 @@ int gmz_seg_bn_forward(int dtype, const void *x_dev, const uint8_t *row_mask_dev
 int gmz_seg_bn_backward(int dtype, const void *x_dev, const float *dy_dev, const uint8_t *row_mask_dev, int nseg, int B,
                         int S, int C, const float *gamma_dev, const float *stats_dev, size_t stats_bytes, void *dx_dev,
                         float *dgamma_dev, float *dbeta_dev, int accumulate, void *stream);
+/* gmz_seg_bn_forward / _backward for a FEW channels (1 <= C <= 8: the 1- and 2-channel prediction heads' BatchNorms,
+ * network.py:62,65): the same results (variance as E[x^2] - mean^2 in f64) computed by (segment, chunk) workgroups
+ * over every channel at once — partials, a one-workgroup finalisation, an elementwise pass — instead of one
+ * workgroup per channel.  workspace_dev: gmz_seg_bn_small_workspace_bytes(nseg, C).  (Round 6, additive) */
+int gmz_seg_bn_small_workspace_bytes(int nseg, int C, size_t *out);
+int gmz_seg_bn_forward_small(int dtype, const void *x_dev, const uint8_t *row_mask_dev, int nseg, int B, int S, int C,
+                             const float *gamma_dev, const float *beta_dev, float eps, float *y_dev, float *stats_dev,
+                             size_t stats_bytes, int update, float momentum, float *running_mean_dev,
+                             float *running_var_dev, int64_t *num_batches_dev, const float *pre_stats_dev,
+                             void *workspace_dev, size_t ws_bytes, void *stream);
+int gmz_seg_bn_backward_small(int dtype, const void *x_dev, const float *dy_dev, const uint8_t *row_mask_dev, int nseg,
+                              int B, int S, int C, const float *gamma_dev, const float *stats_dev, size_t stats_bytes,
+                              void *dx_dev, float *dgamma_dev, float *dbeta_dev, int accumulate, void *workspace_dev,
+                              size_t ws_bytes, void *stream);
 /* bytes of the backward's workspace for P positions and O = O0 + O1 outputs */
 int gmz_head_conv1x1_workspace_bytes(long P, int O, size_t *out);
 /* The backward of gmz_head_conv1x1_forward: dx_dev [P][128] = round(sum_o dy[p][o] W[o][c]) over BOTH heads

@@ -51,6 +51,8 @@ ap.add_argument("--op-sources", type=int, default=0, metavar="N",
                 help="with --eager: profile one more step and print the N trainer.py lines launching the most PyTorch kernels")
 ap.add_argument("--bn-bwd-stats", action="store_true",
                 help="BatchNorm backward sums in the input-gradient conv's epilogue (trainer.FUSED_BN_BWD_STATS on)")
+ap.add_argument("--torch-small-bn", action="store_true",
+                help="the 1- and 2-channel heads' segmented BatchNorms on PyTorch (trainer.SEG_BN_SMALL off)")
 ap.add_argument("--torch-opt", action="store_true",
                 help="PyTorch's unscale_ / clip_grad_norm_ / fused Adam / foreach soft update (trainer.FUSED_OPT off)")
 ap.add_argument("--no-defer-bn", action="store_true",
@@ -85,6 +87,7 @@ T.TARGET_F16 = T.TARGET_F16 and not a.target_f32
 T.DEFER_WGRAD = T.DEFER_WGRAD and not a.no_defer_wgrad
 T.DEFER_BN_APPLY = T.DEFER_BN_APPLY and not a.no_defer_bn
 T.FUSED_OPT = T.FUSED_OPT and not a.torch_opt
+T.SEG_BN_SMALL = T.SEG_BN_SMALL and not a.torch_small_bn
 T.FUSED_BN_BWD_STATS = T.FUSED_BN_BWD_STATS or a.bn_bwd_stats
 
 cfg = T.TrainConfig(BOARD_SIZE=a.size, NUM_RES_BLOCKS=a.blocks, PHYSICAL_BATCH_SIZE=a.batch,
