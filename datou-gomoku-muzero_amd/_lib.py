@@ -67,6 +67,8 @@ _SIGS = {
     "gmz_bn_eval": ([I, I, P, P, I, I, I, P, P, P, P, ctypes.c_float, I, P, P, SZ, P], I),
     "gmz_conv3x3_pack": ([I, P, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, I, P, P], I),
     "gmz_conv3x3_forward": ([I, I, P, P, P, I, P], I),
+    "gmz_conv3x3_pack_job_bytes": ([ctypes.POINTER(SZ)], I),
+    "gmz_conv3x3_pack_many": ([I, P, I, P], I),
     "gmz_conv3x3_forward_add": ([I, I, P, P, P, P, I, P], I),
     "gmz_conv3x3_stats_slots": ([I, ctypes.POINTER(ctypes.c_int)], I),
     "gmz_conv3x3_wgrad_workspace_bytes": ([I, ctypes.POINTER(ctypes.c_size_t)], I),

@@ -99,6 +99,39 @@ __global__ void __launch_bounds__(256) k_pack_conv(const float *__restrict__ w, 
   *(uint4 *)(out + (size_t)i * 8) = r;
 }
 
+// Many weights packed in ONE launch (the trainer re-packs every cached conv weight right after its optimiser step,
+// gmz_conv3x3_pack_many): grid.y = the table entry, grid.x covers one weight's fragments as k_pack_conv does.
+struct PackJob {
+  const float *w;
+  long long s0, s1, s2, s3;
+  uint16_t *out;
+  int transpose, pad;
+};
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_pack_many(const PackJob *__restrict__ jobs) {
+  const PackJob j = jobs[blockIdx.y];
+  const int i = blockIdx.x * 256 + threadIdx.x;  // (t, ks, nt, l)
+  if (i >= CKSTEPS * 8 * 64) return;
+  const int l = i & 63, nt = (i >> 6) & 7, st = i >> 9, t = st >> 2, ks = st & 3;
+  const int n = nt * 16 + (l & 15);
+  u16x4_t lo, hi;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int c = chunk_of(ks, l >> 4) * 8 + e;
+    const int o = j.transpose ? c : n, ci = j.transpose ? n : c, tt = j.transpose ? 8 - t : t;
+    const uint16_t b = Mfma<T>::bits(j.w[o * j.s0 + ci * j.s1 + (tt / 3) * j.s2 + (tt % 3) * j.s3]);
+    if (e < 4) lo[e] = b;
+    else hi[e - 4] = b;
+  }
+  uint4 r;
+  r.x = (uint32_t)lo[0] | ((uint32_t)lo[1] << 16);
+  r.y = (uint32_t)lo[2] | ((uint32_t)lo[3] << 16);
+  r.z = (uint32_t)hi[0] | ((uint32_t)hi[1] << 16);
+  r.w = (uint32_t)hi[2] | ((uint32_t)hi[3] << 16);
+  *(uint4 *)(j.out + (size_t)i * 8) = r;
+}
+
 // The BatchNorm whose backward the output feeds (BWD statistics, gmz_conv3x3_forward_bwdstats): its input
 // x, its output y (after its ReLU) and its saved (mean, invstd) f32 [2][128]
 struct BnBwd {
@@ -793,6 +826,23 @@ GMZ_EXPORT int gmz_conv3x3_pack(int dtype, const float *w, int64_t s0, int64_t s
   else
     hipLaunchKernelGGL(k_pack_conv<__hip_bfloat16>, dim3((n + 255) / 256), dim3(256), 0, st, w, (long)s0, (long)s1,
                        (long)s2, (long)s3, transpose, (uint16_t *)packed);
+  GMZ_LAUNCH_CHECK();
+  return 0;
+}
+
+GMZ_EXPORT int gmz_conv3x3_pack_job_bytes(size_t *out) {
+  if (!out) return fail("gmz_conv3x3_pack_job_bytes: null");
+  *out = sizeof(PackJob);
+  return 0;
+}
+
+GMZ_EXPORT int gmz_conv3x3_pack_many(int dtype, const void *jobs, int n_jobs, void *stream) {
+  if (!jobs || n_jobs <= 0 || n_jobs > 65535) return fail("gmz_conv3x3_pack_many: 1 <= n_jobs <= 65535 jobs");
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 grid((CKSTEPS * 8 * 64 + 255) / 256, n_jobs);
+  if (dtype == 1) hipLaunchKernelGGL(k_pack_many<__half>, grid, dim3(256), 0, st, (const PackJob *)jobs);
+  else if (dtype == 2) hipLaunchKernelGGL(k_pack_many<__hip_bfloat16>, grid, dim3(256), 0, st, (const PackJob *)jobs);
+  else return fail("gmz_conv3x3_pack_many: dtype must be 1 (f16) or 2 (bf16)");
   GMZ_LAUNCH_CHECK();
   return 0;
 }

@@ -210,6 +210,11 @@ GRAPH_ALLREDUCE = True
 # instead of a pass of its own: one launch and one read of the BatchNorm's input fewer per use
 DEFER_BN_APPLY = True
 
+# every packed 3x3 conv weight the step uses (_packed_conv_weight's caches on the model's and the target's parameters)
+# re-packed by ONE gmz_conv3x3_pack_many launch at the top of the step instead of one gmz_conv3x3_pack per weight at
+# its first use (87 launches per 15x15 step; A/B: False)
+BATCH_REPACK = True
+
 
 class _PendingBN:
     """A deferred BatchNorm output's recipe, attached to the (not yet written) output tensor as ``_gmz_pending``:
@@ -532,12 +537,62 @@ def _packed_conv_weight(w, dtype, transpose, parent=None):
     hit = cache.get(key)
     if hit is not None and hit[0] == owner._version:
         return hit[1]
-    out = torch.empty(147456, dtype=torch.int16, device=w.device)
+    out = hit[1] if hit is not None else torch.empty(147456, dtype=torch.int16, device=w.device)
     s = w.stride()
     _lib.check(_lib.load().gmz_conv3x3_pack(_CONV_DTYPES[dtype], _lib.ptr(w.detach()), s[0], s[1], s[2], s[3],
                                             int(transpose), _lib.ptr(out), _lib.stream_ptr()))
-    cache[key] = (owner._version, out)
+    # (version, packed, source view, transpose, dtype): _repack_stale re-packs the entry in place from the source
+    cache[key] = (owner._version, out, w.detach(), int(transpose), dtype)
     return out
+
+
+_PACK_JOB = np.dtype([("w", "<u8"), ("s", "<i8", 4), ("out", "<u8"), ("transpose", "<i4"), ("pad", "<i4")])
+
+
+def _repack_stale(owners, tables, prepare=False):
+    """BATCH_REPACK: every _packed_conv_weight entry cached on ``owners`` whose parameter changed since it was packed
+    (the optimiser step), re-packed into its own buffer by one gmz_conv3x3_pack_many launch per dtype; the entries are
+    then current, so the step's forward and backward find them packed.  ``tables``: the device job tables by content
+    (a captured step replays the one it was captured with; inside a capture only an existing table is used — an
+    unseen set of stale weights is left to the per-use packs; ``prepare``: only build the tables, before a capture)."""
+    from . import _lib
+    jobs = {}
+    for owner in owners:
+        cache = owner.__dict__.get("_gmz_pack")
+        if not cache:
+            continue
+        for key, hit in cache.items():
+            if len(hit) == 5 and hit[0] != owner._version:
+                jobs.setdefault(hit[4], []).append((owner, key, hit))
+    if not jobs:
+        return 0
+    capturing = torch.cuda.is_current_stream_capturing()
+    n = 0
+    for dtype, js in jobs.items():
+        sig = (dtype,) + tuple((h[2].data_ptr(), h[2].stride(), h[1].data_ptr(), h[3]) for _, _, h in js)
+        table = tables.get(sig)
+        if table is None:
+            if capturing:
+                continue
+            if "job_bytes" not in tables:
+                import ctypes
+                nb = ctypes.c_size_t()
+                _lib.check(_lib.load().gmz_conv3x3_pack_job_bytes(ctypes.byref(nb)))
+                if nb.value != _PACK_JOB.itemsize:
+                    raise _lib.GmzError("gmz_conv3x3_pack_job_bytes: %d, expected %d" % (nb.value, _PACK_JOB.itemsize))
+                tables["job_bytes"] = nb.value
+            arr = np.zeros(len(js), dtype=_PACK_JOB)
+            for i, (_, _, h) in enumerate(js):
+                arr[i] = (h[2].data_ptr(), h[2].stride(), h[1].data_ptr(), h[3], 0)
+            table = torch.from_numpy(arr.view(np.uint8)).to(js[0][2][1].device)
+            tables[sig] = table
+        if prepare:
+            continue
+        _lib.check(_lib.load().gmz_conv3x3_pack_many(_CONV_DTYPES[dtype], _lib.ptr(table), len(js), _lib.stream_ptr()))
+        for owner, key, h in js:
+            owner.__dict__["_gmz_pack"][key] = (owner._version,) + tuple(h[1:])
+        n += len(js)
+    return n
 
 
 _STATS_SLOTS = {}
@@ -2164,11 +2219,14 @@ class Trainer:
         self._fopt = None  # FUSED_OPT's buffers (built at the first update)
         self.graph_allreduce = False  # True once the captured step holds the RCCL all-reduces
         self._static = None
+        self._pack_tables = {}  # BATCH_REPACK's job tables
 
     # ------------------------------------------------------------------ step pieces
     def _forward_backward(self, batch, is_weights, acc=1, k=None, flip=None, augmented=False, flush=True):
         """Loss and backward; ``flush`` = False leaves the deferred 3x3 weight gradients queued (bucket B) for
         ``flush_wgrads`` after bucket A's all-reduce has been issued."""
+        if BATCH_REPACK and self.device.type == "cuda":
+            _repack_stale(list(self.model.parameters()) + list(self.target.parameters()), self._pack_tables)
         loss, logs, td = muzero_loss(self.model, self.target, batch, is_weights, self.cfg, k=k, flip=flip,
                                      amp=self.amp, amp_dtype=self.amp_dtype, sync_logs=False, augmented=augmented)
         _DIRECT_GRAD[0] = True
@@ -2434,6 +2492,9 @@ class Trainer:
         if self.graph and self.step_count >= self.graph_warmup:
             self._augment_into_static(batch, is_weights, k, flip)
             if self._graphs is None:
+                if BATCH_REPACK:  # the job table the captured step will replay, built before the capture
+                    _repack_stale(list(self.model.parameters()) + list(self.target.parameters()), self._pack_tables,
+                                  prepare=True)
                 self._capture()
             if isinstance(self._graphs, tuple):  # collectives not capturable: the all-reduces between replays
                 g1, gf, g2 = self._graphs

@@ -373,6 +373,12 @@ int gmz_bn_eval(int dtype, int layout, const void *x_dev, const void *res_dev, i
  * gmz_conv3x3_forward: x_dev, packed_dev and y_dev 16-B aligned, N >= 1. */
 int gmz_conv3x3_pack(int dtype, const float *w_dev, int64_t s0, int64_t s1, int64_t s2, int64_t s3, int transpose,
                      void *packed_dev, void *stream);
+/* gmz_conv3x3_pack of n_jobs weights in one launch: jobs_dev (device memory, gmz_conv3x3_pack_job_bytes each) =
+ * {const float *w; int64 s0, s1, s2, s3; uint16 *out; int32 transpose; int32 pad} per weight, every out 294,912
+ * bytes and 16-B aligned.  The trainer re-packs its cached conv weights this way after every optimiser step.
+ * (Round 6, additive) */
+int gmz_conv3x3_pack_job_bytes(size_t *out);
+int gmz_conv3x3_pack_many(int dtype, const void *jobs_dev, int n_jobs, void *stream);
 /* gmz_conv3x3_forward_stats with the BatchNorm statistics partials per BOARD: stats_dev f64 [128][N][3] (sum,
  * sum of squares, valid pixels of board n; 0 for a masked-out board), for gmz_bn_forward_seg; stats_slots must be
  * N.  (ABI 8; stats_slots ABI 10) */

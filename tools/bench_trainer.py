@@ -53,6 +53,8 @@ ap.add_argument("--bn-bwd-stats", action="store_true",
                 help="BatchNorm backward sums in the input-gradient conv's epilogue (trainer.FUSED_BN_BWD_STATS on)")
 ap.add_argument("--torch-small-bn", action="store_true",
                 help="the 1- and 2-channel heads' segmented BatchNorms on PyTorch (trainer.SEG_BN_SMALL off)")
+ap.add_argument("--no-batch-repack", action="store_true",
+                help="each packed conv weight re-packed at its first use, one launch each (trainer.BATCH_REPACK off)")
 ap.add_argument("--torch-opt", action="store_true",
                 help="PyTorch's unscale_ / clip_grad_norm_ / fused Adam / foreach soft update (trainer.FUSED_OPT off)")
 ap.add_argument("--no-defer-bn", action="store_true",
@@ -88,6 +90,7 @@ T.DEFER_WGRAD = T.DEFER_WGRAD and not a.no_defer_wgrad
 T.DEFER_BN_APPLY = T.DEFER_BN_APPLY and not a.no_defer_bn
 T.FUSED_OPT = T.FUSED_OPT and not a.torch_opt
 T.SEG_BN_SMALL = T.SEG_BN_SMALL and not a.torch_small_bn
+T.BATCH_REPACK = T.BATCH_REPACK and not a.no_batch_repack
 T.FUSED_BN_BWD_STATS = T.FUSED_BN_BWD_STATS or a.bn_bwd_stats
 
 cfg = T.TrainConfig(BOARD_SIZE=a.size, NUM_RES_BLOCKS=a.blocks, PHYSICAL_BATCH_SIZE=a.batch,
