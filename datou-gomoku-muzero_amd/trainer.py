@@ -1846,7 +1846,8 @@ def muzero_loss(model, target_model, batch, is_weights, cfg, k=None, flip=None, 
             # after obs[0]'s (the representation BatchNorms' running statistics update in the
             # reference's order); their projections stay on this stream, interleaved with the dynamics'
             # projections as in the reference (the projection BatchNorm's running statistics)
-            masks = [act[:, s] != -1 for s in range(c.NUM_UNROLL_STEPS)]
+            live_act = (act != -1).t().contiguous()  # [U, B]: each step's mask a contiguous row (2 launches, not U)
+            masks = list(live_act)
             side[1].wait_stream(main)
             tru_h, tru_ev = [], []
             with torch.cuda.stream(side[1]), torch.no_grad():
@@ -1872,15 +1873,16 @@ def muzero_loss(model, target_model, batch, is_weights, cfg, k=None, flip=None, 
             zsup = scalar_to_support(z.t().contiguous(), *vsup)       # [U+1, B, bins]
             rsupt = scalar_to_support(rew.t().contiguous(), *rsup)    # [U, B, bins]
             h0, hks, mks = h, [], []
-            steps = zero
-            live_act = (act != -1).t().contiguous()                     # [U, B]: each step's mask a contiguous row
+            if side is None:
+                live_act = (act != -1).t().contiguous()                 # [U, B]: each step's mask a contiguous row
             a_all = torch.where(live_act, act_aug.t(), torch.zeros_like(act_aug.t())).reshape(-1)  # step-major [U*B]
             dyn_net = model.dynamics_net
             emb_all = None if _dyn_stem_hip_ok(dyn_net, h) else dyn_net.embed(a_all, h)  # every step's embedding
             B0 = h.shape[0]
+            # a step with no live row counts nothing (loss.py:90-91); a count of 0/1 terms: exact in any order
+            steps = live_act.any(1).to(torch.float32).sum()
             for s in range(U):
                 m = live_act[s]
-                steps = steps + m.any().to(torch.float32)   # a step with no live row counts nothing (loss.py:90-91)
                 hk, _ = model.dynamics(h, a_all[s * B0:(s + 1) * B0], mask=m, reward=False,
                                        emb=None if emb_all is None else emb_all[s * B0:(s + 1) * B0])
                 hks.append(hk)
