@@ -119,3 +119,8 @@ def test_round6_entry_points_check_before_launching():
                                            ctypes.c_void_p((1 << 20) + 4096), 360, None, None, 0, None) < 0
     assert "alias" in err()
     assert lib.gmz_comm_stamp(fake, 3, None) < 0 and "phase" in err()
+    # the batched conv-weight re-pack: its job record is the trainer's numpy layout; empty tables and bad dtypes refused
+    jb = ctypes.c_size_t()
+    assert lib.gmz_conv3x3_pack_job_bytes(ctypes.byref(jb)) == 0 and jb.value == 56
+    assert lib.gmz_conv3x3_pack_many(1, fake, 0, None) < 0 and "n_jobs" in err()
+    assert lib.gmz_conv3x3_pack_many(3, fake, 2, None) < 0 and "dtype" in err()
