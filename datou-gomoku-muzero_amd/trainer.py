@@ -2378,6 +2378,7 @@ class Trainer:
             # re-pack — and a graph capture after this step records the packs
             from torch.autograd.graph import increment_version
             increment_version(f["versioned"])
+            self.opt._opt_called = True  # what Optimizer.step records for the LR scheduler's call-order check
             if f["fallback"]:
                 with torch.no_grad():
                     tp, sp = [t for t, _ in f["fallback"]], [p for _, p in f["fallback"]]
