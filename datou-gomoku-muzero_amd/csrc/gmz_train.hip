@@ -97,6 +97,9 @@ __global__ void __launch_bounds__(BN_THREADS) k_bn_stats(const T *__restrict__ x
 //  forward : save = (mean, invstd), running-stat update (nn.BatchNorm training: unbiased variance)
 //  backward: dgamma = sum dz*xhat, dbeta = sum dz, coef = (mean dz, mean dz*xhat) over the masked rows
 constexpr int FIN_MAX_WAVES = 4;
+#ifndef GMZ_FIN_UNROLL  // partial records per thread loaded before any is summed (A/B; the summation order is the same)
+#define GMZ_FIN_UNROLL 2
+#endif
 __global__ void __launch_bounds__(WAVE * FIN_MAX_WAVES) k_bn_finalize(const double *__restrict__ ws, int C, int ns, int cs,
                                                                       int ts, int backward, float eps, float momentum,
                                                                       float *save, float *running_mean,
@@ -104,7 +107,7 @@ __global__ void __launch_bounds__(WAVE * FIN_MAX_WAVES) k_bn_finalize(const doub
                                                                       float *dgamma, float *dbeta, float *coef) {
   const int c = blockIdx.x, nt = blockDim.x;
   double a = 0.0, b = 0.0, n = 0.0;
-#pragma unroll 2
+#pragma unroll GMZ_FIN_UNROLL
   for (int t = threadIdx.x; t < ns; t += nt) {
     const double *p = ws + ((size_t)c * cs + (size_t)t * ts) * 3;
     a += p[0];
